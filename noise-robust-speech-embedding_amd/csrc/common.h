@@ -1,0 +1,89 @@
+// Shared device helpers for the gfx950 kernels of libnrse_hip.so.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/nrse_hip.h"
+
+typedef unsigned short bf16_t;  // storage type for bf16 in memory
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short short4v __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define NRSE_DEV __device__ __forceinline__
+
+NRSE_DEV float bf2f(bf16_t x) { return __uint_as_float(((uint32_t)x) << 16); }
+NRSE_DEV bf16_t f2bf(float x) {
+  __bf16 b = (__bf16)x;  // v_cvt_pk_bf16_f32: round-to-nearest-even, NaN stays NaN
+  return *reinterpret_cast<bf16_t*>(&b);
+}
+
+template <typename T> NRSE_DEV float to_f(T x);
+template <> NRSE_DEV float to_f<float>(float x) { return x; }
+template <> NRSE_DEV float to_f<bf16_t>(bf16_t x) { return bf2f(x); }
+template <typename T> NRSE_DEV T from_f(float x);
+template <> NRSE_DEV float from_f<float>(float x) { return x; }
+template <> NRSE_DEV bf16_t from_f<bf16_t>(float x) { return f2bf(x); }
+
+NRSE_DEV float load_as_f(const void* p, int dtype, long long i) {
+  return dtype == NRSE_BF16 ? bf2f(((const bf16_t*)p)[i]) : ((const float*)p)[i];
+}
+NRSE_DEV void store_from_f(void* p, int dtype, long long i, float v) {
+  if (dtype == NRSE_BF16) ((bf16_t*)p)[i] = f2bf(v);
+  else ((float*)p)[i] = v;
+}
+
+// Exact (erf) GELU as ACT2FN["gelu"] ([TF] activations.GELUActivation -> F.gelu default).
+NRSE_DEV float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+NRSE_DEV float gelu_grad_f(float x) {
+  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+// Counter-based dropout hash (bijective 32-bit mixer, "lowbias32"). The mask of element i at
+// a dropout site seeded with `seed` is keep = hash(i ^ mix(seed)) >= p * 2^32. Deterministic
+// and stateless, so backward regenerates the forward mask from (seed, i).
+NRSE_DEV uint32_t mix32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+  return x;
+}
+NRSE_DEV uint32_t site_key(uint32_t seed) { return mix32(seed * 0x9e3779b9U + 0x632be5abU); }
+NRSE_DEV bool dropout_keep(uint32_t key, uint32_t idx, uint32_t thresh) {
+  return mix32(idx ^ key) >= thresh;
+}
+__host__ __device__ inline uint32_t dropout_threshold(float p) {
+  double t = (double)p * 4294967296.0;
+  if (t >= 4294967295.0) return 0xffffffffU;
+  return (uint32_t)t;
+}
+
+// Wave-wide reductions (wave64).
+NRSE_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+NRSE_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+NRSE_DEV double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Error reporting shared by the C-ABI translation units.
+void nrse_set_error(const char* fmt, ...);
+int nrse_check_launch(const char* what);
+
+#define NRSE_REQUIRE(cond, ...)              \
+  do {                                       \
+    if (!(cond)) {                           \
+      nrse_set_error(__VA_ARGS__);           \
+      return NRSE_ERR_ARG;                   \
+    }                                        \
+  } while (0)
+
+static inline int nrse_cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }

@@ -1,0 +1,48 @@
+"""ORACLE (test infrastructure only — imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg, never by the product path).
+
+numpy restatement of the counter-hash dropout masks the HIP kernels draw
+(noise-robust-speech-embedding_amd/csrc/common.h: mix32 / site_key / dropout_keep), so the CPU
+oracle can replay a stochastic training step with the identical masks. The reference draws its
+masks from torch's Philox stream (torch.nn.Dropout, [TF]modeling_wavlm.py:99/287-294/482) which
+no other implementation can bit-match; what is pinned against the reference is the semantics
+(keep probability 1-p, scale 1/(1-p), mask per element) — see tests/test_stochastic_gpu.py.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+M32 = np.uint64(0xFFFFFFFF)
+
+
+def mix32(x):
+    x = np.asarray(x, dtype=np.uint64) & M32
+    x ^= x >> np.uint64(16)
+    x = (x * np.uint64(0x7FEB352D)) & M32
+    x ^= x >> np.uint64(15)
+    x = (x * np.uint64(0x846CA68B)) & M32
+    x ^= x >> np.uint64(16)
+    return x
+
+
+def site_key(seed: int) -> np.uint64:
+    return mix32((np.uint64(seed) * np.uint64(0x9E3779B9) + np.uint64(0x632BE5AB)) & M32)
+
+
+def threshold(p: float) -> int:
+    t = p * 4294967296.0
+    return 0xFFFFFFFF if t >= 4294967295.0 else int(t)
+
+
+def keep_mask(seed: int, p: float, n: int, start: int = 0) -> np.ndarray:
+    """keep[i] for flat element indices start..start+n-1 of one dropout site."""
+    idx = np.arange(start, start + n, dtype=np.uint64)
+    h = mix32(idx ^ site_key(seed))
+    return h >= np.uint64(threshold(p))
+
+
+def dropout_mask(seed: int, p: float, shape) -> np.ndarray:
+    """Multiplicative mask (0 or 1/(1-p)) over a row-major tensor of `shape`."""
+    n = int(np.prod(shape))
+    k = keep_mask(seed, p, n).reshape(shape)
+    return k.astype(np.float32) * np.float32(1.0 / (1.0 - p)) if p < 1 else np.zeros(shape, np.float32)

@@ -1,0 +1,292 @@
+"""ORACLE (test infrastructure only — imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg; never by the product path, which must run on libnrse_hip.so or fail).
+
+fp32 PyTorch-eager CPU restatement of the reference BYOL-on-WavLM training step, written
+fresh from the reference's algorithm (no transformers import). Pinned against golden
+fixtures produced by the reference itself (tests/golden/make_golden.py) in
+tests/test_oracle_golden.py.
+
+Followed line by line:
+  conv feature encoder      [TF]modeling_wavlm.py:712-720, 773-783
+  feature projection        [TF]modeling_wavlm.py:93-105
+  SpecAugment (time masks)  [TF]modeling_wavlm.py:985-1011 (mask indices are inputs here)
+  positional conv           [TF]modeling_wavlm.py:48-90 (weight_norm dim=2)
+  stable-LN encoder         [TF]modeling_wavlm.py:465-513 (LayerDrop decisions are inputs)
+  layer                     [TF]modeling_wavlm.py:355-373
+  gated rel-pos attention   [TF]modeling_wavlm.py:147-271, [TORCH]functional.py:6206 (SDPA)
+  FFN                       [TF]modeling_wavlm.py:274-295
+  time-mean shim            SURVEY.md §0.2 (documented deviation)
+  heads                     src/models/multi_layer_heads.py:4-48
+  BYOL forward / EMA        src/models/byol.py:62-97
+  loss                      src/models/byol.py:104-128
+  step                      train_byol.py:56-74 (zero_grad, backward, clip 1.0, AdamW, EMA)
+
+Dropout masks: the counter hash of oracle/masks.py (identical to the HIP kernels) driven by
+nrse_amd.rng site seeds; with every probability at 0 (the "det" arch) it is exactly the
+reference's train-mode computation.
+"""
+from __future__ import annotations
+
+import math
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(_HERE), "noise-robust-speech-embedding_amd"))
+from nrse_amd import rng  # noqa: E402  (seed derivation only; no compute)
+
+from . import masks  # noqa: E402
+
+
+# ------------------------------------------------------------------------- relative buckets
+def rel_bucket(rel: np.ndarray, num_buckets: int = 320, max_distance: int = 800) -> np.ndarray:
+    """[TF]modeling_wavlm.py:253-271 in numpy; float32 log like torch's `.float()` path."""
+    nb = num_buckets // 2
+    out = (rel > 0).astype(np.int64) * nb
+    rp = np.abs(rel)
+    max_exact = nb // 2
+    is_small = rp < max_exact
+    with np.errstate(divide="ignore"):
+        lg = np.log(rp.astype(np.float32) / np.float32(max_exact)).astype(np.float32)
+    lg = (lg / np.float32(math.log(max_distance / max_exact))).astype(np.float32)
+    lg = (lg * np.float32(nb - max_exact)).astype(np.float32)
+    large = (np.float32(max_exact) + lg)
+    large = np.where(np.isfinite(large), large, 0).astype(np.int64)
+    large = np.minimum(large, nb - 1)
+    return out + np.where(is_small, rp, large)
+
+
+def bucket_vector(T: int, num_buckets: int = 320, max_distance: int = 800) -> np.ndarray:
+    """bucket(j - i) for d = j - i in [-(T-1), T-1], index d + T - 1."""
+    d = np.arange(-(T - 1), T, dtype=np.int64)
+    return rel_bucket(d, num_buckets, max_distance)
+
+
+def position_bias(E: torch.Tensor, T: int, nb: int, md: int) -> torch.Tensor:
+    """compute_bias ([TF]modeling_wavlm.py:243-251): [H, T, T] from rel_attn_embed [nb, H]."""
+    i = np.arange(T)[:, None]
+    j = np.arange(T)[None, :]
+    b = torch.from_numpy(rel_bucket(j - i, nb, md))
+    return E[b].permute(2, 0, 1)
+
+
+# ------------------------------------------------------------------------- pieces
+def _drop(x: torch.Tensor, p: float, seed: int) -> torch.Tensor:
+    if p <= 0:
+        return x
+    m = torch.from_numpy(masks.dropout_mask(seed, p, tuple(x.shape)))
+    return x * m
+
+
+def conv_stack(P: dict, a, wav: torch.Tensor) -> torch.Tensor:
+    """wav [B, L] -> extract_features [B, T, C]."""
+    x = wav[:, None]
+    for i, (k, s) in enumerate(zip(a.conv_kernel, a.conv_stride)):
+        pre = f"feature_extractor.conv_layers.{i}."
+        x = F.conv1d(x, P[pre + "conv.weight"], stride=s)
+        x = F.layer_norm(x.transpose(1, 2), (x.shape[1],), P[pre + "layer_norm.weight"], P[pre + "layer_norm.bias"],
+                         a.eps).transpose(1, 2)
+        x = F.gelu(x)
+    return x.transpose(1, 2)
+
+
+def weight_norm_w(g: torch.Tensor, v: torch.Tensor) -> torch.Tensor:
+    """torch.nn.utils.parametrizations.weight_norm(dim=2): w = g * v / ||v|| (norm over 0,1)."""
+    return v * (g / v.pow(2).sum(dim=(0, 1), keepdim=True).sqrt())
+
+
+def gate(P: dict, pre: str, x1: torch.Tensor, heads: int) -> torch.Tensor:
+    """[TF]modeling_wavlm.py:164-176: gate [B, H, T]."""
+    B, T, H = x1.shape
+    gh = x1.view(B, T, heads, -1).permute(0, 2, 1, 3)
+    proj = F.linear(gh, P[pre + "gru_rel_pos_linear.weight"], P[pre + "gru_rel_pos_linear.bias"])
+    proj = proj.view(B, heads, T, 2, 4).sum(-1)
+    ga, gb = torch.sigmoid(proj).chunk(2, dim=-1)
+    c = P[pre + "gru_rel_pos_const"].view(1, heads, 1, 1)
+    return (ga * (gb * c - 1.0) + 2.0).squeeze(-1)
+
+
+def attention(P: dict, a, li: int, x1: torch.Tensor, pbias: torch.Tensor, fseed: int, train: bool):
+    B, T, H = x1.shape
+    nh, hd = a.heads, a.head_dim
+    pre = f"encoder.layers.{li}.attention."
+    q = F.linear(x1, P[pre + "q_proj.weight"], P[pre + "q_proj.bias"])
+    k = F.linear(x1, P[pre + "k_proj.weight"], P[pre + "k_proj.bias"])
+    v = F.linear(x1, P[pre + "v_proj.weight"], P[pre + "v_proj.bias"])
+    q = q.view(B, T, nh, hd).transpose(1, 2)
+    k = k.view(B, T, nh, hd).transpose(1, 2)
+    v = v.view(B, T, nh, hd).transpose(1, 2)
+    g = gate(P, pre, x1, nh)                               # [B, nh, T]
+    s = (q @ k.transpose(-1, -2)) / math.sqrt(hd) + g[..., None] * pbias[None]
+    p = torch.softmax(s, dim=-1)
+    if train:
+        p = _drop(p, a.attention_dropout, rng.site_seed(fseed, rng.site_attn_probs(li)))
+    ctx = (p @ v).transpose(1, 2).reshape(B, T, H)
+    return F.linear(ctx, P[pre + "out_proj.weight"], P[pre + "out_proj.bias"])
+
+
+def encoder_forward(P: dict, a, wav: torch.Tensor, *, train: bool = False, fseed: int = 0,
+                    layer_skip=None, mask_time=None) -> torch.Tensor:
+    """WavLMModel.forward ([TF]modeling_wavlm.py:1032-1096) -> last_hidden_state [B, T, H]."""
+    feats = conv_stack(P, a, wav)
+    B, T, C = feats.shape
+    xn = F.layer_norm(feats, (C,), P["feature_projection.layer_norm.weight"], P["feature_projection.layer_norm.bias"],
+                      a.eps)
+    h = F.linear(xn, P["feature_projection.projection.weight"], P["feature_projection.projection.bias"])
+    if train:
+        h = _drop(h, a.feat_proj_dropout, rng.site_seed(fseed, rng.SITE_FEAT_PROJ))
+    if train and mask_time is not None:
+        m = torch.as_tensor(mask_time, dtype=torch.bool)
+        h = torch.where(m[..., None], P["masked_spec_embed"].view(1, 1, -1), h)
+    pre = "encoder.pos_conv_embed.conv."
+    w = weight_norm_w(P[pre + "parametrizations.weight.original0"], P[pre + "parametrizations.weight.original1"])
+    pc = F.conv1d(h.transpose(1, 2), w, P[pre + "bias"], padding=a.pos_kernel // 2, groups=a.pos_groups)
+    if a.pos_kernel % 2 == 0:
+        pc = pc[:, :, :-1]
+    h = h + F.gelu(pc).transpose(1, 2)
+    if train:
+        h = _drop(h, a.hidden_dropout, rng.site_seed(fseed, rng.SITE_POS))
+    pbias = position_bias(P["encoder.layers.0.attention.rel_attn_embed.weight"], T, a.num_buckets, a.max_distance)
+    for li in range(a.layers):
+        if train and layer_skip is not None and layer_skip[li]:
+            continue
+        pre = f"encoder.layers.{li}."
+        x1 = F.layer_norm(h, (h.shape[-1],), P[pre + "layer_norm.weight"], P[pre + "layer_norm.bias"], a.eps)
+        att = attention(P, a, li, x1, pbias, fseed, train)
+        if train:
+            att = _drop(att, a.hidden_dropout, rng.site_seed(fseed, rng.site_attn_out(li)))
+        h = h + att
+        x2 = F.layer_norm(h, (h.shape[-1],), P[pre + "final_layer_norm.weight"], P[pre + "final_layer_norm.bias"],
+                          a.eps)
+        f = F.gelu(F.linear(x2, P[pre + "feed_forward.intermediate_dense.weight"],
+                            P[pre + "feed_forward.intermediate_dense.bias"]))
+        if train:
+            f = _drop(f, a.activation_dropout, rng.site_seed(fseed, rng.site_act(li)))
+        f = F.linear(f, P[pre + "feed_forward.output_dense.weight"], P[pre + "feed_forward.output_dense.bias"])
+        if train:
+            f = _drop(f, a.hidden_dropout, rng.site_seed(fseed, rng.site_ffn_out(li)))
+        h = h + f
+    return F.layer_norm(h, (h.shape[-1],), P["encoder.layer_norm.weight"], P["encoder.layer_norm.bias"], a.eps)
+
+
+def bn_train(x, w, b, run_mean, run_var, momentum=0.1, eps=1e-5, train=True):
+    """nn.BatchNorm1d: batch stats (biased var) in train mode, running stats updated with the
+    unbiased var; running stats in eval mode."""
+    return F.batch_norm(x, run_mean, run_var, w, b, training=train, momentum=momentum, eps=eps)
+
+
+def projector(P: dict, x, buf: dict, train=True):
+    x = F.linear(x, P["layers.0.weight"], P["layers.0.bias"])
+    x = torch.relu(bn_train(x, P["layers.1.weight"], P["layers.1.bias"], buf["layers.1.running_mean"],
+                            buf["layers.1.running_var"], train=train))
+    x = F.linear(x, P["layers.3.weight"], P["layers.3.bias"])
+    return bn_train(x, P["layers.4.weight"], P["layers.4.bias"], buf["layers.4.running_mean"],
+                    buf["layers.4.running_var"], train=train)
+
+
+def predictor(P: dict, x, buf: dict, train=True):
+    x = F.linear(x, P["layers.0.weight"], P["layers.0.bias"])
+    x = torch.relu(bn_train(x, P["layers.1.weight"], P["layers.1.bias"], buf["layers.1.running_mean"],
+                            buf["layers.1.running_var"], train=train))
+    x = F.linear(x, P["layers.3.weight"], P["layers.3.bias"])
+    x = torch.relu(bn_train(x, P["layers.4.weight"], P["layers.4.bias"], buf["layers.4.running_mean"],
+                            buf["layers.4.running_var"], train=train))
+    return F.linear(x, P["layers.6.weight"], P["layers.6.bias"])
+
+
+def byol_loss(p: torch.Tensor, z: torch.Tensor) -> torch.Tensor:
+    """src/models/byol.py:104-128."""
+    p = F.normalize(p + 1e-10, dim=1, eps=1e-10)
+    z = F.normalize(z + 1e-10, dim=1, eps=1e-10)
+    s = torch.clamp((p * z).sum(1), -1.0, 1.0)
+    return 2 - 2 * s.mean()
+
+
+def split_flat(layout, flat: torch.Tensor, target: bool = False) -> dict:
+    """{'encoder': {...}, 'projector': {...}, 'predictor': {...}} of module-relative views."""
+    out = {"encoder": {}, "projector": {}, "predictor": {}}
+    for gname, s in layout.specs:
+        if target and gname == "predictor":
+            continue
+        key = {"encoder": "online_encoder.model.", "projector": "online_projector.",
+               "predictor": "online_predictor."}[gname] + s.name
+        off, n, shp = layout.offsets[key]
+        out[gname][s.name] = flat[off:off + n].view(shp)
+    return out
+
+
+def head_buffers(proj_dim: int, pred_dim: int) -> dict:
+    def bn(c):
+        return {"running_mean": torch.zeros(c), "running_var": torch.ones(c)}
+    return {
+        "online_projector": {f"layers.{i}.{k}": v for i in (1, 4) for k, v in bn(proj_dim).items()},
+        "target_projector": {f"layers.{i}.{k}": v for i in (1, 4) for k, v in bn(proj_dim).items()},
+        "online_predictor": {**{f"layers.1.{k}": v for k, v in bn(pred_dim).items()},
+                             **{f"layers.4.{k}": v for k, v in bn(pred_dim).items()}},
+    }
+
+
+class OracleState:
+    """Full training state of the oracle: flat online / target params + AdamW moments."""
+
+    def __init__(self, layout, flat: torch.Tensor):
+        self.layout = layout
+        self.online = flat.clone()
+        self.target = flat[:layout.ema_numel].clone()
+        self.m = torch.zeros_like(self.online)
+        self.v = torch.zeros_like(self.online)
+        self.step = 0
+        self.buffers = head_buffers(layout.proj_dim, layout.pred_dim)
+
+
+def forward(state: OracleState, clean, noisy, *, train: bool, step_seed: int = 0, online_flat=None,
+            layer_skip=(None, None), mask_time=(None, None), time_mean: bool = True):
+    """BYOLSpeechModel.forward (src/models/byol.py:75-97) -> (online_pred, target_proj, emb)."""
+    a = state.layout.arch
+    on = split_flat(state.layout, state.online if online_flat is None else online_flat)
+    tg = split_flat(state.layout, state.target, target=True)
+    h = encoder_forward(on["encoder"], a, clean, train=train, fseed=rng.forward_seed(step_seed, 0),
+                        layer_skip=layer_skip[0], mask_time=mask_time[0])
+    emb = h.mean(1) if time_mean else h
+    proj = projector(on["projector"], emb, state.buffers["online_projector"], train)
+    pred = predictor(on["predictor"], proj, state.buffers["online_predictor"], train)
+    with torch.no_grad():
+        ht = encoder_forward(tg["encoder"], a, noisy, train=train, fseed=rng.forward_seed(step_seed, 1),
+                             layer_skip=layer_skip[1], mask_time=mask_time[1])
+        tproj = projector(tg["projector"], ht.mean(1), state.buffers["target_projector"], train)
+    return pred, tproj, emb
+
+
+def train_step(state: OracleState, clean, noisy, *, lr: float, weight_decay: float, ema_decay: float,
+               max_norm: float = 1.0, step_seed: int = 0, layer_skip=(None, None), mask_time=(None, None)):
+    """One iteration of train_byol.py:56-74; returns dict of diagnostics."""
+    p = state.online.clone().requires_grad_(True)
+    pred, tproj, emb = forward(state, clean, noisy, train=True, step_seed=step_seed, online_flat=p,
+                               layer_skip=layer_skip, mask_time=mask_time)
+    loss = byol_loss(pred, tproj)
+    loss.backward()
+    g = p.grad.detach()
+    # clip_grad_norm_: norm of the per-parameter norms ([TORCH]nn/utils/clip_grad.py); a single
+    # fp32 norm over the 3e8-element flat vector loses the small entries.
+    per = [g[off:off + n].norm() for (off, n, _) in state.layout.offsets.values()]
+    total_norm = torch.stack(per).norm()
+    coef = min(1.0, max_norm / (float(total_norm) + 1e-6))
+    g = g * coef
+    # torch.optim.AdamW (decoupled wd, bias-corrected, eps outside sqrt)
+    state.step += 1
+    b1, b2, eps = 0.9, 0.999, 1e-8
+    w = state.online * (1 - lr * weight_decay)
+    state.m.mul_(b1).add_(g, alpha=1 - b1)
+    state.v.mul_(b2).addcmul_(g, g, value=1 - b2)
+    bc1 = 1 - b1 ** state.step
+    bc2 = 1 - b2 ** state.step
+    denom = state.v.sqrt() / math.sqrt(bc2) + eps
+    state.online = w - (lr / bc1) * state.m / denom
+    # EMA of encoder + projector parameters (src/models/byol.py:62-73)
+    state.target = ema_decay * state.target + (1 - ema_decay) * state.online[:state.layout.ema_numel]
+    return {"loss": float(loss.detach()), "grad_norm": float(total_norm), "pred": pred.detach(), "tproj": tproj.detach(),
+            "emb": emb.detach(), "grad": g / coef}

@@ -1,0 +1,108 @@
+"""Pin the CPU oracle (oracle/) against golden fixtures produced by the reference itself
+(tests/golden/make_golden.py). CPU only."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import snr_mix as SM
+from oracle import wavlm_byol as O
+from nrse_amd import arch as A, params as PR
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def rel(a, b):
+    a = np.asarray(a, np.float64); b = np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def test_buckets_match_reference():
+    z = np.load(os.path.join(GOLD, "buckets.npz"))
+    for key in z.files:
+        T = int(key[1:])
+        np.testing.assert_array_equal(O.bucket_vector(T).astype(np.int32), z[key])
+
+
+def test_snr_mix_matches_reference():
+    z = np.load(os.path.join(GOLD, "snr_mix.npz"))
+    for i in range(int(z["n_cases"])):
+        s, n, snr = z[f"c{i}_speech"], z[f"c{i}_noise"], float(z[f"c{i}_snr"])
+        c, y, st, k = SM.mix_pair(s, n, snr, do_normalize=True)
+        if int(z[f"c{i}_ok"]) == 0:
+            assert st != SM.OK, i
+            continue
+        assert st == SM.OK, (i, st)
+        yraw, _, _ = SM.add_noise(s, n, snr)
+        assert rel(yraw, z[f"c{i}_noisy_raw"]) < 1e-6
+        assert rel(c, z[f"c{i}_clean_iv"]) < 1e-5
+        assert rel(y, z[f"c{i}_noisy_iv"]) < 1e-5
+
+
+def inputs(z):
+    """Fixture inputs: stored (tiny) or regenerated from the seed (large), as make_golden did."""
+    if "clean" in z.files:
+        return torch.from_numpy(z["clean"]), torch.from_numpy(z["noisy"])
+    g = torch.Generator().manual_seed(int(z["seed"]) + 1)
+    B, L = int(z["B"]), int(z["L"])
+    clean = torch.randn(B, 1, L, generator=g)
+    noisy = clean + 0.3 * torch.randn(B, 1, L, generator=g)
+    return clean.squeeze(1), noisy.squeeze(1)
+
+
+def _state(tag, arch):
+    z = np.load(os.path.join(GOLD, f"byol_{tag}.npz"))
+    layout = PR.byol_layout(arch, int(z["proj_dim"]), int(z["pred_dim"]))
+    flat = PR.init_byol_flat(layout, int(z["seed"]))
+    return z, layout, O.OracleState(layout, flat)
+
+
+@pytest.mark.parametrize("tag", ["tiny", "large"])
+def test_oracle_eval_forward(tag):
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    arch = (A.TINY if tag == "tiny" else A.LARGE).deterministic()
+    z, layout, st = _state(tag, arch)
+    clean, noisy = inputs(z)
+    with torch.no_grad():
+        pred, tproj, emb = O.forward(st, clean, noisy, train=False)
+        loss = O.byol_loss(pred, tproj)
+    assert rel(emb, z["eval_emb"]) < 1e-5
+    assert rel(pred, z["eval_pred"]) < 1e-4
+    assert rel(tproj, z["eval_tproj"]) < 1e-4
+    assert abs(float(loss) - float(z["eval_loss"])) < 1e-4
+    if tag == "tiny":
+        on = O.split_flat(layout, st.online)
+        h = O.encoder_forward(on["encoder"], arch, clean)
+        assert rel(h, z["eval_hidden"]) < 1e-5
+
+
+@pytest.mark.parametrize("tag", ["tiny", "large"])
+def test_oracle_train_step(tag):
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    arch = (A.TINY if tag == "tiny" else A.LARGE).deterministic()
+    z, layout, st = _state(tag, arch)
+    flat0 = st.online.clone()
+    clean, noisy = inputs(z)
+    r = O.train_step(st, clean, noisy, lr=float(z["lr"]), weight_decay=float(z["wd"]), ema_decay=float(z["ema"]))
+    assert abs(r["loss"] - float(z["train_loss"])) < 1e-4
+    # BatchNorm backward in the heads amplifies fp32 summation-order differences (~1e-4)
+    assert abs(r["grad_norm"] - float(z["train_grad_norm"])) / float(z["train_grad_norm"]) < 1e-3
+    norms = []
+    for gname, s in layout.specs:
+        off, cnt, _ = layout.offsets[PR.GROUP_PREFIX[gname] + s.name]
+        norms.append(float(r["grad"][off:off + cnt].norm()))
+    norms = np.array(norms)
+    ref = z["grad_tensor_norms"]
+    big = ref > 1e-3 * ref.max()
+    assert np.max(np.abs(norms[big] - ref[big]) / ref[big]) < 1e-3
+    idx = z["grad_idx"]
+    assert rel(r["grad"][idx].numpy(), z["grad_sample"]) < 1e-3
+    # AdamW first step moves each weight by ~lr*sign(g) (+ decoupled wd): compare in units of lr
+    lr = float(z["lr"])
+    d = (st.online - flat0)[idx].numpy()
+    mism = np.abs(d - z["online_delta_sample"]) > 0.05 * lr
+    assert mism.mean() < 0.01, mism.mean()
+    tidx = z["target_idx"]
+    dt = (st.target - flat0[:layout.ema_numel])[tidx].numpy()
+    assert np.max(np.abs(dt - z["target_delta_sample"])) < 0.05 * lr
