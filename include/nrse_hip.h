@@ -104,6 +104,7 @@ typedef struct {
   long long ldc, c_z1, c_z2, c_split;
   /* epilogue operands */
   const float* bias;
+  long long bias_z1, bias_z2;  /* batch offsets of bias (grouped pos-conv) */
   const void* aux;       /* GELU pre-activation store (GELU) or load (GELU_BWD) */
   int aux_dtype;
   long long ldaux, aux_z1, aux_z2;
@@ -111,11 +112,205 @@ typedef struct {
   int resid_dtype;
   long long ldr, r_z1, r_z2;
   float dropout_p;
-  uint32_t seed;         /* dropout mask = hash(seed, m*N + n) */
+  uint32_t seed;         /* dropout mask = hash(seed, element offset of C[m,n] from c) */
   float* colsum;
 } nrse_gemm_params;
 
 int nrse_gemm(const nrse_gemm_params* p, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * LayerNorm over the last (channel) dim of channels-last rows, fp32 statistics.
+ *   conv layers       [TF]modeling_wavlm.py:712-720 (LN(512) + GELU, fused: flags |= NRSE_LN_GELU)
+ *   feature projection[TF]modeling_wavlm.py:101
+ *   encoder layers    [TF]modeling_wavlm.py:357, 369, final 513
+ * fwd: y = act(LN(x)) ; saves mean/rstd per row.
+ * bwd: dy is read directly ([rows, C]), through col2im of a conv dgrad GEMM output
+ *      (dy_mode = NRSE_DY_COL2IM: dy[b, tau] = sum_j G[b, (tau-j)/s, j*C + c] over valid j), or
+ *      broadcast per utterance (NRSE_DY_BCAST: dy[b, t] = dy_vec[b] * dy_scale, the time-mean
+ *      shim). dx = resid + LN'(...) (resid optional, f32). dgamma/dbeta accumulate (f32 atomics).
+ * ------------------------------------------------------------------------------------------ */
+enum { NRSE_LN_GELU = 1 };
+enum { NRSE_DY_DIRECT = 0, NRSE_DY_COL2IM = 1, NRSE_DY_BCAST = 2 };
+
+typedef struct {
+  const void* x; int x_dtype;
+  const float* gamma; const float* beta;
+  void* y; int y_dtype;
+  float* mean; float* rstd;
+  long long rows; int C; float eps; int flags;
+} nrse_ln_fwd_params;
+
+typedef struct {
+  const void* dy; int dy_dtype; int dy_mode;
+  int col_k, col_s, col_tout, col_tin;   /* NRSE_DY_COL2IM geometry; rows = batch * col_tin */
+  int bcast_t; float dy_scale;           /* NRSE_DY_BCAST: rows per utterance, scale */
+  const void* x; int x_dtype;
+  const float* gamma; const float* beta;
+  const float* mean; const float* rstd;
+  void* dx; int dx_dtype;
+  const float* resid;                    /* optional f32 [rows, C] added to dx */
+  float* dgamma; float* dbeta;
+  long long rows; int C; int flags;
+} nrse_ln_bwd_params;
+
+int nrse_layernorm_fwd(const nrse_ln_fwd_params* p, void* stream);
+int nrse_layernorm_bwd(const nrse_ln_bwd_params* p, void* stream);
+
+/* Final encoder LN fused with the time-mean pooling shim:
+ * emb[b, c] = mean_t LN(h[b, t])[c]; emb must be zeroed by the caller. */
+int nrse_ln_mean_fwd(const float* h, const float* gamma, const float* beta, float* emb, float* mean, float* rstd,
+                     int batch, int T, int C, float eps, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Gated relative-position attention, WavLMAttention ([TF]modeling_wavlm.py:147-271) with
+ * F.multi_head_attention_forward / SDPA ([TORCH]functional.py:6206, 6629).
+ * Layouts: qkv [B*T, 3*Hd] rows = (q | k | v), head h at columns h*64..h*64+63 (head_dim 64);
+ * ctx [B*T, Hd]; gate, lse, delta [B, H, T] f32; bias [H, T, T] f32 (layer-0 table, reused by
+ * every layer as in [TF]modeling_wavlm.py:505); bucket [2T-1] int32 = bucket(j - i) at j-i+T-1.
+ * Dropout on the attention probabilities: keep(i) = hash(seed, ((b*H+h)*T+i)*T+j).
+ * ------------------------------------------------------------------------------------------ */
+int nrse_rel_bias_fwd(const float* E, const int* bucket, float* bias, int H, int T, int nb, void* stream);
+/* dE[bucket[d], h] += diag[h, d] (compute_bias backward). */
+int nrse_rel_bias_bwd(const float* diag, const int* bucket, float* dE, int H, int T, void* stream);
+
+/* gate[b,h,t] = a*(b_*c_h - 1) + 2 with (a, b_) = sigmoid(pair sums of gru_rel_pos_linear(x_h))
+ * ([TF]modeling_wavlm.py:164-176). x1 [B*T, Hd] (the LN1 output), W [8, 64], bias [8], c [H]. */
+int nrse_gate_fwd(const void* x1, int x_dtype, const float* W, const float* bvec, const float* c, float* gate,
+                  int batch, int T, int H, void* stream);
+/* dx1 (f32, accumulated) += dgate path; dW [8,64], db [8], dc [H] accumulated (f32);
+ * scratch: f32 [B*T*H*9] (caller-provided). */
+int nrse_gate_bwd(const void* x1, int x_dtype, const float* W, const float* bvec, const float* c, const float* dgate,
+                  float* dx1, float* dW, float* db, float* dc, float* scratch, int batch, int T, int H, void* stream);
+
+typedef struct {
+  const void* qkv; int dtype;     /* q/k/v (bf16 or f32) */
+  const float* gate; const float* bias;
+  void* ctx;                      /* [B*T, Hd] same dtype as qkv */
+  float* lse;                     /* [B, H, T] */
+  int batch, T, H, head_dim;
+  float scale;                    /* 1/sqrt(head_dim) */
+  float dropout_p; uint32_t seed;
+} nrse_attn_fwd_params;
+
+typedef struct {
+  const void* qkv; int dtype;
+  const float* gate; const float* bias;
+  const void* ctx; const void* dctx;   /* O and dO */
+  const float* lse;
+  float* delta;                        /* scratch [B, H, T]: rowsum(dO * O) */
+  void* dqkv;                          /* [B*T, 3*Hd] */
+  float* dgate;                        /* [B, H, T] */
+  float* diag;                         /* [H, 2T-1] f32, accumulated: sum_b gate * dS along j-i */
+  int batch, T, H, head_dim;
+  float scale; float dropout_p; uint32_t seed;
+} nrse_attn_bwd_params;
+
+int nrse_attn_fwd(const nrse_attn_fwd_params* p, void* stream);
+int nrse_attn_bwd(const nrse_attn_bwd_params* p, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Conv feature encoder front end and the positional-conv weight norm.
+ * conv0 = Conv1d(1 -> C, k, stride s, no bias) + LN(C) + GELU ([TF]modeling_wavlm.py:712-720),
+ * channels-last output [B, T0, C]. Backward recomputes conv0 from the waveform, applies the
+ * LN+GELU backward and accumulates only dW (the waveform needs no gradient); dy may come
+ * through col2im of conv1's dgrad GEMM (same geometry fields as nrse_ln_bwd_params).
+ * ------------------------------------------------------------------------------------------ */
+typedef struct {
+  const float* wav; int L;        /* [B, L] f32 */
+  const float* w;                 /* [C, k] */
+  const float* gamma; const float* beta;
+  void* out; int out_dtype;       /* [B, T0, C] = gelu(LN(conv)) */
+  float* mean; float* rstd;       /* [B*T0] */
+  const void* dy; int dy_dtype; int dy_mode; int col_k, col_s, col_tout;   /* bwd only */
+  float* dw; float* dgamma; float* dbeta;                                  /* bwd only */
+  int batch, T0, C, k, s; float eps;
+} nrse_conv0_params;
+int nrse_conv0_fwd(const nrse_conv0_params* p, void* stream);
+int nrse_conv0_bwd(const nrse_conv0_params* p, void* stream);
+
+/* weight_norm(dim=2) of the grouped pos-conv ([TF]modeling_wavlm.py:61-77):
+ * w[o, i, j] = g[j] * v[o, i, j] / ||v[:, :, j]||.  Writes the two GEMM weight layouts
+ *   wf [G][cpg][K*cpg]: wf[g][o][j*cpg + i]        (forward:  B operand, n = o)
+ *   wd [G][cpg][K*cpg]: wd[g][i][j'*cpg + o] = w[g*cpg+o][i][K-1-j']  (dgrad, flipped taps)
+ * and norms[K]. Backward takes dWf in the wf layout (f32) and produces dg [K], dv [H, cpg, K]. */
+int nrse_weight_norm_fwd(const float* g, const float* v, void* wf, void* wd, int w_dtype, float* norms, int H,
+                         int cpg, int K, void* stream);
+int nrse_weight_norm_bwd(const float* dWf, const float* g, const float* v, const float* norms, float* dg, float* dv,
+                         float* scratch, int H, int cpg, int K, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Elementwise / data-movement kernels of the step.
+ * ------------------------------------------------------------------------------------------ */
+/* dst[b, pad_front + t, :] = (mask[b,t] ? embed : src[b, t, :]) (cast to dst dtype); the pad
+ * rows of dst are zeroed. If h_inout is non-null the SpecAugment row replacement is also
+ * applied in place to the f32 hidden state ([TF]modeling_wavlm.py:1006-1011). */
+int nrse_specaug_pad(float* h_inout, const unsigned char* mask, const float* embed, void* dst, int dst_dtype,
+                     int batch, int T, int C, int pad_front, int pad_back, void* stream);
+/* generic padded copy: dst[b, pad_front + t, :] = src[b, t, :], pad rows zeroed */
+int nrse_pad_rows(const void* src, int src_dtype, void* dst, int dst_dtype, int batch, int T, int C, int pad_front,
+                  int pad_back, void* stream);
+/* SpecAugment + dropout backward on the feature-projection output:
+ * dembed[c] += sum over masked rows of dh; out = (masked ? 0 : dh) * dropout_mask(seed, p). */
+int nrse_specaug_bwd(const float* dh, const unsigned char* mask, float* dembed, void* out, int out_dtype, int batch,
+                     int T, int C, float dropout_p, uint32_t seed, void* stream);
+/* out[i] = in[i] * dropout_mask(seed, p)[i] (cast); in f32, out f32/bf16 */
+int nrse_dropout_cast(const float* in, void* out, int out_dtype, long long n, float dropout_p, uint32_t seed,
+                      void* stream);
+/* colsum[c] += sum_r x[r, c] (f32 atomics) */
+int nrse_colsum(const void* x, int dtype, float* colsum, long long rows, int C, void* stream);
+/* y = x cast (f32 <-> bf16), n elements */
+int nrse_cast(const void* x, int x_dtype, void* y, int y_dtype, long long n, void* stream);
+/* dst[a][c][b] (+)= src[a][b][c]  (conv weight [co][ci][k] <-> implicit-GEMM layout [co][k][ci]) */
+int nrse_swap12(const void* src, int src_dtype, void* dst, int dst_dtype, int d0, int d1, int d2, int accumulate,
+                void* stream);
+/* out[b, pad_front + t, c] = dy[b, t, c] * gelu'(pre[b, t, c]); pad rows zeroed */
+int nrse_gelu_bwd_pad(const float* dy, const void* pre, int pre_dtype, void* out, int out_dtype, int batch, int T,
+                      int C, int pad_front, int pad_back, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Heads + loss: BatchNorm1d (train: batch stats, running stats momentum / unbiased var;
+ * eval: running stats) with optional fused ReLU (multi_layer_heads.py:16-20, 39-45) and the
+ * BYOL loss forward+backward (src/models/byol.py:104-128).
+ * ------------------------------------------------------------------------------------------ */
+int nrse_bn_fwd(const float* x, const float* w, const float* b, float* y, float* run_mean, float* run_var,
+                float* save_mean, float* save_invstd, int rows, int C, float momentum, float eps, int train, int relu,
+                void* stream);
+int nrse_bn_bwd(const float* dy, const float* x, const float* y, const float* w, const float* save_mean,
+                const float* save_invstd, float* dx, float* dw, float* db, int rows, int C, int relu, void* stream);
+/* loss[0] = 2 - 2 mean_b clamp(<p_b/|p_b|, z_b/|z_b|>, -1, 1) (+1e-10 offsets, eps 1e-10);
+ * dp = dloss/dp (scaled by grad_scale); stats[0..1] = NaN flags before/after normalisation. */
+int nrse_byol_loss(const float* p, const float* z, float* loss, float* dp, float* stats, int rows, int D,
+                   float grad_scale, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Optimiser tail over the flat f32 parameter / gradient buffers (train_byol.py:67-71,
+ * src/models/byol.py:62-73): sum of squares (f64 accumulation), clip + AdamW, target EMA.
+ * ------------------------------------------------------------------------------------------ */
+int nrse_sumsq(const float* x, long long n, double* out, void* stream);
+typedef struct {
+  float* p; const float* g; float* m; float* v; void* p_shadow; int shadow_dtype;
+  long long n;
+  float lr, beta1, beta2, eps, weight_decay; int step;
+  float max_norm; const double* sumsq;    /* clip coefficient min(1, max_norm/(sqrt(sumsq)+1e-6)) */
+  float grad_scale;                       /* extra multiplier on g (e.g. 1/world_size) */
+} nrse_adamw_params;
+int nrse_adamw(const nrse_adamw_params* p, void* stream);
+int nrse_ema(float* target, const float* online, void* t_shadow, int shadow_dtype, long long n, float decay,
+             void* stream);
+/* health check (train_byol.py:52-59 / debugging_utils.py:4-30): flags[0..3] |= nan, inf,
+ * sum|x| (f32 accumulated into stats[0]), max|x| (stats[1]) */
+int nrse_health(const void* x, int dtype, long long n, float* stats, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Fused on-GPU SNR mix (src/data/augment.py:4-66 + noisy_speech_dataset.py:88-129):
+ * per pair b: tile/truncate noise to L, k = sqrt(Ps / (Pn * 10^(snr/10))), y = s + k n,
+ * peak-normalise both, optional zero-mean/unit-var (feature extractor do_normalize).
+ * status[b] follows oracle/snr_mix.py codes (0 = ok); outputs of failed pairs are zeroed.
+ * scratch: f64 [batch * 16] (caller zeroes).
+ * ------------------------------------------------------------------------------------------ */
+int nrse_snr_mix(const float* clean, const float* noise, const int* noise_len, long long noise_stride,
+                 const float* snr_db, float* clean_out, float* noisy_out, int* status, float* kscale, double* scratch,
+                 int batch, int L, int do_normalize, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,339 @@
+// Conv feature-encoder front end (conv0 + LN + GELU, fused fwd and fused bwd/wgrad) and the
+// weight_norm of the grouped positional conv. Conv layers 1..6 and the pos-conv contraction run
+// as implicit GEMMs in gemm.hip.
+//   conv0         [TF]modeling_wavlm.py:712-720 (Conv1d(1, C, 10, 5, bias=False), LN, GELU)
+//   weight norm   [TF]modeling_wavlm.py:61-77 (parametrizations.weight_norm, dim=2)
+#include "common.h"
+
+namespace {
+
+constexpr int KMAX = 10;
+
+// One wave per output row (b, t); lane owns channels c = (q*64 + lane)*4 + e, q < NQ.
+template <int NQ>
+__global__ __launch_bounds__(256) void conv0_fwd_kernel(const nrse_conv0_params p) {
+  const int lane = threadIdx.x & 63;
+  const int C = p.C;
+  float w[NQ][4][KMAX];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int j = 0; j < KMAX; ++j) {
+        const int c = (q * 64 + lane) * 4 + e;
+        w[q][e][j] = j < p.k ? p.w[c * p.k + j] : 0.f;
+      }
+  float ga[NQ][4], be[NQ][4];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int c = (q * 64 + lane) * 4 + e;
+      ga[q][e] = p.gamma[c];
+      be[q][e] = p.beta[c];
+    }
+  const long long rows = (long long)p.batch * p.T0;
+  const long long nw = (long long)gridDim.x * 4;
+  for (long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += nw) {
+    const long long b = row / p.T0;
+    const int t = (int)(row - b * p.T0);
+    const float* x = p.wav + b * p.L + (long long)t * p.s;
+    float xs[KMAX];
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) xs[j] = j < p.k ? x[j] : 0.f;
+    float y[NQ][4];
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float a = 0.f;
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) a += w[q][e][j] * xs[j];
+        y[q][e] = a;
+        s += a;
+      }
+    const float mean = wave_sum(s) / C;
+    float v = 0.f;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { const float d = y[q][e] - mean; v += d * d; }
+    const float rstd = rsqrtf(wave_sum(v) / C + p.eps);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      float o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = gelu_f((y[q][e] - mean) * rstd * ga[q][e] + be[q][e]);
+      const long long off = row * C + (q * 64 + lane) * 4;
+      if (p.out_dtype == NRSE_BF16) {
+        uint2 u;
+        u.x = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
+        u.y = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
+        *reinterpret_cast<uint2*>((bf16_t*)p.out + off) = u;
+      } else {
+        *reinterpret_cast<float4*>((float*)p.out + off) = make_float4(o[0], o[1], o[2], o[3]);
+      }
+    }
+    if (lane == 0) {
+      p.mean[row] = mean;
+      p.rstd[row] = rstd;
+    }
+  }
+}
+
+NRSE_DEV void ld4(const void* p, int dt, long long i, float* o) {
+  if (dt == NRSE_BF16) {
+    uint2 v = *reinterpret_cast<const uint2*>((const bf16_t*)p + i);
+    o[0] = __uint_as_float(v.x << 16); o[1] = __uint_as_float(v.x & 0xffff0000u);
+    o[2] = __uint_as_float(v.y << 16); o[3] = __uint_as_float(v.y & 0xffff0000u);
+  } else {
+    float4 v = *reinterpret_cast<const float4*>((const float*)p + i);
+    o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+  }
+}
+
+template <int NQ>
+__global__ __launch_bounds__(256) void conv0_bwd_kernel(const nrse_conv0_params p) {
+  __shared__ float red[4][NQ * 256];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int C = p.C;
+  float w[NQ][4][KMAX], dw[NQ][4][KMAX];
+  float ga[NQ][4], be[NQ][4], dga[NQ][4], dbe[NQ][4];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int c = (q * 64 + lane) * 4 + e;
+#pragma unroll
+      for (int j = 0; j < KMAX; ++j) {
+        w[q][e][j] = j < p.k ? p.w[c * p.k + j] : 0.f;
+        dw[q][e][j] = 0.f;
+      }
+      ga[q][e] = p.gamma[c];
+      be[q][e] = p.beta[c];
+      dga[q][e] = dbe[q][e] = 0.f;
+    }
+  const long long rows = (long long)p.batch * p.T0;
+  const long long nw = (long long)gridDim.x * 4;
+  for (long long row = (long long)blockIdx.x * 4 + wv; row < rows; row += nw) {
+    const long long b = row / p.T0;
+    const int t = (int)(row - b * p.T0);
+    const float* x = p.wav + b * p.L + (long long)t * p.s;
+    float xs[KMAX];
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) xs[j] = j < p.k ? x[j] : 0.f;
+    const float mean = p.mean[row], rstd = p.rstd[row];
+    float xh[NQ][4], g[NQ][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int c0 = (q * 64 + lane) * 4;
+      float dy[4] = {0.f, 0.f, 0.f, 0.f};
+      if (p.dy_mode == NRSE_DY_DIRECT) {
+        ld4(p.dy, p.dy_dtype, row * C + c0, dy);
+      } else {
+        const long long kc = (long long)p.col_k * C;
+        for (int j = 0; j < p.col_k; ++j) {
+          const int d = t - j;
+          if (d < 0 || (d % p.col_s) != 0) continue;
+          const int tt = d / p.col_s;
+          if (tt >= p.col_tout) continue;
+          float u[4];
+          ld4(p.dy, p.dy_dtype, (b * p.col_tout + tt) * kc + (long long)j * C + c0, u);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) dy[e] += u[e];
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float a = 0.f;
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) a += w[q][e][j] * xs[j];
+        xh[q][e] = (a - mean) * rstd;
+        const float gg = dy[e] * gelu_grad_f(xh[q][e] * ga[q][e] + be[q][e]);
+        dga[q][e] += gg * xh[q][e];
+        dbe[q][e] += gg;
+        g[q][e] = gg * ga[q][e];
+        s1 += g[q][e];
+        s2 += g[q][e] * xh[q][e];
+      }
+    }
+    s1 = wave_sum(s1) / C;
+    s2 = wave_sum(s2) / C;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float dc = rstd * (g[q][e] - s1 - xh[q][e] * s2);
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) dw[q][e][j] += dc * xs[j];
+      }
+  }
+  // block reduce: dw (C*k), dgamma, dbeta
+  for (int j = 0; j < p.k + 2; ++j) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v;
+        if (j < p.k) {
+          v = 0.f;
+#pragma unroll
+          for (int jj = 0; jj < KMAX; ++jj) if (jj == j) v = dw[q][e][jj];
+        } else {
+          v = (j == p.k) ? dga[q][e] : dbe[q][e];
+        }
+        red[wv][(q * 64 + lane) * 4 + e] = v;
+      }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += 256) {
+      const float v = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+      if (j < p.k) atomicAdd(p.dw + c * p.k + j, v);
+      else if (j == p.k) atomicAdd(p.dgamma + c, v);
+      else atomicAdd(p.dbeta + c, v);
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------- weight norm (dim = 2)
+// v [H][cpg][K] ; per tap j: norm_j = ||v[:, :, j]||
+__global__ __launch_bounds__(256) void wn_norm_kernel(const float* __restrict__ v, float* __restrict__ norms,
+                                                      const float* __restrict__ dWf, float* __restrict__ sdot, int H,
+                                                      int cpg, int K) {
+  __shared__ double red[4];
+  const int j = blockIdx.x;
+  const long long n = (long long)H * cpg;
+  double a = 0.0;
+  for (long long e = threadIdx.x; e < n; e += 256) {
+    const float x = v[e * K + j];
+    if (dWf) {
+      // dWf layout [g][o][j*cpg + i], e = (g*cpg + o)*cpg + i
+      const long long go = e / cpg;
+      const int i = (int)(e % cpg);
+      a += (double)x * dWf[go * (long long)K * cpg + (long long)j * cpg + i];
+    } else {
+      a += (double)x * x;
+    }
+  }
+  a = wave_sum_d(a);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = a;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double s = red[0] + red[1] + red[2] + red[3];
+    if (dWf) sdot[j] = (float)s;
+    else norms[j] = (float)sqrt(s);
+  }
+}
+
+template <typename T>
+__global__ void wn_apply_kernel(const float* __restrict__ g, const float* __restrict__ v,
+                                const float* __restrict__ norms, T* __restrict__ wf, T* __restrict__ wd, int H, int cpg,
+                                int K) {
+  const long long total = (long long)H * cpg * K;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    // e enumerates wf: [G][o][j][i]
+    const int i = (int)(e % cpg);
+    const long long r = e / cpg;
+    const int j = (int)(r % K);
+    const long long go = r / K;          // g*cpg + o
+    const long long gi = go / cpg;
+    const int o = (int)(go % cpg);
+    const float wv = v[(go * cpg + i) * K + j] * (g[j] / norms[j]);
+    wf[e] = from_f<T>(wv);
+    // wd[g][i][(K-1-j)*cpg + o]
+    wd[((gi * cpg + i) * K + (K - 1 - j)) * cpg + o] = from_f<T>(wv);
+  }
+}
+
+__global__ void wn_bwd_kernel(const float* __restrict__ dWf, const float* __restrict__ g, const float* __restrict__ v,
+                              const float* __restrict__ norms, const float* __restrict__ sdot, float* __restrict__ dv,
+                              int H, int cpg, int K) {
+  const long long total = (long long)H * cpg * K;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    // e enumerates v: [go][i][j]
+    const int j = (int)(e % K);
+    const long long r = e / K;
+    const int i = (int)(r % cpg);
+    const long long go = r / cpg;
+    const float nj = norms[j];
+    const float dw = dWf[go * (long long)K * cpg + (long long)j * cpg + i];
+    dv[e] += (g[j] / nj) * (dw - (sdot[j] / (nj * nj)) * v[e]);
+  }
+}
+
+__global__ void wn_dg_kernel(const float* __restrict__ sdot, const float* __restrict__ norms, float* __restrict__ dg,
+                             int K) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < K) dg[j] += sdot[j] / norms[j];
+}
+
+}  // namespace
+
+extern "C" int nrse_conv0_fwd(const nrse_conv0_params* p, void* stream) {
+  NRSE_REQUIRE(p && p->wav && p->w && p->gamma && p->beta && p->out && p->mean && p->rstd, "nrse_conv0_fwd: bad args");
+  NRSE_REQUIRE(p->k > 0 && p->k <= KMAX && p->T0 == (p->L - p->k) / p->s + 1, "nrse_conv0_fwd: bad geometry");
+  const long long rows = (long long)p->batch * p->T0;
+  long long blocks = (rows + 3) / 4;
+  if (blocks > 2048) blocks = 2048;
+  hipStream_t st = (hipStream_t)stream;
+  switch (p->C) {
+    case 256: hipLaunchKernelGGL(conv0_fwd_kernel<1>, dim3(blocks), dim3(256), 0, st, *p); break;
+    case 512: hipLaunchKernelGGL(conv0_fwd_kernel<2>, dim3(blocks), dim3(256), 0, st, *p); break;
+    default: nrse_set_error("nrse_conv0_fwd: C=%d unsupported", p->C); return NRSE_ERR_UNSUPPORTED;
+  }
+  return nrse_check_launch("nrse_conv0_fwd");
+}
+
+extern "C" int nrse_conv0_bwd(const nrse_conv0_params* p, void* stream) {
+  NRSE_REQUIRE(p && p->wav && p->w && p->gamma && p->beta && p->mean && p->rstd && p->dy && p->dw && p->dgamma &&
+               p->dbeta, "nrse_conv0_bwd: bad args");
+  NRSE_REQUIRE(p->k > 0 && p->k <= KMAX, "nrse_conv0_bwd: bad k");
+  if (p->dy_mode == NRSE_DY_COL2IM) NRSE_REQUIRE(p->col_k > 0 && p->col_s > 0 && p->col_tout > 0, "nrse_conv0_bwd: col2im");
+  const long long rows = (long long)p->batch * p->T0;
+  long long blocks = (rows + 3) / 4;
+  if (blocks > 1024) blocks = 1024;
+  hipStream_t st = (hipStream_t)stream;
+  switch (p->C) {
+    case 256: hipLaunchKernelGGL(conv0_bwd_kernel<1>, dim3(blocks), dim3(256), 0, st, *p); break;
+    case 512: hipLaunchKernelGGL(conv0_bwd_kernel<2>, dim3(blocks), dim3(256), 0, st, *p); break;
+    default: nrse_set_error("nrse_conv0_bwd: C=%d unsupported", p->C); return NRSE_ERR_UNSUPPORTED;
+  }
+  return nrse_check_launch("nrse_conv0_bwd");
+}
+
+extern "C" int nrse_weight_norm_fwd(const float* g, const float* v, void* wf, void* wd, int w_dtype, float* norms,
+                                    int H, int cpg, int K, void* stream) {
+  NRSE_REQUIRE(g && v && wf && wd && norms && H > 0 && cpg > 0 && K > 0 && H % cpg == 0, "nrse_weight_norm_fwd: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(wn_norm_kernel, dim3(K), dim3(256), 0, st, v, norms, (const float*)nullptr, (float*)nullptr, H,
+                     cpg, K);
+  const long long total = (long long)H * cpg * K;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  if (w_dtype == NRSE_BF16)
+    hipLaunchKernelGGL(wn_apply_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, g, v, norms, (bf16_t*)wf, (bf16_t*)wd,
+                       H, cpg, K);
+  else
+    hipLaunchKernelGGL(wn_apply_kernel<float>, dim3(blocks), dim3(256), 0, st, g, v, norms, (float*)wf, (float*)wd, H,
+                       cpg, K);
+  return nrse_check_launch("nrse_weight_norm_fwd");
+}
+
+extern "C" int nrse_weight_norm_bwd(const float* dWf, const float* g, const float* v, const float* norms, float* dg,
+                                    float* dv, float* scratch, int H, int cpg, int K, void* stream) {
+  NRSE_REQUIRE(dWf && g && v && norms && dg && dv && scratch, "nrse_weight_norm_bwd: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(wn_norm_kernel, dim3(K), dim3(256), 0, st, v, (float*)nullptr, dWf, scratch, H, cpg, K);
+  const long long total = (long long)H * cpg * K;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(wn_bwd_kernel, dim3(blocks), dim3(256), 0, st, dWf, g, v, norms, scratch, dv, H, cpg, K);
+  hipLaunchKernelGGL(wn_dg_kernel, dim3((K + 255) / 256), dim3(256), 0, st, scratch, norms, dg, K);
+  return nrse_check_launch("nrse_weight_norm_bwd");
+}

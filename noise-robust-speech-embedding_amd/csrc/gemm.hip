@@ -281,7 +281,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const nrse_gemm_params p)
   for (int tn = 0; tn < 4; ++tn) {
     const int n = n0 + wn * 64 + tn * 16 + li;
     const bool nok = n < p.N;
-    const float bias = ((flags & NRSE_EPI_BIAS) && nok) ? p.bias[n] : 0.f;
+    const float bias = ((flags & NRSE_EPI_BIAS) && nok) ? p.bias[zq * p.bias_z1 + zr * p.bias_z2 + n] : 0.f;
     float csum = 0.f;
 #pragma unroll
     for (int tm = 0; tm < 4; ++tm) {
@@ -296,14 +296,14 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const nrse_gemm_params p)
         }
         if (flags & NRSE_EPI_GELU_BWD) v *= gelu_grad_f(load_as_f(p.aux, p.aux_dtype, abase + (long long)m * p.ldaux + n));
         if (flags & NRSE_EPI_RELU) v = fmaxf(v, 0.f);
-        const uint32_t eidx = (uint32_t)((long long)m * p.N + n);
+        const long long ci = cbase + (long long)m * p.ldc + n;
+        const uint32_t eidx = (uint32_t)ci;
         if ((flags & NRSE_EPI_DROPOUT) && !(flags & NRSE_EPI_DROP_AFTER))
           v = dropout_keep(key, eidx, thresh) ? v * dscale : 0.f;
         if (flags & NRSE_EPI_RESID) v += load_as_f(p.resid, p.resid_dtype, rbase + (long long)m * p.ldr + n);
         if ((flags & NRSE_EPI_DROPOUT) && (flags & NRSE_EPI_DROP_AFTER))
           v = dropout_keep(key, eidx, thresh) ? v * dscale : 0.f;
         csum += v;
-        const long long ci = cbase + (long long)m * p.ldc + n;
         if (flags & NRSE_EPI_ATOMIC) {
           atomicAdd((float*)p.c + ci, v);
         } else {

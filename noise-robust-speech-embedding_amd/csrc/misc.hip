@@ -1,0 +1,244 @@
+// Elementwise / data-movement kernels of the step (HBM-bound; 16-byte vectors where the row
+// width allows).
+//   SpecAugment apply/bwd  [TF]modeling_wavlm.py:1006-1011
+//   dropout backward       [TF]modeling_wavlm.py:99, 294, 482 (nn.Dropout)
+//   bias gradients         column sums of the output gradients of every nn.Linear
+#include "common.h"
+
+namespace {
+
+template <typename T> NRSE_DEV void st1(void* p, long long i, float v) { ((T*)p)[i] = from_f<T>(v); }
+
+__global__ void specaug_pad_kernel(float* __restrict__ h, const unsigned char* __restrict__ mask,
+                                   const float* __restrict__ embed, void* __restrict__ dst, int dst_dtype, int batch,
+                                   int T, int C, int pf, int pb) {
+  const int Tp = T + pf + pb;
+  const long long total = (long long)batch * Tp * C;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % C);
+    const long long r = e / C;
+    const int tp = (int)(r % Tp);
+    const long long b = r / Tp;
+    const int t = tp - pf;
+    float v = 0.f;
+    if (t >= 0 && t < T) {
+      const long long si = (b * T + t) * C + c;
+      if (mask && mask[b * T + t]) {
+        v = embed[c];
+        if (h) h[si] = v;
+      } else {
+        v = h ? h[si] : 0.f;
+      }
+    }
+    store_from_f(dst, dst_dtype, e, v);
+  }
+}
+
+__global__ void pad_rows_kernel(const void* __restrict__ src, int sdt, void* __restrict__ dst, int ddt, int batch,
+                                int T, int C, int pf, int pb) {
+  const int Tp = T + pf + pb;
+  const long long total = (long long)batch * Tp * C;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % C);
+    const long long r = e / C;
+    const int tp = (int)(r % Tp);
+    const long long b = r / Tp;
+    const int t = tp - pf;
+    const float v = (t >= 0 && t < T) ? load_as_f(src, sdt, (b * T + t) * C + c) : 0.f;
+    store_from_f(dst, ddt, e, v);
+  }
+}
+
+// one block per row chunk; thread per column
+__global__ void specaug_bwd_kernel(const float* __restrict__ dh, const unsigned char* __restrict__ mask,
+                                   float* __restrict__ dembed, void* __restrict__ out, int odt, int batch, int T, int C,
+                                   float p, uint32_t seed) {
+  const long long rows = (long long)batch * T;
+  const uint32_t key = site_key(seed);
+  const uint32_t thr = dropout_threshold(p);
+  const float sc = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float acc = 0.f;
+    for (long long r = blockIdx.x; r < rows; r += gridDim.x) {
+      const long long i = r * C + c;
+      const float g = dh[i];
+      float o;
+      if (mask && mask[r]) {
+        acc += g;
+        o = 0.f;
+      } else {
+        o = g;
+        if (p > 0.f) o = dropout_keep(key, (uint32_t)i, thr) ? g * sc : 0.f;
+      }
+      store_from_f(out, odt, i, o);
+    }
+    if (mask && dembed && acc != 0.f) atomicAdd(dembed + c, acc);
+  }
+}
+
+__global__ void dropout_cast_kernel(const float* __restrict__ in, void* __restrict__ out, int odt, long long n, float p,
+                                    uint32_t seed) {
+  const uint32_t key = site_key(seed);
+  const uint32_t thr = dropout_threshold(p);
+  const float sc = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const long long n4 = n / 4;
+  for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (long long)gridDim.x * blockDim.x) {
+    float4 v = reinterpret_cast<const float4*>(in)[q];
+    float o[4] = {v.x, v.y, v.z, v.w};
+    if (p > 0.f) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = dropout_keep(key, (uint32_t)(q * 4 + e), thr) ? o[e] * sc : 0.f;
+    }
+    if (odt == NRSE_BF16) {
+      uint2 u;
+      u.x = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
+      u.y = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
+      reinterpret_cast<uint2*>(out)[q] = u;
+    } else {
+      reinterpret_cast<float4*>(out)[q] = make_float4(o[0], o[1], o[2], o[3]);
+    }
+  }
+  for (long long i = n4 * 4 + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    float v = in[i];
+    if (p > 0.f) v = dropout_keep(key, (uint32_t)i, thr) ? v * sc : 0.f;
+    store_from_f(out, odt, i, v);
+  }
+}
+
+// colsum: grid (ceil(C/256), row chunks)
+__global__ void colsum_kernel(const void* __restrict__ x, int dt, float* __restrict__ out, long long rows, int C,
+                              int chunk) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const long long r0 = (long long)blockIdx.y * chunk;
+  const long long r1 = min(rows, r0 + chunk);
+  float a = 0.f;
+  for (long long r = r0; r < r1; ++r) a += load_as_f(x, dt, r * C + c);
+  atomicAdd(out + c, a);
+}
+
+__global__ void cast_kernel(const void* __restrict__ x, int xdt, void* __restrict__ y, int ydt, long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    store_from_f(y, ydt, i, load_as_f(x, xdt, i));
+}
+
+__global__ void swap12_kernel(const void* __restrict__ src, int sdt, void* __restrict__ dst, int ddt, int d0, int d1,
+                              int d2, int acc) {
+  const long long total = (long long)d0 * d1 * d2;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    // e enumerates dst [a][c][b]
+    const int b = (int)(e % d1);
+    const long long r = e / d1;
+    const int c = (int)(r % d2);
+    const long long a = r / d2;
+    float v = load_as_f(src, sdt, (a * d1 + b) * d2 + c);
+    if (acc) v += load_as_f(dst, ddt, e);
+    store_from_f(dst, ddt, e, v);
+  }
+}
+
+__global__ void gelu_bwd_pad_kernel(const float* __restrict__ dy, const void* __restrict__ pre, int pdt,
+                                    void* __restrict__ out, int odt, int batch, int T, int C, int pf, int pb) {
+  const int Tp = T + pf + pb;
+  const long long total = (long long)batch * Tp * C;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % C);
+    const long long r = e / C;
+    const int tp = (int)(r % Tp);
+    const long long b = r / Tp;
+    const int t = tp - pf;
+    float v = 0.f;
+    if (t >= 0 && t < T) {
+      const long long i = (b * T + t) * C + c;
+      v = dy[i] * gelu_grad_f(load_as_f(pre, pdt, i));
+    }
+    store_from_f(out, odt, e, v);
+  }
+}
+
+int blocks_for(long long n, int per = 256, int cap = 8192) {
+  long long b = (n + per - 1) / per;
+  if (b > cap) b = cap;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+}  // namespace
+
+extern "C" int nrse_specaug_pad(float* h, const unsigned char* mask, const float* embed, void* dst, int dst_dtype,
+                                int batch, int T, int C, int pf, int pb, void* stream) {
+  NRSE_REQUIRE(dst && batch > 0 && T > 0 && C > 0 && pf >= 0 && pb >= 0, "nrse_specaug_pad: bad args");
+  NRSE_REQUIRE(!mask || embed, "nrse_specaug_pad: mask without embed");
+  const long long total = (long long)batch * (T + pf + pb) * C;
+  hipLaunchKernelGGL(specaug_pad_kernel, dim3(blocks_for(total)), dim3(256), 0, (hipStream_t)stream, h, mask, embed,
+                     dst, dst_dtype, batch, T, C, pf, pb);
+  return nrse_check_launch("nrse_specaug_pad");
+}
+
+extern "C" int nrse_pad_rows(const void* src, int sdt, void* dst, int ddt, int batch, int T, int C, int pf, int pb,
+                             void* stream) {
+  NRSE_REQUIRE(src && dst && batch > 0 && T > 0 && C > 0, "nrse_pad_rows: bad args");
+  const long long total = (long long)batch * (T + pf + pb) * C;
+  hipLaunchKernelGGL(pad_rows_kernel, dim3(blocks_for(total)), dim3(256), 0, (hipStream_t)stream, src, sdt, dst, ddt,
+                     batch, T, C, pf, pb);
+  return nrse_check_launch("nrse_pad_rows");
+}
+
+extern "C" int nrse_specaug_bwd(const float* dh, const unsigned char* mask, float* dembed, void* out, int odt,
+                                int batch, int T, int C, float p, uint32_t seed, void* stream) {
+  NRSE_REQUIRE(dh && out && batch > 0 && T > 0 && C > 0, "nrse_specaug_bwd: bad args");
+  const long long rows = (long long)batch * T;
+  int blocks = (int)(rows < 2048 ? rows : 2048);
+  hipLaunchKernelGGL(specaug_bwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, dh, mask, dembed, out, odt,
+                     batch, T, C, p, seed);
+  return nrse_check_launch("nrse_specaug_bwd");
+}
+
+extern "C" int nrse_dropout_cast(const float* in, void* out, int odt, long long n, float p, uint32_t seed,
+                                 void* stream) {
+  NRSE_REQUIRE(in && out && n >= 0, "nrse_dropout_cast: bad args");
+  if (n == 0) return NRSE_OK;
+  hipLaunchKernelGGL(dropout_cast_kernel, dim3(blocks_for(n / 4 + 1)), dim3(256), 0, (hipStream_t)stream, in, out, odt,
+                     n, p, seed);
+  return nrse_check_launch("nrse_dropout_cast");
+}
+
+extern "C" int nrse_colsum(const void* x, int dt, float* colsum, long long rows, int C, void* stream) {
+  NRSE_REQUIRE(x && colsum && rows > 0 && C > 0, "nrse_colsum: bad args");
+  int chunk = 64;
+  long long nchunks = (rows + chunk - 1) / chunk;
+  while (nchunks > 4096) { chunk *= 2; nchunks = (rows + chunk - 1) / chunk; }
+  hipLaunchKernelGGL(colsum_kernel, dim3((C + 255) / 256, (unsigned)nchunks), dim3(256), 0, (hipStream_t)stream, x, dt,
+                     colsum, rows, C, chunk);
+  return nrse_check_launch("nrse_colsum");
+}
+
+extern "C" int nrse_cast(const void* x, int xdt, void* y, int ydt, long long n, void* stream) {
+  NRSE_REQUIRE(x && y && n >= 0, "nrse_cast: bad args");
+  if (n == 0) return NRSE_OK;
+  hipLaunchKernelGGL(cast_kernel, dim3(blocks_for(n)), dim3(256), 0, (hipStream_t)stream, x, xdt, y, ydt, n);
+  return nrse_check_launch("nrse_cast");
+}
+
+extern "C" int nrse_swap12(const void* src, int sdt, void* dst, int ddt, int d0, int d1, int d2, int acc,
+                           void* stream) {
+  NRSE_REQUIRE(src && dst && d0 > 0 && d1 > 0 && d2 > 0, "nrse_swap12: bad args");
+  const long long total = (long long)d0 * d1 * d2;
+  hipLaunchKernelGGL(swap12_kernel, dim3(blocks_for(total)), dim3(256), 0, (hipStream_t)stream, src, sdt, dst, ddt, d0,
+                     d1, d2, acc);
+  return nrse_check_launch("nrse_swap12");
+}
+
+extern "C" int nrse_gelu_bwd_pad(const float* dy, const void* pre, int pdt, void* out, int odt, int batch, int T, int C,
+                                 int pf, int pb, void* stream) {
+  NRSE_REQUIRE(dy && pre && out && batch > 0 && T > 0 && C > 0, "nrse_gelu_bwd_pad: bad args");
+  const long long total = (long long)batch * (T + pf + pb) * C;
+  hipLaunchKernelGGL(gelu_bwd_pad_kernel, dim3(blocks_for(total)), dim3(256), 0, (hipStream_t)stream, dy, pre, pdt,
+                     out, odt, batch, T, C, pf, pb);
+  return nrse_check_launch("nrse_gelu_bwd_pad");
+}

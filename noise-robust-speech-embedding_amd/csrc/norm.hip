@@ -1,0 +1,293 @@
+// Row LayerNorm kernels (one wave64 per row, fp32 statistics by wave shuffles).
+//   conv LN+GELU      [TF]modeling_wavlm.py:712-720
+//   feature-proj LN   [TF]modeling_wavlm.py:101
+//   encoder LNs       [TF]modeling_wavlm.py:357, 369, 513 (+ time-mean shim)
+// Memory-bound: each lane moves 4-element vectors (8 B bf16 / 16 B f32) so one wave
+// instruction covers 512 B - 1 KiB of a row; gamma/beta grads are accumulated per lane across
+// the rows a wave visits (grid-stride), reduced across the block in LDS, then one f32 atomic
+// per column per block.
+#include "common.h"
+
+namespace {
+
+constexpr int CH = 4;  // elements per lane-vector
+
+template <typename T> struct V4;
+template <> struct V4<float> {
+  static NRSE_DEV void load(const float* p, float* o) {
+    float4 v = *reinterpret_cast<const float4*>(p);
+    o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+  }
+  static NRSE_DEV void store(float* p, const float* o) {
+    *reinterpret_cast<float4*>(p) = make_float4(o[0], o[1], o[2], o[3]);
+  }
+};
+template <> struct V4<bf16_t> {
+  static NRSE_DEV void load(const bf16_t* p, float* o) {
+    uint2 v = *reinterpret_cast<const uint2*>(p);
+    o[0] = __uint_as_float(v.x << 16); o[1] = __uint_as_float(v.x & 0xffff0000u);
+    o[2] = __uint_as_float(v.y << 16); o[3] = __uint_as_float(v.y & 0xffff0000u);
+  }
+  static NRSE_DEV void store(bf16_t* p, const float* o) {
+    uint2 v;
+    v.x = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
+    v.y = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
+    *reinterpret_cast<uint2*>(p) = v;
+  }
+};
+
+NRSE_DEV void load4(const void* p, int dt, long long i, float* o) {
+  if (dt == NRSE_BF16) V4<bf16_t>::load((const bf16_t*)p + i, o);
+  else V4<float>::load((const float*)p + i, o);
+}
+NRSE_DEV void store4(void* p, int dt, long long i, const float* o) {
+  if (dt == NRSE_BF16) V4<bf16_t>::store((bf16_t*)p + i, o);
+  else V4<float>::store((float*)p + i, o);
+}
+
+// element c of a row held by this lane: c = (k*64 + lane)*4 + e, k < NK = C/256
+template <int NK>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const nrse_ln_fwd_params p) {
+  const int lane = threadIdx.x & 63;
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= p.rows) return;
+  const int C = p.C;
+  float v[NK][CH];
+  const long long base = row * C;
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    load4(p.x, p.x_dtype, base + (k * 64 + lane) * CH, v[k]);
+#pragma unroll
+    for (int e = 0; e < CH; ++e) s += v[k][e];
+  }
+  const float mean = wave_sum(s) / C;
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < NK; ++k)
+#pragma unroll
+    for (int e = 0; e < CH; ++e) { const float d = v[k][e] - mean; q += d * d; }
+  const float rstd = rsqrtf(wave_sum(q) / C + p.eps);
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const int c0 = (k * 64 + lane) * CH;
+    float4 g = *reinterpret_cast<const float4*>(p.gamma + c0);
+    float4 b = *reinterpret_cast<const float4*>(p.beta + c0);
+    float o[CH] = {(v[k][0] - mean) * rstd * g.x + b.x, (v[k][1] - mean) * rstd * g.y + b.y,
+                   (v[k][2] - mean) * rstd * g.z + b.z, (v[k][3] - mean) * rstd * g.w + b.w};
+    if (p.flags & NRSE_LN_GELU) {
+#pragma unroll
+      for (int e = 0; e < CH; ++e) o[e] = gelu_f(o[e]);
+    }
+    store4(p.y, p.y_dtype, base + c0, o);
+  }
+  if (lane == 0) {
+    if (p.mean) p.mean[row] = mean;
+    if (p.rstd) p.rstd[row] = rstd;
+  }
+}
+
+NRSE_DEV float load_dy(const nrse_ln_bwd_params& p, long long row, int c, float* o) {
+  // fills o[0..3] = dy[row, c..c+3]
+  if (p.dy_mode == NRSE_DY_DIRECT) {
+    load4(p.dy, p.dy_dtype, row * p.C + c, o);
+  } else if (p.dy_mode == NRSE_DY_BCAST) {
+    const long long b = row / p.bcast_t;
+    load4(p.dy, p.dy_dtype, b * p.C + c, o);
+#pragma unroll
+    for (int e = 0; e < CH; ++e) o[e] *= p.dy_scale;
+  } else {
+    const long long b = row / p.col_tin;
+    const int tau = (int)(row - b * p.col_tin);
+    o[0] = o[1] = o[2] = o[3] = 0.f;
+    const long long kc = (long long)p.col_k * p.C;
+    for (int j = 0; j < p.col_k; ++j) {
+      const int d = tau - j;
+      if (d < 0 || (d % p.col_s) != 0) continue;
+      const int t = d / p.col_s;
+      if (t >= p.col_tout) continue;
+      float w[CH];
+      load4(p.dy, p.dy_dtype, (b * p.col_tout + t) * kc + (long long)j * p.C + c, w);
+#pragma unroll
+      for (int e = 0; e < CH; ++e) o[e] += w[e];
+    }
+  }
+  return 0.f;
+}
+
+template <int NK>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const nrse_ln_bwd_params p) {
+  __shared__ float red[2][4][NK * 64 * CH];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int C = p.C;
+  float dg[NK][CH], db[NK][CH];
+#pragma unroll
+  for (int k = 0; k < NK; ++k)
+#pragma unroll
+    for (int e = 0; e < CH; ++e) dg[k][e] = db[k][e] = 0.f;
+  const long long nw = (long long)gridDim.x * 4;
+  for (long long row = (long long)blockIdx.x * 4 + w; row < p.rows; row += nw) {
+    const float mean = p.mean[row], rstd = p.rstd[row];
+    float xh[NK][CH], g[NK][CH];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      const int c0 = (k * 64 + lane) * CH;
+      float xv[CH], dy[CH];
+      load4(p.x, p.x_dtype, row * C + c0, xv);
+      load_dy(p, row, c0, dy);
+      float4 ga = *reinterpret_cast<const float4*>(p.gamma + c0);
+      const float gam[CH] = {ga.x, ga.y, ga.z, ga.w};
+      float be[CH] = {0.f, 0.f, 0.f, 0.f};
+      if (p.flags & NRSE_LN_GELU) {
+        float4 bb = *reinterpret_cast<const float4*>(p.beta + c0);
+        be[0] = bb.x; be[1] = bb.y; be[2] = bb.z; be[3] = bb.w;
+      }
+#pragma unroll
+      for (int e = 0; e < CH; ++e) {
+        xh[k][e] = (xv[e] - mean) * rstd;
+        float gg = dy[e];
+        if (p.flags & NRSE_LN_GELU) gg *= gelu_grad_f(xh[k][e] * gam[e] + be[e]);
+        dg[k][e] += gg * xh[k][e];
+        db[k][e] += gg;
+        g[k][e] = gg * gam[e];
+        s1 += g[k][e];
+        s2 += g[k][e] * xh[k][e];
+      }
+    }
+    s1 = wave_sum(s1) / C;
+    s2 = wave_sum(s2) / C;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      const int c0 = (k * 64 + lane) * CH;
+      float o[CH];
+#pragma unroll
+      for (int e = 0; e < CH; ++e) o[e] = rstd * (g[k][e] - s1 - xh[k][e] * s2);
+      if (p.resid) {
+        float r[CH];
+        V4<float>::load(p.resid + row * C + c0, r);
+#pragma unroll
+        for (int e = 0; e < CH; ++e) o[e] += r[e];
+      }
+      store4(p.dx, p.dx_dtype, row * C + c0, o);
+    }
+  }
+  if (p.dgamma == nullptr) return;
+#pragma unroll
+  for (int k = 0; k < NK; ++k)
+#pragma unroll
+    for (int e = 0; e < CH; ++e) {
+      red[0][w][(k * 64 + lane) * CH + e] = dg[k][e];
+      red[1][w][(k * 64 + lane) * CH + e] = db[k][e];
+    }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const float a = red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c];
+    const float b = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
+    atomicAdd(p.dgamma + c, a);
+    atomicAdd(p.dbeta + c, b);
+  }
+}
+
+// Final LN + time-mean: grid (ceil(T / RPB), batch); 4 waves, each a row at a time.
+template <int NK>
+__global__ __launch_bounds__(256) void ln_mean_kernel(const float* __restrict__ h, const float* __restrict__ gamma,
+                                                      const float* __restrict__ beta, float* __restrict__ emb,
+                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                      int T, int C, float eps, int rpb) {
+  __shared__ float red[4][NK * 64 * CH];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int b = blockIdx.y;
+  const int t0 = blockIdx.x * rpb;
+  const int t1 = min(T, t0 + rpb);
+  float acc[NK][CH];
+#pragma unroll
+  for (int k = 0; k < NK; ++k)
+#pragma unroll
+    for (int e = 0; e < CH; ++e) acc[k][e] = 0.f;
+  for (int t = t0 + w; t < t1; t += 4) {
+    const long long row = (long long)b * T + t;
+    float v[NK][CH];
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      V4<float>::load(h + row * C + (k * 64 + lane) * CH, v[k]);
+#pragma unroll
+      for (int e = 0; e < CH; ++e) s += v[k][e];
+    }
+    const float mean = wave_sum(s) / C;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < NK; ++k)
+#pragma unroll
+      for (int e = 0; e < CH; ++e) { const float d = v[k][e] - mean; q += d * d; }
+    const float rstd = rsqrtf(wave_sum(q) / C + eps);
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      const int c0 = (k * 64 + lane) * CH;
+#pragma unroll
+      for (int e = 0; e < CH; ++e) acc[k][e] += (v[k][e] - mean) * rstd * gamma[c0 + e] + beta[c0 + e];
+    }
+    if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
+  }
+#pragma unroll
+  for (int k = 0; k < NK; ++k)
+#pragma unroll
+    for (int e = 0; e < CH; ++e) red[w][(k * 64 + lane) * CH + e] = acc[k][e];
+  __syncthreads();
+  const float inv = 1.0f / T;
+  for (int c = threadIdx.x; c < C; c += 256)
+    atomicAdd(emb + (long long)b * C + c, (red[0][c] + red[1][c] + red[2][c] + red[3][c]) * inv);
+}
+
+#define NRSE_DISPATCH_NK(KERNEL, C, GRID, ST, ARG)                                  \
+  switch ((C) / 256) {                                                              \
+    case 1: hipLaunchKernelGGL(KERNEL<1>, GRID, dim3(256), 0, ST, ARG); break;     \
+    case 2: hipLaunchKernelGGL(KERNEL<2>, GRID, dim3(256), 0, ST, ARG); break;     \
+    default: hipLaunchKernelGGL(KERNEL<4>, GRID, dim3(256), 0, ST, ARG); break;    \
+  }
+
+bool c_ok(int C) { return C == 256 || C == 512 || C == 1024; }
+
+}  // namespace
+
+extern "C" int nrse_layernorm_fwd(const nrse_ln_fwd_params* p, void* stream) {
+  NRSE_REQUIRE(p && p->x && p->y && p->gamma && p->beta && p->rows > 0, "nrse_layernorm_fwd: bad args");
+  if (!c_ok(p->C)) { nrse_set_error("nrse_layernorm_fwd: C=%d not in {256,512,1024}", p->C); return NRSE_ERR_UNSUPPORTED; }
+  dim3 grid((unsigned)((p->rows + 3) / 4));
+  NRSE_DISPATCH_NK(ln_fwd_kernel, p->C, grid, (hipStream_t)stream, *p);
+  return nrse_check_launch("nrse_layernorm_fwd");
+}
+
+extern "C" int nrse_layernorm_bwd(const nrse_ln_bwd_params* p, void* stream) {
+  NRSE_REQUIRE(p && p->dy && p->x && p->gamma && p->mean && p->rstd && p->dx && p->rows > 0,
+               "nrse_layernorm_bwd: bad args");
+  NRSE_REQUIRE(!(p->flags & NRSE_LN_GELU) || p->beta, "nrse_layernorm_bwd: GELU needs beta");
+  NRSE_REQUIRE((p->dgamma == nullptr) == (p->dbeta == nullptr), "nrse_layernorm_bwd: dgamma/dbeta together");
+  if (p->dy_mode == NRSE_DY_COL2IM)
+    NRSE_REQUIRE(p->col_k > 0 && p->col_s > 0 && p->col_tin > 0 && p->col_tout > 0 && p->rows % p->col_tin == 0,
+                 "nrse_layernorm_bwd: bad col2im geometry");
+  if (p->dy_mode == NRSE_DY_BCAST) NRSE_REQUIRE(p->bcast_t > 0, "nrse_layernorm_bwd: bad bcast_t");
+  if (!c_ok(p->C)) { nrse_set_error("nrse_layernorm_bwd: C=%d not in {256,512,1024}", p->C); return NRSE_ERR_UNSUPPORTED; }
+  long long blocks = (p->rows + 3) / 4;
+  if (blocks > 4096) blocks = 4096;
+  NRSE_DISPATCH_NK(ln_bwd_kernel, p->C, dim3((unsigned)blocks), (hipStream_t)stream, *p);
+  return nrse_check_launch("nrse_layernorm_bwd");
+}
+
+extern "C" int nrse_ln_mean_fwd(const float* h, const float* gamma, const float* beta, float* emb, float* mean,
+                                float* rstd, int batch, int T, int C, float eps, void* stream) {
+  NRSE_REQUIRE(h && gamma && beta && emb && mean && rstd && batch > 0 && T > 0, "nrse_ln_mean_fwd: bad args");
+  if (!c_ok(C)) { nrse_set_error("nrse_ln_mean_fwd: C=%d unsupported", C); return NRSE_ERR_UNSUPPORTED; }
+  const int rpb = 32;
+  dim3 grid((T + rpb - 1) / rpb, batch);
+  hipStream_t st = (hipStream_t)stream;
+  switch (C / 256) {
+    case 1: hipLaunchKernelGGL(ln_mean_kernel<1>, grid, dim3(256), 0, st, h, gamma, beta, emb, mean, rstd, T, C, eps, rpb); break;
+    case 2: hipLaunchKernelGGL(ln_mean_kernel<2>, grid, dim3(256), 0, st, h, gamma, beta, emb, mean, rstd, T, C, eps, rpb); break;
+    default: hipLaunchKernelGGL(ln_mean_kernel<4>, grid, dim3(256), 0, st, h, gamma, beta, emb, mean, rstd, T, C, eps, rpb); break;
+  }
+  return nrse_check_launch("nrse_ln_mean_fwd");
+}

@@ -1,0 +1,177 @@
+// Optimiser tail over the flat f32 buffers (HBM-bound, float4 per lane):
+//   clip_grad_norm_(max_norm=1.0)   train_byol.py:67  (sum of squares in f64: a single f32
+//                                   reduction over 3.3e8 entries loses the small ones)
+//   AdamW.step (decoupled wd)       train_byol.py:68, torch.optim.AdamW semantics
+//   target EMA                      src/models/byol.py:62-73
+//   health checks                   train_byol.py:52-59, src/utils/debugging_utils.py:4-30
+// The clip coefficient is read from device memory by the AdamW kernel: no host sync.
+#include "common.h"
+
+namespace {
+
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x, long long n, double* __restrict__ out) {
+  __shared__ double red[4];
+  double a = 0.0;
+  const long long n4 = n / 4;
+  for (long long q = (long long)blockIdx.x * 256 + threadIdx.x; q < n4; q += (long long)gridDim.x * 256) {
+    const float4 v = reinterpret_cast<const float4*>(x)[q];
+    a += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+  }
+  for (long long i = n4 * 4 + (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
+    a += (double)x[i] * x[i];
+  a = wave_sum_d(a);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = a;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(out, red[0] + red[1] + red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(256) void adamw_kernel(const nrse_adamw_params p) {
+  const double ss = p.sumsq ? *p.sumsq : 0.0;
+  float coef = 1.f;
+  if (p.sumsq) {
+    const float tn = (float)sqrt(ss);
+    coef = fminf(1.f, p.max_norm / (tn + 1e-6f));
+  }
+  coef *= p.grad_scale;
+  const float bc1 = 1.f - powf(p.beta1, (float)p.step);
+  const float bc2 = 1.f - powf(p.beta2, (float)p.step);
+  const float step_size = p.lr / bc1;
+  const float bc2s = sqrtf(bc2);
+  const float decay = 1.f - p.lr * p.weight_decay;
+  const long long n4 = p.n / 4;
+  for (long long q = (long long)blockIdx.x * 256 + threadIdx.x; q < n4; q += (long long)gridDim.x * 256) {
+    float4 pv = reinterpret_cast<float4*>(p.p)[q];
+    const float4 gv = reinterpret_cast<const float4*>(p.g)[q];
+    float4 mv = reinterpret_cast<float4*>(p.m)[q];
+    float4 vv = reinterpret_cast<float4*>(p.v)[q];
+    float* pa = &pv.x; const float* ga = &gv.x; float* ma = &mv.x; float* va = &vv.x;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float g = ga[e] * coef;
+      float w = pa[e] * decay;
+      ma[e] = p.beta1 * ma[e] + (1.f - p.beta1) * g;
+      va[e] = p.beta2 * va[e] + (1.f - p.beta2) * g * g;
+      const float denom = sqrtf(va[e]) / bc2s + p.eps;
+      pa[e] = w - step_size * ma[e] / denom;
+    }
+    reinterpret_cast<float4*>(p.p)[q] = pv;
+    reinterpret_cast<float4*>(p.m)[q] = mv;
+    reinterpret_cast<float4*>(p.v)[q] = vv;
+    if (p.p_shadow) {
+      if (p.shadow_dtype == NRSE_BF16) {
+        uint2 u;
+        u.x = (uint32_t)f2bf(pa[0]) | ((uint32_t)f2bf(pa[1]) << 16);
+        u.y = (uint32_t)f2bf(pa[2]) | ((uint32_t)f2bf(pa[3]) << 16);
+        reinterpret_cast<uint2*>(p.p_shadow)[q] = u;
+      } else {
+        reinterpret_cast<float4*>(p.p_shadow)[q] = pv;
+      }
+    }
+  }
+  for (long long i = n4 * 4 + (long long)blockIdx.x * 256 + threadIdx.x; i < p.n; i += (long long)gridDim.x * 256) {
+    const float g = p.g[i] * coef;
+    const float w = p.p[i] * decay;
+    p.m[i] = p.beta1 * p.m[i] + (1.f - p.beta1) * g;
+    p.v[i] = p.beta2 * p.v[i] + (1.f - p.beta2) * g * g;
+    const float denom = sqrtf(p.v[i]) / bc2s + p.eps;
+    p.p[i] = w - step_size * p.m[i] / denom;
+    if (p.p_shadow) store_from_f(p.p_shadow, p.shadow_dtype, i, p.p[i]);
+  }
+}
+
+__global__ __launch_bounds__(256) void ema_kernel(float* __restrict__ t, const float* __restrict__ o,
+                                                  void* __restrict__ ts, int sdt, long long n, float decay) {
+  const float om = 1.f - decay;
+  const long long n4 = n / 4;
+  for (long long q = (long long)blockIdx.x * 256 + threadIdx.x; q < n4; q += (long long)gridDim.x * 256) {
+    float4 tv = reinterpret_cast<float4*>(t)[q];
+    const float4 ov = reinterpret_cast<const float4*>(o)[q];
+    tv.x = decay * tv.x + om * ov.x; tv.y = decay * tv.y + om * ov.y;
+    tv.z = decay * tv.z + om * ov.z; tv.w = decay * tv.w + om * ov.w;
+    reinterpret_cast<float4*>(t)[q] = tv;
+    if (ts) {
+      if (sdt == NRSE_BF16) {
+        uint2 u;
+        u.x = (uint32_t)f2bf(tv.x) | ((uint32_t)f2bf(tv.y) << 16);
+        u.y = (uint32_t)f2bf(tv.z) | ((uint32_t)f2bf(tv.w) << 16);
+        reinterpret_cast<uint2*>(ts)[q] = u;
+      } else {
+        reinterpret_cast<float4*>(ts)[q] = tv;
+      }
+    }
+  }
+  for (long long i = n4 * 4 + (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    t[i] = decay * t[i] + om * o[i];
+    if (ts) store_from_f(ts, sdt, i, t[i]);
+  }
+}
+
+__global__ __launch_bounds__(256) void health_kernel(const void* __restrict__ x, int dt, long long n,
+                                                     float* __restrict__ stats) {
+  __shared__ float red[3][4];
+  float nan = 0.f, inf = 0.f, sabs = 0.f, mabs = 0.f;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const float v = load_as_f(x, dt, i);
+    if (isnan(v)) nan += 1.f;
+    else if (isinf(v)) inf += 1.f;
+    else { sabs += fabsf(v); mabs = fmaxf(mabs, fabsf(v)); }
+  }
+  nan = wave_sum(nan); inf = wave_sum(inf); sabs = wave_sum(sabs); mabs = wave_max(mabs);
+  const int w = threadIdx.x >> 6;
+  __shared__ float rmax[4];
+  if ((threadIdx.x & 63) == 0) { red[0][w] = nan; red[1][w] = inf; red[2][w] = sabs; rmax[w] = mabs; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float a = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    const float b = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+    const float c = red[2][0] + red[2][1] + red[2][2] + red[2][3];
+    const float m = fmaxf(fmaxf(rmax[0], rmax[1]), fmaxf(rmax[2], rmax[3]));
+    if (a != 0.f) atomicAdd(stats + 0, a);
+    if (b != 0.f) atomicAdd(stats + 1, b);
+    atomicAdd(stats + 2, c);
+    atomicMax(reinterpret_cast<int*>(stats + 3), __float_as_int(m));  // non-negative floats order as ints
+  }
+}
+
+int grid_for(long long n) {
+  long long b = (n / 4 + 255) / 256;
+  if (b > 4096) b = 4096;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+}  // namespace
+
+extern "C" int nrse_sumsq(const float* x, long long n, double* out, void* stream) {
+  NRSE_REQUIRE(x && out && n >= 0, "nrse_sumsq: bad args");
+  NRSE_REQUIRE(((uintptr_t)x & 15) == 0, "nrse_sumsq: x must be 16-byte aligned");
+  if (n == 0) return NRSE_OK;
+  hipLaunchKernelGGL(sumsq_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, n, out);
+  return nrse_check_launch("nrse_sumsq");
+}
+
+extern "C" int nrse_adamw(const nrse_adamw_params* p, void* stream) {
+  NRSE_REQUIRE(p && p->p && p->g && p->m && p->v && p->n >= 0 && p->step >= 1, "nrse_adamw: bad args");
+  NRSE_REQUIRE((((uintptr_t)p->p | (uintptr_t)p->g | (uintptr_t)p->m | (uintptr_t)p->v) & 15) == 0,
+               "nrse_adamw: buffers must be 16-byte aligned");
+  if (p->n == 0) return NRSE_OK;
+  hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(p->n)), dim3(256), 0, (hipStream_t)stream, *p);
+  return nrse_check_launch("nrse_adamw");
+}
+
+extern "C" int nrse_ema(float* t, const float* o, void* ts, int sdt, long long n, float decay, void* stream) {
+  NRSE_REQUIRE(t && o && n >= 0, "nrse_ema: bad args");
+  NRSE_REQUIRE((((uintptr_t)t | (uintptr_t)o) & 15) == 0, "nrse_ema: buffers must be 16-byte aligned");
+  if (n == 0) return NRSE_OK;
+  hipLaunchKernelGGL(ema_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, t, o, ts, sdt, n, decay);
+  return nrse_check_launch("nrse_ema");
+}
+
+extern "C" int nrse_health(const void* x, int dt, long long n, float* stats, void* stream) {
+  NRSE_REQUIRE(x && stats && n >= 0, "nrse_health: bad args");
+  if (n == 0) return NRSE_OK;
+  long long b = (n + 255) / 256;
+  if (b > 1024) b = 1024;
+  hipLaunchKernelGGL(health_kernel, dim3((int)b), dim3(256), 0, (hipStream_t)stream, x, dt, n, stats);
+  return nrse_check_launch("nrse_health");
+}

@@ -25,39 +25,118 @@ EPI_ATOMIC = 1 << 7
 EPI_COLSUM = 1 << 8
 EPI_RELU = 1 << 9
 
+LN_GELU = 1
+DY_DIRECT, DY_COL2IM, DY_BCAST = 0, 1, 2
+
 c_ll = ctypes.c_longlong
 c_vp = ctypes.c_void_p
+c_int = ctypes.c_int
+c_f = ctypes.c_float
+c_u32 = ctypes.c_uint32
 
 
 class NrseCaps(ctypes.Structure):
-    _fields_ = [("device", ctypes.c_int), ("cu_count", ctypes.c_int), ("xcd_count", ctypes.c_int),
-                ("lds_bytes_per_cu", ctypes.c_int), ("hbm_bytes", c_ll), ("arch", ctypes.c_char * 32)]
+    _fields_ = [("device", c_int), ("cu_count", c_int), ("xcd_count", c_int),
+                ("lds_bytes_per_cu", c_int), ("hbm_bytes", c_ll), ("arch", ctypes.c_char * 32)]
 
 
 class GemmOperand(ctypes.Structure):
-    _fields_ = [("ptr", c_vp), ("dtype", ctypes.c_int), ("kcontig", ctypes.c_int), ("chunk_shift", ctypes.c_int),
+    _fields_ = [("ptr", c_vp), ("dtype", c_int), ("kcontig", c_int), ("chunk_shift", c_int),
                 ("ld", c_ll), ("ld_chunk", c_ll), ("seg_stride", c_ll), ("z1", c_ll), ("z2", c_ll)]
 
 
 class GemmParams(ctypes.Structure):
     _fields_ = [("a", GemmOperand), ("b", GemmOperand),
-                ("M", ctypes.c_int), ("N", ctypes.c_int), ("K", ctypes.c_int), ("nseg", ctypes.c_int),
-                ("splits", ctypes.c_int), ("batch", ctypes.c_int), ("zdiv", ctypes.c_int),
-                ("alpha", ctypes.c_float), ("flags", ctypes.c_int),
-                ("c", c_vp), ("c_dtype", ctypes.c_int), ("ldc", c_ll), ("c_z1", c_ll), ("c_z2", c_ll),
+                ("M", c_int), ("N", c_int), ("K", c_int), ("nseg", c_int),
+                ("splits", c_int), ("batch", c_int), ("zdiv", c_int),
+                ("alpha", c_f), ("flags", c_int),
+                ("c", c_vp), ("c_dtype", c_int), ("ldc", c_ll), ("c_z1", c_ll), ("c_z2", c_ll),
                 ("c_split", c_ll),
-                ("bias", c_vp), ("aux", c_vp), ("aux_dtype", ctypes.c_int), ("ldaux", c_ll), ("aux_z1", c_ll),
-                ("aux_z2", c_ll), ("resid", c_vp), ("resid_dtype", ctypes.c_int), ("ldr", c_ll), ("r_z1", c_ll),
-                ("r_z2", c_ll), ("dropout_p", ctypes.c_float), ("seed", ctypes.c_uint32), ("colsum", c_vp)]
+                ("bias", c_vp), ("bias_z1", c_ll), ("bias_z2", c_ll),
+                ("aux", c_vp), ("aux_dtype", c_int), ("ldaux", c_ll), ("aux_z1", c_ll),
+                ("aux_z2", c_ll), ("resid", c_vp), ("resid_dtype", c_int), ("ldr", c_ll), ("r_z1", c_ll),
+                ("r_z2", c_ll), ("dropout_p", c_f), ("seed", c_u32), ("colsum", c_vp)]
 
 
+class LnFwdParams(ctypes.Structure):
+    _fields_ = [("x", c_vp), ("x_dtype", c_int), ("gamma", c_vp), ("beta", c_vp), ("y", c_vp), ("y_dtype", c_int),
+                ("mean", c_vp), ("rstd", c_vp), ("rows", c_ll), ("C", c_int), ("eps", c_f), ("flags", c_int)]
+
+
+class LnBwdParams(ctypes.Structure):
+    _fields_ = [("dy", c_vp), ("dy_dtype", c_int), ("dy_mode", c_int),
+                ("col_k", c_int), ("col_s", c_int), ("col_tout", c_int), ("col_tin", c_int),
+                ("bcast_t", c_int), ("dy_scale", c_f),
+                ("x", c_vp), ("x_dtype", c_int), ("gamma", c_vp), ("beta", c_vp), ("mean", c_vp), ("rstd", c_vp),
+                ("dx", c_vp), ("dx_dtype", c_int), ("resid", c_vp), ("dgamma", c_vp), ("dbeta", c_vp),
+                ("rows", c_ll), ("C", c_int), ("flags", c_int)]
+
+
+class AttnFwdParams(ctypes.Structure):
+    _fields_ = [("qkv", c_vp), ("dtype", c_int), ("gate", c_vp), ("bias", c_vp), ("ctx", c_vp), ("lse", c_vp),
+                ("batch", c_int), ("T", c_int), ("H", c_int), ("head_dim", c_int), ("scale", c_f),
+                ("dropout_p", c_f), ("seed", c_u32)]
+
+
+class AttnBwdParams(ctypes.Structure):
+    _fields_ = [("qkv", c_vp), ("dtype", c_int), ("gate", c_vp), ("bias", c_vp), ("ctx", c_vp), ("dctx", c_vp),
+                ("lse", c_vp), ("delta", c_vp), ("dqkv", c_vp), ("dgate", c_vp), ("diag", c_vp),
+                ("batch", c_int), ("T", c_int), ("H", c_int), ("head_dim", c_int), ("scale", c_f),
+                ("dropout_p", c_f), ("seed", c_u32)]
+
+
+class Conv0Params(ctypes.Structure):
+    _fields_ = [("wav", c_vp), ("L", c_int), ("w", c_vp), ("gamma", c_vp), ("beta", c_vp), ("out", c_vp),
+                ("out_dtype", c_int), ("mean", c_vp), ("rstd", c_vp),
+                ("dy", c_vp), ("dy_dtype", c_int), ("dy_mode", c_int), ("col_k", c_int), ("col_s", c_int),
+                ("col_tout", c_int), ("dw", c_vp), ("dgamma", c_vp), ("dbeta", c_vp),
+                ("batch", c_int), ("T0", c_int), ("C", c_int), ("k", c_int), ("s", c_int), ("eps", c_f)]
+
+
+class AdamWParams(ctypes.Structure):
+    _fields_ = [("p", c_vp), ("g", c_vp), ("m", c_vp), ("v", c_vp), ("p_shadow", c_vp), ("shadow_dtype", c_int),
+                ("n", c_ll), ("lr", c_f), ("beta1", c_f), ("beta2", c_f), ("eps", c_f), ("weight_decay", c_f),
+                ("step", c_int), ("max_norm", c_f), ("sumsq", c_vp), ("grad_scale", c_f)]
+
+
+_P = ctypes.POINTER
 # Every symbol include/nrse_hip.h declares, with its ctypes signature (argtypes, restype).
 # tests/test_abi.py checks this table against the header.
 _SIGNATURES = {
-    "nrse_init": ([ctypes.c_int, ctypes.POINTER(NrseCaps)], ctypes.c_int),
+    "nrse_init": ([c_int, _P(NrseCaps)], c_int),
     "nrse_last_error": ([], ctypes.c_char_p),
-    "nrse_abi_version": ([], ctypes.c_int),
-    "nrse_gemm": ([ctypes.POINTER(GemmParams), c_vp], ctypes.c_int),
+    "nrse_abi_version": ([], c_int),
+    "nrse_gemm": ([_P(GemmParams), c_vp], c_int),
+    "nrse_layernorm_fwd": ([_P(LnFwdParams), c_vp], c_int),
+    "nrse_layernorm_bwd": ([_P(LnBwdParams), c_vp], c_int),
+    "nrse_ln_mean_fwd": ([c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_f, c_vp], c_int),
+    "nrse_rel_bias_fwd": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp], c_int),
+    "nrse_rel_bias_bwd": ([c_vp, c_vp, c_vp, c_int, c_int, c_vp], c_int),
+    "nrse_gate_fwd": ([c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp], c_int),
+    "nrse_gate_bwd": ([c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp],
+                      c_int),
+    "nrse_attn_fwd": ([_P(AttnFwdParams), c_vp], c_int),
+    "nrse_attn_bwd": ([_P(AttnBwdParams), c_vp], c_int),
+    "nrse_conv0_fwd": ([_P(Conv0Params), c_vp], c_int),
+    "nrse_conv0_bwd": ([_P(Conv0Params), c_vp], c_int),
+    "nrse_weight_norm_fwd": ([c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_vp], c_int),
+    "nrse_weight_norm_bwd": ([c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp], c_int),
+    "nrse_specaug_pad": ([c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
+    "nrse_pad_rows": ([c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
+    "nrse_specaug_bwd": ([c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_f, c_u32, c_vp], c_int),
+    "nrse_dropout_cast": ([c_vp, c_vp, c_int, c_ll, c_f, c_u32, c_vp], c_int),
+    "nrse_colsum": ([c_vp, c_int, c_vp, c_ll, c_int, c_vp], c_int),
+    "nrse_cast": ([c_vp, c_int, c_vp, c_int, c_ll, c_vp], c_int),
+    "nrse_swap12": ([c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
+    "nrse_gelu_bwd_pad": ([c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
+    "nrse_bn_fwd": ([c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_f, c_f, c_int, c_int, c_vp], c_int),
+    "nrse_bn_bwd": ([c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp], c_int),
+    "nrse_byol_loss": ([c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_f, c_vp], c_int),
+    "nrse_sumsq": ([c_vp, c_ll, c_vp, c_vp], c_int),
+    "nrse_adamw": ([_P(AdamWParams), c_vp], c_int),
+    "nrse_ema": ([c_vp, c_vp, c_vp, c_int, c_ll, c_f, c_vp], c_int),
+    "nrse_health": ([c_vp, c_int, c_ll, c_vp, c_vp], c_int),
+    "nrse_snr_mix": ([c_vp, c_vp, c_vp, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp], c_int),
 }
 
 

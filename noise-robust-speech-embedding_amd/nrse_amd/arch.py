@@ -70,7 +70,7 @@ class WavLMArch:
 
 
 LARGE = WavLMArch()
-TINY = WavLMArch(hidden=256, layers=2, heads=4, ffn=512, conv_dim=(128,) * 7)
+TINY = WavLMArch(hidden=256, layers=2, heads=4, ffn=512, conv_dim=(256,) * 7)
 
 _PRESETS = {
     "microsoft/wavlm-large": LARGE,

@@ -1,0 +1,636 @@
+"""MI355X-native BYOL-on-WavLM training engine over libnrse_hip.so.
+
+One object holds the whole training state in HBM as flat buffers (SURVEY.md §8a layout):
+  online   f32 [numel]        master weights: encoder | projector | predictor
+  target   f32 [ema_numel]    target encoder + projector (EMA of the online prefix)
+  grad     f32 [numel]        gradient buffer (zeroed per step; DDP all-reduces it in buckets)
+  m, v     f32 [numel]        AdamW moments
+  *_sh     bf16 shadows       GEMM operand copies written by the AdamW / EMA kernels
+Activations are channels-last ([B*T, C] rows); the residual stream is f32, every GEMM operand
+is in the compute dtype (bf16, or f32 in parity mode). Forward and backward are explicit
+kernel sequences (no autograd), mirroring:
+  train_one_epoch body  train_byol.py:47-77
+  BYOLSpeechModel       src/models/byol.py:75-97 (+ time-mean shim)
+  WavLMModel            [TF]modeling_wavlm.py:1032-1096
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from . import _lib
+from . import kernels as K
+from . import params as PR
+from . import rng as R
+from .arch import WavLMArch
+from .hostside import bucket_vector, compute_mask_indices, layerdrop_decisions
+
+F32 = torch.float32
+
+
+def _divisor_at_most(n: int, cap: int) -> int:
+    cap = max(1, min(n, cap))
+    for d in range(cap, 0, -1):
+        if n % d == 0:
+            return d
+    return 1
+
+
+@dataclass
+class StepConfig:
+    lr: float = 1e-5
+    weight_decay: float = 1e-5
+    betas: tuple = (0.9, 0.999)
+    eps: float = 1e-8
+    max_norm: float = 1.0
+    ema_decay: float = 0.997
+
+
+@dataclass
+class Tape:
+    """Activations the backward pass needs (one encoder forward)."""
+    B: int = 0
+    T: int = 0
+    wav: torch.Tensor | None = None
+    conv: list = field(default_factory=list)
+    feats: torch.Tensor | None = None
+    fp_mean: torch.Tensor | None = None
+    fp_rstd: torch.Tensor | None = None
+    xn: torch.Tensor | None = None
+    mask: torch.Tensor | None = None
+    hpad: torch.Tensor | None = None
+    pos_pre: torch.Tensor | None = None
+    pos: dict | None = None
+    bias_tab: torch.Tensor | None = None
+    layers: list = field(default_factory=list)
+    final: tuple | None = None
+    fseed: int = 0
+
+
+class EncoderWeights:
+    """Per-forward view of one encoder's weights: f32 master views, compute-dtype shadow views,
+    and the per-step derived layouts (conv weights in implicit-GEMM order, weight-normed
+    pos-conv in forward and flipped-dgrad order)."""
+
+    def __init__(self, eng: "ByolEngine", master: torch.Tensor, shadow: torch.Tensor | None):
+        self.eng = eng
+        self.m = eng.group_views(master, "encoder")
+        self.s = eng.group_views(shadow, "encoder") if shadow is not None else self.m
+        a = eng.arch
+        cdt = eng.cdt
+        # conv 1..6 weights [co][ci][k] -> [co][k][ci] in the compute dtype
+        self.conv_r = []
+        for i in range(1, len(a.conv_dim)):
+            w = self.m[f"feature_extractor.conv_layers.{i}.conv.weight"]
+            co, ci, k = w.shape
+            r = torch.empty(co, k * ci, device=eng.dev, dtype=cdt)
+            K.swap12(w, r, co, ci, k)
+            self.conv_r.append(r)
+        # pos-conv weight norm
+        H, G, pk = a.hidden, a.pos_groups, a.pos_kernel
+        cpg = H // G
+        pre = "encoder.pos_conv_embed.conv.parametrizations.weight."
+        self.wf = torch.empty(G, cpg, pk * cpg, device=eng.dev, dtype=cdt)
+        self.wd = torch.empty(G, cpg, pk * cpg, device=eng.dev, dtype=cdt)
+        self.wn_norms = torch.empty(pk, device=eng.dev, dtype=F32)
+        K.weight_norm_fwd(self.m[pre + "original0"], self.m[pre + "original1"], self.wf, self.wd, self.wn_norms, H,
+                          cpg, pk)
+
+
+class ByolEngine:
+    def __init__(self, arch: WavLMArch, proj_dim: int, pred_dim: int, *, device="cuda", compute_dtype=torch.bfloat16,
+                 seed: int = 1234, step_cfg: StepConfig | None = None, init_flat: torch.Tensor | None = None,
+                 do_normalize: bool = True):
+        if arch.head_dim != 64:
+            raise _lib.NrseError(f"head_dim {arch.head_dim} unsupported (attention kernels are head_dim 64)")
+        self.arch = arch
+        self.dev = torch.device(device)
+        _lib.init_device(self.dev.index or 0)
+        self.cdt = compute_dtype
+        self.cfg = step_cfg or StepConfig()
+        self.layout = PR.byol_layout(arch, proj_dim, pred_dim)
+        self.proj_dim, self.pred_dim = proj_dim, pred_dim
+        self.do_normalize = do_normalize
+        flat = init_flat if init_flat is not None else PR.init_byol_flat(self.layout, seed)
+        n, ne = self.layout.numel, self.layout.ema_numel
+        self.online = flat.to(self.dev, F32).contiguous()
+        self.target = self.online[:ne].clone()
+        self.grad = torch.zeros(n, device=self.dev, dtype=F32)
+        self.m = torch.zeros(n, device=self.dev, dtype=F32)
+        self.v = torch.zeros(n, device=self.dev, dtype=F32)
+        if self.cdt == F32:
+            self.online_sh = None
+            self.target_sh = None
+        else:
+            self.online_sh = torch.empty(n, device=self.dev, dtype=self.cdt)
+            self.target_sh = torch.empty(ne, device=self.dev, dtype=self.cdt)
+            K.cast(self.online, self.online_sh)
+            K.cast(self.target, self.target_sh)
+        self.step_count = 0
+        self._offsets = {}
+        for gname, s in self.layout.specs:
+            off, cnt, shp = self.layout.offsets[PR.GROUP_PREFIX[gname] + s.name]
+            self._offsets.setdefault(gname, {})[s.name] = (off, cnt, shp)
+        self._check_fused_views()
+        # BatchNorm running statistics (buffers, not EMA'd: src/models/byol.py:62-73)
+        self.bn = {}
+        for net, dims in (("online_projector", (proj_dim, proj_dim)), ("target_projector", (proj_dim, proj_dim)),
+                          ("online_predictor", (pred_dim, pred_dim))):
+            for li, c in zip((1, 4), dims):
+                self.bn[f"{net}.layers.{li}"] = (torch.zeros(c, device=self.dev), torch.ones(c, device=self.dev),
+                                                 torch.zeros((), dtype=torch.long, device=self.dev))
+        self._buckets = {}
+        self.sumsq_buf = torch.zeros(1, device=self.dev, dtype=torch.float64)
+        self.loss_buf = torch.zeros(1, device=self.dev, dtype=F32)
+        self.health_buf = torch.zeros(4, 4, device=self.dev, dtype=F32)
+        self.loss_stats = torch.zeros(2, device=self.dev, dtype=F32)
+        self.executed_layers = [0, 0]
+
+    # ------------------------------------------------------------------ views
+    def group_views(self, flat: torch.Tensor, group: str) -> dict:
+        out = {}
+        for name, (off, cnt, shp) in self._offsets[group].items():
+            out[name] = flat[off:off + cnt].view(shp)
+        return out
+
+    def fused(self, flat: torch.Tensor, layer: int, kind: str) -> torch.Tensor:
+        H = self.arch.hidden
+        pre = f"encoder.layers.{layer}.attention."
+        if kind == "qkv_w":
+            off = self._offsets["encoder"][pre + "q_proj.weight"][0]
+            return flat[off:off + 3 * H * H].view(3 * H, H)
+        off = self._offsets["encoder"][pre + "q_proj.bias"][0]
+        return flat[off:off + 3 * H]
+
+    def _check_fused_views(self):
+        H = self.arch.hidden
+        for li in range(self.arch.layers):
+            pre = f"encoder.layers.{li}.attention."
+            o = self._offsets["encoder"]
+            qw, kw, vw = (o[pre + n + "_proj.weight"][0] for n in "qkv")
+            qb, kb, vb = (o[pre + n + "_proj.bias"][0] for n in "qkv")
+            assert kw == qw + H * H and vw == kw + H * H, "q/k/v weights must be adjacent in the flat layout"
+            assert kb == qb + H and vb == kb + H, "q/k/v biases must be adjacent in the flat layout"
+
+    def buckets(self, T: int) -> torch.Tensor:
+        if T not in self._buckets:
+            a = self.arch
+            self._buckets[T] = torch.from_numpy(bucket_vector(T, a.num_buckets, a.max_distance)).to(self.dev)
+        return self._buckets[T]
+
+    # ------------------------------------------------------------------ encoder forward
+    def encoder_forward(self, W: EncoderWeights, wav: torch.Tensor, *, train: bool, fseed: int = 0, skip=None,
+                        mask_np=None, need_grad: bool = False):
+        """WavLMModel.forward -> time-mean embedding [B, H] (f32) and the backward tape."""
+        a = self.arch
+        cdt = self.cdt
+        dev = self.dev
+        B, L = wav.shape
+        Pm, Ps = W.m, W.s
+        tape = Tape(B=B, wav=wav, fseed=fseed) if need_grad else None
+        # -------- conv feature encoder ([TF]modeling_wavlm.py:712-720, 773-783)
+        k0, s0, C0 = a.conv_kernel[0], a.conv_stride[0], a.conv_dim[0]
+        T0 = (L - k0) // s0 + 1
+        y = torch.empty(B * T0, C0, device=dev, dtype=cdt)
+        mean = torch.empty(B * T0, device=dev, dtype=F32)
+        rstd = torch.empty(B * T0, device=dev, dtype=F32)
+        pre0 = "feature_extractor.conv_layers.0."
+        K.conv0_fwd(wav, Pm[pre0 + "conv.weight"], Pm[pre0 + "layer_norm.weight"], Pm[pre0 + "layer_norm.bias"], y,
+                    mean, rstd, T0, k0, s0, a.eps)
+        if need_grad:
+            tape.conv.append(dict(mean=mean, rstd=rstd, T=T0))
+        x, Tin, Cin = y, T0, C0
+        for i in range(1, len(a.conv_dim)):
+            k, s, C = a.conv_kernel[i], a.conv_stride[i], a.conv_dim[i]
+            Tout = (Tin - k) // s + 1
+            pre_out = torch.empty(B * Tout, C, device=dev, dtype=cdt)
+            K.gemm(K.Operand(x, True, s * Cin, z1=Tin * Cin), K.Operand(W.conv_r[i - 1], True, k * Cin), pre_out,
+                   Tout, C, k * Cin, ldc=C, batch=B, c_z1=Tout * C)
+            yo = torch.empty(B * Tout, C, device=dev, dtype=cdt)
+            mo = torch.empty(B * Tout, device=dev, dtype=F32)
+            ro = torch.empty(B * Tout, device=dev, dtype=F32)
+            p = f"feature_extractor.conv_layers.{i}."
+            K.ln_fwd(pre_out, Pm[p + "layer_norm.weight"], Pm[p + "layer_norm.bias"], yo, mo, ro, a.eps, gelu=True)
+            if need_grad:
+                tape.conv.append(dict(x=x, pre=pre_out, mean=mo, rstd=ro, Tin=Tin, T=Tout, k=k, s=s))
+            x, Tin, Cin = yo, Tout, C
+        T = Tin
+        C = Cin
+        H = a.hidden
+        BT = B * T
+        feats = x
+        # -------- feature projection + dropout ([TF]modeling_wavlm.py:93-105)
+        xn = torch.empty(BT, C, device=dev, dtype=cdt)
+        fm = torch.empty(BT, device=dev, dtype=F32)
+        fr = torch.empty(BT, device=dev, dtype=F32)
+        K.ln_fwd(feats, Pm["feature_projection.layer_norm.weight"], Pm["feature_projection.layer_norm.bias"], xn, fm,
+                 fr, a.eps)
+        h = torch.empty(BT, H, device=dev, dtype=F32)
+        pfp = a.feat_proj_dropout if train else 0.0
+        K.linear_fwd(xn, Ps["feature_projection.projection.weight"], h, bias=Pm["feature_projection.projection.bias"],
+                     dropout_p=pfp, seed=R.site_seed(fseed, R.SITE_FEAT_PROJ))
+        # -------- SpecAugment ([TF]modeling_wavlm.py:985-1011) + padded copy for the pos-conv
+        pk, G = a.pos_kernel, a.pos_groups
+        cpg = H // G
+        mask = None
+        if train and mask_np is not None and mask_np.any():
+            mask = torch.from_numpy(mask_np.astype(np.uint8)).to(dev, non_blocking=True)
+        hpad = torch.empty(B, T + pk, H, device=dev, dtype=cdt)
+        K.specaug_pad(h, mask, Pm.get("masked_spec_embed"), hpad, B, T, H, pk // 2, pk - pk // 2)
+        # -------- positional conv + residual + dropout ([TF]modeling_wavlm.py:48-90, 476-483)
+        h0 = torch.empty(BT, H, device=dev, dtype=F32)
+        pos_pre = torch.empty(BT, H, device=dev, dtype=cdt)
+        php = a.hidden_dropout if train else 0.0
+        cs = int(math.log2(cpg))
+        K.gemm(K.Operand(hpad, True, H, chunk_shift=cs, ld_chunk=H, z1=(T + pk) * H, z2=cpg),
+               K.Operand(W.wf, True, pk * cpg, z2=cpg * pk * cpg), h0, T, cpg, pk * cpg, ldc=H, batch=B * G, zdiv=G,
+               c_z1=T * H, c_z2=cpg, bias=Pm["encoder.pos_conv_embed.conv.bias"], bias_z2=cpg,
+               flags=_lib.EPI_GELU | _lib.EPI_DROP_AFTER, aux=pos_pre, ldaux=H, aux_z1=T * H, aux_z2=cpg,
+               resid=h, ldr=H, r_z1=T * H, r_z2=cpg, dropout_p=php, seed=R.site_seed(fseed, R.SITE_POS))
+        # -------- relative position bias table (layer 0 computes it, every layer reuses it)
+        nh = a.heads
+        bias_tab = torch.empty(nh, T, T, device=dev, dtype=F32)
+        K.rel_bias_fwd(Pm["encoder.layers.0.attention.rel_attn_embed.weight"], self.buckets(T), bias_tab, nh, T)
+        if need_grad:
+            tape.T = T
+            tape.feats, tape.fp_mean, tape.fp_rstd, tape.xn = feats, fm, fr, xn
+            tape.mask, tape.hpad, tape.pos_pre, tape.bias_tab = mask, hpad, pos_pre, bias_tab
+            tape.pos = dict(W=W)
+        del xn, feats
+        # -------- transformer layers ([TF]modeling_wavlm.py:488-513, 355-373)
+        F_ = a.ffn
+        hcur = h0
+        pat = a.attention_dropout if train else 0.0
+        pact = a.activation_dropout if train else 0.0
+        executed = 0
+        for li in range(a.layers):
+            if train and skip is not None and skip[li]:
+                continue
+            executed += 1
+            p = f"encoder.layers.{li}."
+            x1 = torch.empty(BT, H, device=dev, dtype=cdt)
+            m1 = torch.empty(BT, device=dev, dtype=F32)
+            r1 = torch.empty(BT, device=dev, dtype=F32)
+            K.ln_fwd(hcur, Pm[p + "layer_norm.weight"], Pm[p + "layer_norm.bias"], x1, m1, r1, a.eps)
+            qkv = torch.empty(BT, 3 * H, device=dev, dtype=cdt)
+            K.linear_fwd(x1, self.fused(W.s_flat, li, "qkv_w"), qkv, bias=self.fused(W.m_flat, li, "qkv_b"))
+            gate = torch.empty(B, nh, T, device=dev, dtype=F32)
+            at = p + "attention."
+            K.gate_fwd(x1, Pm[at + "gru_rel_pos_linear.weight"], Pm[at + "gru_rel_pos_linear.bias"],
+                       Pm[at + "gru_rel_pos_const"], gate, B, T, nh)
+            ctx = torch.empty(BT, H, device=dev, dtype=cdt)
+            lse = torch.empty(B, nh, T, device=dev, dtype=F32)
+            K.attn_fwd(qkv, gate, bias_tab, ctx, lse, B, T, nh, pat, R.site_seed(fseed, R.site_attn_probs(li)))
+            hmid = torch.empty(BT, H, device=dev, dtype=F32)
+            K.linear_fwd(ctx, Ps[at + "out_proj.weight"], hmid, bias=Pm[at + "out_proj.bias"], resid=hcur, ldr=H,
+                         dropout_p=php, seed=R.site_seed(fseed, R.site_attn_out(li)))
+            x2 = torch.empty(BT, H, device=dev, dtype=cdt)
+            m2 = torch.empty(BT, device=dev, dtype=F32)
+            r2 = torch.empty(BT, device=dev, dtype=F32)
+            K.ln_fwd(hmid, Pm[p + "final_layer_norm.weight"], Pm[p + "final_layer_norm.bias"], x2, m2, r2, a.eps)
+            f1pre = torch.empty(BT, F_, device=dev, dtype=cdt) if need_grad else None
+            g1 = torch.empty(BT, F_, device=dev, dtype=cdt)
+            K.linear_fwd(x2, Ps[p + "feed_forward.intermediate_dense.weight"], g1,
+                         bias=Pm[p + "feed_forward.intermediate_dense.bias"], flags=_lib.EPI_GELU, aux=f1pre,
+                         ldaux=F_, dropout_p=pact, seed=R.site_seed(fseed, R.site_act(li)))
+            hout = torch.empty(BT, H, device=dev, dtype=F32)
+            K.linear_fwd(g1, Ps[p + "feed_forward.output_dense.weight"], hout,
+                         bias=Pm[p + "feed_forward.output_dense.bias"], resid=hmid, ldr=H, dropout_p=php,
+                         seed=R.site_seed(fseed, R.site_ffn_out(li)))
+            if need_grad:
+                tape.layers.append(dict(li=li, h_in=hcur, x1=x1, m1=m1, r1=r1, qkv=qkv, gate=gate, ctx=ctx, lse=lse,
+                                        hmid=hmid, x2=x2, m2=m2, r2=r2, f1pre=f1pre, g1=g1))
+            hcur = hout
+        # -------- final LN + time-mean shim
+        emb = torch.zeros(B, H, device=dev, dtype=F32)
+        mf = torch.empty(BT, device=dev, dtype=F32)
+        rf = torch.empty(BT, device=dev, dtype=F32)
+        K.ln_mean_fwd(hcur, Pm["encoder.layer_norm.weight"], Pm["encoder.layer_norm.bias"], emb, mf, rf, B, T, H,
+                      a.eps)
+        if need_grad:
+            tape.final = (hcur, mf, rf)
+        return emb, tape, executed
+
+    # ------------------------------------------------------------------ encoder backward
+    def encoder_backward(self, tape: Tape, demb: torch.Tensor, Gv: dict, W: EncoderWeights) -> None:
+        """Accumulate d(loss)/d(encoder params) into the grad views Gv given d(loss)/d(emb)."""
+        a = self.arch
+        cdt = self.cdt
+        dev = self.dev
+        B, T = tape.B, tape.T
+        H, F_, nh = a.hidden, a.ffn, a.heads
+        BT = B * T
+        Pm, Ps = W.m, W.s
+        fseed = tape.fseed
+        train = True
+        php, pat, pact = a.hidden_dropout, a.attention_dropout, a.activation_dropout
+        # final LN (+ time-mean): dy[b,t] = demb[b] / T
+        hfin, mf, rf = tape.final
+        dh = torch.empty(BT, H, device=dev, dtype=F32)
+        K.ln_bwd(demb, hfin, Pm["encoder.layer_norm.weight"], mf, rf, dh, dgamma=Gv["encoder.layer_norm.weight"],
+                 dbeta=Gv["encoder.layer_norm.bias"], mode=_lib.DY_BCAST, bcast_t=T, dy_scale=1.0 / T, rows=BT)
+        tape.final = None
+        diag = torch.zeros(nh, 2 * T - 1, device=dev, dtype=F32)
+        gate_scratch = torch.empty(BT * nh * 9, device=dev, dtype=F32)
+        delta = torch.empty(B, nh, T, device=dev, dtype=F32)
+        for L_ in reversed(tape.layers):
+            li = L_["li"]
+            p = f"encoder.layers.{li}."
+            at = p + "attention."
+            # FFN branch
+            dv2 = torch.empty(BT, H, device=dev, dtype=cdt)
+            K.dropout_cast(dh, dv2, php, R.site_seed(fseed, R.site_ffn_out(li)))
+            df1 = torch.empty(BT, F_, device=dev, dtype=cdt)
+            K.linear_dgrad(dv2, Ps[p + "feed_forward.output_dense.weight"], df1, flags=_lib.EPI_GELU_BWD,
+                           aux=L_["f1pre"], ldaux=F_, dropout_p=pact, seed=R.site_seed(fseed, R.site_act(li)),
+                           colsum=Gv[p + "feed_forward.intermediate_dense.bias"])
+            K.linear_wgrad(dv2, L_["g1"], Gv[p + "feed_forward.output_dense.weight"])
+            K.colsum(dv2, Gv[p + "feed_forward.output_dense.bias"])
+            K.linear_wgrad(df1, L_["x2"], Gv[p + "feed_forward.intermediate_dense.weight"])
+            dx2 = torch.empty(BT, H, device=dev, dtype=F32)
+            K.linear_dgrad(df1, Ps[p + "feed_forward.intermediate_dense.weight"], dx2)
+            del df1, dv2
+            dhmid = torch.empty(BT, H, device=dev, dtype=F32)
+            K.ln_bwd(dx2, L_["hmid"], Pm[p + "final_layer_norm.weight"], L_["m2"], L_["r2"], dhmid, resid=dh,
+                     dgamma=Gv[p + "final_layer_norm.weight"], dbeta=Gv[p + "final_layer_norm.bias"])
+            del dx2
+            # attention branch
+            dv1 = torch.empty(BT, H, device=dev, dtype=cdt)
+            K.dropout_cast(dhmid, dv1, php, R.site_seed(fseed, R.site_attn_out(li)))
+            dctx = torch.empty(BT, H, device=dev, dtype=cdt)
+            K.linear_dgrad(dv1, Ps[at + "out_proj.weight"], dctx)
+            K.linear_wgrad(dv1, L_["ctx"], Gv[at + "out_proj.weight"])
+            K.colsum(dv1, Gv[at + "out_proj.bias"])
+            del dv1
+            dqkv = torch.empty(BT, 3 * H, device=dev, dtype=cdt)
+            dgate = torch.empty(B, nh, T, device=dev, dtype=F32)
+            K.attn_bwd(L_["qkv"], L_["gate"], tape.bias_tab, L_["ctx"], dctx, L_["lse"], delta, dqkv, dgate, diag, B,
+                       T, nh, pat, R.site_seed(fseed, R.site_attn_probs(li)))
+            del dctx
+            K.linear_wgrad(dqkv, L_["x1"], self.fused(self.grad_flat_for(Gv), li, "qkv_w"))
+            K.colsum(dqkv, self.fused(self.grad_flat_for(Gv), li, "qkv_b"))
+            dx1 = torch.empty(BT, H, device=dev, dtype=F32)
+            K.linear_dgrad(dqkv, self.fused(W.s_flat, li, "qkv_w"), dx1)
+            del dqkv
+            K.gate_bwd(L_["x1"], Pm[at + "gru_rel_pos_linear.weight"], Pm[at + "gru_rel_pos_linear.bias"],
+                       Pm[at + "gru_rel_pos_const"], dgate, dx1, Gv[at + "gru_rel_pos_linear.weight"],
+                       Gv[at + "gru_rel_pos_linear.bias"], Gv[at + "gru_rel_pos_const"], gate_scratch, B, T, nh)
+            dhin = torch.empty(BT, H, device=dev, dtype=F32)
+            K.ln_bwd(dx1, L_["h_in"], Pm[p + "layer_norm.weight"], L_["m1"], L_["r1"], dhin, resid=dhmid,
+                     dgamma=Gv[p + "layer_norm.weight"], dbeta=Gv[p + "layer_norm.bias"])
+            del dx1, dhmid
+            L_.clear()
+            dh = dhin
+        tape.layers = []
+        K.rel_bias_bwd(diag, self.buckets(T), Gv["encoder.layers.0.attention.rel_attn_embed.weight"], nh, T)
+        # positional conv block: h0 = drop(h + gelu(conv(hpad) + b))
+        pk, G = a.pos_kernel, a.pos_groups
+        cpg = H // G
+        cs = int(math.log2(cpg))
+        ds = torch.empty(BT, H, device=dev, dtype=F32)
+        K.dropout_cast(dh, ds, php, R.site_seed(fseed, R.SITE_POS))
+        del dh
+        dypad = torch.empty(B, T + pk, H, device=dev, dtype=cdt)
+        K.gelu_bwd_pad(ds, tape.pos_pre, dypad, B, T, H, pk // 2 - 1, pk - pk // 2 + 1)
+        K.colsum(dypad, Gv["encoder.pos_conv_embed.conv.bias"])
+        # dgrad: ds += conv_transpose(dpre) (flipped taps, dypad has pk/2-1 leading zero rows)
+        K.gemm(K.Operand(dypad, True, H, chunk_shift=cs, ld_chunk=H, z1=(T + pk) * H, z2=cpg),
+               K.Operand(W.wd, True, pk * cpg, z2=cpg * pk * cpg), ds, T, cpg, pk * cpg, ldc=H, batch=B * G, zdiv=G,
+               c_z1=T * H, c_z2=cpg, flags=_lib.EPI_ACCUM)
+        # wgrad over (b, t) -> dWf [G][cpg][pk*cpg]
+        dWf = torch.zeros(G, cpg, pk * cpg, device=dev, dtype=F32)
+        S = _divisor_at_most(B, 8)
+        off = (pk // 2 - 1) * H
+        K.gemm(K.Operand(dypad, False, H, offset=off, seg_stride=(T + pk) * H, z1=cpg),
+               K.Operand(tape.hpad, False, H, chunk_shift=cs, ld_chunk=H, seg_stride=(T + pk) * H, z1=cpg),
+               dWf, cpg, pk * cpg, T, ldc=pk * cpg, nseg=B // S, splits=S, batch=G, c_z1=cpg * pk * cpg,
+               flags=_lib.EPI_ATOMIC)
+        del dypad
+        pre = "encoder.pos_conv_embed.conv.parametrizations.weight."
+        wn_scratch = torch.empty(pk, device=dev, dtype=F32)
+        K.weight_norm_bwd(dWf, Pm[pre + "original0"], Pm[pre + "original1"], W.wn_norms, Gv[pre + "original0"],
+                          Gv[pre + "original1"], wn_scratch, H, cpg, pk)
+        del dWf
+        # SpecAugment + feature-projection dropout backward
+        dproj = torch.empty(BT, H, device=dev, dtype=cdt)
+        K.specaug_bwd(ds, tape.mask, Gv.get("masked_spec_embed"), dproj, B, T, H, a.feat_proj_dropout,
+                      R.site_seed(fseed, R.SITE_FEAT_PROJ))
+        del ds
+        K.linear_wgrad(dproj, tape.xn, Gv["feature_projection.projection.weight"])
+        K.colsum(dproj, Gv["feature_projection.projection.bias"])
+        C = a.conv_dim[-1]
+        dxn = torch.empty(BT, C, device=dev, dtype=F32)
+        K.linear_dgrad(dproj, Ps["feature_projection.projection.weight"], dxn)
+        del dproj
+        dfeat = torch.empty(BT, C, device=dev, dtype=cdt)
+        K.ln_bwd(dxn, tape.feats, Pm["feature_projection.layer_norm.weight"], tape.fp_mean, tape.fp_rstd, dfeat,
+                 dgamma=Gv["feature_projection.layer_norm.weight"], dbeta=Gv["feature_projection.layer_norm.bias"])
+        del dxn
+        tape.feats = tape.xn = tape.hpad = tape.pos_pre = None
+        # conv stack backward (LN+GELU bwd with col2im of the next layer's dgrad GEMM)
+        dy_src, col = dfeat, None
+        for i in range(len(a.conv_dim) - 1, 0, -1):
+            c = tape.conv[i]
+            p = f"feature_extractor.conv_layers.{i}."
+            Cc = a.conv_dim[i]
+            Cin = a.conv_dim[i - 1]
+            Tout, Tin, k, s = c["T"], c["Tin"], c["k"], c["s"]
+            dpre = torch.empty(B * Tout, Cc, device=dev, dtype=cdt)
+            if col is None:
+                K.ln_bwd(dy_src, c["pre"], Pm[p + "layer_norm.weight"], c["mean"], c["rstd"], dpre,
+                         beta=Pm[p + "layer_norm.bias"], gelu=True, dgamma=Gv[p + "layer_norm.weight"],
+                         dbeta=Gv[p + "layer_norm.bias"])
+            else:
+                K.ln_bwd(dy_src, c["pre"], Pm[p + "layer_norm.weight"], c["mean"], c["rstd"], dpre,
+                         beta=Pm[p + "layer_norm.bias"], gelu=True, dgamma=Gv[p + "layer_norm.weight"],
+                         dbeta=Gv[p + "layer_norm.bias"], mode=_lib.DY_COL2IM, col=col)
+            del dy_src
+            # wgrad -> [co][k*ci] then into the [co][ci][k] grad layout
+            dWr = torch.zeros(Cc, k * Cin, device=dev, dtype=F32)
+            tiles = ((Cc + 127) // 128) * ((k * Cin + 127) // 128)
+            S = _divisor_at_most(B, max(1, 512 // tiles))
+            K.gemm(K.Operand(dpre, False, Cc, seg_stride=Tout * Cc), K.Operand(c["x"], False, s * Cin,
+                                                                               seg_stride=Tin * Cin),
+                   dWr, Cc, k * Cin, Tout, ldc=k * Cin, nseg=B // S, splits=S, flags=_lib.EPI_ATOMIC)
+            K.swap12(dWr, Gv[p + "conv.weight"], Cc, k, Cin, accumulate=True)
+            del dWr
+            # dgrad -> G [B*Tout, k*Cin] (col2im folded into the next LN backward)
+            Gd = torch.empty(B * Tout, k * Cin, device=dev, dtype=cdt)
+            K.gemm(K.Operand(dpre, True, Cc), K.Operand(W.conv_r[i - 1], False, k * Cin), Gd, B * Tout, k * Cin, Cc,
+                   ldc=k * Cin)
+            del dpre
+            tape.conv[i] = None
+            dy_src, col = Gd, (k, s, Tout, Tin)
+        c0 = tape.conv[0]
+        p = "feature_extractor.conv_layers.0."
+        K.conv0_bwd(tape.wav, Pm[p + "conv.weight"], Pm[p + "layer_norm.weight"], Pm[p + "layer_norm.bias"],
+                    c0["mean"], c0["rstd"], dy_src, Gv[p + "conv.weight"], Gv[p + "layer_norm.weight"],
+                    Gv[p + "layer_norm.bias"], c0["T"], a.conv_kernel[0], a.conv_stride[0], col[:3])
+        tape.conv = []
+
+    def grad_flat_for(self, Gv):
+        return self.grad
+
+    # ------------------------------------------------------------------ heads
+    def _linear(self, x, w, b, out_dim):
+        y = torch.empty(x.shape[0], out_dim, device=self.dev, dtype=F32)
+        K.linear_fwd(x, w, y, bias=b)
+        return y
+
+    def _bn(self, x, P, name, bn_key, train, relu):
+        C = x.shape[1]
+        y = torch.empty_like(x)
+        sm = torch.empty(C, device=self.dev, dtype=F32)
+        si = torch.empty(C, device=self.dev, dtype=F32)
+        rm, rv, nbt = self.bn[bn_key]
+        K.bn_fwd(x, P[name + ".weight"], P[name + ".bias"], y, rm, rv, sm, si, train, relu)
+        if train:
+            nbt.add_(1)
+        return y, (x, y, sm, si)
+
+    def projector_forward(self, emb, P, net, train):
+        z0 = self._linear(emb, P["layers.0.weight"], P["layers.0.bias"], P["layers.0.weight"].shape[0])
+        z1, c1 = self._bn(z0, P, "layers.1", f"{net}.layers.1", train, True)
+        z3 = self._linear(z1, P["layers.3.weight"], P["layers.3.bias"], P["layers.3.weight"].shape[0])
+        z4, c4 = self._bn(z3, P, "layers.4", f"{net}.layers.4", train, False)
+        return z4, dict(emb=emb, z1=z1, c1=c1, c4=c4)
+
+    def predictor_forward(self, x, P, train):
+        net = "online_predictor"
+        q0 = self._linear(x, P["layers.0.weight"], P["layers.0.bias"], P["layers.0.weight"].shape[0])
+        q1, c1 = self._bn(q0, P, "layers.1", f"{net}.layers.1", train, True)
+        q3 = self._linear(q1, P["layers.3.weight"], P["layers.3.bias"], P["layers.3.weight"].shape[0])
+        q4, c4 = self._bn(q3, P, "layers.4", f"{net}.layers.4", train, True)
+        q6 = self._linear(q4, P["layers.6.weight"], P["layers.6.bias"], P["layers.6.weight"].shape[0])
+        return q6, dict(x=x, q1=q1, c1=c1, q4=q4, c4=c4)
+
+    def _lin_bwd(self, dy, x, w, Gw, Gb):
+        K.linear_wgrad(dy, x, Gw)
+        K.colsum(dy, Gb)
+        dx = torch.empty(dy.shape[0], w.shape[1], device=self.dev, dtype=F32)
+        K.linear_dgrad(dy, w, dx)
+        return dx
+
+    def _bn_bwd(self, dy, cache, P, G, name, relu):
+        x, y, sm, si = cache
+        dx = torch.empty_like(x)
+        K.bn_bwd(dy, x, y, P[name + ".weight"], sm, si, dx, G[name + ".weight"], G[name + ".bias"], relu)
+        return dx
+
+    def predictor_backward(self, dpred, cache, P, G):
+        dq4 = self._lin_bwd(dpred, cache["q4"], P["layers.6.weight"], G["layers.6.weight"], G["layers.6.bias"])
+        dq3 = self._bn_bwd(dq4, cache["c4"], P, G, "layers.4", True)
+        dq1 = self._lin_bwd(dq3, cache["q1"], P["layers.3.weight"], G["layers.3.weight"], G["layers.3.bias"])
+        dq0 = self._bn_bwd(dq1, cache["c1"], P, G, "layers.1", True)
+        return self._lin_bwd(dq0, cache["x"], P["layers.0.weight"], G["layers.0.weight"], G["layers.0.bias"])
+
+    def projector_backward(self, dz4, cache, P, G):
+        dz3 = self._bn_bwd(dz4, cache["c4"], P, G, "layers.4", False)
+        dz1 = self._lin_bwd(dz3, cache["z1"], P["layers.3.weight"], G["layers.3.weight"], G["layers.3.bias"])
+        dz0 = self._bn_bwd(dz1, cache["c1"], P, G, "layers.1", True)
+        return self._lin_bwd(dz0, cache["emb"], P["layers.0.weight"], G["layers.0.weight"], G["layers.0.bias"])
+
+    # ------------------------------------------------------------------ public API
+    def weights(self, which: str) -> EncoderWeights:
+        if which == "online":
+            W = EncoderWeights(self, self.online, self.online_sh)
+            W.m_flat, W.s_flat = self.online, (self.online_sh if self.online_sh is not None else self.online)
+        else:
+            W = EncoderWeights(self, self.target, self.target_sh)
+            W.m_flat, W.s_flat = self.target, (self.target_sh if self.target_sh is not None else self.target)
+        return W
+
+    def stochastic_inputs(self, step_seed: int, B: int, T: int, train: bool):
+        """LayerDrop decisions (rank-shared) and SpecAugment masks for both branches."""
+        a = self.arch
+        if not train:
+            return (None, None), (None, None)
+        g = np.random.default_rng([step_seed, 7])
+        skips = (layerdrop_decisions(g, a.layers, a.layerdrop), layerdrop_decisions(g, a.layers, a.layerdrop))
+        masks = (compute_mask_indices(g, B, T, a.mask_time_prob, a.mask_time_length, a.mask_time_min_masks),
+                 compute_mask_indices(g, B, T, a.mask_time_prob, a.mask_time_length, a.mask_time_min_masks))
+        return skips, masks
+
+    def forward(self, clean: torch.Tensor, noisy: torch.Tensor, *, train: bool, step_seed: int = 0, rank: int = 0,
+                need_grad: bool = False, skips=None, masks=None):
+        """BYOLSpeechModel.forward -> (online_pred, target_proj, ctx for backward)."""
+        B, L = clean.shape
+        T = self.arch.frames(L)
+        if skips is None or masks is None:
+            s2, m2 = self.stochastic_inputs(step_seed, B, T, train)
+            skips = skips if skips is not None else s2
+            masks = masks if masks is not None else m2
+        Wo = self.weights("online")
+        emb, tape, ex0 = self.encoder_forward(Wo, clean, train=train, fseed=R.forward_seed(step_seed, 0, rank),
+                                              skip=skips[0], mask_np=masks[0], need_grad=need_grad)
+        Pon = self.group_views(self.online, "projector")
+        Ppr = self.group_views(self.online, "predictor")
+        proj, pc = self.projector_forward(emb, Pon, "online_projector", train)
+        pred, qc = self.predictor_forward(proj, Ppr, train)
+        Wt = self.weights("target")
+        temb, _, ex1 = self.encoder_forward(Wt, noisy, train=train, fseed=R.forward_seed(step_seed, 1, rank),
+                                            skip=skips[1], mask_np=masks[1], need_grad=False)
+        Ptp = self.group_views(self.target, "projector")
+        tproj, _ = self.projector_forward(temb, Ptp, "target_projector", train)
+        self.executed_layers = [ex0, ex1]
+        ctx = dict(tape=tape, W=Wo, pc=pc, qc=qc, emb=emb, Pon=Pon, Ppr=Ppr)
+        return pred, tproj, ctx
+
+    def backward(self, dpred: torch.Tensor, ctx: dict) -> None:
+        """Accumulate all online-parameter gradients into self.grad from d(loss)/d(pred)."""
+        Gp = self.group_views(self.grad, "predictor")
+        Gj = self.group_views(self.grad, "projector")
+        Ge = self.group_views(self.grad, "encoder")
+        dproj = self.predictor_backward(dpred, ctx["qc"], ctx["Ppr"], Gp)
+        demb = self.projector_backward(dproj, ctx["pc"], ctx["Pon"], Gj)
+        self.encoder_backward(ctx["tape"], demb, Ge, ctx["W"])
+
+    def optimizer_step(self, lr: float, grad_scale: float = 1.0) -> None:
+        """clip_grad_norm_(1.0) + AdamW + target EMA (train_byol.py:67-71), no host sync."""
+        c = self.cfg
+        self.step_count += 1
+        self.sumsq_buf.zero_()
+        K.sumsq(self.grad, self.sumsq_buf)
+        K.adamw(self.online, self.grad, self.m, self.v, self.online_sh, lr=lr, beta1=c.betas[0], beta2=c.betas[1],
+                eps=c.eps, weight_decay=c.weight_decay, step=self.step_count, max_norm=c.max_norm,
+                sumsq_buf=self.sumsq_buf, grad_scale=grad_scale)
+        ne = self.layout.ema_numel
+        K.ema(self.target, self.online[:ne], self.target_sh, c.ema_decay)
+
+    def grad_norm(self) -> float:
+        """Pre-clip global gradient norm of the last step (host sync)."""
+        return float(self.sumsq_buf.sqrt())
+
+    def train_step(self, clean: torch.Tensor, noisy: torch.Tensor, *, lr: float, step_seed: int, rank: int = 0,
+                   allreduce=None, world_size: int = 1) -> torch.Tensor:
+        """One iteration of train_one_epoch (train_byol.py:47-77): forward, loss, backward,
+        clip, AdamW, EMA. Returns the device-resident loss (no sync)."""
+        B = clean.shape[0]
+        K.health(clean, self.health_buf[0])
+        K.health(noisy, self.health_buf[1])
+        pred, tproj, ctx = self.forward(clean, noisy, train=True, step_seed=step_seed, rank=rank, need_grad=True)
+        K.health(pred, self.health_buf[2])
+        K.health(tproj, self.health_buf[3])
+        self.loss_buf.zero_()
+        dpred = torch.empty_like(pred)
+        K.byol_loss(pred, tproj, self.loss_buf, dpred, self.loss_stats)
+        self.grad.zero_()
+        self.backward(dpred, ctx)
+        if allreduce is not None:
+            allreduce(self.grad)
+        self.optimizer_step(lr, grad_scale=1.0)
+        return self.loss_buf
+
+    def eval_forward(self, clean, noisy):
+        with torch.no_grad():
+            pred, tproj, _ = self.forward(clean, noisy, train=False, need_grad=False)
+        loss = torch.zeros(1, device=self.dev, dtype=F32)
+        K.byol_loss(pred, tproj, loss)
+        return pred, tproj, loss
+
+    def embed(self, wav: torch.Tensor, which: str = "online") -> torch.Tensor:
+        emb, _, _ = self.encoder_forward(self.weights(which), wav, train=False)
+        return emb

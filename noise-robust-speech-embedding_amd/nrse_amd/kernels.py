@@ -11,7 +11,8 @@ from dataclasses import dataclass
 import torch
 
 from . import _lib
-from ._lib import GemmOperand, GemmParams
+from ._lib import (AdamWParams, AttnBwdParams, AttnFwdParams, Conv0Params, GemmOperand, GemmParams, LnBwdParams,
+                   LnFwdParams)
 
 _DT = {torch.float32: _lib.F32, torch.bfloat16: _lib.BF16}
 
@@ -27,12 +28,16 @@ def stream_ptr() -> int:
     return torch.cuda.current_stream().cuda_stream
 
 
-def ptr(t: torch.Tensor | None, offset_elems: int = 0) -> int | None:
+def ptr(t: torch.Tensor | None, offset_elems: int = 0):
     if t is None:
         return None
     if not t.is_cuda:
         raise _lib.NrseError("libnrse_hip ops take device tensors")
     return t.data_ptr() + offset_elems * t.element_size()
+
+
+def _call(name, *args):
+    _lib.check(getattr(_lib.lib(), name)(*args), name)
 
 
 @dataclass
@@ -56,14 +61,21 @@ class Operand:
 def gemm(A: Operand, B: Operand, C: torch.Tensor, M: int, N: int, K: int, *, ldc: int, c_offset: int = 0,
          nseg: int = 1, splits: int = 1, batch: int = 1, zdiv: int = 1, c_z1: int = 0, c_z2: int = 0,
          c_split: int = 0, alpha: float = 1.0, flags: int = 0, bias: torch.Tensor | None = None,
+         bias_z1: int = 0, bias_z2: int = 0,
          aux: torch.Tensor | None = None, ldaux: int = 0, aux_z1: int = 0, aux_z2: int = 0,
          resid: torch.Tensor | None = None, ldr: int = 0, r_z1: int = 0, r_z2: int = 0,
          dropout_p: float = 0.0, seed: int = 0, colsum: torch.Tensor | None = None) -> None:
     """C[m,n] = epilogue(alpha * sum_k A(m,k) B(n,k)); see nrse_gemm."""
     if bias is not None:
-        assert bias.dtype == torch.float32 and bias.is_contiguous()
+        assert bias.dtype == torch.float32
+        flags |= _lib.EPI_BIAS
     if colsum is not None:
         assert colsum.dtype == torch.float32
+        flags |= _lib.EPI_COLSUM
+    if resid is not None:
+        flags |= _lib.EPI_RESID
+    if dropout_p > 0:
+        flags |= _lib.EPI_DROPOUT
     p = GemmParams()
     p.a = A.c()
     p.b = B.c()
@@ -74,6 +86,7 @@ def gemm(A: Operand, B: Operand, C: torch.Tensor, M: int, N: int, K: int, *, ldc
     p.c_dtype = dtype_code(C)
     p.ldc, p.c_z1, p.c_z2, p.c_split = ldc, c_z1, c_z2, c_split
     p.bias = ptr(bias)
+    p.bias_z1, p.bias_z2 = bias_z1, bias_z2
     if aux is not None:
         p.aux = ptr(aux)
         p.aux_dtype = dtype_code(aux)
@@ -94,8 +107,6 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, *, bias=None
     M, K = x.shape
     N = w.shape[0]
     assert w.shape[1] == K and out.shape[-1] >= N
-    if bias is not None:
-        flags |= _lib.EPI_BIAS
     gemm(Operand(x, True, x.stride(0)), Operand(w, True, w.stride(0)), out, M, N, K, ldc=out.stride(0),
          bias=bias, flags=flags, **kw)
 
@@ -109,30 +120,205 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, dx: torch.Tensor, *, flags: 
          flags=flags, **kw)
 
 
-def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, *, splits: int = 1, colsum=None,
-                 accumulate: bool = True) -> None:
-    """dw[N,K] (+)= dy[M,N]^T @ x[M,K]  (f32 dw). Optionally colsum(dy) -> bias grad."""
+def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, *, splits: int = 0) -> None:
+    """dw[N,K] += dy[M,N]^T @ x[M,K]  (f32 dw, atomics)."""
     M, N = dy.shape
     K = x.shape[1]
     assert x.shape[0] == M and dw.shape == (N, K) and dw.dtype == torch.float32
-    splits = max(1, min(splits, M // 256))
+    if splits <= 0:
+        tiles = ((N + 127) // 128) * ((K + 127) // 128)
+        splits = max(1, min(16, 512 // max(tiles, 1)))
+    splits = max(1, min(splits, M // 64))
     seg = (M + splits - 1) // splits
     seg = (seg + 7) // 8 * 8
-    nseg_total = (M + seg - 1) // seg
-    if nseg_total * seg != M:
-        # ragged last split: run the bulk split-K and the tail separately
-        bulk = (M // seg) * seg
-        if bulk:
-            linear_wgrad(dy[:bulk], x[:bulk], dw, splits=bulk // seg, accumulate=accumulate)
-        linear_wgrad(dy[bulk:], x[bulk:], dw, splits=1, accumulate=True)
-        if colsum is not None:
-            from . import ops_small
-            ops_small.colsum(dy, colsum)
-        return
-    flags = _lib.EPI_ATOMIC if (splits > 1 or accumulate) else 0
-    gemm(Operand(dy, False, dy.stride(0), seg_stride=seg * dy.stride(0)),
-         Operand(x, False, x.stride(0), seg_stride=seg * x.stride(0)),
-         dw, N, K, seg, ldc=dw.stride(0), nseg=1, splits=splits, flags=flags)
-    if colsum is not None:
-        from . import ops_small
-        ops_small.colsum(dy, colsum)
+    bulk = (M // seg) * seg
+    if bulk:
+        gemm(Operand(dy, False, dy.stride(0), seg_stride=seg * dy.stride(0)),
+             Operand(x, False, x.stride(0), seg_stride=seg * x.stride(0)),
+             dw, N, K, seg, ldc=dw.stride(0), nseg=1, splits=bulk // seg, flags=_lib.EPI_ATOMIC)
+    if bulk < M:
+        gemm(Operand(dy, False, dy.stride(0), offset=bulk * dy.stride(0)),
+             Operand(x, False, x.stride(0), offset=bulk * x.stride(0)),
+             dw, N, K, M - bulk, ldc=dw.stride(0), flags=_lib.EPI_ATOMIC)
+
+
+# ----------------------------------------------------------------------------- layernorm
+def ln_fwd(x, gamma, beta, y, mean, rstd, eps, gelu=False):
+    rows, C = x.shape[0] if x.dim() == 2 else x.numel() // x.shape[-1], x.shape[-1]
+    p = LnFwdParams(ptr(x), dtype_code(x), ptr(gamma), ptr(beta), ptr(y), dtype_code(y), ptr(mean), ptr(rstd),
+                    rows, C, eps, _lib.LN_GELU if gelu else 0)
+    _call("nrse_layernorm_fwd", ctypes.byref(p), stream_ptr())
+
+
+def ln_bwd(dy, x, gamma, mean, rstd, dx, *, beta=None, gelu=False, resid=None, dgamma=None, dbeta=None,
+           mode=_lib.DY_DIRECT, col=(0, 0, 0, 0), bcast_t=0, dy_scale=1.0, rows=None):
+    C = x.shape[-1]
+    rows = rows if rows is not None else x.numel() // C
+    p = LnBwdParams()
+    p.dy, p.dy_dtype, p.dy_mode = ptr(dy), dtype_code(dy), mode
+    p.col_k, p.col_s, p.col_tout, p.col_tin = col
+    p.bcast_t, p.dy_scale = bcast_t, dy_scale
+    p.x, p.x_dtype = ptr(x), dtype_code(x)
+    p.gamma, p.beta, p.mean, p.rstd = ptr(gamma), ptr(beta), ptr(mean), ptr(rstd)
+    p.dx, p.dx_dtype = ptr(dx), dtype_code(dx)
+    p.resid = ptr(resid)
+    p.dgamma, p.dbeta = ptr(dgamma), ptr(dbeta)
+    p.rows, p.C, p.flags = rows, C, (_lib.LN_GELU if gelu else 0)
+    _call("nrse_layernorm_bwd", ctypes.byref(p), stream_ptr())
+
+
+def ln_mean_fwd(h, gamma, beta, emb, mean, rstd, batch, T, C, eps):
+    _call("nrse_ln_mean_fwd", ptr(h), ptr(gamma), ptr(beta), ptr(emb), ptr(mean), ptr(rstd), batch, T, C, eps,
+          stream_ptr())
+
+
+# ----------------------------------------------------------------------------- attention
+def rel_bias_fwd(E, bucket, bias, H, T):
+    _call("nrse_rel_bias_fwd", ptr(E), ptr(bucket), ptr(bias), H, T, E.shape[0], stream_ptr())
+
+
+def rel_bias_bwd(diag, bucket, dE, H, T):
+    _call("nrse_rel_bias_bwd", ptr(diag), ptr(bucket), ptr(dE), H, T, stream_ptr())
+
+
+def gate_fwd(x1, W, b, c, gate, batch, T, H):
+    _call("nrse_gate_fwd", ptr(x1), dtype_code(x1), ptr(W), ptr(b), ptr(c), ptr(gate), batch, T, H, stream_ptr())
+
+
+def gate_bwd(x1, W, b, c, dgate, dx1, dW, db, dc, scratch, batch, T, H):
+    _call("nrse_gate_bwd", ptr(x1), dtype_code(x1), ptr(W), ptr(b), ptr(c), ptr(dgate), ptr(dx1), ptr(dW), ptr(db),
+          ptr(dc), ptr(scratch), batch, T, H, stream_ptr())
+
+
+def attn_fwd(qkv, gate, bias, ctx, lse, batch, T, H, dropout_p=0.0, seed=0):
+    p = AttnFwdParams(ptr(qkv), dtype_code(qkv), ptr(gate), ptr(bias), ptr(ctx), ptr(lse), batch, T, H, 64,
+                      0.125, dropout_p, seed & 0xFFFFFFFF)
+    _call("nrse_attn_fwd", ctypes.byref(p), stream_ptr())
+
+
+def attn_bwd(qkv, gate, bias, ctx, dctx, lse, delta, dqkv, dgate, diag, batch, T, H, dropout_p=0.0, seed=0):
+    p = AttnBwdParams(ptr(qkv), dtype_code(qkv), ptr(gate), ptr(bias), ptr(ctx), ptr(dctx), ptr(lse), ptr(delta),
+                      ptr(dqkv), ptr(dgate), ptr(diag), batch, T, H, 64, 0.125, dropout_p, seed & 0xFFFFFFFF)
+    _call("nrse_attn_bwd", ctypes.byref(p), stream_ptr())
+
+
+# ----------------------------------------------------------------------------- conv front end
+def conv0_fwd(wav, w, gamma, beta, out, mean, rstd, T0, k, s, eps):
+    B, L = wav.shape
+    C = w.shape[0]
+    p = Conv0Params()
+    p.wav, p.L, p.w, p.gamma, p.beta = ptr(wav), L, ptr(w), ptr(gamma), ptr(beta)
+    p.out, p.out_dtype, p.mean, p.rstd = ptr(out), dtype_code(out), ptr(mean), ptr(rstd)
+    p.batch, p.T0, p.C, p.k, p.s, p.eps = B, T0, C, k, s, eps
+    _call("nrse_conv0_fwd", ctypes.byref(p), stream_ptr())
+
+
+def conv0_bwd(wav, w, gamma, beta, mean, rstd, dy, dw, dgamma, dbeta, T0, k, s, col):
+    B, L = wav.shape
+    C = w.shape[0]
+    p = Conv0Params()
+    p.wav, p.L, p.w, p.gamma, p.beta = ptr(wav), L, ptr(w), ptr(gamma), ptr(beta)
+    p.mean, p.rstd = ptr(mean), ptr(rstd)
+    p.dy, p.dy_dtype = ptr(dy), dtype_code(dy)
+    if col is None:
+        p.dy_mode = _lib.DY_DIRECT
+    else:
+        p.dy_mode = _lib.DY_COL2IM
+        p.col_k, p.col_s, p.col_tout = col
+    p.dw, p.dgamma, p.dbeta = ptr(dw), ptr(dgamma), ptr(dbeta)
+    p.batch, p.T0, p.C, p.k, p.s = B, T0, C, k, s
+    _call("nrse_conv0_bwd", ctypes.byref(p), stream_ptr())
+
+
+def weight_norm_fwd(g, v, wf, wd, norms, H, cpg, K):
+    _call("nrse_weight_norm_fwd", ptr(g), ptr(v), ptr(wf), ptr(wd), dtype_code(wf), ptr(norms), H, cpg, K,
+          stream_ptr())
+
+
+def weight_norm_bwd(dWf, g, v, norms, dg, dv, scratch, H, cpg, K):
+    _call("nrse_weight_norm_bwd", ptr(dWf), ptr(g), ptr(v), ptr(norms), ptr(dg), ptr(dv), ptr(scratch), H, cpg, K,
+          stream_ptr())
+
+
+# ----------------------------------------------------------------------------- elementwise
+def specaug_pad(h, mask, embed, dst, batch, T, C, pf, pb):
+    _call("nrse_specaug_pad", ptr(h), ptr(mask), ptr(embed), ptr(dst), dtype_code(dst), batch, T, C, pf, pb,
+          stream_ptr())
+
+
+def pad_rows(src, dst, batch, T, C, pf, pb):
+    _call("nrse_pad_rows", ptr(src), dtype_code(src), ptr(dst), dtype_code(dst), batch, T, C, pf, pb, stream_ptr())
+
+
+def specaug_bwd(dh, mask, dembed, out, batch, T, C, p, seed):
+    _call("nrse_specaug_bwd", ptr(dh), ptr(mask), ptr(dembed), ptr(out), dtype_code(out), batch, T, C, p,
+          seed & 0xFFFFFFFF, stream_ptr())
+
+
+def dropout_cast(x, out, p=0.0, seed=0):
+    assert x.dtype == torch.float32 and x.numel() == out.numel()
+    _call("nrse_dropout_cast", ptr(x), ptr(out), dtype_code(out), x.numel(), p, seed & 0xFFFFFFFF, stream_ptr())
+
+
+def colsum(x, out):
+    C = x.shape[-1]
+    _call("nrse_colsum", ptr(x), dtype_code(x), ptr(out), x.numel() // C, C, stream_ptr())
+
+
+def cast(x, y):
+    assert x.numel() == y.numel()
+    _call("nrse_cast", ptr(x), dtype_code(x), ptr(y), dtype_code(y), x.numel(), stream_ptr())
+
+
+def swap12(src, dst, d0, d1, d2, accumulate=False):
+    _call("nrse_swap12", ptr(src), dtype_code(src), ptr(dst), dtype_code(dst), d0, d1, d2, int(accumulate),
+          stream_ptr())
+
+
+def gelu_bwd_pad(dy, pre, out, batch, T, C, pf, pb):
+    _call("nrse_gelu_bwd_pad", ptr(dy), ptr(pre), dtype_code(pre), ptr(out), dtype_code(out), batch, T, C, pf, pb,
+          stream_ptr())
+
+
+# ----------------------------------------------------------------------------- heads / loss / optim
+def bn_fwd(x, w, b, y, rm, rv, sm, si, train, relu, momentum=0.1, eps=1e-5):
+    rows, C = x.shape
+    _call("nrse_bn_fwd", ptr(x), ptr(w), ptr(b), ptr(y), ptr(rm), ptr(rv), ptr(sm), ptr(si), rows, C, momentum, eps,
+          int(train), int(relu), stream_ptr())
+
+
+def bn_bwd(dy, x, y, w, sm, si, dx, dw, db, relu):
+    rows, C = x.shape
+    _call("nrse_bn_bwd", ptr(dy), ptr(x), ptr(y), ptr(w), ptr(sm), ptr(si), ptr(dx), ptr(dw), ptr(db), rows, C,
+          int(relu), stream_ptr())
+
+
+def byol_loss(p, z, loss, dp=None, stats=None, grad_scale=1.0):
+    rows, D = p.shape
+    _call("nrse_byol_loss", ptr(p), ptr(z), ptr(loss), ptr(dp), ptr(stats), rows, D, grad_scale, stream_ptr())
+
+
+def sumsq(x, out):
+    _call("nrse_sumsq", ptr(x), x.numel(), ptr(out), stream_ptr())
+
+
+def adamw(p, g, m, v, shadow, *, lr, beta1, beta2, eps, weight_decay, step, max_norm, sumsq_buf, grad_scale=1.0):
+    prm = AdamWParams(ptr(p), ptr(g), ptr(m), ptr(v), ptr(shadow),
+                      dtype_code(shadow) if shadow is not None else 0, p.numel(), lr, beta1, beta2, eps,
+                      weight_decay, step, max_norm, ptr(sumsq_buf), grad_scale)
+    _call("nrse_adamw", ctypes.byref(prm), stream_ptr())
+
+
+def ema(t, o, shadow, decay):
+    _call("nrse_ema", ptr(t), ptr(o), ptr(shadow), dtype_code(shadow) if shadow is not None else 0, t.numel(), decay,
+          stream_ptr())
+
+
+def health(x, stats):
+    _call("nrse_health", ptr(x), dtype_code(x), x.numel(), ptr(stats), stream_ptr())
+
+
+def snr_mix(clean, noise, noise_len, snr_db, clean_out, noisy_out, status, kscale, do_normalize=True):
+    B, L = clean.shape
+    _call("nrse_snr_mix", ptr(clean), ptr(noise), ptr(noise_len), noise.stride(0), ptr(snr_db), ptr(clean_out),
+          ptr(noisy_out), ptr(status), ptr(kscale), None, B, L, int(do_normalize), stream_ptr())

@@ -1,0 +1,97 @@
+"""Full BYOL step on the HIP path vs the CPU oracle (oracle/wavlm_byol.py, itself pinned to the
+reference by tests/test_oracle_golden.py), on the tiny WavLM arch.
+
+Tolerances (stated per the north star): fp32 parity mode uses exact-f32 MFMA / f32 kernels,
+so embeddings and loss agree to ~1e-5 rel-L2; bf16 mode (bf16 GEMM operands, f32 accumulate,
+f32 residual stream) is checked at 2e-2 rel-L2 on embeddings.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import wavlm_byol as O
+from nrse_amd import arch as A, params as PR, rng as R
+
+pytestmark = pytest.mark.gpu
+
+PROJ, PRED = 256, 512
+
+
+def rel(a, b):
+    a = torch.as_tensor(a).double().cpu(); b = torch.as_tensor(b).double().cpu()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def make(arch, dtype, B=4, L=16000, seed=1234):
+    from nrse_amd.engine import ByolEngine
+    layout = PR.byol_layout(arch, PROJ, PRED)
+    flat = PR.init_byol_flat(layout, seed)
+    eng = ByolEngine(arch, PROJ, PRED, compute_dtype=dtype, init_flat=flat)
+    st = O.OracleState(layout, flat)
+    g = torch.Generator().manual_seed(5)
+    clean = torch.randn(B, L, generator=g)
+    noisy = clean + 0.3 * torch.randn(B, L, generator=g)
+    return eng, st, clean, noisy
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-5), (torch.bfloat16, 2e-2)])
+def test_eval_forward_matches_oracle(nrse_device, dtype, tol):
+    arch = A.TINY.deterministic()
+    eng, st, clean, noisy = make(arch, dtype)
+    pred, tproj, loss = eng.eval_forward(clean.cuda(), noisy.cuda())
+    with torch.no_grad():
+        rp, rt, remb = O.forward(st, clean, noisy, train=False)
+        rl = O.byol_loss(rp, rt)
+    emb = eng.embed(clean.cuda())
+    assert rel(emb, remb) < tol
+    assert rel(pred, rp) < 5 * tol
+    assert rel(tproj, rt) < 5 * tol
+    assert abs(float(loss) - float(rl)) < 5 * tol
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-4), (torch.bfloat16, 5e-2)])
+def test_train_step_matches_oracle(nrse_device, dtype, tol):
+    arch = A.TINY.deterministic()
+    eng, st, clean, noisy = make(arch, dtype, B=8)
+    flat0 = st.online.clone()
+    lr, wd, ema = 1e-4, 1e-5, 0.99
+    eng.cfg.ema_decay = ema
+    eng.cfg.weight_decay = wd
+    loss = eng.train_step(clean.cuda(), noisy.cuda(), lr=lr, step_seed=3)
+    r = O.train_step(st, clean, noisy, lr=lr, weight_decay=wd, ema_decay=ema, step_seed=3)
+    assert abs(float(loss) - r["loss"]) < tol
+    g = eng.grad.cpu()
+    assert abs(eng.grad_norm() - r["grad_norm"]) / r["grad_norm"] < 10 * tol
+    worst = []
+    for gname, s in eng.layout.specs:
+        off, cnt, _ = eng.layout.offsets[PR.GROUP_PREFIX[gname] + s.name]
+        ref = r["grad"][off:off + cnt]
+        if ref.norm() < 1e-6 * r["grad_norm"]:
+            continue
+        worst.append((rel(g[off:off + cnt], ref), s.name))
+    worst.sort(reverse=True)
+    assert worst[0][0] < 20 * tol, worst[:5]
+    # AdamW + EMA: parameter deltas in units of lr. The first Adam step is ~lr*sign(g), so
+    # entries with near-zero gradients flip sign under bf16 rounding of the operands.
+    d = (eng.online.cpu() - flat0)
+    dr = (st.online - flat0)
+    assert (torch.abs(d - dr) > 0.05 * lr).float().mean() < (0.002 if dtype == torch.float32 else 0.15)
+    dt = eng.target.cpu() - flat0[:eng.layout.ema_numel]
+    drt = st.target - flat0[:eng.layout.ema_numel]
+    assert float(torch.abs(dt - drt).max()) < 0.05 * lr
+
+
+def test_stochastic_step_matches_oracle_with_same_masks(nrse_device):
+    """Dropout / attention dropout / LayerDrop / SpecAugment on: the oracle replays the same
+    counter-hash masks and the engine's host-side LayerDrop + span decisions."""
+    arch = A.TINY
+    eng, st, clean, noisy = make(arch, torch.float32, B=8)
+    lr = 1e-4
+    eng.cfg.ema_decay = 0.99
+    B, T = clean.shape[0], arch.frames(clean.shape[1])
+    skips, masks = eng.stochastic_inputs(11, B, T, True)
+    loss = eng.train_step(clean.cuda(), noisy.cuda(), lr=lr, step_seed=11)
+    r = O.train_step(st, clean, noisy, lr=lr, weight_decay=eng.cfg.weight_decay, ema_decay=0.99, step_seed=11,
+                     layer_skip=skips, mask_time=masks)
+    assert abs(float(loss) - r["loss"]) < 1e-4
+    assert abs(eng.grad_norm() - r["grad_norm"]) / r["grad_norm"] < 1e-3
