@@ -1,0 +1,200 @@
+"""bench.py — BYOL utterance-pairs/sec for WavLM-Large, 8 s @ 16 kHz, batch 32 per GPU
+(BASELINE.json metric), on N MI355X (one process per GPU, RCCL over xGMI).
+
+A step = fused on-GPU SNR mix of 32 synthetic (clean, noise) pairs resident in HBM ->
+BYOLSpeechModel forward (online on clean, target on noisy) -> BYOL loss -> backward ->
+gradient all-reduce (N > 1) -> clip + AdamW -> target EMA, i.e. the train_one_epoch body
+(train_byol.py:47-77) with the dataset mixing of src/data/augment.py moved on device.
+Synthetic data, random-init WavLM-Large weights (pretrained weights are unavailable offline).
+
+Usage: python bench.py [--gpus N --steps K --warmup W]; N > 1 under torch.distributed.run.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "noise-robust-speech-embedding_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
+BF16_DENSE_PEAK_TFS = 2500.0   # dense bf16 MFMA (no sparsity)
+F32_MFMA_PEAK_TFS = 157.3
+SNR_RANGE = [2, 5, 10, 15, 20]  # config/default_wavlm-large_byol.yaml:28
+
+
+def flops_per_pair(arch, L, executed):
+    """Algorithmic FLOPs per BYOL pair (SURVEY §8d model): online fwd + 2x bwd + target fwd,
+    conv0 input-grad excluded; `executed` = transformer layers run (online, target)."""
+    conv = 0.0
+    T = L
+    cin = 1
+    for k, s, c in zip(arch.conv_kernel, arch.conv_stride, arch.conv_dim):
+        T = (T - k) // s + 1
+        conv += 2.0 * T * c * cin * k
+        cin = c
+    H, Fd = arch.hidden, arch.ffn
+    proj = 2.0 * T * cin * H
+    pos = 2.0 * T * H * (H // arch.pos_groups) * arch.pos_kernel
+    layer = 2.0 * T * H * 3 * H + 2.0 * T * H * H + 2 * 2.0 * T * T * H + 2 * 2.0 * T * H * Fd
+    enc_fixed = conv + proj + pos
+    online = enc_fixed + executed[0] * layer
+    target = enc_fixed + executed[1] * layer
+    return 3.0 * online + target, dict(conv=conv, proj=proj, pos=pos, layer=layer, T=T)
+
+
+def cpu_baseline(arch_large, seconds_hint=20.0):
+    """Oracle (fp32 PyTorch-eager CPU restatement, oracle/wavlm_byol.py) training step on the
+    host cores: bounded sample of the same workload (B=2 pairs of 8 s, one timed step after one
+    warm-up step). Reported baseline only."""
+    from oracle import wavlm_byol as O
+    from nrse_amd import params as PR
+    # the GPU box's CPU share is 16 cores per GPU (os.cpu_count() reports the whole machine);
+    # more threads oversubscribe and run slower
+    torch.set_num_threads(max(1, min(os.cpu_count() or 1, 16)))
+    layout = PR.byol_layout(arch_large, 1024, 2048)
+    flat = PR.init_byol_flat(layout, 1234)
+    st = O.OracleState(layout, flat)
+    g = torch.Generator().manual_seed(0)
+    B, L = 2, 128000
+    clean = torch.randn(B, L, generator=g) * 0.1
+    noisy = clean + 0.05 * torch.randn(B, L, generator=g)
+    O.train_step(st, clean, noisy, lr=1e-5, weight_decay=1e-5, ema_decay=0.997, step_seed=0)
+    t0 = time.perf_counter()
+    O.train_step(st, clean, noisy, lr=1e-5, weight_decay=1e-5, ema_decay=0.997, step_seed=1)
+    dt = time.perf_counter() - t0
+    return {"value": B / dt, "unit": "pairs/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"oracle fp32 CPU train step, WavLM-Large, B={B} x 8 s, 1 warm-up + 1 timed step "
+                      f"({dt:.1f} s/step), cpu={platform.processor() or platform.machine()}, "
+                      f"os.cpu_count()={os.cpu_count()}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--seconds", type=float, default=8.0)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--detail", default=None, help="write per-shape GEMM timings here (json)")
+    args = ap.parse_args()
+
+    from nrse_amd import arch as A, ddp, kernels as K
+    from nrse_amd.engine import ByolEngine, StepConfig
+
+    rank, world, local = ddp.init_from_env()
+    if world != args.gpus and not (world == 1 and args.gpus == 1):
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    arch = A.LARGE
+    B = args.batch
+    L = int(args.seconds * 16000)
+    cdt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    eng = ByolEngine(arch, 1024, 2048, device=dev, compute_dtype=cdt, seed=1234,
+                     step_cfg=StepConfig(ema_decay=0.997))
+    allreduce = ddp.GradAllReduce() if world > 1 else None
+
+    # synthetic pairs resident in HBM: clean ~ N(0, 0.1^2), noise ~ N(0, 1), SNR from the YAML
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1234 + 1000 * rank)
+    clean_raw = torch.randn(B, L, device=dev, generator=gen) * 0.1
+    noise_raw = torch.randn(B, L, device=dev, generator=gen)
+    noise_len = torch.full((B,), L, device=dev, dtype=torch.int32)
+    snr = torch.tensor([SNR_RANGE[(i + rank) % len(SNR_RANGE)] for i in range(B)], device=dev, dtype=torch.float32)
+    clean_iv = torch.empty(B, L, device=dev)
+    noisy_iv = torch.empty(B, L, device=dev)
+    status = torch.empty(B, device=dev, dtype=torch.int32)
+    kscale = torch.empty(B, device=dev)
+    total_steps = 1_000_000
+
+    def lr_at(step):  # CosineAnnealingLR(T_max) stepped per iteration (train_byol.py:149-150)
+        return 0.5 * 1e-5 * (1 + math.cos(math.pi * step / total_steps))
+
+    def step(i):
+        K.snr_mix(clean_raw, noise_raw, noise_len, snr, clean_iv, noisy_iv, status, kscale, True)
+        return eng.train_step(clean_iv, noisy_iv, lr=lr_at(i), step_seed=i, rank=rank, allreduce=allreduce,
+                              world_size=world)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    executed = [0, 0]
+    probe = []
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    K.set_gemm_probe(probe)
+    for i in range(args.steps):
+        step(args.warmup + i)
+        executed[0] += eng.executed_layers[0]
+        executed[1] += eng.executed_layers[1]
+    K.set_gemm_probe(None)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], device=dev)
+        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+        dt = float(tt)
+    loss = float(eng.loss_buf)
+    st_ok = int((status == 0).sum())
+    # live roofline of the dominant kernel family (nrse_gemm, MFMA-bound)
+    gflops = sum(f for f, _, _, _ in probe)
+    gms = sum(e0.elapsed_time(e1) for _, e0, e1, _ in probe)
+    n_launch = len(probe)
+    achieved_tfs = gflops / (gms * 1e-3) / 1e12 if gms > 0 else 0.0
+    if args.detail and rank == 0:
+        per = {}
+        for f, e0, e1, shp in probe:
+            k = str(shp)
+            d = per.setdefault(k, [0.0, 0.0, 0])
+            d[0] += f; d[1] += e0.elapsed_time(e1); d[2] += 1
+        with open(args.detail, "w") as fh:
+            json.dump({k: {"tflops": v[0] / (v[1] * 1e-3) / 1e12, "ms_total": v[1], "launches": v[2]}
+                       for k, v in sorted(per.items(), key=lambda kv: -kv[1][1])}, fh, indent=1)
+    avg_exec = (executed[0] / args.steps, executed[1] / args.steps)
+    fpp, _ = flops_per_pair(arch, L, avg_exec)
+    pairs = B * world * args.steps
+    value = pairs / dt
+    result = {
+        "metric": "BYOL utterance-pairs/sec, WavLM-large, 8s@16kHz, batch=32 per GPU",
+        "value": round(value, 3), "unit": "pairs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 2), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (N(0,0.1^2) speech, N(0,1) noise, on-GPU SNR "
+                                                         "mix), random-init WavLM-Large weights",
+        "config": {"workload": "configs[1]: WavLM-large BYOL train step, synthetic 8s@16kHz clean/noisy pairs, "
+                               "batch=32 per GPU", "global_batch": B * world, "seq_len": L, "frames": arch.frames(L),
+                   "parallelism": f"dp{world}", "layerdrop_executed_layers": avg_exec},
+        "roofline": {"bound": "mfma", "kernel": "nrse_gemm (all launches in the timed region)",
+                     "achieved": round(achieved_tfs, 1), "peak": BF16_DENSE_PEAK_TFS if cdt == torch.bfloat16 else
+                     F32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                     "frac": round(achieved_tfs / (BF16_DENSE_PEAK_TFS if cdt == torch.bfloat16 else F32_MFMA_PEAK_TFS),
+                                   4),
+                     "traffic": None, "avg_launch_ms": round(gms / max(n_launch, 1), 4), "launches": n_launch,
+                     "gemm_share_of_step": round(gms / (dt * 1e3), 3)},
+        "step_tflops": round(fpp * value / world / 1e12, 1),
+        "loss_last": round(loss, 5), "snr_mix_ok": st_ok,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(A.LARGE)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

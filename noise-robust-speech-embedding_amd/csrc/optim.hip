@@ -29,7 +29,9 @@ __global__ __launch_bounds__(256) void adamw_kernel(const nrse_adamw_params p) {
   const double ss = p.sumsq ? *p.sumsq : 0.0;
   float coef = 1.f;
   if (p.sumsq) {
-    const float tn = (float)sqrt(ss);
+    // sumsq is over the (possibly summed-over-ranks) gradient; the clipped gradient is
+    // grad_scale * g (the rank average), whose norm is grad_scale * sqrt(sumsq).
+    const float tn = (float)sqrt(ss) * p.grad_scale;
     coef = fminf(1.f, p.max_norm / (tn + 1e-6f));
   }
   coef *= p.grad_scale;

@@ -600,9 +600,9 @@ class ByolEngine:
         ne = self.layout.ema_numel
         K.ema(self.target, self.online[:ne], self.target_sh, c.ema_decay)
 
-    def grad_norm(self) -> float:
+    def grad_norm(self, world_size: int = 1) -> float:
         """Pre-clip global gradient norm of the last step (host sync)."""
-        return float(self.sumsq_buf.sqrt())
+        return float(self.sumsq_buf.sqrt()) / world_size
 
     def train_step(self, clean: torch.Tensor, noisy: torch.Tensor, *, lr: float, step_seed: int, rank: int = 0,
                    allreduce=None, world_size: int = 1) -> torch.Tensor:
@@ -619,9 +619,9 @@ class ByolEngine:
         K.byol_loss(pred, tproj, self.loss_buf, dpred, self.loss_stats)
         self.grad.zero_()
         self.backward(dpred, ctx)
-        if allreduce is not None:
+        if allreduce is not None and world_size > 1:
             allreduce(self.grad)
-        self.optimizer_step(lr, grad_scale=1.0)
+        self.optimizer_step(lr, grad_scale=1.0 / world_size)
         return self.loss_buf
 
     def eval_forward(self, clean, noisy):

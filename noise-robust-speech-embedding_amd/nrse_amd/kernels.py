@@ -98,7 +98,25 @@ def gemm(A: Operand, B: Operand, C: torch.Tensor, M: int, N: int, K: int, *, ldc
     p.dropout_p = dropout_p
     p.seed = seed & 0xFFFFFFFF
     p.colsum = ptr(colsum)
+    probe = _GEMM_PROBE
+    if probe is not None:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
     _lib.check(_lib.lib().nrse_gemm(ctypes.byref(p), stream_ptr()), "nrse_gemm")
+    if probe is not None:
+        e1.record()
+        probe.append((2.0 * M * N * K * nseg * splits * batch, e0, e1, (M, N, K * nseg * splits, batch)))
+
+
+# When set to a list, every nrse_gemm launch appends (algorithmic FLOPs, start event, end event,
+# shape) recorded on the launch stream: bench.py's live roofline measurement.
+_GEMM_PROBE = None
+
+
+def set_gemm_probe(lst):
+    global _GEMM_PROBE
+    _GEMM_PROBE = lst
 
 
 # ----------------------------------------------------------------------------- linear helpers
