@@ -165,10 +165,12 @@ int nrse_ln_mean_fwd(const float* h, const float* gamma, const float* beta, floa
  * Gated relative-position attention, WavLMAttention ([TF]modeling_wavlm.py:147-271) with
  * F.multi_head_attention_forward / SDPA ([TORCH]functional.py:6206, 6629).
  * Layouts: qkv [B*T, 3*Hd] rows = (q | k | v), head h at columns h*64..h*64+63 (head_dim 64);
- * ctx [B*T, Hd]; gate, lse, delta [B, H, T] f32; bias [H, T, T] f32 (layer-0 table, reused by
- * every layer as in [TF]modeling_wavlm.py:505); bucket [2T-1] int32 = bucket(j - i) at j-i+T-1.
+ * ctx [B*T, Hd]; gate, lse, delta [B, H, T] f32; bias [H, T, Tb] f32 with Tb = nrse_bias_ld(T)
+ * (rows padded to a multiple of 64 with zeros; layer-0 table, reused by every layer as in
+ * [TF]modeling_wavlm.py:505); bucket [2T-1] int32 = bucket(j - i) at j-i+T-1.
  * Dropout on the attention probabilities: keep(i) = hash(seed, ((b*H+h)*T+i)*T+j).
  * ------------------------------------------------------------------------------------------ */
+int nrse_bias_ld(int T);
 int nrse_rel_bias_fwd(const float* E, const int* bucket, float* bias, int H, int T, int nb, void* stream);
 /* dE[bucket[d], h] += diag[h, d] (compute_bias backward). */
 int nrse_rel_bias_bwd(const float* diag, const int* bucket, float* dE, int H, int T, void* stream);

@@ -12,13 +12,16 @@ constexpr int HD = 64;  // head_dim (WavLM base/large)
 template <typename T> NRSE_DEV float ld(const void* p, long long i) { return to_f<T>(((const T*)p)[i]); }
 template <typename T> NRSE_DEV void st(void* p, long long i, float v) { ((T*)p)[i] = from_f<T>(v); }
 
+NRSE_DEV int bias_ld_dev(int T) { return (T + 63) & ~63; }
+
 __global__ void rel_bias_kernel(const float* __restrict__ E, const int* __restrict__ bucket, float* __restrict__ bias,
                                 int H, int T) {
-  const long long n = (long long)T * T;
+  const int Tb = bias_ld_dev(T);
+  const long long n = (long long)T * Tb;
   const int h = blockIdx.y;
   for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
-    const int i = (int)(e / T), j = (int)(e % T);
-    bias[(long long)h * n + e] = E[bucket[j - i + T - 1] * H + h];
+    const int i = (int)(e / Tb), j = (int)(e % Tb);
+    bias[(long long)h * n + e] = j < T ? E[bucket[j - i + T - 1] * H + h] : 0.f;
   }
 }
 
@@ -144,7 +147,7 @@ __global__ __launch_bounds__(64) void attn_fwd_f32_kernel(const nrse_attn_fwd_pa
     o[d] = 0.f;
   }
   const float g = valid ? p.gate[((long long)b * H + h) * Tn + i] : 0.f;
-  const float* brow = p.bias + ((long long)h * Tn + (valid ? i : 0)) * Tn;
+  const float* brow = p.bias + ((long long)h * Tn + (valid ? i : 0)) * bias_ld_dev(Tn);
   const uint32_t key = site_key(p.seed);
   const uint32_t thr = dropout_threshold(p.dropout_p);
   const float dsc = p.dropout_p > 0.f ? 1.f / (1.f - p.dropout_p) : 1.f;
@@ -261,7 +264,7 @@ __global__ __launch_bounds__(64) void attn_bwd_kv_f32_kernel(const nrse_attn_bwd
 #pragma unroll
         for (int d = 0; d < HD; ++d) { s += Qs[ii][d] * k[d]; dpd += Os[ii][d] * v[d]; }
         const float gi = rowc[2][ii];
-        const float bij = p.bias[((long long)h * Tn + i) * Tn + j];
+        const float bij = p.bias[((long long)h * Tn + i) * bias_ld_dev(Tn) + j];
         s += gi * bij;
         const float pr = __expf(s - rowc[0][ii]);
         float pd = pr, dp = dpd;
@@ -315,7 +318,7 @@ __global__ __launch_bounds__(64) void attn_bwd_q_f32_kernel(const nrse_attn_bwd_
   const float lse = valid ? p.lse[ri] : 0.f;
   const float delta = valid ? p.delta[ri] : 0.f;
   const float g = valid ? p.gate[ri] : 0.f;
-  const float* brow = p.bias + ((long long)h * Tn + (valid ? i : 0)) * Tn;
+  const float* brow = p.bias + ((long long)h * Tn + (valid ? i : 0)) * bias_ld_dev(Tn);
   const uint32_t key = site_key(p.seed);
   const uint32_t thr = dropout_threshold(p.dropout_p);
   const float dsc = p.dropout_p > 0.f ? 1.f / (1.f - p.dropout_p) : 1.f;
@@ -359,9 +362,11 @@ __global__ __launch_bounds__(64) void attn_bwd_q_f32_kernel(const nrse_attn_bwd_
 
 }  // namespace
 
+extern "C" int nrse_bias_ld(int T) { return (T + 63) & ~63; }
+
 extern "C" int nrse_rel_bias_fwd(const float* E, const int* bucket, float* bias, int H, int T, int nb, void* stream) {
   NRSE_REQUIRE(E && bucket && bias && H > 0 && T > 0 && nb > 0, "nrse_rel_bias_fwd: bad args");
-  long long n = (long long)T * T;
+  long long n = (long long)T * ((T + 63) & ~63);
   int blocks = (int)((n + 255) / 256);
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(rel_bias_kernel, dim3(blocks, H), dim3(256), 0, (hipStream_t)stream, E, bucket, bias, H, T);

@@ -1,7 +1,421 @@
-// MFMA flash-attention kernels for the gated relative-position attention (bf16).
-// Placeholder dispatch until the MFMA kernels land: the exact-f32 kernels of attention.hip run.
+// MFMA flash attention for the gated relative-position attention of WavLM (bf16 operands, f32
+// softmax/accumulation), head_dim 64:
+//   scores = (q . k) / 8 + gate[b,h,i] * bias[h,i,j]   ([TF]modeling_wavlm.py:164-184)
+//   P = softmax_j(scores), dropout(P), O = P V         ([TORCH]functional.py:6629 SDPA)
+// Three kernels, all 256 threads = 4 waves, one wave = 16 rows, 64-row tiles staged in LDS:
+//   fwd   : grid (q-blocks, H, B); S^T = K Q^T so the softmax row (one query) is lane-local
+//           (lane = query, 16 keys per lane per 64-key tile); online softmax; P feeds P.V
+//           straight from registers (permuted k order) with V read by ds_read_b64_tr_b16.
+//   bwd_kv: grid (k-blocks, H, B); S = Q K^T (lane = key); dV += Pd^T dO, dK += dS^T Q with the
+//           accumulator tiles used as MFMA A operands; sum_b gate*dS accumulated per diagonal
+//           j-i in LDS (rel_attn_embed gradient) then one atomic per diagonal per workgroup.
+//   bwd_q : grid (q-blocks, H, B); dQ += dS K (K by transposed LDS read), dgate = sum_j dS*bias.
+// LDS tiles are [64 rows][64 bf16] (128-byte rows) with the 16-byte chunk XOR-swizzled by
+// ((row>>1)&3)<<1 so both ds_read_b128 row reads and ds_read_b64_tr_b16 column reads of one
+// image stay (nearly) conflict-free.
 #include "common.h"
 
-int nrse_attn_use_mfma(int dtype, int head_dim) { return 0; }
-int nrse_attn_fwd_mfma(const nrse_attn_fwd_params* p, hipStream_t st) { return NRSE_ERR_UNSUPPORTED; }
-int nrse_attn_bwd_mfma(const nrse_attn_bwd_params* p, hipStream_t st) { return NRSE_ERR_UNSUPPORTED; }
+namespace {
+
+constexpr int D = 64;
+constexpr int TILE_B = 64 * 128;  // bytes per 64x64 bf16 tile
+typedef short short8v __attribute__((ext_vector_type(8)));
+
+NRSE_DEV int loff(int row, int chunk) { return row * 128 + ((chunk ^ (((row >> 1) & 3) << 1)) << 4); }
+
+// 16-byte row fragment (MFMA A/B operand "row" layout): row, 8 contiguous d starting at 8*chunk
+NRSE_DEV bf16x8 rd_row(const char* t, int row, int chunk) {
+  return *reinterpret_cast<const bf16x8*>(t + loff(row, chunk));
+}
+
+// transposed fragment: lane (group g, i=l&15) gets rows r0+4g.. (elements 0..3) and
+// r1+4g.. (elements 4..7) of column c0 + i
+NRSE_DEV bf16x8 rd_tr(const char* t, int r0, int r1, int c0, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const int q = i >> 2, p = i & 3;
+  const int col = c0 + 4 * p;
+  const int chunk = col >> 3, half = (col >> 2) & 1;
+  short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) short4v*)(t + loff(r0 + 4 * g + q, chunk) + half * 8));
+  short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) short4v*)(t + loff(r1 + 4 * g + q, chunk) + half * 8));
+  short8v v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+NRSE_DEV bf16x8 pack8(const float* a, const float* b) {
+  bf16x8 v;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { v[j] = (__bf16)a[j]; v[4 + j] = (__bf16)b[j]; }
+  return v;
+}
+
+// Stage a 64-row x 64-d bf16 tile (rows row0.., column offset col_off in a row of ld elements)
+// with 256 threads: each thread two 16-byte chunks.
+NRSE_DEV void stage_tile(char* t, const bf16_t* base, long long ld, int row0, int nrows, int tid) {
+  const int row = tid >> 2;
+  const int c0 = (tid & 3) * 2;
+  uint4 a = make_uint4(0, 0, 0, 0), b = make_uint4(0, 0, 0, 0);
+  if (row0 + row < nrows) {
+    const bf16_t* src = base + (long long)(row0 + row) * ld + c0 * 8;
+    a = *reinterpret_cast<const uint4*>(src);
+    b = *reinterpret_cast<const uint4*>(src + 8);
+  }
+  *reinterpret_cast<uint4*>(t + loff(row, c0)) = a;
+  *reinterpret_cast<uint4*>(t + loff(row, c0 + 1)) = b;
+}
+
+// ------------------------------------------------------------------------------ forward
+__global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_params p) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * TILE_B];
+  char* Kt = lds;
+  char* Vt = lds + TILE_B;
+  const int T = p.T, H = p.H, Hd = H * D;
+  const long long ld3 = 3LL * Hd;
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, i16 = lane & 15;
+  const int qi = blockIdx.x * 64 + w * 16 + i16;
+  const bool qv = qi < T;
+  const int Tb = (T + 63) & ~63;
+  const bf16_t* qkv = (const bf16_t*)p.qkv + (long long)b * T * ld3;
+  // Q fragments (B operand of S^T = K Q^T): Q[qi][8g + 32s .. +8]
+  bf16x8 qf[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    uint4 u = make_uint4(0, 0, 0, 0);
+    if (qv) u = *reinterpret_cast<const uint4*>(qkv + (long long)qi * ld3 + h * D + 8 * g + 32 * s);
+    qf[s] = __builtin_bit_cast(bf16x8, u);
+  }
+  const long long bh = (long long)b * H + h;
+  const float gi = qv ? p.gate[bh * T + qi] : 0.f;
+  const float* brow = p.bias + ((long long)h * T + (qv ? qi : T - 1)) * Tb;
+  const uint32_t key = site_key(p.seed);
+  const uint32_t thr = dropout_threshold(p.dropout_p);
+  const bool drop = p.dropout_p > 0.f;
+  const float dsc = drop ? 1.f / (1.f - p.dropout_p) : 1.f;
+  const uint32_t rowidx = (uint32_t)((bh * T + qi) * T);
+  float m = -INFINITY, lpart = 0.f;
+  f32x4 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int kb = 0; kb < T; kb += 64) {
+    __syncthreads();
+    stage_tile(Kt, qkv + Hd + h * D, ld3, kb, T, tid);
+    stage_tile(Vt, qkv + 2 * Hd + h * D, ld3, kb, T, tid);
+    __syncthreads();
+    f32x4 s[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rd_row(Kt, 16 * t + i16, 4 * ss + g), qf[ss], s[t], 0, 0, 0);
+    }
+    float v[4][4];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int k0 = kb + 16 * t + 4 * g;
+      const float4 bv = *reinterpret_cast<const float4*>(brow + k0);
+      const float bb[4] = {bv.x, bv.y, bv.z, bv.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float x = s[t][r] * p.scale + gi * bb[r];
+        v[t][r] = (k0 + r < T) ? x : -INFINITY;
+        mx = fmaxf(mx, v[t][r]);
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float alpha = __expf(m - mn);
+    m = mn;
+    float pd[4][4];
+    float ps = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float e = __expf(v[t][r] - mn);
+        ps += e;
+        const int kj = kb + 16 * t + 4 * g + r;
+        pd[t][r] = (drop && !dropout_keep(key, rowidx + kj, thr)) ? 0.f : e * dsc;
+      }
+    lpart = lpart * alpha + ps;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float ar = __shfl(alpha, 4 * g + r, 64);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) o[dt][r] *= ar;
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const bf16x8 pa = pack8(pd[2 * c], pd[2 * c + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, rd_tr(Vt, 32 * c, 32 * c + 16, 16 * dt, lane), o[dt], 0, 0, 0);
+    }
+  }
+  float l = lpart + __shfl_xor(lpart, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  bf16_t* ctx = (bf16_t*)p.ctx;
+  const int qrow0 = blockIdx.x * 64 + w * 16;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float lr = __shfl(l, 4 * g + r, 64);
+    const float inv = 1.f / lr;
+    const int q = qrow0 + 4 * g + r;
+    if (q < T) {
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) ctx[((long long)b * T + q) * Hd + h * D + 16 * dt + i16] = f2bf(o[dt][r] * inv);
+    }
+  }
+  if (g == 0 && qv) p.lse[bh * T + qi] = m + __logf(l);
+}
+
+// ------------------------------------------------------------------------------ bwd: dQ, dgate
+__global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_params p) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * TILE_B];
+  char* Kt = lds;
+  char* Vt = lds + TILE_B;
+  const int T = p.T, H = p.H, Hd = H * D;
+  const long long ld3 = 3LL * Hd;
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, i16 = lane & 15;
+  const int qi = blockIdx.x * 64 + w * 16 + i16;
+  const bool qv = qi < T;
+  const int Tb = (T + 63) & ~63;
+  const bf16_t* qkv = (const bf16_t*)p.qkv + (long long)b * T * ld3;
+  const bf16_t* dctx = (const bf16_t*)p.dctx + (long long)b * T * Hd;
+  bf16x8 qf[2], dof[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    uint4 u = make_uint4(0, 0, 0, 0), d = make_uint4(0, 0, 0, 0);
+    if (qv) {
+      u = *reinterpret_cast<const uint4*>(qkv + (long long)qi * ld3 + h * D + 8 * g + 32 * s);
+      d = *reinterpret_cast<const uint4*>(dctx + (long long)qi * Hd + h * D + 8 * g + 32 * s);
+    }
+    qf[s] = __builtin_bit_cast(bf16x8, u);
+    dof[s] = __builtin_bit_cast(bf16x8, d);
+  }
+  const long long bh = (long long)b * H + h;
+  const float gi = qv ? p.gate[bh * T + qi] : 0.f;
+  const float lse = qv ? p.lse[bh * T + qi] : 0.f;
+  const float delta = qv ? p.delta[bh * T + qi] : 0.f;
+  const float* brow = p.bias + ((long long)h * T + (qv ? qi : T - 1)) * Tb;
+  const uint32_t key = site_key(p.seed);
+  const uint32_t thr = dropout_threshold(p.dropout_p);
+  const bool drop = p.dropout_p > 0.f;
+  const float dsc = drop ? 1.f / (1.f - p.dropout_p) : 1.f;
+  const uint32_t rowidx = (uint32_t)((bh * T + qi) * T);
+  float dgate = 0.f;
+  f32x4 dq[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int kb = 0; kb < T; kb += 64) {
+    __syncthreads();
+    stage_tile(Kt, qkv + Hd + h * D, ld3, kb, T, tid);
+    stage_tile(Vt, qkv + 2 * Hd + h * D, ld3, kb, T, tid);
+    __syncthreads();
+    f32x4 s[4], dp[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dp[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rd_row(Kt, 16 * t + i16, 4 * ss + g), qf[ss], s[t], 0, 0, 0);
+        dp[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rd_row(Vt, 16 * t + i16, 4 * ss + g), dof[ss], dp[t], 0, 0, 0);
+      }
+    }
+    float ds[4][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int k0 = kb + 16 * t + 4 * g;
+      const float4 bv = *reinterpret_cast<const float4*>(brow + k0);
+      const float bb[4] = {bv.x, bv.y, bv.z, bv.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int kj = k0 + r;
+        float d = 0.f;
+        if (kj < T && qv) {
+          const float pr = __expf(s[t][r] * p.scale + gi * bb[r] - lse);
+          float dpv = dp[t][r];
+          if (drop) dpv = dropout_keep(key, rowidx + kj, thr) ? dpv * dsc : 0.f;
+          d = pr * (dpv - delta);
+        }
+        ds[t][r] = d;
+        dgate += d * bb[r];
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const bf16x8 da = pack8(ds[2 * c], ds[2 * c + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+        dq[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, rd_tr(Kt, 32 * c, 32 * c + 16, 16 * dt, lane), dq[dt], 0, 0, 0);
+    }
+  }
+  dgate += __shfl_xor(dgate, 16, 64);
+  dgate += __shfl_xor(dgate, 32, 64);
+  if (g == 0 && qv) p.dgate[bh * T + qi] = dgate;
+  bf16_t* dqkv = (bf16_t*)p.dqkv + (long long)b * T * ld3;
+  const int qrow0 = blockIdx.x * 64 + w * 16;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int q = qrow0 + 4 * g + r;
+    if (q < T) {
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) dqkv[(long long)q * ld3 + h * D + 16 * dt + i16] = f2bf(dq[dt][r] * p.scale);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------ bwd: dK, dV, diag
+__global__ __launch_bounds__(256) void attn_bwd_kv_kernel(const nrse_attn_bwd_params p) {
+  extern __shared__ __attribute__((aligned(16))) char dyn[];
+  char* Qt = dyn;
+  char* Ot = dyn + TILE_B;
+  float* rowc = reinterpret_cast<float*>(dyn + 2 * TILE_B);  // lse[64], delta[64], gate[64]
+  float* diag = rowc + 192;                                  // [T + 64]
+  const int T = p.T, H = p.H, Hd = H * D;
+  const long long ld3 = 3LL * Hd;
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, i16 = lane & 15;
+  const int kb0 = blockIdx.x * 64;
+  const int kj = kb0 + w * 16 + i16;
+  const bool kv = kj < T;
+  const int Tb = (T + 63) & ~63;
+  const bf16_t* qkv = (const bf16_t*)p.qkv + (long long)b * T * ld3;
+  const bf16_t* dctx = (const bf16_t*)p.dctx + (long long)b * T * Hd;
+  bf16x8 kf[2], vf[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    uint4 a = make_uint4(0, 0, 0, 0), c = make_uint4(0, 0, 0, 0);
+    if (kv) {
+      a = *reinterpret_cast<const uint4*>(qkv + (long long)kj * ld3 + Hd + h * D + 8 * g + 32 * s);
+      c = *reinterpret_cast<const uint4*>(qkv + (long long)kj * ld3 + 2 * Hd + h * D + 8 * g + 32 * s);
+    }
+    kf[s] = __builtin_bit_cast(bf16x8, a);
+    vf[s] = __builtin_bit_cast(bf16x8, c);
+  }
+  const int ndiag = T + 64;
+  for (int e = tid; e < ndiag; e += 256) diag[e] = 0.f;
+  const long long bh = (long long)b * H + h;
+  const uint32_t key = site_key(p.seed);
+  const uint32_t thr = dropout_threshold(p.dropout_p);
+  const bool drop = p.dropout_p > 0.f;
+  const float dsc = drop ? 1.f / (1.f - p.dropout_p) : 1.f;
+  const float* bcol = p.bias + (long long)h * T * Tb + kj;
+  f32x4 dk[4], dv[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) dk[dt] = dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // diag index of (query qi, key kj): (kj - qi) - (kb0 - T + 1)
+  const int dbase = kb0 - T + 1;
+  for (int qb = 0; qb < T; qb += 64) {
+    __syncthreads();
+    stage_tile(Qt, qkv + h * D, ld3, qb, T, tid);
+    stage_tile(Ot, dctx + h * D, Hd, qb, T, tid);
+    if (tid < 64) {
+      const int q = qb + tid;
+      const bool ok = q < T;
+      rowc[tid] = ok ? p.lse[bh * T + q] : 0.f;
+      rowc[64 + tid] = ok ? p.delta[bh * T + q] : 0.f;
+      rowc[128 + tid] = ok ? p.gate[bh * T + q] : 0.f;
+    }
+    __syncthreads();
+    f32x4 s[4], dp[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dp[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rd_row(Qt, 16 * t + i16, 4 * ss + g), kf[ss], s[t], 0, 0, 0);
+        dp[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rd_row(Ot, 16 * t + i16, 4 * ss + g), vf[ss], dp[t], 0, 0, 0);
+      }
+    }
+    // element (query qb + 16t + 4g + r, key kj)
+    float pd[4][4], ds[4][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ql = 16 * t + 4 * g + r;
+        const int q = qb + ql;
+        float pv = 0.f, d = 0.f;
+        if (q < T && kv) {
+          const float gq = rowc[128 + ql];
+          const float x = s[t][r] * p.scale + gq * bcol[(long long)q * Tb];
+          const float pr = __expf(x - rowc[ql]);
+          float dpv = dp[t][r];
+          pv = pr * dsc;
+          if (drop) {
+            const bool keep = dropout_keep(key, (uint32_t)((bh * T + q) * T + kj), thr);
+            if (!keep) { pv = 0.f; dpv = 0.f; }
+            else dpv *= dsc;
+          }
+          d = pr * (dpv - rowc[64 + ql]);
+          atomicAdd(&diag[kj - q - dbase], d * gq);
+        }
+        pd[t][r] = pv;
+        ds[t][r] = d;
+      }
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const bf16x8 pa = pack8(pd[2 * c], pd[2 * c + 1]);
+      const bf16x8 da = pack8(ds[2 * c], ds[2 * c + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        dv[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, rd_tr(Ot, 32 * c, 32 * c + 16, 16 * dt, lane), dv[dt], 0, 0, 0);
+        dk[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, rd_tr(Qt, 32 * c, 32 * c + 16, 16 * dt, lane), dk[dt], 0, 0, 0);
+      }
+    }
+  }
+  bf16_t* dqkv = (bf16_t*)p.dqkv + (long long)b * T * ld3;
+  const int krow0 = kb0 + w * 16;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int k = krow0 + 4 * g + r;
+    if (k < T) {
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        dqkv[(long long)k * ld3 + Hd + h * D + 16 * dt + i16] = f2bf(dk[dt][r] * p.scale);
+        dqkv[(long long)k * ld3 + 2 * Hd + h * D + 16 * dt + i16] = f2bf(dv[dt][r]);
+      }
+    }
+  }
+  __syncthreads();
+  if (p.diag) {
+    const int nd = 2 * T - 1;
+    for (int e = tid; e < ndiag; e += 256) {
+      const int dd = dbase + e + T - 1;  // index of d = kj - qi in [0, 2T-1)
+      if (dd >= 0 && dd < nd && diag[e] != 0.f) atomicAdd(p.diag + (long long)h * nd + dd, diag[e]);
+    }
+  }
+}
+
+}  // namespace
+
+int nrse_attn_use_mfma(int dtype, int head_dim) { return dtype == NRSE_BF16 && head_dim == D; }
+
+int nrse_attn_fwd_mfma(const nrse_attn_fwd_params* p, hipStream_t st) {
+  dim3 grid((p->T + 63) / 64, p->H, p->batch);
+  hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), 0, st, *p);
+  return nrse_check_launch("nrse_attn_fwd(mfma)");
+}
+
+int nrse_attn_bwd_mfma(const nrse_attn_bwd_params* p, hipStream_t st) {
+  dim3 grid((p->T + 63) / 64, p->H, p->batch);
+  const size_t lds_kv = 2 * TILE_B + (192 + p->T + 64) * sizeof(float);
+  if (lds_kv > 160 * 1024) {
+    nrse_set_error("nrse_attn_bwd: T=%d too long for the LDS diagonal accumulator", p->T);
+    return NRSE_ERR_UNSUPPORTED;
+  }
+  hipLaunchKernelGGL(attn_bwd_kv_kernel, grid, dim3(256), lds_kv, st, *p);
+  hipLaunchKernelGGL(attn_bwd_q_kernel, grid, dim3(256), 0, st, *p);
+  return nrse_check_launch("nrse_attn_bwd(mfma)");
+}

@@ -110,6 +110,7 @@ _SIGNATURES = {
     "nrse_layernorm_fwd": ([_P(LnFwdParams), c_vp], c_int),
     "nrse_layernorm_bwd": ([_P(LnBwdParams), c_vp], c_int),
     "nrse_ln_mean_fwd": ([c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_f, c_vp], c_int),
+    "nrse_bias_ld": ([c_int], c_int),
     "nrse_rel_bias_fwd": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp], c_int),
     "nrse_rel_bias_bwd": ([c_vp, c_vp, c_vp, c_int, c_int, c_vp], c_int),
     "nrse_gate_fwd": ([c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp], c_int),

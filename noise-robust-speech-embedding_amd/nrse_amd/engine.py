@@ -252,7 +252,7 @@ class ByolEngine:
                resid=h, ldr=H, r_z1=T * H, r_z2=cpg, dropout_p=php, seed=R.site_seed(fseed, R.SITE_POS))
         # -------- relative position bias table (layer 0 computes it, every layer reuses it)
         nh = a.heads
-        bias_tab = torch.empty(nh, T, T, device=dev, dtype=F32)
+        bias_tab = torch.empty(nh, T, K.bias_ld(T), device=dev, dtype=F32)
         K.rel_bias_fwd(Pm["encoder.layers.0.attention.rel_attn_embed.weight"], self.buckets(T), bias_tab, nh, T)
         if need_grad:
             tape.T = T

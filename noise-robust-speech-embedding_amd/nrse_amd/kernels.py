@@ -191,7 +191,13 @@ def ln_mean_fwd(h, gamma, beta, emb, mean, rstd, batch, T, C, eps):
 
 
 # ----------------------------------------------------------------------------- attention
+def bias_ld(T: int) -> int:
+    """Row stride of the [H, T, Tb] relative-position bias table (nrse_bias_ld)."""
+    return int(_lib.lib().nrse_bias_ld(T))
+
+
 def rel_bias_fwd(E, bucket, bias, H, T):
+    assert bias.shape[-1] == bias_ld(T)
     _call("nrse_rel_bias_fwd", ptr(E), ptr(bucket), ptr(bias), H, T, E.shape[0], stream_ptr())
 
 

@@ -1,0 +1,77 @@
+"""Gated rel-pos attention kernels (MFMA bf16 and exact-f32 paths) vs a float64 PyTorch
+reference of the same op ([TF]modeling_wavlm.py:164-184 + SDPA), forward and backward,
+including attention dropout with the counter-hash masks (oracle/masks.py)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import masks as MK
+
+pytestmark = pytest.mark.gpu
+
+
+def reference(qkv, gate, bias, B, T, H, p, seed):
+    """float64 autograd reference -> (ctx, lse, grads dict) for a random upstream dctx."""
+    D = 64
+    x = qkv.double().clone().requires_grad_(True)
+    g = gate.double().clone().requires_grad_(True)
+    bt = bias[:, :, :T].double().clone().requires_grad_(True)
+    q = x[:, :H * D].view(B, T, H, D).transpose(1, 2)
+    k = x[:, H * D:2 * H * D].view(B, T, H, D).transpose(1, 2)
+    v = x[:, 2 * H * D:].view(B, T, H, D).transpose(1, 2)
+    s = q @ k.transpose(-1, -2) / 8.0 + g[..., None] * bt[None]
+    lse = torch.logsumexp(s, -1)
+    pr = torch.softmax(s, -1)
+    if p > 0:
+        m = torch.from_numpy(MK.dropout_mask(seed, p, (B, H, T, T))).double().to(qkv.device)
+        pr = pr * m
+    ctx = (pr @ v).transpose(1, 2).reshape(B * T, H * D)
+    return x, g, bt, ctx, lse
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("T", [49, 130, 399])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_attention_fwd_bwd(nrse_device, dtype, T, p):
+    from nrse_amd import kernels as K
+    dev = nrse_device
+    B, H = 2, 4
+    torch.manual_seed(T)
+    qkv = (torch.randn(B * T, 3 * H * 64, device=dev) * 0.5).to(dtype)
+    gate = torch.rand(B, H, T, device=dev) + 1.0
+    Tb = K.bias_ld(T)
+    bias = torch.zeros(H, T, Tb, device=dev)
+    bias[:, :, :T] = torch.randn(H, T, T, device=dev)
+    seed = 77
+    ctx = torch.empty(B * T, H * 64, device=dev, dtype=dtype)
+    lse = torch.empty(B, H, T, device=dev)
+    K.attn_fwd(qkv, gate, bias, ctx, lse, B, T, H, p, seed)
+    x, g, bt, rctx, rlse = reference(qkv, gate, bias, B, T, H, p, seed)
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+    e = ((ctx.double() - rctx).norm() / rctx.norm()).item()
+    assert e < tol, e
+    assert ((lse.double() - rlse).abs().max()).item() < 10 * tol
+    # backward
+    dctx = (torch.randn(B * T, H * 64, device=dev) * 0.5).to(dtype)
+    rctx.backward(dctx.double())
+    dqkv = torch.empty_like(qkv)
+    dgate = torch.empty(B, H, T, device=dev)
+    diag = torch.zeros(H, 2 * T - 1, device=dev)
+    delta = torch.empty(B, H, T, device=dev)
+    K.attn_bwd(qkv, gate, bias, ctx, dctx, lse, delta, dqkv, dgate, diag, B, T, H, p, seed)
+    for name, got, ref in (("dq", dqkv[:, :H * 64], x.grad[:, :H * 64]),
+                           ("dk", dqkv[:, H * 64:2 * H * 64], x.grad[:, H * 64:2 * H * 64]),
+                           ("dv", dqkv[:, 2 * H * 64:], x.grad[:, 2 * H * 64:]),
+                           ("dgate", dgate, g.grad)):
+        e = ((got.double() - ref).norm() / ref.norm()).item()
+        assert e < 3 * tol, (name, e)
+    # diag: sum over b, i of gate * dS along j - i  == d(bias)[h, i, j] summed per diagonal
+    dbias = bt.grad  # [H, T, T]
+    ref_diag = torch.zeros(H, 2 * T - 1, device=dev, dtype=torch.float64)
+    ii = torch.arange(T, device=dev)[:, None]
+    jj = torch.arange(T, device=dev)[None, :]
+    idx = (jj - ii + T - 1).expand(T, T).reshape(-1)
+    for h in range(H):
+        ref_diag[h].index_add_(0, idx, dbias[h].reshape(-1))
+    e = ((diag.double() - ref_diag).norm() / ref_diag.norm()).item()
+    assert e < 3 * tol, ("diag", e)
