@@ -15,7 +15,11 @@
 //    grouped positional conv run through this kernel without im2col buffers.
 //  - Fused epilogues: bias, erf-GELU (+pre-activation store), GELU backward, dropout (counter
 //    hash), residual add, accumulate/atomic, column sums (bias gradients).
+#include <cstdlib>
 #include "common.h"
+
+bool nrse_gemm_dma_ok(const nrse_gemm_params* p);        // gemm_dma.hip
+int nrse_gemm_dma(const nrse_gemm_params* p, hipStream_t st);
 
 namespace {
 
@@ -375,5 +379,7 @@ extern "C" int nrse_gemm(const nrse_gemm_params* p, void* stream) {
   NRSE_REQUIRE(!(p->flags & NRSE_EPI_COLSUM) || p->colsum, "nrse_gemm: COLSUM without colsum");
   NRSE_REQUIRE((long long)nrse_cdiv(p->M, BM) <= 65535, "nrse_gemm: M too large for grid.y (%d)", p->M);
   hipStream_t st = (hipStream_t)stream;
+  static const bool force_v1 = getenv("NRSE_GEMM_V1") != nullptr;
+  if (!force_v1 && nrse_gemm_dma_ok(p)) return nrse_gemm_dma(p, st);
   return p->a.dtype == NRSE_BF16 ? launch_dt<bf16_t>(p, st) : launch_dt<float>(p, st);
 }

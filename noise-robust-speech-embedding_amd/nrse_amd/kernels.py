@@ -147,8 +147,13 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, *, splits:
         tiles = ((N + 127) // 128) * ((K + 127) // 128)
         splits = max(1, min(16, 512 // max(tiles, 1)))
     splits = max(1, min(splits, M // 64))
+    # equal token segments (the reduction dim is the outer index of both operands, so any
+    # segment length works): prefer a divisor of M to avoid a ragged tail launch
+    for s in range(splits, 0, -1):
+        if M % s == 0 and (splits <= 2 or s * 2 > splits):
+            splits = s
+            break
     seg = (M + splits - 1) // splits
-    seg = (seg + 7) // 8 * 8
     bulk = (M // seg) * seg
     if bulk:
         gemm(Operand(dy, False, dy.stride(0), seg_stride=seg * dy.stride(0)),
