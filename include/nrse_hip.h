@@ -179,10 +179,11 @@ int nrse_rel_bias_bwd(const float* diag, const int* bucket, float* dE, int H, in
  * ([TF]modeling_wavlm.py:164-176). x1 [B*T, Hd] (the LN1 output), W [8, 64], bias [8], c [H]. */
 int nrse_gate_fwd(const void* x1, int x_dtype, const float* W, const float* bvec, const float* c, float* gate,
                   int batch, int T, int H, void* stream);
-/* dx1 (f32, accumulated) += dgate path; dW [8,64], db [8], dc [H] accumulated (f32);
- * scratch: f32 [B*T*H*9] (caller-provided). */
+/* Gate backward, one wave per (row, head): dx1 (f32) += W^T dproj; writes dproj [B*T*H, 8]
+ * (x dtype; row n = row*H + h, so d(gru_rel_pos_linear.weight) = dproj^T x1.view(-1, 64) is a
+ * GEMM and d(bias) a column sum) and dcterm [B*T, H] f32 (d(gru_rel_pos_const) = its column sum). */
 int nrse_gate_bwd(const void* x1, int x_dtype, const float* W, const float* bvec, const float* c, const float* dgate,
-                  float* dx1, float* dW, float* db, float* dc, float* scratch, int batch, int T, int H, void* stream);
+                  float* dx1, void* dproj, float* dcterm, int batch, int T, int H, void* stream);
 
 typedef struct {
   const void* qkv; int dtype;     /* q/k/v (bf16 or f32) */

@@ -60,73 +60,41 @@ __global__ void gate_fwd_kernel(const void* __restrict__ x1, const float* __rest
   gate[(bi * H + h) * Tn + t] = a * (b * c[h] - 1.f) + 2.f;
 }
 
-// gate bwd stage 1: per (row, head): dproj[8] and dc-term into scratch; dx1 += W^T dproj
+// gate backward: one wave per (row, head), lane = head dim i. Recomputes the 8 projections
+// with wave reductions, then dx1[i] += sum_r dproj[r] W[r][i] (coalesced read-modify-write),
+// dproj [n][8] and dcterm [n] out for the GEMM / column-sum reductions done by the caller.
 template <typename T>
-__global__ void gate_bwd1_kernel(const void* __restrict__ x1, const float* __restrict__ W, const float* __restrict__ bv,
-                                 const float* __restrict__ c, const float* __restrict__ dgate, float* __restrict__ dx1,
-                                 float* __restrict__ scratch, int batch, int Tn, int H) {
-  __shared__ float w[8 * HD];
-  for (int i = threadIdx.x; i < 8 * HD; i += blockDim.x) w[i] = W[i];
-  __syncthreads();
-  const long long n = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void gate_bwd_kernel(const void* __restrict__ x1, const float* __restrict__ W,
+                                                       const float* __restrict__ bv, const float* __restrict__ c,
+                                                       const float* __restrict__ dgate, float* __restrict__ dx1,
+                                                       T* __restrict__ dproj, float* __restrict__ dcterm, int batch,
+                                                       int Tn, int H) {
+  const int lane = threadIdx.x & 63;
+  const long long n = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const long long total = (long long)batch * Tn * H;
   if (n >= total) return;
   const long long row = n / H;
   const int h = (int)(n % H);
-  float pr[8];
-#pragma unroll
-  for (int r = 0; r < 8; ++r) pr[r] = bv[r];
   const long long base = row * (long long)H * HD + h * HD;
-  for (int i = 0; i < HD; ++i) {
-    const float x = ld<T>(x1, base + i);
+  const float x = ld<T>(x1, base + lane);
+  float w[8];
 #pragma unroll
-    for (int r = 0; r < 8; ++r) pr[r] += x * w[r * HD + i];
-  }
-  const float a = 1.f / (1.f + __expf(-(pr[0] + pr[1] + pr[2] + pr[3])));
-  const float b = 1.f / (1.f + __expf(-(pr[4] + pr[5] + pr[6] + pr[7])));
+  for (int r = 0; r < 8; ++r) w[r] = W[r * HD + lane];
+  float sa = 0.f, sb = 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) { sa += x * w[r]; sb += x * w[4 + r]; }
+  sa = wave_sum(sa) + bv[0] + bv[1] + bv[2] + bv[3];
+  sb = wave_sum(sb) + bv[4] + bv[5] + bv[6] + bv[7];
+  const float a = 1.f / (1.f + __expf(-sa));
+  const float b = 1.f / (1.f + __expf(-sb));
   const long long bi = row / Tn, t = row % Tn;
   const float dg = dgate[(bi * H + h) * Tn + t];
   const float ch = c[h];
-  const float da = dg * (b * ch - 1.f);
-  const float db = dg * a * ch;
-  const float dpa = da * a * (1.f - a);
-  const float dpb = db * b * (1.f - b);
-  float* sc = scratch + n * 9;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) { sc[r] = dpa; sc[4 + r] = dpb; }
-  sc[8] = dg * a * b;
-  for (int i = 0; i < HD; ++i) {
-    float s = 0.f;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) s += dpa * w[r * HD + i] + dpb * w[(4 + r) * HD + i];
-    dx1[base + i] += s;
-  }
-}
-
-// gate bwd stage 2: dW[r][i] = sum_n dproj[n][r] x[n][i]; db[r] = sum dproj; dc[h] = sum dcterm
-template <typename T>
-__global__ __launch_bounds__(512) void gate_bwd2_kernel(const void* __restrict__ x1, const float* __restrict__ scratch,
-                                                        float* __restrict__ dW, float* __restrict__ db,
-                                                        float* __restrict__ dc, long long total, int H, int chunk) {
-  const int r = threadIdx.x >> 6, i = threadIdx.x & 63;
-  const long long n0 = (long long)blockIdx.x * chunk;
-  const long long n1 = min(total, n0 + chunk);
-  float acc = 0.f, accb = 0.f;
-  __shared__ float dch[64];
-  if (threadIdx.x < 64) dch[threadIdx.x] = 0.f;
-  __syncthreads();
-  for (long long n = n0; n < n1; ++n) {
-    const long long row = n / H;
-    const int h = (int)(n % H);
-    const float dp = scratch[n * 9 + r];
-    acc += dp * ld<T>(x1, row * (long long)H * HD + h * HD + i);
-    if (i == 0) accb += dp;
-    if (threadIdx.x == 0) dch[h] += scratch[n * 9 + 8];
-  }
-  atomicAdd(dW + r * HD + i, acc);
-  if (i == 0) atomicAdd(db + r, accb);
-  __syncthreads();
-  if (threadIdx.x < H) atomicAdd(dc + threadIdx.x, dch[threadIdx.x]);
+  const float dpa = dg * (b * ch - 1.f) * a * (1.f - a);
+  const float dpb = dg * a * ch * b * (1.f - b);
+  dx1[base + lane] += dpa * (w[0] + w[1] + w[2] + w[3]) + dpb * (w[4] + w[5] + w[6] + w[7]);
+  if (lane < 8) dproj[n * 8 + lane] = from_f<T>(lane < 4 ? dpa : dpb);
+  if (lane == 8) dcterm[n] = dg * a * b;
 }
 
 // ---------------------------------------------------------------- f32 attention (row per lane)
@@ -393,21 +361,19 @@ extern "C" int nrse_gate_fwd(const void* x1, int x_dtype, const float* W, const 
 }
 
 extern "C" int nrse_gate_bwd(const void* x1, int x_dtype, const float* W, const float* bvec, const float* c,
-                             const float* dgate, float* dx1, float* dW, float* db, float* dc, float* scratch, int batch,
-                             int T, int H, void* stream) {
-  NRSE_REQUIRE(x1 && W && bvec && c && dgate && dx1 && dW && db && dc && scratch && H <= 64, "nrse_gate_bwd: bad args");
+                             const float* dgate, float* dx1, void* dproj, float* dcterm, int batch, int T, int H,
+                             void* stream) {
+  NRSE_REQUIRE(x1 && W && bvec && c && dgate && dx1 && dproj && dcterm && batch > 0 && T > 0 && H > 0,
+               "nrse_gate_bwd: bad args");
   const long long total = (long long)batch * T * H;
   hipStream_t st = (hipStream_t)stream;
-  dim3 grid((unsigned)((total + 255) / 256));
-  const int chunk = 512;
-  dim3 grid2((unsigned)((total + chunk - 1) / chunk));
-  if (x_dtype == NRSE_BF16) {
-    hipLaunchKernelGGL(gate_bwd1_kernel<bf16_t>, grid, dim3(256), 0, st, x1, W, bvec, c, dgate, dx1, scratch, batch, T, H);
-    hipLaunchKernelGGL(gate_bwd2_kernel<bf16_t>, grid2, dim3(512), 0, st, x1, scratch, dW, db, dc, total, H, chunk);
-  } else {
-    hipLaunchKernelGGL(gate_bwd1_kernel<float>, grid, dim3(256), 0, st, x1, W, bvec, c, dgate, dx1, scratch, batch, T, H);
-    hipLaunchKernelGGL(gate_bwd2_kernel<float>, grid2, dim3(512), 0, st, x1, scratch, dW, db, dc, total, H, chunk);
-  }
+  dim3 grid((unsigned)((total + 3) / 4));
+  if (x_dtype == NRSE_BF16)
+    hipLaunchKernelGGL(gate_bwd_kernel<bf16_t>, grid, dim3(256), 0, st, x1, W, bvec, c, dgate, dx1, (bf16_t*)dproj,
+                       dcterm, batch, T, H);
+  else
+    hipLaunchKernelGGL(gate_bwd_kernel<float>, grid, dim3(256), 0, st, x1, W, bvec, c, dgate, dx1, (float*)dproj,
+                       dcterm, batch, T, H);
   return nrse_check_launch("nrse_gate_bwd");
 }
 
@@ -432,11 +398,11 @@ extern "C" int nrse_attn_bwd(const nrse_attn_bwd_params* p, void* stream) {
                p->batch > 0 && p->T > 0 && p->H > 0, "nrse_attn_bwd: bad args");
   if (p->head_dim != HD) { nrse_set_error("nrse_attn_bwd: head_dim %d != 64", p->head_dim); return NRSE_ERR_UNSUPPORTED; }
   hipStream_t st = (hipStream_t)stream;
+  if (nrse_attn_use_mfma(p->dtype, p->head_dim)) return nrse_attn_bwd_mfma(p, st);  // computes delta itself
   const long long total = (long long)p->batch * p->H * p->T;
   dim3 g1((unsigned)((total + 255) / 256));
   if (p->dtype == NRSE_BF16) hipLaunchKernelGGL(attn_delta_kernel<bf16_t>, g1, dim3(256), 0, st, *p);
   else hipLaunchKernelGGL(attn_delta_kernel<float>, g1, dim3(256), 0, st, *p);
-  if (nrse_attn_use_mfma(p->dtype, p->head_dim)) return nrse_attn_bwd_mfma(p, st);
   dim3 grid((p->T + 63) / 64, p->H, p->batch);
   if (p->dtype == NRSE_BF16) {
     hipLaunchKernelGGL(attn_bwd_kv_f32_kernel<bf16_t>, grid, dim3(64), 0, st, *p);

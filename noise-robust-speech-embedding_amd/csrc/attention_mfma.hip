@@ -190,20 +190,31 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
   const bf16_t* qkv = (const bf16_t*)p.qkv + (long long)b * T * ld3;
   const bf16_t* dctx = (const bf16_t*)p.dctx + (long long)b * T * Hd;
   bf16x8 qf[2], dof[2];
+  const bf16_t* octx = (const bf16_t*)p.ctx + (long long)b * T * Hd;
+  float dsum = 0.f;  // delta = rowsum(dO * O) for this lane's 16 of the 64 dims
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    uint4 u = make_uint4(0, 0, 0, 0), d = make_uint4(0, 0, 0, 0);
+    uint4 u = make_uint4(0, 0, 0, 0), d = make_uint4(0, 0, 0, 0), o = make_uint4(0, 0, 0, 0);
     if (qv) {
       u = *reinterpret_cast<const uint4*>(qkv + (long long)qi * ld3 + h * D + 8 * g + 32 * s);
       d = *reinterpret_cast<const uint4*>(dctx + (long long)qi * Hd + h * D + 8 * g + 32 * s);
+      o = *reinterpret_cast<const uint4*>(octx + (long long)qi * Hd + h * D + 8 * g + 32 * s);
     }
     qf[s] = __builtin_bit_cast(bf16x8, u);
     dof[s] = __builtin_bit_cast(bf16x8, d);
+    const unsigned dw[4] = {d.x, d.y, d.z, d.w}, ow[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      dsum += __uint_as_float(dw[e] << 16) * __uint_as_float(ow[e] << 16) +
+              __uint_as_float(dw[e] & 0xffff0000u) * __uint_as_float(ow[e] & 0xffff0000u);
   }
+  dsum += __shfl_xor(dsum, 16, 64);
+  dsum += __shfl_xor(dsum, 32, 64);
   const long long bh = (long long)b * H + h;
   const float gi = qv ? p.gate[bh * T + qi] : 0.f;
   const float lse = qv ? p.lse[bh * T + qi] : 0.f;
-  const float delta = qv ? p.delta[bh * T + qi] : 0.f;
+  const float delta = dsum;
+  if (g == 0 && qv) p.delta[bh * T + qi] = delta;  // consumed by attn_bwd_kv_kernel (launched after)
   const float* brow = p.bias + ((long long)h * T + (qv ? qi : T - 1)) * Tb;
   const uint32_t key = site_key(p.seed);
   const uint32_t thr = dropout_threshold(p.dropout_p);
@@ -415,7 +426,8 @@ int nrse_attn_bwd_mfma(const nrse_attn_bwd_params* p, hipStream_t st) {
     nrse_set_error("nrse_attn_bwd: T=%d too long for the LDS diagonal accumulator", p->T);
     return NRSE_ERR_UNSUPPORTED;
   }
-  hipLaunchKernelGGL(attn_bwd_kv_kernel, grid, dim3(256), lds_kv, st, *p);
+  // the dQ kernel also produces delta = rowsum(dO * O), which the dK/dV kernel reads
   hipLaunchKernelGGL(attn_bwd_q_kernel, grid, dim3(256), 0, st, *p);
+  hipLaunchKernelGGL(attn_bwd_kv_kernel, grid, dim3(256), lds_kv, st, *p);
   return nrse_check_launch("nrse_attn_bwd(mfma)");
 }

@@ -1,29 +1,54 @@
 // Conv feature-encoder front end (conv0 + LN + GELU, fused fwd and fused bwd/wgrad) and the
 // weight_norm of the grouped positional conv. Conv layers 1..6 and the pos-conv contraction run
-// as implicit GEMMs in gemm.hip.
+// as implicit GEMMs in gemm.hip / gemm_dma.hip.
 //   conv0         [TF]modeling_wavlm.py:712-720 (Conv1d(1, C, 10, 5, bias=False), LN, GELU)
 //   weight norm   [TF]modeling_wavlm.py:61-77 (parametrizations.weight_norm, dim=2)
+// conv0 has K = 10: vector-ALU work, HBM-bound on its [B*T0, C] output (the largest activation
+// of the step). One wave per output row; the [k][C] weight is held in LDS (read as float4 per
+// tap), lane owns 4*NQ channels.
 #include "common.h"
 
 namespace {
 
 constexpr int KMAX = 10;
 
-// One wave per output row (b, t); lane owns channels c = (q*64 + lane)*4 + e, q < NQ.
+NRSE_DEV long long uniform_ll(long long v) {
+  const int lo = __builtin_amdgcn_readfirstlane((int)(v & 0xffffffff));
+  const int hi = __builtin_amdgcn_readfirstlane((int)(v >> 32));
+  return ((long long)hi << 32) | (unsigned)lo;
+}
+
+// LDS weight image wT[j][c] (tap-major) so lane reads 4 consecutive channels per tap
+NRSE_DEV void load_wT(float* wT, const float* w, int C, int k) {
+  for (int e = threadIdx.x; e < C * KMAX; e += blockDim.x) {
+    const int j = e / C, c = e % C;
+    wT[e] = j < k ? w[c * k + j] : 0.f;
+  }
+}
+
+template <int NQ>
+NRSE_DEV void conv_row(const float* wT, int C, int lane, const float* xs, float (&y)[NQ][4]) {
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int c0 = (q * 64 + lane) * 4;
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) {
+      const float4 wv = *reinterpret_cast<const float4*>(wT + j * C + c0);
+      a[0] += wv.x * xs[j]; a[1] += wv.y * xs[j]; a[2] += wv.z * xs[j]; a[3] += wv.w * xs[j];
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) y[q][e] = a[e];
+  }
+}
+
 template <int NQ>
 __global__ __launch_bounds__(256) void conv0_fwd_kernel(const nrse_conv0_params p) {
+  __shared__ __attribute__((aligned(16))) float wT[KMAX * 512];
   const int lane = threadIdx.x & 63;
   const int C = p.C;
-  float w[NQ][4][KMAX];
-#pragma unroll
-  for (int q = 0; q < NQ; ++q)
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-#pragma unroll
-      for (int j = 0; j < KMAX; ++j) {
-        const int c = (q * 64 + lane) * 4 + e;
-        w[q][e][j] = j < p.k ? p.w[c * p.k + j] : 0.f;
-      }
+  load_wT(wT, p.w, C, p.k);
+  __syncthreads();
   float ga[NQ][4], be[NQ][4];
 #pragma unroll
   for (int q = 0; q < NQ; ++q)
@@ -35,7 +60,8 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(const nrse_conv0_params 
     }
   const long long rows = (long long)p.batch * p.T0;
   const long long nw = (long long)gridDim.x * 4;
-  for (long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += nw) {
+  for (long long r0 = (long long)blockIdx.x * 4 + (threadIdx.x >> 6); r0 < rows; r0 += nw) {
+    const long long row = uniform_ll(r0);
     const long long b = row / p.T0;
     const int t = (int)(row - b * p.T0);
     const float* x = p.wav + b * p.L + (long long)t * p.s;
@@ -43,17 +69,12 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(const nrse_conv0_params 
 #pragma unroll
     for (int j = 0; j < KMAX; ++j) xs[j] = j < p.k ? x[j] : 0.f;
     float y[NQ][4];
+    conv_row<NQ>(wT, C, lane, xs, y);
     float s = 0.f;
 #pragma unroll
     for (int q = 0; q < NQ; ++q)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float a = 0.f;
-#pragma unroll
-        for (int j = 0; j < KMAX; ++j) a += w[q][e][j] * xs[j];
-        y[q][e] = a;
-        s += a;
-      }
+      for (int e = 0; e < 4; ++e) s += y[q][e];
     const float mean = wave_sum(s) / C;
     float v = 0.f;
 #pragma unroll
@@ -96,11 +117,14 @@ NRSE_DEV void ld4(const void* p, int dt, long long i, float* o) {
 
 template <int NQ>
 __global__ __launch_bounds__(256) void conv0_bwd_kernel(const nrse_conv0_params p) {
+  __shared__ __attribute__((aligned(16))) float wT[KMAX * 512];
   __shared__ float red[4][NQ * 256];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const int C = p.C;
-  float w[NQ][4][KMAX], dw[NQ][4][KMAX];
+  load_wT(wT, p.w, C, p.k);
+  __syncthreads();
+  float dw[NQ][4][KMAX];
   float ga[NQ][4], be[NQ][4], dga[NQ][4], dbe[NQ][4];
 #pragma unroll
   for (int q = 0; q < NQ; ++q)
@@ -108,17 +132,16 @@ __global__ __launch_bounds__(256) void conv0_bwd_kernel(const nrse_conv0_params 
     for (int e = 0; e < 4; ++e) {
       const int c = (q * 64 + lane) * 4 + e;
 #pragma unroll
-      for (int j = 0; j < KMAX; ++j) {
-        w[q][e][j] = j < p.k ? p.w[c * p.k + j] : 0.f;
-        dw[q][e][j] = 0.f;
-      }
+      for (int j = 0; j < KMAX; ++j) dw[q][e][j] = 0.f;
       ga[q][e] = p.gamma[c];
       be[q][e] = p.beta[c];
       dga[q][e] = dbe[q][e] = 0.f;
     }
   const long long rows = (long long)p.batch * p.T0;
   const long long nw = (long long)gridDim.x * 4;
-  for (long long row = (long long)blockIdx.x * 4 + wv; row < rows; row += nw) {
+  const bool s2 = p.col_s == 2;
+  for (long long r0 = (long long)blockIdx.x * 4 + wv; r0 < rows; r0 += nw) {
+    const long long row = uniform_ll(r0);
     const long long b = row / p.T0;
     const int t = (int)(row - b * p.T0);
     const float* x = p.wav + b * p.L + (long long)t * p.s;
@@ -126,8 +149,10 @@ __global__ __launch_bounds__(256) void conv0_bwd_kernel(const nrse_conv0_params 
 #pragma unroll
     for (int j = 0; j < KMAX; ++j) xs[j] = j < p.k ? x[j] : 0.f;
     const float mean = p.mean[row], rstd = p.rstd[row];
+    float y[NQ][4];
+    conv_row<NQ>(wT, C, lane, xs, y);
     float xh[NQ][4], g[NQ][4];
-    float s1 = 0.f, s2 = 0.f;
+    float s1 = 0.f, s2v = 0.f;
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const int c0 = (q * 64 + lane) * 4;
@@ -138,8 +163,9 @@ __global__ __launch_bounds__(256) void conv0_bwd_kernel(const nrse_conv0_params 
         const long long kc = (long long)p.col_k * C;
         for (int j = 0; j < p.col_k; ++j) {
           const int d = t - j;
-          if (d < 0 || (d % p.col_s) != 0) continue;
-          const int tt = d / p.col_s;
+          if (d < 0) break;
+          if (s2 ? (d & 1) : (d % p.col_s)) continue;
+          const int tt = s2 ? (d >> 1) : d / p.col_s;
           if (tt >= p.col_tout) continue;
           float u[4];
           ld4(p.dy, p.dy_dtype, (b * p.col_tout + tt) * kc + (long long)j * C + c0, u);
@@ -149,25 +175,22 @@ __global__ __launch_bounds__(256) void conv0_bwd_kernel(const nrse_conv0_params 
       }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        float a = 0.f;
-#pragma unroll
-        for (int j = 0; j < KMAX; ++j) a += w[q][e][j] * xs[j];
-        xh[q][e] = (a - mean) * rstd;
+        xh[q][e] = (y[q][e] - mean) * rstd;
         const float gg = dy[e] * gelu_grad_f(xh[q][e] * ga[q][e] + be[q][e]);
         dga[q][e] += gg * xh[q][e];
         dbe[q][e] += gg;
         g[q][e] = gg * ga[q][e];
         s1 += g[q][e];
-        s2 += g[q][e] * xh[q][e];
+        s2v += g[q][e] * xh[q][e];
       }
     }
     s1 = wave_sum(s1) / C;
-    s2 = wave_sum(s2) / C;
+    s2v = wave_sum(s2v) / C;
 #pragma unroll
     for (int q = 0; q < NQ; ++q)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float dc = rstd * (g[q][e] - s1 - xh[q][e] * s2);
+        const float dc = rstd * (g[q][e] - s1 - xh[q][e] * s2v);
 #pragma unroll
         for (int j = 0; j < KMAX; ++j) dw[q][e][j] += dc * xs[j];
       }
@@ -280,7 +303,7 @@ extern "C" int nrse_conv0_fwd(const nrse_conv0_params* p, void* stream) {
   NRSE_REQUIRE(p->k > 0 && p->k <= KMAX && p->T0 == (p->L - p->k) / p->s + 1, "nrse_conv0_fwd: bad geometry");
   const long long rows = (long long)p->batch * p->T0;
   long long blocks = (rows + 3) / 4;
-  if (blocks > 2048) blocks = 2048;
+  if (blocks > 4096) blocks = 4096;
   hipStream_t st = (hipStream_t)stream;
   switch (p->C) {
     case 256: hipLaunchKernelGGL(conv0_fwd_kernel<1>, dim3(blocks), dim3(256), 0, st, *p); break;
@@ -297,7 +320,7 @@ extern "C" int nrse_conv0_bwd(const nrse_conv0_params* p, void* stream) {
   if (p->dy_mode == NRSE_DY_COL2IM) NRSE_REQUIRE(p->col_k > 0 && p->col_s > 0 && p->col_tout > 0, "nrse_conv0_bwd: col2im");
   const long long rows = (long long)p->batch * p->T0;
   long long blocks = (rows + 3) / 4;
-  if (blocks > 1024) blocks = 1024;
+  if (blocks > 2048) blocks = 2048;
   hipStream_t st = (hipStream_t)stream;
   switch (p->C) {
     case 256: hipLaunchKernelGGL(conv0_bwd_kernel<1>, dim3(blocks), dim3(256), 0, st, *p); break;

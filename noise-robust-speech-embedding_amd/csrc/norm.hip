@@ -271,8 +271,15 @@ extern "C" int nrse_layernorm_bwd(const nrse_ln_bwd_params* p, void* stream) {
                  "nrse_layernorm_bwd: bad col2im geometry");
   if (p->dy_mode == NRSE_DY_BCAST) NRSE_REQUIRE(p->bcast_t > 0, "nrse_layernorm_bwd: bad bcast_t");
   if (!c_ok(p->C)) { nrse_set_error("nrse_layernorm_bwd: C=%d not in {256,512,1024}", p->C); return NRSE_ERR_UNSUPPORTED; }
+  // grid-stride: enough waves to stream the rows, few enough blocks that the per-block
+  // dgamma/dbeta atomics (2*C per block) stay small next to the row traffic
   long long blocks = (p->rows + 3) / 4;
-  if (blocks > 4096) blocks = 4096;
+  long long cap = 8192;
+  if (p->dgamma) {
+    cap = p->rows / 256;
+    cap = cap < 512 ? 512 : (cap > 4096 ? 4096 : cap);
+  }
+  if (blocks > cap) blocks = cap;
   NRSE_DISPATCH_NK(ln_bwd_kernel, p->C, dim3((unsigned)blocks), (hipStream_t)stream, *p);
   return nrse_check_launch("nrse_layernorm_bwd");
 }

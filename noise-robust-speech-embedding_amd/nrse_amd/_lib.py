@@ -114,8 +114,7 @@ _SIGNATURES = {
     "nrse_rel_bias_fwd": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp], c_int),
     "nrse_rel_bias_bwd": ([c_vp, c_vp, c_vp, c_int, c_int, c_vp], c_int),
     "nrse_gate_fwd": ([c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp], c_int),
-    "nrse_gate_bwd": ([c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp],
-                      c_int),
+    "nrse_gate_bwd": ([c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp], c_int),
     "nrse_attn_fwd": ([_P(AttnFwdParams), c_vp], c_int),
     "nrse_attn_bwd": ([_P(AttnBwdParams), c_vp], c_int),
     "nrse_conv0_fwd": ([_P(Conv0Params), c_vp], c_int),

@@ -334,7 +334,6 @@ class ByolEngine:
                  dbeta=Gv["encoder.layer_norm.bias"], mode=_lib.DY_BCAST, bcast_t=T, dy_scale=1.0 / T, rows=BT)
         tape.final = None
         diag = torch.zeros(nh, 2 * T - 1, device=dev, dtype=F32)
-        gate_scratch = torch.empty(BT * nh * 9, device=dev, dtype=F32)
         delta = torch.empty(B, nh, T, device=dev, dtype=F32)
         for L_ in reversed(tape.layers):
             li = L_["li"]
@@ -377,7 +376,7 @@ class ByolEngine:
             del dqkv
             K.gate_bwd(L_["x1"], Pm[at + "gru_rel_pos_linear.weight"], Pm[at + "gru_rel_pos_linear.bias"],
                        Pm[at + "gru_rel_pos_const"], dgate, dx1, Gv[at + "gru_rel_pos_linear.weight"],
-                       Gv[at + "gru_rel_pos_linear.bias"], Gv[at + "gru_rel_pos_const"], gate_scratch, B, T, nh)
+                       Gv[at + "gru_rel_pos_linear.bias"], Gv[at + "gru_rel_pos_const"], B, T, nh)
             dhin = torch.empty(BT, H, device=dev, dtype=F32)
             K.ln_bwd(dx1, L_["h_in"], Pm[p + "layer_norm.weight"], L_["m1"], L_["r1"], dhin, resid=dhmid,
                      dgamma=Gv[p + "layer_norm.weight"], dbeta=Gv[p + "layer_norm.bias"])

@@ -146,7 +146,7 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, *, splits:
     if splits <= 0:
         tiles = ((N + 127) // 128) * ((K + 127) // 128)
         splits = max(1, min(16, 512 // max(tiles, 1)))
-    splits = max(1, min(splits, M // 64))
+    splits = max(1, min(splits, M // 64, 4096))
     # equal token segments (the reduction dim is the outer index of both operands, so any
     # segment length works): prefer a divisor of M to avoid a ragged tail launch
     for s in range(splits, 0, -1):
@@ -214,9 +214,16 @@ def gate_fwd(x1, W, b, c, gate, batch, T, H):
     _call("nrse_gate_fwd", ptr(x1), dtype_code(x1), ptr(W), ptr(b), ptr(c), ptr(gate), batch, T, H, stream_ptr())
 
 
-def gate_bwd(x1, W, b, c, dgate, dx1, dW, db, dc, scratch, batch, T, H):
-    _call("nrse_gate_bwd", ptr(x1), dtype_code(x1), ptr(W), ptr(b), ptr(c), ptr(dgate), ptr(dx1), ptr(dW), ptr(db),
-          ptr(dc), ptr(scratch), batch, T, H, stream_ptr())
+def gate_bwd(x1, W, b, c, dgate, dx1, dW, db, dc, batch, T, H):
+    """dx1 += gate-path gradient; dW/db/dc accumulated (dW via an MFMA GEMM over B*T*H rows)."""
+    n = batch * T * H
+    dproj = torch.empty(n, 8, device=x1.device, dtype=x1.dtype)
+    dcterm = torch.empty(batch * T, H, device=x1.device, dtype=torch.float32)
+    _call("nrse_gate_bwd", ptr(x1), dtype_code(x1), ptr(W), ptr(b), ptr(c), ptr(dgate), ptr(dx1), ptr(dproj),
+          ptr(dcterm), batch, T, H, stream_ptr())
+    linear_wgrad(dproj, x1.view(n, 64), dW, splits=256)
+    colsum(dproj, db)
+    colsum(dcterm, dc.view(-1))
 
 
 def attn_fwd(qkv, gate, bias, ctx, lse, batch, T, H, dropout_p=0.0, seed=0):
