@@ -19,6 +19,7 @@ namespace {
 
 constexpr int D = 64;
 constexpr int TILE_B = 64 * 128;  // bytes per 64x64 bf16 tile
+constexpr int BT_LD = 68;         // f32 bias tile row stride (dK/dV kernel)
 typedef short short8v __attribute__((ext_vector_type(8)));
 
 NRSE_DEV int loff(int row, int chunk) { return row * 128 + ((chunk ^ (((row >> 1) & 3) << 1)) << 4); }
@@ -290,7 +291,8 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(const nrse_attn_bwd_pa
   char* Qt = dyn;
   char* Ot = dyn + TILE_B;
   float* rowc = reinterpret_cast<float*>(dyn + 2 * TILE_B);  // lse[64], delta[64], gate[64]
-  float* diag = rowc + 192;                                  // [T + 64]
+  float* btile = rowc + 192;                                 // bias tile [64 q][BT_LD]
+  float* diag = btile + 64 * BT_LD;                          // [4 lane groups][T + 64]
   const int T = p.T, H = p.H, Hd = H * D;
   const long long ld3 = 3LL * Hd;
   const int b = blockIdx.z, h = blockIdx.y;
@@ -313,14 +315,18 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(const nrse_attn_bwd_pa
     kf[s] = __builtin_bit_cast(bf16x8, a);
     vf[s] = __builtin_bit_cast(bf16x8, c);
   }
+  // one diagonal accumulator per lane group g: the 16 lanes of a group hit distinct diagonals,
+  // so an LDS atomic wave instruction never serialises on one address
   const int ndiag = T + 64;
-  for (int e = tid; e < ndiag; e += 256) diag[e] = 0.f;
+  for (int e = tid; e < 4 * ndiag; e += 256) diag[e] = 0.f;
+  float* mydiag = diag + g * ndiag;
   const long long bh = (long long)b * H + h;
   const uint32_t key = site_key(p.seed);
   const uint32_t thr = dropout_threshold(p.dropout_p);
   const bool drop = p.dropout_p > 0.f;
   const float dsc = drop ? 1.f / (1.f - p.dropout_p) : 1.f;
-  const float* bcol = p.bias + (long long)h * T * Tb + kj;
+  const float* bsrc = p.bias + (long long)h * T * Tb + kb0;
+  const int kl = w * 16 + i16;  // key within the 64-key block
   f32x4 dk[4], dv[4];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) dk[dt] = dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -336,6 +342,14 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(const nrse_attn_bwd_pa
       rowc[tid] = ok ? p.lse[bh * T + q] : 0.f;
       rowc[64 + tid] = ok ? p.delta[bh * T + q] : 0.f;
       rowc[128 + tid] = ok ? p.gate[bh * T + q] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {  // bias[h, qb:qb+64, kb0:kb0+64] -> LDS (rows padded in the table)
+      const int e = tid + 256 * u;
+      const int row = e >> 4, c4 = (e & 15) * 4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (qb + row < T) v = *reinterpret_cast<const float4*>(bsrc + (long long)(qb + row) * Tb + c4);
+      *reinterpret_cast<float4*>(btile + row * BT_LD + c4) = v;
     }
     __syncthreads();
     f32x4 s[4], dp[4];
@@ -360,7 +374,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(const nrse_attn_bwd_pa
         float pv = 0.f, d = 0.f;
         if (q < T && kv) {
           const float gq = rowc[128 + ql];
-          const float x = s[t][r] * p.scale + gq * bcol[(long long)q * Tb];
+          const float x = s[t][r] * p.scale + gq * btile[ql * BT_LD + kl];
           const float pr = __expf(x - rowc[ql]);
           float dpv = dp[t][r];
           pv = pr * dsc;
@@ -370,7 +384,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(const nrse_attn_bwd_pa
             else dpv *= dsc;
           }
           d = pr * (dpv - rowc[64 + ql]);
-          atomicAdd(&diag[kj - q - dbase], d * gq);
+          if (p.diag) atomicAdd(&mydiag[kj - q - dbase], d * gq);
         }
         pd[t][r] = pv;
         ds[t][r] = d;
@@ -404,7 +418,8 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(const nrse_attn_bwd_pa
     const int nd = 2 * T - 1;
     for (int e = tid; e < ndiag; e += 256) {
       const int dd = dbase + e + T - 1;  // index of d = kj - qi in [0, 2T-1)
-      if (dd >= 0 && dd < nd && diag[e] != 0.f) atomicAdd(p.diag + (long long)h * nd + dd, diag[e]);
+      const float v = diag[e] + diag[ndiag + e] + diag[2 * ndiag + e] + diag[3 * ndiag + e];
+      if (dd >= 0 && dd < nd && v != 0.f) atomicAdd(p.diag + (long long)h * nd + dd, v);
     }
   }
 }
@@ -421,7 +436,7 @@ int nrse_attn_fwd_mfma(const nrse_attn_fwd_params* p, hipStream_t st) {
 
 int nrse_attn_bwd_mfma(const nrse_attn_bwd_params* p, hipStream_t st) {
   dim3 grid((p->T + 63) / 64, p->H, p->batch);
-  const size_t lds_kv = 2 * TILE_B + (192 + p->T + 64) * sizeof(float);
+  const size_t lds_kv = 2 * TILE_B + (192 + 64 * BT_LD + 4 * (p->T + 64)) * sizeof(float);
   if (lds_kv > 160 * 1024) {
     nrse_set_error("nrse_attn_bwd: T=%d too long for the LDS diagonal accumulator", p->T);
     return NRSE_ERR_UNSUPPORTED;

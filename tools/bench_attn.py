@@ -1,0 +1,36 @@
+"""Micro-benchmark of the attention kernels at the WavLM-Large step shape (B=32, T=399, H=16)."""
+import os, sys
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "noise-robust-speech-embedding_amd"))
+import torch
+from nrse_amd import kernels as K, _lib
+
+_lib.init_device(0)
+dev = "cuda"
+B, T, H = 32, 399, 16
+qkv = (torch.randn(B * T, 3 * H * 64, device=dev) * 0.5).bfloat16()
+gate = torch.rand(B, H, T, device=dev) + 1
+bias = torch.randn(H, T, K.bias_ld(T), device=dev)
+ctx = torch.empty(B * T, H * 64, device=dev, dtype=torch.bfloat16)
+lse = torch.empty(B, H, T, device=dev)
+dctx = torch.randn_like(ctx)
+dqkv = torch.empty_like(qkv)
+dgate = torch.empty(B, H, T, device=dev)
+diag = torch.zeros(H, 2 * T - 1, device=dev)
+delta = torch.empty(B, H, T, device=dev)
+
+
+def timeit(fn, iters=20):
+    for _ in range(3): fn()
+    torch.cuda.synchronize()
+    s = torch.cuda.Event(enable_timing=True); e = torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters): fn()
+    e.record(); torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+for p in (0.0, 0.1):
+    tf = timeit(lambda: K.attn_fwd(qkv, gate, bias, ctx, lse, B, T, H, p, 1))
+    tb = timeit(lambda: K.attn_bwd(qkv, gate, bias, ctx, dctx, lse, delta, dqkv, dgate, diag, B, T, H, p, 1))
+    tbn = timeit(lambda: K.attn_bwd(qkv, gate, bias, ctx, dctx, lse, delta, dqkv, dgate, None, B, T, H, p, 1))
+    fl = 4.0 * B * H * T * T * 64
+    print(f"p={p}: fwd {tf*1e3:.1f}us ({fl/tf/1e9:.0f} TF) | bwd {tb*1e3:.1f}us ({2.5*fl/tb/1e9:.0f} TF) | bwd no-diag {tbn*1e3:.1f}us", flush=True)
