@@ -122,7 +122,7 @@ def main():
         return 0.5 * 1e-5 * (1 + math.cos(math.pi * step / total_steps))
 
     def step(i):
-        K.snr_mix(clean_raw, noise_raw, noise_len, snr, clean_iv, noisy_iv, status, kscale, True)
+        K.snr_mix(clean_raw, noise_raw, noise_len, snr, clean_iv, noisy_iv, status, kscale, K.SNR_PEAK_ZMUV)
         return eng.train_step(clean_iv, noisy_iv, lr=lr_at(i), step_seed=i, rank=rank, allreduce=allreduce,
                               world_size=world)
 

@@ -308,8 +308,10 @@ int nrse_health(const void* x, int dtype, long long n, float* stats, void* strea
  * Fused on-GPU SNR mix (src/data/augment.py:4-66 + noisy_speech_dataset.py:88-129):
  * per pair b: tile/truncate noise to L, k = sqrt(Ps / (Pn * 10^(snr/10))), y = s + k n,
  * peak-normalise both, optional zero-mean/unit-var (feature extractor do_normalize).
+ * mode (`do_normalize` argument): 0 = raw mix y = s + k n (add_noise_to_speech), 1 = + peak
+ * normalisation, 2 = + feature-extractor normalisation. noise_len[b] <= noise_stride.
  * status[b] follows oracle/snr_mix.py codes (0 = ok); outputs of failed pairs are zeroed.
- * scratch: f64 [batch * 16] (caller zeroes).
+ * scratch: unused (may be null).
  * ------------------------------------------------------------------------------------------ */
 int nrse_snr_mix(const float* clean, const float* noise, const int* noise_len, long long noise_stride,
                  const float* snr_db, float* clean_out, float* noisy_out, int* status, float* kscale, double* scratch,

@@ -93,9 +93,13 @@ __global__ __launch_bounds__(NT) void snr_mix_kernel(const float* __restrict__ c
   ymax = block_max(ymax, redf);
   ynan = __syncthreads_or(ynan);
   if (st == 0 && ynan) st = 7;
-  if (st == 0 && smax < 1e-8f) st = 8;
-  if (st == 0 && ymax < 1e-8f) st = 9;
-  const float cden = smax + 1e-8f, yden = ymax + 1e-8f;
+  // mode 0 = add_noise_to_speech only (augment.py:4-66); 1 = + peak normalisation
+  // (noisy_speech_dataset.py:88-103); 2 = + feature-extractor zero-mean/unit-var
+  const int mode = do_norm;
+  if (mode >= 1 && st == 0 && smax < 1e-8f) st = 8;
+  if (mode >= 1 && st == 0 && ymax < 1e-8f) st = 9;
+  const float cden = mode >= 1 ? smax + 1e-8f : 1.f, yden = mode >= 1 ? ymax + 1e-8f : 1.f;
+  do_norm = mode == 2;
   // pass 3: statistics of the peak-normalised views
   double cs = 0.0, cq = 0.0, ys = 0.0, yq = 0.0;
   if (st == 0 && do_norm) {

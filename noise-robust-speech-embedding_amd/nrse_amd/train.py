@@ -1,0 +1,176 @@
+"""Training entry: the train_byol.py loop (train_byol.py:20-245) on the fused MI355X step.
+
+    python -m nrse_amd.train --config <reference yaml> [--device cuda:0 --batch_size --epochs --lr]
+    torchrun --nproc-per-node 8 -m nrse_amd.train --config ...      (data parallel, RCCL)
+
+Per iteration (train_byol.py:47-77): H2D of raw waveforms -> fused SNR mix -> health checks
+(device flags, no host sync) -> forward -> loss -> backward -> [grad all-reduce] -> clip(1.0) +
+AdamW -> EMA -> cosine LR. Validation (evaluate_byol.py:68-123), EarlyStopping
+(train_byol.py:82-116) and checkpoints in the reference's torch.save format
+(train_byol.py:207-240, state-dict keys of BYOLSpeechModel) follow each epoch.
+"""
+from __future__ import annotations
+
+import logging
+import math
+import os
+import time
+
+import torch
+
+from . import ddp
+from .config import get_config
+from .data import GpuMixer, create_dataloaders
+from .model import BYOLSpeechModel
+
+logger = logging.getLogger("nrse")
+
+
+class EarlyStopping:
+    """train_byol.py:82-116."""
+
+    def __init__(self, patience=5, min_delta=0.0, mode="min"):
+        self.patience, self.min_delta, self.mode = patience, min_delta, mode
+        self.counter, self.best_score, self.early_stop = 0, None, False
+
+    def __call__(self, score):
+        if self.best_score is None:
+            self.best_score = score
+            return False
+        improvement = (self.best_score - score > self.min_delta) if self.mode == "min" else \
+            (score - self.best_score > self.min_delta)
+        if improvement:
+            self.best_score, self.counter = score, 0
+        else:
+            self.counter += 1
+            if self.counter >= self.patience:
+                self.early_stop = True
+        return self.early_stop
+
+
+class FusedAdamW(torch.optim.Optimizer):
+    """AdamW over the flat online buffer, executed by the engine's fused clip+AdamW+EMA kernels;
+    a torch Optimizer so torch's LR schedulers (CosineAnnealingLR) drive its lr."""
+
+    def __init__(self, model: BYOLSpeechModel, lr: float, weight_decay: float):
+        super().__init__([model.online_flat], dict(lr=lr, weight_decay=weight_decay))
+        self.model = model
+
+    @property
+    def lr(self):
+        return self.param_groups[0]["lr"]
+
+    def step(self, closure=None):  # used by the unfused path (autograd backward)
+        eng = self.model.engine
+        eng.grad.copy_(self.model.online_flat.grad)
+        eng.optimizer_step(self.lr)
+
+
+def train_one_epoch(model, dataloader, optimizer, scheduler, device, config, mixer=None, allreduce=None,
+                    world=1, rank=0, step0=0, max_steps=None):
+    """train_byol.py:20-79 -> mean epoch loss."""
+    model.train()
+    eng = model.engine
+    mixer = mixer or GpuMixer(device, config["data"].get("do_normalize", True))
+    losses = []
+    steps = 0
+    for raw in dataloader:
+        batch = mixer(raw)
+        loss = eng.train_step(batch["clean_input_values"].squeeze(1), batch["noisy_input_values"].squeeze(1),
+                              lr=optimizer.lr, step_seed=step0 + steps, rank=rank, allreduce=allreduce,
+                              world_size=world)
+        losses.append(loss.clone())
+        scheduler.step()
+        steps += 1
+        if max_steps is not None and step0 + steps >= max_steps:
+            break
+    if not losses:
+        return float("nan"), steps
+    return float(torch.stack(losses).mean()), steps  # one host sync per epoch
+
+
+@torch.no_grad()
+def validate_model(model, val_loader, device, config, mixer=None):
+    """evaluate_byol.py:68-123: per-SNR cosine similarity of online-encoder embeddings of the
+    clean vs noisy views + validation BYOL loss, in eval mode."""
+    model.eval()
+    eng = model.engine
+    mixer = mixer or GpuMixer(device, config["data"].get("do_normalize", True))
+    sims = {snr: [] for snr in config["data"]["snr_range"]}
+    vloss = []
+    for raw in val_loader or []:
+        batch = mixer(raw)
+        c, n = batch["clean_input_values"].squeeze(1), batch["noisy_input_values"].squeeze(1)
+        ec = eng.embed(c)
+        en = eng.embed(n)
+        s = torch.nn.functional.cosine_similarity(ec, en, dim=1)
+        for snr, v in zip(batch["snr"].tolist(), s.tolist()):
+            if snr in sims:
+                sims[snr].append(v)
+        _, _, loss = eng.eval_forward(c, n)
+        vloss.append(float(loss))
+    model.train()
+    avg = {k: (sum(v) / len(v) if v else 0.0) for k, v in sims.items()}
+    return (sum(vloss) / len(vloss) if vloss else float("inf")), {
+        "val_loss": sum(vloss) / len(vloss) if vloss else float("inf"),
+        "val_avg_similarity": sum(avg.values()) / len(avg) if avg else 0.0,
+        "val_similarities": avg}
+
+
+def main(argv=None):
+    config = get_config(argv)
+    rank, world, local = ddp.init_from_env()
+    logging.basicConfig(level=getattr(logging, config.get("logging", {}).get("level", "INFO")))
+    device = torch.device(config["device"]) if world == 1 else torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    t = config["training"]
+    torch.manual_seed(t.get("seed", 42))
+    os.makedirs(t["checkpoint_dir"], exist_ok=True)
+    os.makedirs(t["log_dir"], exist_ok=True)
+    dtype = torch.float32 if config["runtime"]["dtype"] == "f32" else torch.bfloat16
+    model = BYOLSpeechModel(config, device=device, compute_dtype=dtype)
+    train_loader, val_loader = create_dataloaders(config, rank=rank, world=world)
+    optimizer = FusedAdamW(model, lr=float(t["learning_rate"]), weight_decay=float(t["weight_decay"]))
+    total_steps = max(1, len(train_loader) * int(t["num_epochs"]))
+    scheduler = torch.optim.lr_scheduler.CosineAnnealingLR(optimizer, T_max=total_steps)
+    metric = t.get("early_stopping_metric", "val_loss")
+    stopper = EarlyStopping(t.get("early_stopping_patience", 5), t.get("early_stopping_min_delta", 0.0),
+                            "min" if metric == "val_loss" else "max")
+    allreduce = ddp.GradAllReduce() if world > 1 else None
+    mixer = GpuMixer(device, config["data"].get("do_normalize", True))
+    best_loss, best_sim, step = float("inf"), 0.0, 0
+    max_steps = config["runtime"].get("max_steps")
+    for epoch in range(int(t["num_epochs"])):
+        t0 = time.perf_counter()
+        ep_loss, n = train_one_epoch(model, train_loader, optimizer, scheduler, device, config, mixer, allreduce,
+                                     world, rank, step, max_steps)
+        step += n
+        val_loss, vm = validate_model(model, val_loader, device, config, mixer)
+        if rank == 0:
+            print(f"Epoch {epoch + 1}/{t['num_epochs']} - Train Loss: {ep_loss:.4f}, Val Loss: {val_loss:.4f}, "
+                  f"Val Avg Similarity: {vm['val_avg_similarity']:.4f} ({n} steps, "
+                  f"{n * int(t['batch_size']) * world / (time.perf_counter() - t0):.1f} pairs/s)", flush=True)
+            ck = {"epoch": epoch, "model_state_dict": model.state_dict(), "optimizer_state_dict": optimizer.state_dict(),
+                  "loss": val_loss, "similarity": vm["val_avg_similarity"]}
+            if val_loss < best_loss:
+                best_loss = val_loss
+                torch.save(ck, os.path.join(t["checkpoint_dir"], "best_val_loss.pt"))
+            if vm["val_avg_similarity"] > best_sim:
+                best_sim = vm["val_avg_similarity"]
+                torch.save(ck, os.path.join(t["checkpoint_dir"], "best_val_similarity.pt"))
+            if epoch == int(t["num_epochs"]) - 1:
+                torch.save(ck, os.path.join(t["checkpoint_dir"], "last_model.pt"))
+        if stopper(val_loss if metric == "val_loss" else vm["val_avg_similarity"]):
+            if rank == 0:
+                print(f"Early stopping triggered after epoch {epoch + 1}")
+            break
+        if max_steps is not None and step >= max_steps:
+            break
+    if world > 1:
+        torch.distributed.destroy_process_group()
+    if rank == 0:
+        print("Training complete!")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,98 @@
+"""Host-side logic: relative-position buckets, SpecAugment / LayerDrop sampling, parameter
+inventory and naming, config schema, RNG contract (CPU only)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from nrse_amd import arch as A, hostside as HS, params as PR, rng as R
+from oracle import masks as MK
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def test_bucket_vector_matches_reference_fixture():
+    z = np.load(os.path.join(GOLD, "buckets.npz"))
+    for key in z.files:
+        np.testing.assert_array_equal(HS.bucket_vector(int(key[1:])), z[key])
+
+
+def test_span_masks():
+    rng = np.random.default_rng(0)
+    for T in (49, 399, 599):
+        m = HS.compute_mask_indices(rng, 16, T, 0.075, 10, 2)
+        n = m.sum(1)
+        assert (n >= 10).all() and (n <= 10 * max(2, int(0.075 * T / 10 + 1))).all()
+    assert not HS.compute_mask_indices(rng, 4, 100, 0.0, 10, 2).any()
+
+
+def test_layerdrop_never_drops_layer0():
+    rng = np.random.default_rng(1)
+    drops = np.array([HS.layerdrop_decisions(rng, 24, 0.1) for _ in range(2000)])
+    assert not drops[:, 0].any()
+    assert abs(drops[:, 1:].mean() - 0.1) < 0.01
+
+
+def test_large_param_inventory_matches_wavlm_large():
+    # 315,453,120 = WavLM-Large
+    assert PR.count_params(PR.encoder_specs(A.LARGE)) == 315_453_120
+    L = PR.byol_layout(A.LARGE, 1024, 2048)
+    assert sum(n for _, n, _ in L.offsets.values()) == 315_453_120 + 2_103_296 + 8_401_920
+
+
+@pytest.mark.parametrize("arch", [A.TINY, A.TINY.deterministic()])
+def test_state_dict_names_match_transformers(arch):
+    from transformers import WavLMConfig, WavLMModel
+    m = WavLMModel(WavLMConfig(**arch.to_hf_config()))
+    ref = {k: tuple(v.shape) for k, v in m.named_parameters()}
+    ours = {s.name: tuple(s.shape) for s in PR.encoder_specs(arch)}
+    assert ref == ours
+
+
+def test_fused_views_are_contiguous():
+    L = PR.byol_layout(A.LARGE, 1024, 2048)
+    o = L.offsets
+    p = "online_encoder.model.encoder.layers.3.attention."
+    H = 1024
+    assert o[p + "k_proj.weight"][0] == o[p + "q_proj.weight"][0] + H * H
+    assert o[p + "v_proj.bias"][0] == o[p + "k_proj.bias"][0] + H
+
+
+def test_init_is_portable_and_seeded():
+    L = PR.byol_layout(A.TINY, 256, 512)
+    a = PR.init_byol_flat(L, 5)
+    b = PR.init_byol_flat(L, 5)
+    c = PR.init_byol_flat(L, 6)
+    assert torch.equal(a, b) and not torch.equal(a, c)
+
+
+def test_rng_contract_matches_oracle_hash():
+    for x in (0, 1, 12345, 0xFFFFFFFF, 0xDEADBEEF):
+        assert R.mix32(x) == int(MK.mix32(x))
+    keep = MK.keep_mask(R.site_seed(7, 3), 0.1, 200000)
+    assert abs(keep.mean() - 0.9) < 0.005
+    seeds = {R.site_seed(R.forward_seed(s, b, r), site) for s in range(4) for b in (0, 1) for r in range(2)
+             for site in range(30)}
+    assert len(seeds) == 4 * 2 * 2 * 30
+
+
+def test_config_schema_and_cli_overrides(tmp_path):
+    import yaml
+    from nrse_amd.config import get_config
+    cfg = {"model": {"name": "microsoft/wavlm-large", "projection_dim": 1024, "prediction_dim": 2048,
+                     "ema_decay": 0.997},
+           "training": {"batch_size": 36, "num_epochs": 100, "learning_rate": 1e-5, "weight_decay": 1e-5,
+                        "checkpoint_dir": "c", "log_dir": "l", "seed": 42},
+           "data": {"sample_rate": 16000, "max_audio_length": 5.0, "snr_range": [2, 5, 10, 15, 20]},
+           "logging": {"level": "INFO"}}
+    p = tmp_path / "c.yaml"
+    p.write_text(yaml.safe_dump(cfg))
+    out = get_config(["--config", str(p), "--batch_size", "32", "--lr", "3e-5", "--device", "cuda:1"])
+    assert out["training"]["batch_size"] == 32 and out["training"]["learning_rate"] == 3e-5
+    assert out["device"] == "cuda:1" and out["model"]["ema_decay"] == 0.997
+    assert A.arch_from_name(out["model"]["name"]) == A.LARGE
+
+
+def test_frames():
+    assert A.LARGE.frames(128000) == 399 and A.LARGE.frames(80000) == 249

@@ -1,0 +1,204 @@
+"""Per-kernel parity on the GPU: each HIP kernel vs a float64 PyTorch reference of the same op
+(floating-point kernels) or vs the committed golden fixtures (SNR mix)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def rel(a, b):
+    a = a.double(); b = b.double()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize("C", [256, 512, 1024])
+@pytest.mark.parametrize("xdt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("gelu", [False, True])
+def test_layernorm_fwd_bwd(nrse_device, C, xdt, gelu):
+    from nrse_amd import kernels as K
+    dev = nrse_device
+    rows = 333
+    x = (torch.randn(rows, C, device=dev) * 2 + 0.5).to(xdt)
+    g = torch.randn(C, device=dev) * 0.1 + 1
+    b = torch.randn(C, device=dev) * 0.1
+    y = torch.empty(rows, C, device=dev)
+    mean = torch.empty(rows, device=dev); rstd = torch.empty(rows, device=dev)
+    K.ln_fwd(x, g, b, y, mean, rstd, 1e-5, gelu=gelu)
+    xr = x.double().requires_grad_(True)
+    gr, br = g.double().requires_grad_(True), b.double().requires_grad_(True)
+    ref = F.layer_norm(xr, (C,), gr, br, 1e-5)
+    if gelu:
+        ref = F.gelu(ref)
+    assert rel(y, ref) < 1e-5
+    dy = torch.randn(rows, C, device=dev)
+    resid = torch.randn(rows, C, device=dev)
+    dx = torch.empty(rows, C, device=dev)
+    dg = torch.zeros(C, device=dev); db = torch.zeros(C, device=dev)
+    K.ln_bwd(dy, x, g, mean, rstd, dx, beta=b, gelu=gelu, resid=resid, dgamma=dg, dbeta=db)
+    ref.backward(dy.double())
+    assert rel(dx, xr.grad + resid.double()) < 1e-5
+    assert rel(dg, gr.grad) < 1e-5 and rel(db, br.grad) < 1e-5
+
+
+def test_layernorm_bwd_col2im_and_bcast(nrse_device):
+    from nrse_amd import kernels as K, _lib
+    dev = nrse_device
+    B, Tin, C, k, s = 3, 52, 256, 3, 2
+    Tout = (Tin - k) // s + 1
+    x = torch.randn(B * Tin, C, device=dev)
+    g = torch.ones(C, device=dev); b = torch.zeros(C, device=dev)
+    y = torch.empty_like(x); mean = torch.empty(B * Tin, device=dev); rstd = torch.empty_like(mean)
+    K.ln_fwd(x, g, b, y, mean, rstd, 1e-5)
+    G = torch.randn(B * Tout, k * C, device=dev)
+    dy = torch.zeros(B, Tin, C, device=dev, dtype=torch.float64)
+    Gv = G.double().view(B, Tout, k, C)
+    for j in range(k):
+        dy[:, j:j + s * (Tout - 1) + 1:s] += Gv[:, :, j]
+    dx = torch.empty_like(x)
+    K.ln_bwd(G, x, g, mean, rstd, dx, mode=_lib.DY_COL2IM, col=(k, s, Tout, Tin), rows=B * Tin)
+    xr = x.double().requires_grad_(True)
+    F.layer_norm(xr, (C,), None, None, 1e-5).backward(dy.view(B * Tin, C))
+    assert rel(dx, xr.grad) < 1e-6
+    # broadcast (time-mean) mode
+    demb = torch.randn(B, C, device=dev)
+    K.ln_bwd(demb, x, g, mean, rstd, dx, mode=_lib.DY_BCAST, bcast_t=Tin, dy_scale=1.0 / Tin, rows=B * Tin)
+    xr.grad = None
+    F.layer_norm(xr, (C,), None, None, 1e-5).view(B, Tin, C).mean(1).backward(demb.double())
+    assert rel(dx, xr.grad) < 1e-6
+
+
+@pytest.mark.parametrize("C", [256, 512])
+def test_conv0_fwd_bwd(nrse_device, C):
+    from nrse_amd import kernels as K
+    dev = nrse_device
+    B, L, k, s = 2, 4001, 10, 5
+    T0 = (L - k) // s + 1
+    wav = torch.randn(B, L, device=dev)
+    w = torch.randn(C, 1, k, device=dev) * 0.3
+    g = torch.randn(C, device=dev) * 0.1 + 1; b = torch.randn(C, device=dev) * 0.1
+    out = torch.empty(B * T0, C, device=dev)
+    mean = torch.empty(B * T0, device=dev); rstd = torch.empty_like(mean)
+    K.conv0_fwd(wav, w.view(C, k), g, b, out, mean, rstd, T0, k, s, 1e-5)
+    wr = w.double().requires_grad_(True); gr = g.double().requires_grad_(True); br = b.double().requires_grad_(True)
+    ref = F.conv1d(wav.double()[:, None], wr, stride=s)
+    ref = F.gelu(F.layer_norm(ref.transpose(1, 2), (C,), gr, br, 1e-5)).reshape(B * T0, C)
+    assert rel(out, ref) < 1e-5
+    dy = torch.randn(B * T0, C, device=dev)
+    dw = torch.zeros(C, k, device=dev); dg = torch.zeros(C, device=dev); db = torch.zeros(C, device=dev)
+    K.conv0_bwd(wav, w.view(C, k), g, b, mean, rstd, dy, dw, dg, db, T0, k, s, None)
+    ref.backward(dy.double())
+    assert rel(dw, wr.grad.view(C, k)) < 1e-4
+    assert rel(dg, gr.grad) < 1e-5 and rel(db, br.grad) < 1e-5
+
+
+def test_weight_norm_fwd_bwd(nrse_device):
+    from nrse_amd import kernels as K
+    dev = nrse_device
+    H, G, Kk = 256, 16, 128
+    cpg = H // G
+    v = torch.randn(H, cpg, Kk, device=dev)
+    gg = torch.rand(1, 1, Kk, device=dev) + 0.5
+    wf = torch.empty(G, cpg, Kk * cpg, device=dev); wd = torch.empty_like(wf)
+    norms = torch.empty(Kk, device=dev)
+    K.weight_norm_fwd(gg, v, wf, wd, norms, H, cpg, Kk)
+    vr = v.double().requires_grad_(True); gr = gg.double().requires_grad_(True)
+    w = vr * (gr / vr.pow(2).sum(dim=(0, 1), keepdim=True).sqrt())       # [H, cpg, K]
+    ref_wf = w.view(G, cpg, cpg, Kk).permute(0, 1, 3, 2).reshape(G, cpg, Kk * cpg)
+    ref_wd = w.view(G, cpg, cpg, Kk).flip(-1).permute(0, 2, 3, 1).reshape(G, cpg, Kk * cpg)
+    assert rel(wf, ref_wf) < 1e-6 and rel(wd, ref_wd) < 1e-6
+    dWf = torch.randn_like(wf)
+    dg = torch.zeros(1, 1, Kk, device=dev); dv = torch.zeros_like(v)
+    K.weight_norm_bwd(dWf, gg, v, norms, dg, dv, torch.empty(Kk, device=dev), H, cpg, Kk)
+    ref_wf.backward(dWf.double())
+    assert rel(dv, vr.grad) < 1e-5 and rel(dg, gr.grad) < 1e-5
+
+
+def test_batchnorm_relu_and_loss(nrse_device):
+    from nrse_amd import kernels as K
+    dev = nrse_device
+    x = torch.randn(32, 300, device=dev) * 3 + 1
+    w = torch.randn(300, device=dev); b = torch.randn(300, device=dev)
+    rm = torch.zeros(300, device=dev); rv = torch.ones(300, device=dev)
+    y = torch.empty_like(x); sm = torch.empty(300, device=dev); si = torch.empty(300, device=dev)
+    K.bn_fwd(x, w, b, y, rm, rv, sm, si, True, True)
+    xr = x.double().requires_grad_(True); wr = w.double().requires_grad_(True); br = b.double().requires_grad_(True)
+    rm2 = torch.zeros(300, device=dev, dtype=torch.float64); rv2 = torch.ones_like(rm2)
+    ref = torch.relu(F.batch_norm(xr, rm2, rv2, wr, br, training=True, momentum=0.1, eps=1e-5))
+    assert rel(y, ref) < 1e-6 and rel(rm, rm2) < 1e-6 and rel(rv, rv2) < 1e-6
+    dy = torch.randn_like(x)
+    dx = torch.empty_like(x); dw = torch.zeros(300, device=dev); db = torch.zeros(300, device=dev)
+    K.bn_bwd(dy, x, y, w, sm, si, dx, dw, db, True)
+    ref.backward(dy.double())
+    assert rel(dx, xr.grad) < 1e-5 and rel(dw, wr.grad) < 1e-5 and rel(db, br.grad) < 1e-5
+    # BYOL loss fwd + bwd (src/models/byol.py:104-128)
+    p = torch.randn(32, 1024, device=dev); z = torch.randn(32, 1024, device=dev)
+    loss = torch.zeros(1, device=dev); dp = torch.empty_like(p); stats = torch.zeros(2, device=dev)
+    K.byol_loss(p, z, loss, dp, stats)
+    pr = p.double().requires_grad_(True)
+    pn = F.normalize(pr + 1e-10, dim=1, eps=1e-10); zn = F.normalize(z.double() + 1e-10, dim=1, eps=1e-10)
+    rl = 2 - 2 * torch.clamp((pn * zn).sum(1), -1, 1).mean()
+    rl.backward()
+    assert abs(float(loss) - float(rl)) < 1e-6 and rel(dp, pr.grad) < 1e-5
+
+
+def test_adamw_clip_ema(nrse_device):
+    from nrse_amd import kernels as K
+    dev = nrse_device
+    n = 100_003
+    p = torch.randn(n, device=dev); g = torch.randn(n, device=dev) * 3
+    m = torch.zeros(n, device=dev); v = torch.zeros(n, device=dev)
+    sh = torch.empty(n, device=dev, dtype=torch.bfloat16)
+    ss = torch.zeros(1, device=dev, dtype=torch.float64)
+    K.sumsq(g, ss)
+    assert abs(float(ss.sqrt()) - float(g.double().norm())) / float(g.double().norm()) < 1e-12
+    pt = torch.nn.Parameter(p.clone())
+    opt = torch.optim.AdamW([pt], lr=1e-3, weight_decay=1e-2)
+    pt.grad = g.clone()
+    torch.nn.utils.clip_grad_norm_([pt], max_norm=1.0)
+    opt.step()
+    K.adamw(p, g, m, v, sh, lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=1e-2, step=1, max_norm=1.0,
+            sumsq_buf=ss)
+    assert rel(p, pt.detach()) < 1e-6
+    assert rel(sh.float(), p) < 1e-2
+    t = torch.randn(n, device=dev)
+    t_ref = 0.997 * t + 0.003 * p
+    K.ema(t, p, None, 0.997)
+    assert rel(t, t_ref) < 1e-6
+
+
+def test_snr_mix_matches_reference_fixture(nrse_device):
+    from nrse_amd import kernels as K
+    z = np.load(os.path.join(GOLD, "snr_mix.npz"))
+    dev = nrse_device
+    for i in range(int(z["n_cases"])):
+        s = torch.from_numpy(z[f"c{i}_speech"]).to(dev)[None]
+        n = torch.from_numpy(z[f"c{i}_noise"]).to(dev)[None]
+        snr = torch.tensor([float(z[f"c{i}_snr"])], device=dev)
+        nlen = torch.tensor([n.shape[1]], device=dev, dtype=torch.int32)
+        c_out = torch.empty_like(s); n_out = torch.empty_like(s)
+        st = torch.empty(1, device=dev, dtype=torch.int32); ks = torch.empty(1, device=dev)
+        K.snr_mix(s, n, nlen, snr, c_out, n_out, st, ks, K.SNR_PEAK_ZMUV)
+        ok = int(z[f"c{i}_ok"]) == 1
+        assert (int(st) == 0) == ok, (i, int(st))
+        if ok:
+            assert rel(c_out[0], torch.from_numpy(z[f"c{i}_clean_iv"]).to(dev)) < 1e-5
+            assert rel(n_out[0], torch.from_numpy(z[f"c{i}_noisy_iv"]).to(dev)) < 1e-5
+            K.snr_mix(s, n, nlen, snr, c_out, n_out, st, ks, K.SNR_RAW)
+            assert rel(n_out[0], torch.from_numpy(z[f"c{i}_noisy_raw"]).to(dev)) < 1e-6
+
+
+def test_health_flags(nrse_device):
+    from nrse_amd import kernels as K
+    x = torch.randn(10000, device=nrse_device)
+    x[5] = float("nan"); x[7] = float("inf")
+    st = torch.zeros(4, device=nrse_device)
+    K.health(x, st)
+    assert st[0] == 1 and st[1] == 1
+    y = x.clone(); y[5] = 0; y[7] = 0
+    assert abs(float(st[2]) - float(y.abs().sum())) / float(y.abs().sum()) < 1e-5
+    assert float(st[3]) == float(y.abs().max())
