@@ -35,9 +35,8 @@ class _OnlineBranch(torch.autograd.Function):
     engine's explicit encoder/heads backward and returns the flat gradient."""
 
     @staticmethod
-    def forward(ctx, clean, noisy, flat, model):
+    def forward(ctx, clean, noisy, flat, model, need):
         eng = model.engine
-        need = torch.is_grad_enabled() and flat.requires_grad and model.training
         pred, tproj, c = eng.forward(clean, noisy, train=model.training, step_seed=model._next_seed(),
                                      need_grad=need)
         ctx.model = model
@@ -51,7 +50,7 @@ class _OnlineBranch(torch.autograd.Function):
         eng.grad.zero_()
         eng.backward(dpred.contiguous().float(), ctx.c)
         ctx.c = None
-        return None, None, eng.grad.clone(), None
+        return None, None, eng.grad.clone(), None, None
 
 
 class _Loss(torch.autograd.Function):
@@ -147,7 +146,9 @@ class BYOLSpeechModel(nn.Module):
             if x.dim() == 3:
                 x = x.squeeze(1)
             return x.to(self.engine.dev, torch.float32).contiguous()
-        return _OnlineBranch.apply(prep(clean_input_values), prep(noisy_input_values), self.online_flat, self)
+        # grad mode is off inside Function.forward, so decide here whether to keep the tape
+        need = torch.is_grad_enabled() and self.online_flat.requires_grad and self.training
+        return _OnlineBranch.apply(prep(clean_input_values), prep(noisy_input_values), self.online_flat, self, need)
 
     def _update_target_network(self) -> None:
         e = self.engine
