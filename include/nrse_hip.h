@@ -117,6 +117,10 @@ typedef struct {
 } nrse_gemm_params;
 
 int nrse_gemm(const nrse_gemm_params* p, void* stream);
+/* Kernel generation used by nrse_gemm for bf16 operands: 0 = automatic (default), 1 = register
+ * staged 128x128, 2 = LDS-DMA 128x128, 3 = LDS-DMA 256x256 (falls back when a problem does not
+ * fit it). Process-wide; for tests and benchmarks. Returns the previous setting. */
+int nrse_gemm_select(int generation);
 
 /* ------------------------------------------------------------------------------------------
  * LayerNorm over the last (channel) dim of channels-last rows, fp32 statistics.

@@ -20,8 +20,13 @@
 
 bool nrse_gemm_dma_ok(const nrse_gemm_params* p);        // gemm_dma.hip
 int nrse_gemm_dma(const nrse_gemm_params* p, hipStream_t st);
+bool nrse_gemm256_ok(const nrse_gemm_params* p);         // gemm256.hip
+long long nrse_gemm256_tiles(const nrse_gemm_params* p);
+int nrse_gemm256(const nrse_gemm_params* p, hipStream_t st);
 
 namespace {
+
+int g_gemm_gen = getenv("NRSE_GEMM_GEN") ? atoi(getenv("NRSE_GEMM_GEN")) : 0;
 
 constexpr int BM = 128;
 constexpr int BN = 128;
@@ -379,7 +384,20 @@ extern "C" int nrse_gemm(const nrse_gemm_params* p, void* stream) {
   NRSE_REQUIRE(!(p->flags & NRSE_EPI_COLSUM) || p->colsum, "nrse_gemm: COLSUM without colsum");
   NRSE_REQUIRE((long long)nrse_cdiv(p->M, BM) <= 65535, "nrse_gemm: M too large for grid.y (%d)", p->M);
   hipStream_t st = (hipStream_t)stream;
-  static const bool force_v1 = getenv("NRSE_GEMM_V1") != nullptr;
-  if (!force_v1 && nrse_gemm_dma_ok(p)) return nrse_gemm_dma(p, st);
+  // NRSE_GEMM_GEN=1|2|3 pins one kernel generation (benchmarks); by default the 256x256 kernel
+  // takes bf16 problems with enough tiles to fill the chip, the 128x128 one the rest.
+  const int gen = g_gemm_gen;
+  // (split-K atomic problems stay on 128x128: 4x the tiles of a 256x256 decomposition means 4x
+  // fewer K splits for the same occupancy, i.e. 4x less atomic traffic per FLOP)
+  const bool big = nrse_gemm256_tiles(p) >= 128 && !(p->flags & NRSE_EPI_ATOMIC);
+  if (gen != 1 && gen != 2 && nrse_gemm256_ok(p) && (gen == 3 || big))
+    return nrse_gemm256(p, st);
+  if (gen != 1 && nrse_gemm_dma_ok(p)) return nrse_gemm_dma(p, st);
   return p->a.dtype == NRSE_BF16 ? launch_dt<bf16_t>(p, st) : launch_dt<float>(p, st);
+}
+
+extern "C" int nrse_gemm_select(int generation) {
+  const int prev = g_gemm_gen;
+  g_gemm_gen = generation;
+  return prev;
 }

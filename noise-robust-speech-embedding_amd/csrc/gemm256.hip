@@ -1,0 +1,346 @@
+// bf16 MFMA GEMM, generation 3: 256x256 output tile per workgroup, 8 waves, LDS-DMA staging
+// pipelined across barriers.
+//
+// Same contract as nrse_gemm (include/nrse_hip.h); nrse_gemm dispatches here for large bf16
+// problems (nrse_gemm256_ok). Why this shape (MI355X_MICROARCH.md / cdna_hip_programming.md §5):
+//  - a 128x128 tile moves 64 FLOP per L2 byte; at ~30 TB/s of L2 that caps a GEMM near 2 PF
+//    only with perfect L2 hits, and the 2-stage loop with a vmcnt(0) per K-step exposes the
+//    load latency. 256x256 halves the bytes per FLOP and the per-wave tile (128x64, 32
+//    accumulators of 16x16) doubles the MFMAs per LDS byte read.
+//  - one K-tile (BK = 64) is 4 half-tiles of 16 KiB: A-lo = A rows {0-63,128-191}, A-hi = A rows
+//    {64-127,192-255}, B-lo = B cols {wn*64 + 0..31}, B-hi = B cols {wn*64 + 32..63}. Each wave
+//    computes its 128x64 output as 4 quadrants (64x32, 16 MFMAs) in 4 phases: p0 (A-lo,B-lo),
+//    p1 (A-lo,B-hi), p2 (A-hi,B-hi), p3 (A-hi,B-lo), reading A-lo and B-lo in p0, B-hi in p1,
+//    A-hi in p2 and keeping fragments in registers for their second use.
+//  - LDS is a ring of 10 half-tile slots (160 KiB). Half-tiles are numbered in first-read order
+//    (seq = 4t + {A-lo, B-lo, B-hi, A-hi}), seq n lives in slot n % 10, and phase P stages
+//    seq P + 8 (K-tile t+2): every DMA has >= 6 phases (~1.3 us at full MFMA rate, more than the
+//    ~1.1 us issue-to-landed latency of LDS-DMA under load) before its data is needed.
+//  - ping-pong: the waves with wm = 1 run one barrier behind those with wm = 0, so each SIMD
+//    alternates one wave's 16-MFMA segment with the other wave's read+stage segment.
+//    With the barriers numbered globally, group 0's phase P reads in (#2P-1, #2P) and its
+//    MFMAs run in (#2P, #2P+1); group 1 is shifted by one. Hand-off rules that follow:
+//      RAW: data read in phase Q is waited for (vmcnt) by every issuing wave before the FIRST
+//           barrier of phase Q-1: vmcnt(12) there leaves the 6 youngest half-tiles (seq
+//           P+3..P+8) in flight and retires seq <= P+2, which covers phase P+1's reads.
+//      WAR: a slot is restaged >= 2 phases after its last read: seq n is staged in phase n-8
+//           into the slot of seq n-10, last read in phase <= n-10.
+//    No wait is vmcnt(0) and the barriers are raw s_barrier (no fence), so DMAs stay in flight
+//    across them.
+//  - tiles are numbered XCD-aware (consecutive tile ids on one XCD, T1) and grouped 8 M-tiles
+//    deep so the 32 tiles an XCD runs at once share 8 A panels and 4 B panels in its L2.
+//  - the 256x256 f32 result leaves through LDS in four 64-row passes with the same fused
+//    epilogue as gemm_dma.hip (epi8).
+#include "gemm_common.h"
+
+namespace {
+using namespace nrse_gemm_detail;
+
+constexpr int BM = 256, BN = 256, BK = 64, NTHR = 512;
+constexpr int HALF = 16384;             // 128 rows x 64 k bf16
+constexpr int SLOTS = 10;               // ring of half-tile slots (2.5 K-tiles)
+constexpr int LDS_BYTES = SLOTS * HALF; // 160 KiB: the whole LDS
+constexpr int LEAD = 8;                 // half-tiles staged ahead of the phase being computed
+constexpr int CT_LD = 260;          // f32 row stride of a 64 x 256 epilogue pass
+static_assert(64 * CT_LD * 4 <= LDS_BYTES, "epilogue pass must fit the staging LDS");
+
+// Row r (0..127) of half-tile hh of a panel -> row of the 256-row tile.
+//  A: the 64-row blocks {hh*64, 128 + hh*64} (the M-half mh = hh of both M-waves)
+//  B: the 32-col blocks {wn*64 + hh*32 : wn < 4} (the N-half nh = hh of all four N-waves)
+template <bool IS_A>
+NRSE_DEV int tile_row(int hh, int r) {
+  if constexpr (IS_A) return (r >> 6) * 128 + hh * 64 + (r & 63);
+  else return (r >> 5) * 64 + hh * 32 + (r & 31);
+}
+
+struct Ld {
+  __amdgpu_buffer_rsrc_t rs;
+  long long ld, ldc, seg, cmask;
+  int cs;
+  unsigned base[2][2];  // [half][instr] KC: row offset; !KC: column offset (elements)
+  int aux[2][2];        // KC: logical 16-B chunk; !KC: k row within the K-tile
+  bool ok[2][2];
+};
+
+// Per-lane source addresses of the 2 DMA instructions each thread issues per half-tile. The LDS
+// destination of wave w, instruction j is lane-linear (1 KiB at (2w+j) KiB), so the image swizzle
+// is applied on the source side (gemm_common.h frag()).
+template <bool KC, bool IS_A>
+NRSE_DEV void ld_init(Ld& o, const nrse_gemm_operand& d, const char* base, int wave, int lane, int row0,
+                      int rows_total) {
+  o.rs = make_rsrc(base);
+  o.ld = d.ld; o.ldc = d.ld_chunk; o.seg = d.seg_stride;
+  o.cs = d.chunk_shift > 0 ? d.chunk_shift : 62;
+  o.cmask = d.chunk_shift > 0 ? ((1LL << d.chunk_shift) - 1) : -1LL;
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int i = wave * 2 + j;
+      if constexpr (KC) {
+        const int r = 8 * i + (lane >> 3);
+        const int grow = row0 + tile_row<IS_A>(hh, r);
+        o.base[hh][j] = (unsigned)((long long)grow * o.ld);
+        o.aux[hh][j] = (lane & 7) ^ ((r >> 1) & 7);
+        o.ok[hh][j] = grow < rows_total;
+      } else {
+        const int k = 4 * i + (lane >> 4);
+        const int lc = (lane & 15) ^ fbank(k);
+        const long long gcol = row0 + tile_row<IS_A>(hh, lc * 8);
+        o.base[hh][j] = (unsigned)coff(gcol, o.cs, o.cmask, o.ldc);
+        o.aux[hh][j] = k;
+        o.ok[hh][j] = gcol < rows_total;
+      }
+    }
+}
+
+template <bool KC>
+NRSE_DEV void ld_issue(const Ld& o, char* dst, int wave, int hh, long long segoff, int k0, int kseg, bool live) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    unsigned voff;
+    if constexpr (KC) {
+      const int k = k0 + o.aux[hh][j] * 8;
+      const bool v = live && o.ok[hh][j] && k < kseg;
+      voff = v ? (unsigned)((segoff + o.base[hh][j] + coff(k, o.cs, o.cmask, o.ldc)) * 2) : OOB;
+    } else {
+      const int k = k0 + o.aux[hh][j];
+      const bool v = live && o.ok[hh][j] && k < kseg;
+      voff = v ? (unsigned)((segoff + (long long)k * o.ld + o.base[hh][j]) * 2) : OOB;
+    }
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(o.rs, (lds_void*)(dst + (wave * 2 + j) * 1024), 16, voff, 0, 0, 0);
+  }
+}
+
+// raw workgroup barrier: orders LDS accesses for the compiler, emits no vmcnt wait
+#define NRSE_BAR()                            \
+  do {                                        \
+    asm volatile("" ::: "memory");            \
+    __builtin_amdgcn_s_barrier();             \
+    asm volatile("" ::: "memory");            \
+  } while (0)
+
+template <bool AKC, bool BKC>
+__global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params p, int mt, int nt) {
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+
+  // XCD-aware, M-grouped tile order
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int per_z = mt * nt;
+  const int z = wg / per_z;
+  const int tt = wg - z * per_z;
+  constexpr int GM = 8;
+  const int group = tt / (GM * nt);
+  const int first_m = group * GM;
+  const int gm = min(GM, mt - first_m);
+  const int in_g = tt - group * GM * nt;
+  const int m0 = (first_m + in_g % gm) * BM;
+  const int n0 = (in_g / gm) * BN;
+
+  const int zb = z / p.splits;
+  const int split = z % p.splits;
+  const long long zq = zb / p.zdiv, zr = zb % p.zdiv;
+
+  Ld la, lb;
+  ld_init<AKC, true>(la, p.a, (const char*)p.a.ptr + (zq * p.a.z1 + zr * p.a.z2) * 2, wave, lane, m0, p.M);
+  ld_init<BKC, false>(lb, p.b, (const char*)p.b.ptr + (zq * p.b.z1 + zr * p.b.z2) * 2, wave, lane, n0, p.N);
+
+  const int tps = (p.K + BK - 1) / BK;
+  const int seg0 = split * p.nseg;
+  const int ntiles = p.nseg * tps;
+
+  // K-tile t -> (segment, k0); t >= ntiles -> dead (zero-fill loads keep the vmcnt counts uniform)
+  auto tile_pos = [&](int t, int& sg, int& k0) {
+    const int tc = t < ntiles ? t : 0;
+    sg = seg0 + tc / tps;
+    k0 = (tc % tps) * BK;
+  };
+  // half-tile index j of a K-tile in staging (= first-read) order: 0 A-lo, 1 B-lo, 2 B-hi, 3 A-hi
+  auto stage = [&](int j, bool live, int sg, int k0, int slot) {
+    char* dst = smem + slot * HALF;
+    if (j == 0) ld_issue<AKC>(la, dst, wave, 0, (long long)sg * la.seg, k0, p.K, live);
+    else if (j == 1) ld_issue<BKC>(lb, dst, wave, 0, (long long)sg * lb.seg, k0, p.K, live);
+    else if (j == 2) ld_issue<BKC>(lb, dst, wave, 1, (long long)sg * lb.seg, k0, p.K, live);
+    else ld_issue<AKC>(la, dst, wave, 1, (long long)sg * la.seg, k0, p.K, live);
+  };
+  auto wrap = [](int x) { return x >= SLOTS ? x - SLOTS : x; };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: K-tiles 0 and 1 (half-tile sequence numbers 0..7, slot = seq % 10), then wait for
+  // the two read in phase 0 (6 younger half-tiles = 12 DMAs may stay in flight)
+  {
+    int sg, k0;
+    tile_pos(0, sg, k0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) stage(j, 0 < ntiles, sg, k0, j);
+    tile_pos(1, sg, k0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) stage(j, 1 < ntiles, sg, k0, 4 + j);
+  }
+  asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  NRSE_BAR();
+
+  bf16x8 fa[4][2], fbl[2][2], fbh[2][2];
+#define NRSE_READ_A(SLOT)                                                                \
+  _Pragma("unroll") for (int fi = 0; fi < 4; ++fi)                                     \
+  _Pragma("unroll") for (int s = 0; s < 2; ++s)                                        \
+    fa[fi][s] = frag<AKC>(smem + (SLOT) * HALF, wm * 64 + fi * 16, s, lane);
+#define NRSE_READ_B(SLOT, FB)                                                            \
+  _Pragma("unroll") for (int fj = 0; fj < 2; ++fj)                                     \
+  _Pragma("unroll") for (int s = 0; s < 2; ++s)                                        \
+    FB[fj][s] = frag<BKC>(smem + (SLOT) * HALF, wn * 32 + fj * 16, s, lane);
+#define NRSE_QUAD(MH, NH, FB)                                                            \
+  __builtin_amdgcn_s_setprio(1);                                                         \
+  _Pragma("unroll") for (int s = 0; s < 2; ++s)                                        \
+  _Pragma("unroll") for (int fi = 0; fi < 4; ++fi)                                     \
+  _Pragma("unroll") for (int fj = 0; fj < 2; ++fj)                                     \
+    acc[(MH) * 4 + fi][(NH) * 2 + fj] =                                                  \
+        __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[fi][s], FB[fj][s], acc[(MH) * 4 + fi][(NH) * 2 + fj], 0, 0, 0); \
+  __builtin_amdgcn_s_setprio(0);
+// the wait before each phase's first barrier retires every half-tile the NEXT phase reads
+#define NRSE_WAIT() asm volatile("s_waitcnt vmcnt(12)" ::: "memory")
+
+  // ping-pong start: group 1 falls one barrier behind (schedule and hand-off rules: header)
+  if (wm == 1) __builtin_amdgcn_s_barrier();
+  int base = 0;  // slot of half-tile sequence number 4t
+#pragma unroll 1
+  for (int t = 0; t < ntiles; ++t) {
+    const int s0 = base, s1 = wrap(base + 1), s2 = wrap(base + 2), s3 = wrap(base + 3);
+    // phase p stages half-tile j = p of K-tile t+2 (sequence 4t+8+p) into slot (4t+8+p) % 10
+    int sg2, k02;
+    tile_pos(t + 2, sg2, k02);
+    const bool live2 = t + 2 < ntiles;
+    // phase 0: quadrant (M-half 0, N-half 0) from A-lo, B-lo
+    NRSE_READ_A(s0)
+    NRSE_READ_B(s1, fbl)
+    stage(0, live2, sg2, k02, wrap(base + 8));
+    NRSE_WAIT();
+    NRSE_BAR();
+    NRSE_QUAD(0, 0, fbl)
+    NRSE_BAR();
+    // phase 1: (0, 1) from B-hi
+    NRSE_READ_B(s2, fbh)
+    stage(1, live2, sg2, k02, wrap(base + 9));
+    NRSE_WAIT();
+    NRSE_BAR();
+    NRSE_QUAD(0, 1, fbh)
+    NRSE_BAR();
+    // phase 2: (1, 1) from A-hi
+    NRSE_READ_A(s3)
+    stage(2, live2, sg2, k02, base);  // (4t + 10) % 10
+    NRSE_WAIT();
+    NRSE_BAR();
+    NRSE_QUAD(1, 1, fbh)
+    NRSE_BAR();
+    // phase 3: (1, 0) from registers
+    stage(3, live2, sg2, k02, s1);    // (4t + 11) % 10
+    NRSE_WAIT();
+    NRSE_BAR();
+    NRSE_QUAD(1, 0, fbl)
+    NRSE_BAR();
+    base = wrap(base + 4);
+  }
+  if (wm == 0) __builtin_amdgcn_s_barrier();
+#undef NRSE_READ_A
+#undef NRSE_READ_B
+#undef NRSE_QUAD
+#undef NRSE_WAIT
+
+  // ---------------------------------------------------------------- epilogue: 4 x 64-row passes
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing zero-fill DMAs
+  __syncthreads();
+  float* ct = reinterpret_cast<float*>(smem);
+  const int flags = p.flags;
+  const Epi epi(p, zq, zr, split);
+  const bool colsum = (flags & NRSE_EPI_COLSUM) != 0;
+  const int ccol = tid & 255, chalf = tid >> 8;
+  float csum = 0.f;
+  const int g = lane >> 4, li = lane & 15;
+#pragma unroll
+  for (int pass = 0; pass < 4; ++pass) {
+    if (wm == (pass >> 1)) {
+      const int mh = pass & 1;
+#pragma unroll
+      for (int fi = 0; fi < 4; ++fi)
+#pragma unroll
+        for (int fn = 0; fn < 4; ++fn)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            ct[(fi * 16 + 4 * g + r) * CT_LD + wn * 64 + fn * 16 + li] = acc[mh * 4 + fi][fn][r];
+    }
+    __syncthreads();
+    const int mrow0 = m0 + pass * 64;
+    if (flags & NRSE_EPI_ATOMIC) {
+      // one row per wave instruction: 64 lanes on 64 consecutive columns (256-B atomics)
+      for (int row = wave; row < 64; row += 8) {
+        const int m = mrow0 + row;
+        if (m >= p.M) break;
+#pragma unroll
+        for (int hc = 0; hc < 4; ++hc) {
+          const int col = hc * 64 + lane;
+          const int n = n0 + col;
+          if (n < p.N) atomicAdd((float*)p.c + epi.cbase + (long long)m * p.ldc + n, ct[row * CT_LD + col] * p.alpha);
+        }
+      }
+    } else {
+#pragma unroll 1
+      for (int it = 0; it < 4; ++it) {
+        const int sgi = tid + NTHR * it;
+        const int row = sgi >> 5;
+        const int cs = (sgi & 31) * 8;
+        const int m = mrow0 + row, n = n0 + cs;
+        float* cr = ct + row * CT_LD + cs;
+        if (m >= p.M || n >= p.N) {
+          if (colsum) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) cr[e] = 0.f;
+          }
+          continue;
+        }
+        epi8(p, epi, m, n, cr, colsum);
+      }
+      if (colsum) {
+        __syncthreads();
+        for (int r = chalf * 32; r < chalf * 32 + 32; ++r) csum += ct[r * CT_LD + ccol];
+      }
+    }
+    __syncthreads();
+  }
+  if (colsum && n0 + ccol < p.N) atomicAdd(p.colsum + n0 + ccol, csum);
+}
+
+template <bool AKC, bool BKC>
+int launch(const nrse_gemm_params* p, hipStream_t st) {
+  const int mt = nrse_cdiv(p->M, BM), nt = nrse_cdiv(p->N, BN);
+  const long long total = (long long)mt * nt * p->batch * p->splits;
+  hipLaunchKernelGGL((gemm256_kernel<AKC, BKC>), dim3((unsigned)total), dim3(NTHR), 0, st, *p, mt, nt);
+  return nrse_check_launch("nrse_gemm(256)");
+}
+
+}  // namespace
+
+long long nrse_gemm256_tiles(const nrse_gemm_params* p) {
+  return (long long)nrse_cdiv(p->M, BM) * nrse_cdiv(p->N, BN) * p->batch * p->splits;
+}
+
+bool nrse_gemm256_ok(const nrse_gemm_params* p) {
+  return p->M >= 128 && p->N >= 128 && dma_layout_ok(p, 256) && nrse_gemm256_tiles(p) < (1LL << 31);
+}
+
+int nrse_gemm256(const nrse_gemm_params* p, hipStream_t st) {
+  if (p->a.kcontig && p->b.kcontig) return launch<true, true>(p, st);
+  if (p->a.kcontig && !p->b.kcontig) return launch<true, false>(p, st);
+  if (!p->a.kcontig && p->b.kcontig) return launch<false, true>(p, st);
+  return launch<false, false>(p, st);
+}

@@ -11,24 +11,16 @@
 //    step t's MFMAs run; 2 workgroups per CU (72 KiB LDS each) hide each other's waits.
 //  - the 128x128 f32 accumulator tile goes through LDS so every epilogue access (bias,
 //    residual, GELU pre-activation, output) is a 16-32 B vector per lane on contiguous rows.
-#include "common.h"
+#include "gemm_common.h"
 
 namespace {
+using namespace nrse_gemm_detail;
 
 constexpr int BM = 128, BN = 128, BK = 64, NTHR = 256;
 constexpr int TILE = 16384;
 constexpr int STAGE = 2 * TILE;
 constexpr int CT_LD = 132;                       // f32 epilogue tile row stride
 constexpr int LDS_BYTES = BM * CT_LD * 4 + 1024; // >= 2 stages (64 KiB)
-constexpr unsigned OOB = 0x80000000u;
-
-typedef __attribute__((address_space(3))) void lds_void;
-
-NRSE_DEV __amdgpu_buffer_rsrc_t make_rsrc(const char* base) {
-  return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
-}
-
-NRSE_DEV long long coff(long long c, int cs, long long cmask, long long ldc) { return (c >> cs) * ldc + (c & cmask); }
 
 struct OpLoad {
   __amdgpu_buffer_rsrc_t rs;
@@ -82,66 +74,6 @@ NRSE_DEV void op_issue(const OpLoad& o, char* lds_tile, int wave, long long sego
       voff = v ? (unsigned)((segoff + (long long)k * o.ld + o.base_off[j]) * 2) : OOB;
     }
     __builtin_amdgcn_raw_ptr_buffer_load_lds(o.rs, (lds_void*)(lds_tile + (wave * 4 + j) * 1024), 16, voff, 0, 0, 0);
-  }
-}
-
-// fragment readers: identical LDS images to gemm.hip (KC: [row][k] 128 B rows, chunk ^ ((row>>1)&7);
-// !KC: [k][row] 256 B rows, chunk ^ fb(k))
-template <bool KC>
-NRSE_DEV bf16x8 frag(const char* lds, int base, int s, int lane) {
-  const int g = lane >> 4, i = lane & 15;
-  if constexpr (KC) {
-    const int row = base + i;
-    const int chunk = s * 4 + g;
-    return *reinterpret_cast<const bf16x8*>(lds + row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4));
-  } else {
-    const int q = i >> 2, p = i & 3;
-    const int col = base + 4 * p;
-    short4v lo, hi;
-    {
-      const int row = s * 32 + 8 * g + q;
-      const int fb = ((row & 3) | (((row >> 3) & 1) << 2)) << 1;
-      lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-          (__attribute__((address_space(3))) short4v*)(lds + row * 256 + (((col >> 3) ^ fb) << 4) + ((col >> 2) & 1) * 8));
-    }
-    {
-      const int row = s * 32 + 8 * g + 4 + q;
-      const int fb = ((row & 3) | (((row >> 3) & 1) << 2)) << 1;
-      hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-          (__attribute__((address_space(3))) short4v*)(lds + row * 256 + (((col >> 3) ^ fb) << 4) + ((col >> 2) & 1) * 8));
-    }
-    typedef short short8v __attribute__((ext_vector_type(8)));
-    short8v v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    return __builtin_bit_cast(bf16x8, v);
-  }
-}
-
-NRSE_DEV void ld8(const void* p, int dt, long long i, float* o) {
-  if (dt == NRSE_BF16) {
-    const uint4 u = *reinterpret_cast<const uint4*>((const bf16_t*)p + i);
-    const unsigned w[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      o[2 * e] = __uint_as_float(w[e] << 16);
-      o[2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
-    }
-  } else {
-    const float4 a = *reinterpret_cast<const float4*>((const float*)p + i);
-    const float4 b = *reinterpret_cast<const float4*>((const float*)p + i + 4);
-    o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
-  }
-}
-NRSE_DEV void st8(void* p, int dt, long long i, const float* v) {
-  if (dt == NRSE_BF16) {
-    uint4 u;
-    u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-    u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-    u.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
-    u.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
-    *reinterpret_cast<uint4*>((bf16_t*)p + i) = u;
-  } else {
-    *reinterpret_cast<float4*>((float*)p + i) = make_float4(v[0], v[1], v[2], v[3]);
-    *reinterpret_cast<float4*>((float*)p + i + 4) = make_float4(v[4], v[5], v[6], v[7]);
   }
 }
 
@@ -235,12 +167,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_dma_kernel(const nrse_gemm_param
     }
     return;
   }
-  const long long abase = zq * p.aux_z1 + zr * p.aux_z2;
-  const long long rbase = zq * p.r_z1 + zr * p.r_z2;
-  const long long bbase = zq * p.bias_z1 + zr * p.bias_z2;
-  const uint32_t key = site_key(p.seed);
-  const uint32_t thresh = dropout_threshold(p.dropout_p);
-  const float dscale = p.dropout_p < 1.f ? 1.f / (1.f - p.dropout_p) : 0.f;
+  const Epi epi(p, zq, zr, split);
   const bool colsum = (flags & NRSE_EPI_COLSUM) != 0;
 #pragma unroll 1
   for (int it = 0; it < 8; ++it) {
@@ -256,65 +183,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_dma_kernel(const nrse_gemm_param
       }
       continue;
     }
-    float v[8];
-    {
-      const float4 a = *reinterpret_cast<const float4*>(cr);
-      const float4 b = *reinterpret_cast<const float4*>(cr + 4);
-      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] *= p.alpha;
-    if (flags & NRSE_EPI_BIAS) {
-      const float4 a = *reinterpret_cast<const float4*>(p.bias + bbase + n);
-      const float4 b = *reinterpret_cast<const float4*>(p.bias + bbase + n + 4);
-      v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
-    }
-    if (flags & NRSE_EPI_GELU) {
-      if (p.aux) st8((void*)p.aux, p.aux_dtype, abase + (long long)m * p.ldaux + n, v);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = gelu_f(v[e]);
-    }
-    if (flags & NRSE_EPI_GELU_BWD) {
-      float a[8];
-      ld8(p.aux, p.aux_dtype, abase + (long long)m * p.ldaux + n, a);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] *= gelu_grad_f(a[e]);
-    }
-    if (flags & NRSE_EPI_RELU) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
-    }
-    const long long ci = cbase + (long long)m * p.ldc + n;
-    if ((flags & NRSE_EPI_DROPOUT) && !(flags & NRSE_EPI_DROP_AFTER)) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = dropout_keep(key, (uint32_t)(ci + e), thresh) ? v[e] * dscale : 0.f;
-    }
-    if (flags & NRSE_EPI_RESID) {
-      float r[8];
-      ld8(p.resid, p.resid_dtype, rbase + (long long)m * p.ldr + n, r);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += r[e];
-    }
-    if ((flags & NRSE_EPI_DROPOUT) && (flags & NRSE_EPI_DROP_AFTER)) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = dropout_keep(key, (uint32_t)(ci + e), thresh) ? v[e] * dscale : 0.f;
-    }
-    if (colsum) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) cr[e] = v[e];
-    }
-    if (flags & NRSE_EPI_ATOMIC) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) atomicAdd((float*)p.c + ci + e, v[e]);
-    } else {
-      if (flags & NRSE_EPI_ACCUM) {
-        float c[8];
-        ld8(p.c, p.c_dtype, ci, c);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += c[e];
-      }
-      st8(p.c, p.c_dtype, ci, v);
-    }
+    epi8(p, epi, m, n, cr, colsum);
   }
   if (colsum) {
     __syncthreads();
@@ -334,33 +203,9 @@ int launch(const nrse_gemm_params* p, hipStream_t st) {
   return nrse_check_launch("nrse_gemm(dma)");
 }
 
-bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
-bool m8(long long x) { return (x & 7) == 0; }
-
-// max element offset an operand can reach (for the 31-bit buffer offsets)
-long long op_span(const nrse_gemm_operand& o, const nrse_gemm_params* p, int cdim) {
-  const long long segs = (long long)p->nseg * p->splits;
-  const long long rows = o.kcontig ? cdim : p->K;
-  const long long contig = o.kcontig ? p->K : cdim;
-  long long cspan = contig;
-  if (o.chunk_shift > 0) cspan = ((contig - 1) >> o.chunk_shift) * o.ld_chunk + (1LL << o.chunk_shift);
-  return (segs - 1) * (o.seg_stride < 0 ? -o.seg_stride : o.seg_stride) + rows * o.ld + cspan + 64 * o.ld;
-}
-
 }  // namespace
 
-bool nrse_gemm_dma_ok(const nrse_gemm_params* p) {
-  if (p->a.dtype != NRSE_BF16) return false;
-  if (p->M < 64) return false;
-  if (!m8(p->N) || !m8(p->ldc) || !m8(p->c_z1) || !m8(p->c_z2) || !m8(p->c_split) || !al16(p->c)) return false;
-  const bool bias = p->flags & NRSE_EPI_BIAS;
-  if (bias && (!al16(p->bias) || (p->bias_z1 & 3) || (p->bias_z2 & 3))) return false;
-  const bool aux = (p->flags & (NRSE_EPI_GELU | NRSE_EPI_GELU_BWD)) && p->aux;
-  if (aux && (!al16(p->aux) || !m8(p->ldaux) || !m8(p->aux_z1) || !m8(p->aux_z2))) return false;
-  if ((p->flags & NRSE_EPI_RESID) && (!al16(p->resid) || !m8(p->ldr) || !m8(p->r_z1) || !m8(p->r_z2))) return false;
-  if (op_span(p->a, p, p->M) >= (1LL << 30) || op_span(p->b, p, p->N) >= (1LL << 30)) return false;
-  return true;
-}
+bool nrse_gemm_dma_ok(const nrse_gemm_params* p) { return p->M >= 64 && dma_layout_ok(p, 64); }
 
 int nrse_gemm_dma(const nrse_gemm_params* p, hipStream_t st) {
   if (p->a.kcontig && p->b.kcontig) return launch<true, true>(p, st);

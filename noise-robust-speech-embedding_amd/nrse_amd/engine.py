@@ -542,6 +542,11 @@ class ByolEngine:
             W.m_flat, W.s_flat = self.target, (self.target_sh if self.target_sh is not None else self.target)
         return W
 
+    def _side_stream(self) -> torch.cuda.Stream:
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(self.dev)
+        return self._side
+
     def stochastic_inputs(self, step_seed: int, B: int, T: int, train: bool):
         """LayerDrop decisions (rank-shared) and SpecAugment masks for both branches."""
         a = self.arch
@@ -562,6 +567,19 @@ class ByolEngine:
             s2, m2 = self.stochastic_inputs(step_seed, B, T, train)
             skips = skips if skips is not None else s2
             masks = masks if masks is not None else m2
+        # The target view (no tape, no grad) runs on a side stream concurrently with the online
+        # view: the two encoders are independent until the loss, and each one's small kernels and
+        # GEMM tail waves leave CUs idle that the other fills.
+        main = torch.cuda.current_stream(self.dev)
+        side = self._side_stream()
+        side.wait_stream(main)
+        noisy.record_stream(side)
+        with torch.cuda.stream(side):
+            Wt = self.weights("target")
+            temb, _, ex1 = self.encoder_forward(Wt, noisy, train=train, fseed=R.forward_seed(step_seed, 1, rank),
+                                                skip=skips[1], mask_np=masks[1], need_grad=False)
+            Ptp = self.group_views(self.target, "projector")
+            tproj, _ = self.projector_forward(temb, Ptp, "target_projector", train)
         Wo = self.weights("online")
         emb, tape, ex0 = self.encoder_forward(Wo, clean, train=train, fseed=R.forward_seed(step_seed, 0, rank),
                                               skip=skips[0], mask_np=masks[0], need_grad=need_grad)
@@ -569,11 +587,8 @@ class ByolEngine:
         Ppr = self.group_views(self.online, "predictor")
         proj, pc = self.projector_forward(emb, Pon, "online_projector", train)
         pred, qc = self.predictor_forward(proj, Ppr, train)
-        Wt = self.weights("target")
-        temb, _, ex1 = self.encoder_forward(Wt, noisy, train=train, fseed=R.forward_seed(step_seed, 1, rank),
-                                            skip=skips[1], mask_np=masks[1], need_grad=False)
-        Ptp = self.group_views(self.target, "projector")
-        tproj, _ = self.projector_forward(temb, Ptp, "target_projector", train)
+        main.wait_stream(side)
+        tproj.record_stream(main)
         self.executed_layers = [ex0, ex1]
         ctx = dict(tape=tape, W=Wo, pc=pc, qc=qc, emb=emb, Pon=Pon, Ppr=Ppr)
         return pred, tproj, ctx

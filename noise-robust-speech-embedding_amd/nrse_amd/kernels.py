@@ -114,6 +114,11 @@ def gemm(A: Operand, B: Operand, C: torch.Tensor, M: int, N: int, K: int, *, ldc
 _GEMM_PROBE = None
 
 
+def gemm_select(generation: int) -> int:
+    """Pin nrse_gemm's bf16 kernel generation (0 auto, 1/2 = 128x128, 3 = 256x256); returns the old one."""
+    return int(_lib.lib().nrse_gemm_select(int(generation)))
+
+
 def set_gemm_probe(lst):
     global _GEMM_PROBE
     _GEMM_PROBE = lst

@@ -206,17 +206,34 @@ def byol_loss(p: torch.Tensor, z: torch.Tensor) -> torch.Tensor:
     return 2 - 2 * s.mean()
 
 
-def split_flat(layout, flat: torch.Tensor, target: bool = False) -> dict:
-    """{'encoder': {...}, 'projector': {...}, 'predictor': {...}} of module-relative views."""
+def _flat_key(gname: str, name: str) -> str:
+    return {"encoder": "online_encoder.model.", "projector": "online_projector.",
+            "predictor": "online_predictor."}[gname] + name
+
+
+def split_flat(layout, flat: torch.Tensor, target: bool = False, leaves: bool = False) -> dict:
+    """{'encoder': {...}, 'projector': {...}, 'predictor': {...}} of module-relative views.
+    leaves=True: each view becomes its own autograd leaf (a module's parameters), so backward
+    accumulates per-tensor gradients instead of one flat-sized gradient per slice."""
     out = {"encoder": {}, "projector": {}, "predictor": {}}
     for gname, s in layout.specs:
         if target and gname == "predictor":
             continue
-        key = {"encoder": "online_encoder.model.", "projector": "online_projector.",
-               "predictor": "online_predictor."}[gname] + s.name
-        off, n, shp = layout.offsets[key]
-        out[gname][s.name] = flat[off:off + n].view(shp)
+        off, n, shp = layout.offsets[_flat_key(gname, s.name)]
+        v = flat[off:off + n].view(shp)
+        out[gname][s.name] = v.detach().requires_grad_(True) if leaves else v
     return out
+
+
+def gather_grad(layout, params: dict) -> torch.Tensor:
+    """Flat gradient in the parameter layout from a split_flat(..., leaves=True) dict."""
+    g = torch.zeros(layout.numel)
+    for gname, d in params.items():
+        for name, t in d.items():
+            off, n, _ = layout.offsets[_flat_key(gname, name)]
+            if t.grad is not None:
+                g[off:off + n] = t.grad.reshape(-1)
+    return g
 
 
 def head_buffers(proj_dim: int, pred_dim: int) -> dict:
@@ -244,10 +261,11 @@ class OracleState:
 
 
 def forward(state: OracleState, clean, noisy, *, train: bool, step_seed: int = 0, online_flat=None,
-            layer_skip=(None, None), mask_time=(None, None), time_mean: bool = True):
+            layer_skip=(None, None), mask_time=(None, None), time_mean: bool = True, online_params=None):
     """BYOLSpeechModel.forward (src/models/byol.py:75-97) -> (online_pred, target_proj, emb)."""
     a = state.layout.arch
-    on = split_flat(state.layout, state.online if online_flat is None else online_flat)
+    on = online_params if online_params is not None else \
+        split_flat(state.layout, state.online if online_flat is None else online_flat)
     tg = split_flat(state.layout, state.target, target=True)
     h = encoder_forward(on["encoder"], a, clean, train=train, fseed=rng.forward_seed(step_seed, 0),
                         layer_skip=layer_skip[0], mask_time=mask_time[0])
@@ -264,12 +282,12 @@ def forward(state: OracleState, clean, noisy, *, train: bool, step_seed: int = 0
 def train_step(state: OracleState, clean, noisy, *, lr: float, weight_decay: float, ema_decay: float,
                max_norm: float = 1.0, step_seed: int = 0, layer_skip=(None, None), mask_time=(None, None)):
     """One iteration of train_byol.py:56-74; returns dict of diagnostics."""
-    p = state.online.clone().requires_grad_(True)
-    pred, tproj, emb = forward(state, clean, noisy, train=True, step_seed=step_seed, online_flat=p,
+    params = split_flat(state.layout, state.online, leaves=True)
+    pred, tproj, emb = forward(state, clean, noisy, train=True, step_seed=step_seed, online_params=params,
                                layer_skip=layer_skip, mask_time=mask_time)
     loss = byol_loss(pred, tproj)
     loss.backward()
-    g = p.grad.detach()
+    g = gather_grad(state.layout, params)
     # clip_grad_norm_: norm of the per-parameter norms ([TORCH]nn/utils/clip_grad.py); a single
     # fp32 norm over the 3e8-element flat vector loses the small entries.
     per = [g[off:off + n].norm() for (off, n, _) in state.layout.offsets.values()]
