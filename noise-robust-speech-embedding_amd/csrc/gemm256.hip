@@ -33,6 +33,13 @@
 //    epilogue as gemm_dma.hip (epi8).
 #include "gemm_common.h"
 
+// Diagnostic builds only (tools/build_diag.sh): 1 = global loads dropped (zero-record
+// descriptors), 2 = LDS fragment reads replaced by register values, 3 = MFMAs removed,
+// 4 = main-loop barriers removed, 5 = no LDS-DMA instructions, 6 = neither LDS-DMA nor MFMAs. Outputs of those builds are wrong; only their time matters.
+#ifndef NRSE_G3_ABLATE
+#define NRSE_G3_ABLATE 0
+#endif
+
 namespace {
 using namespace nrse_gemm_detail;
 
@@ -53,79 +60,97 @@ NRSE_DEV int tile_row(int hh, int r) {
   else return (r >> 5) * 64 + hh * 32 + (r & 31);
 }
 
+NRSE_DEV bf16x8 fake_frag(int x) {
+  typedef short short8v __attribute__((ext_vector_type(8)));
+  short8v v = {(short)x, (short)(x + 1), (short)(x + 2), (short)(x + 3), (short)(x + 4), (short)(x + 5),
+               (short)(x + 6), (short)(x + 7)};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// Operand loader. Every DMA source offset splits into a per-lane part fixed for the whole kernel
+// (row/column inside the tile, 16-B chunk, k row inside the K-tile) and a wave-uniform part fixed
+// per K-tile (segment + k0), which goes in the instruction's SGPR soffset: the main loop spends no
+// vector instructions on addresses. Lanes outside the operand hold an out-of-range offset (zero
+// fill); dead K-tiles (past the end) use a zero-record descriptor.
 struct Ld {
-  __amdgpu_buffer_rsrc_t rs;
-  long long ld, ldc, seg, cmask;
-  int cs;
-  unsigned base[2][2];  // [half][instr] KC: row offset; !KC: column offset (elements)
-  int aux[2][2];        // KC: logical 16-B chunk; !KC: k row within the K-tile
-  bool ok[2][2];
+  __amdgpu_buffer_rsrc_t rs, dead;
+  long long ld, seg;
+  unsigned voff[2][2];  // [half][instr] per-lane byte offset, or OOB
+  int kpos[2][2];       // k of the lane inside the K-tile (K-tail masking)
 };
 
-// Per-lane source addresses of the 2 DMA instructions each thread issues per half-tile. The LDS
-// destination of wave w, instruction j is lane-linear (1 KiB at (2w+j) KiB), so the image swizzle
-// is applied on the source side (gemm_common.h frag()).
 template <bool KC, bool IS_A>
 NRSE_DEV void ld_init(Ld& o, const nrse_gemm_operand& d, const char* base, int wave, int lane, int row0,
                       int rows_total) {
+#if NRSE_G3_ABLATE == 1
+  o.rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0, 0x00020000);
+#else
   o.rs = make_rsrc(base);
-  o.ld = d.ld; o.ldc = d.ld_chunk; o.seg = d.seg_stride;
-  o.cs = d.chunk_shift > 0 ? d.chunk_shift : 62;
-  o.cmask = d.chunk_shift > 0 ? ((1LL << d.chunk_shift) - 1) : -1LL;
+#endif
+  o.dead = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0, 0x00020000);
+  o.ld = d.ld; o.seg = d.seg_stride;
 #pragma unroll
   for (int hh = 0; hh < 2; ++hh)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int i = wave * 2 + j;
       if constexpr (KC) {
+        // [row][k] image: 8 rows x 8 chunks per instruction, chunk position ^ ((row>>1)&7)
         const int r = 8 * i + (lane >> 3);
         const int grow = row0 + tile_row<IS_A>(hh, r);
-        o.base[hh][j] = (unsigned)((long long)grow * o.ld);
-        o.aux[hh][j] = (lane & 7) ^ ((r >> 1) & 7);
-        o.ok[hh][j] = grow < rows_total;
+        const int lc = (lane & 7) ^ ((r >> 1) & 7);
+        o.voff[hh][j] = grow < rows_total ? (unsigned)(((long long)grow * o.ld + lc * 8) * 2) : OOB;
+        o.kpos[hh][j] = lc * 8;
       } else {
+        // [k][row] image: 4 k rows x 16 chunks per instruction, chunk position ^ fbank(k)
         const int k = 4 * i + (lane >> 4);
         const int lc = (lane & 15) ^ fbank(k);
-        const long long gcol = row0 + tile_row<IS_A>(hh, lc * 8);
-        o.base[hh][j] = (unsigned)coff(gcol, o.cs, o.cmask, o.ldc);
-        o.aux[hh][j] = k;
-        o.ok[hh][j] = gcol < rows_total;
+        const int gcol = row0 + tile_row<IS_A>(hh, lc * 8);
+        o.voff[hh][j] = gcol < rows_total ? (unsigned)(((long long)k * o.ld + gcol) * 2) : OOB;
+        o.kpos[hh][j] = k;
       }
     }
 }
 
+// uniform byte offset of K-tile (segment sg, k0)
 template <bool KC>
-NRSE_DEV void ld_issue(const Ld& o, char* dst, int wave, int hh, long long segoff, int k0, int kseg, bool live) {
+NRSE_DEV unsigned ld_soff(const Ld& o, int sg, int k0) {
+  return (unsigned)(((long long)sg * o.seg + (KC ? (long long)k0 : (long long)k0 * o.ld)) * 2);
+}
+
+// stage half-tile hh: the 2 DMA instructions of this thread; krem = K - k0 (< BK only on a tail)
+NRSE_DEV void ld_issue(const Ld& o, char* dst, int wave, int hh, unsigned soff, int krem, bool live) {
+  const __amdgpu_buffer_rsrc_t rs = live ? o.rs : o.dead;
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    unsigned voff;
-    if constexpr (KC) {
-      const int k = k0 + o.aux[hh][j] * 8;
-      const bool v = live && o.ok[hh][j] && k < kseg;
-      voff = v ? (unsigned)((segoff + o.base[hh][j] + coff(k, o.cs, o.cmask, o.ldc)) * 2) : OOB;
-    } else {
-      const int k = k0 + o.aux[hh][j];
-      const bool v = live && o.ok[hh][j] && k < kseg;
-      voff = v ? (unsigned)((segoff + (long long)k * o.ld + o.base[hh][j]) * 2) : OOB;
-    }
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(o.rs, (lds_void*)(dst + (wave * 2 + j) * 1024), 16, voff, 0, 0, 0);
+    unsigned voff = o.voff[hh][j];
+    if (krem < BK) voff = o.kpos[hh][j] < krem ? voff : OOB;
+#if NRSE_G3_ABLATE == 5 || NRSE_G3_ABLATE == 6
+    asm volatile("" ::"v"(voff), "s"(soff));
+#else
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(dst + (wave * 2 + j) * 1024), 16, voff, soff, 0, 0);
+#endif
   }
 }
 
 // raw workgroup barrier: orders LDS accesses for the compiler, emits no vmcnt wait
+#if NRSE_G3_ABLATE == 4
+#define NRSE_BAR() asm volatile("" ::: "memory")
+#else
 #define NRSE_BAR()                            \
   do {                                        \
     asm volatile("" ::: "memory");            \
     __builtin_amdgcn_s_barrier();             \
     asm volatile("" ::: "memory");            \
   } while (0)
+#endif
 
 template <bool AKC, bool BKC>
 __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params p, int mt, int nt) {
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
 
   // XCD-aware, M-grouped tile order
@@ -155,19 +180,26 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
   const int seg0 = split * p.nseg;
   const int ntiles = p.nseg * tps;
 
-  // K-tile t -> (segment, k0); t >= ntiles -> dead (zero-fill loads keep the vmcnt counts uniform)
-  auto tile_pos = [&](int t, int& sg, int& k0) {
-    const int tc = t < ntiles ? t : 0;
-    sg = seg0 + tc / tps;
-    k0 = (tc % tps) * BK;
+  // K-tile t -> uniform source offsets of A and B and the K remainder; t >= ntiles -> dead
+  struct TilePos { unsigned sa, sb; int krem; bool live; };
+  auto tile_pos = [&](int t) {
+    TilePos q;
+    q.live = t < ntiles;
+    const int tc = q.live ? t : 0;
+    const int sg = seg0 + tc / tps;
+    const int k0 = (tc % tps) * BK;
+    q.sa = ld_soff<AKC>(la, sg, k0);
+    q.sb = ld_soff<BKC>(lb, sg, k0);
+    q.krem = p.K - k0;
+    return q;
   };
   // half-tile index j of a K-tile in staging (= first-read) order: 0 A-lo, 1 B-lo, 2 B-hi, 3 A-hi
-  auto stage = [&](int j, bool live, int sg, int k0, int slot) {
+  auto stage = [&](int j, const TilePos& q, int slot) {
     char* dst = smem + slot * HALF;
-    if (j == 0) ld_issue<AKC>(la, dst, wave, 0, (long long)sg * la.seg, k0, p.K, live);
-    else if (j == 1) ld_issue<BKC>(lb, dst, wave, 0, (long long)sg * lb.seg, k0, p.K, live);
-    else if (j == 2) ld_issue<BKC>(lb, dst, wave, 1, (long long)sg * lb.seg, k0, p.K, live);
-    else ld_issue<AKC>(la, dst, wave, 1, (long long)sg * la.seg, k0, p.K, live);
+    if (j == 0) ld_issue(la, dst, wave, 0, q.sa, q.krem, q.live);
+    else if (j == 1) ld_issue(lb, dst, wave, 0, q.sb, q.krem, q.live);
+    else if (j == 2) ld_issue(lb, dst, wave, 1, q.sb, q.krem, q.live);
+    else ld_issue(la, dst, wave, 1, q.sa, q.krem, q.live);
   };
   auto wrap = [](int x) { return x >= SLOTS ? x - SLOTS : x; };
 
@@ -180,33 +212,40 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
   // prologue: K-tiles 0 and 1 (half-tile sequence numbers 0..7, slot = seq % 10), then wait for
   // the two read in phase 0 (6 younger half-tiles = 12 DMAs may stay in flight)
   {
-    int sg, k0;
-    tile_pos(0, sg, k0);
+    const TilePos q0 = tile_pos(0), q1 = tile_pos(1);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) stage(j, 0 < ntiles, sg, k0, j);
-    tile_pos(1, sg, k0);
+    for (int j = 0; j < 4; ++j) stage(j, q0, j);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) stage(j, 1 < ntiles, sg, k0, 4 + j);
+    for (int j = 0; j < 4; ++j) stage(j, q1, 4 + j);
   }
   asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
   NRSE_BAR();
 
   bf16x8 fa[4][2], fbl[2][2], fbh[2][2];
+#if NRSE_G3_ABLATE == 2
+#define NRSE_FRAG(KC, L, B, S, LN) fake_frag((B) + (S) + (LN) + t)
+#else
+#define NRSE_FRAG(KC, L, B, S, LN) frag<KC>(L, B, S, LN)
+#endif
+#if NRSE_G3_ABLATE == 3 || NRSE_G3_ABLATE == 6
+#define NRSE_MFMA(C, A, B) asm volatile("" ::"v"(A), "v"(B))
+#else
+#define NRSE_MFMA(C, A, B) C = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B, C, 0, 0, 0)
+#endif
 #define NRSE_READ_A(SLOT)                                                                \
   _Pragma("unroll") for (int fi = 0; fi < 4; ++fi)                                     \
   _Pragma("unroll") for (int s = 0; s < 2; ++s)                                        \
-    fa[fi][s] = frag<AKC>(smem + (SLOT) * HALF, wm * 64 + fi * 16, s, lane);
+    fa[fi][s] = NRSE_FRAG(AKC, smem + (SLOT) * HALF, wm * 64 + fi * 16, s, lane);
 #define NRSE_READ_B(SLOT, FB)                                                            \
   _Pragma("unroll") for (int fj = 0; fj < 2; ++fj)                                     \
   _Pragma("unroll") for (int s = 0; s < 2; ++s)                                        \
-    FB[fj][s] = frag<BKC>(smem + (SLOT) * HALF, wn * 32 + fj * 16, s, lane);
+    FB[fj][s] = NRSE_FRAG(BKC, smem + (SLOT) * HALF, wn * 32 + fj * 16, s, lane);
 #define NRSE_QUAD(MH, NH, FB)                                                            \
   __builtin_amdgcn_s_setprio(1);                                                         \
   _Pragma("unroll") for (int s = 0; s < 2; ++s)                                        \
   _Pragma("unroll") for (int fi = 0; fi < 4; ++fi)                                     \
   _Pragma("unroll") for (int fj = 0; fj < 2; ++fj)                                     \
-    acc[(MH) * 4 + fi][(NH) * 2 + fj] =                                                  \
-        __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[fi][s], FB[fj][s], acc[(MH) * 4 + fi][(NH) * 2 + fj], 0, 0, 0); \
+    NRSE_MFMA(acc[(MH) * 4 + fi][(NH) * 2 + fj], fa[fi][s], FB[fj][s]);                  \
   __builtin_amdgcn_s_setprio(0);
 // the wait before each phase's first barrier retires every half-tile the NEXT phase reads
 #define NRSE_WAIT() asm volatile("s_waitcnt vmcnt(12)" ::: "memory")
@@ -218,33 +257,31 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
   for (int t = 0; t < ntiles; ++t) {
     const int s0 = base, s1 = wrap(base + 1), s2 = wrap(base + 2), s3 = wrap(base + 3);
     // phase p stages half-tile j = p of K-tile t+2 (sequence 4t+8+p) into slot (4t+8+p) % 10
-    int sg2, k02;
-    tile_pos(t + 2, sg2, k02);
-    const bool live2 = t + 2 < ntiles;
+    const TilePos q2 = tile_pos(t + 2);
     // phase 0: quadrant (M-half 0, N-half 0) from A-lo, B-lo
     NRSE_READ_A(s0)
     NRSE_READ_B(s1, fbl)
-    stage(0, live2, sg2, k02, wrap(base + 8));
+    stage(0, q2, wrap(base + 8));
     NRSE_WAIT();
     NRSE_BAR();
     NRSE_QUAD(0, 0, fbl)
     NRSE_BAR();
     // phase 1: (0, 1) from B-hi
     NRSE_READ_B(s2, fbh)
-    stage(1, live2, sg2, k02, wrap(base + 9));
+    stage(1, q2, wrap(base + 9));
     NRSE_WAIT();
     NRSE_BAR();
     NRSE_QUAD(0, 1, fbh)
     NRSE_BAR();
     // phase 2: (1, 1) from A-hi
     NRSE_READ_A(s3)
-    stage(2, live2, sg2, k02, base);  // (4t + 10) % 10
+    stage(2, q2, base);  // (4t + 10) % 10
     NRSE_WAIT();
     NRSE_BAR();
     NRSE_QUAD(1, 1, fbh)
     NRSE_BAR();
     // phase 3: (1, 0) from registers
-    stage(3, live2, sg2, k02, s1);    // (4t + 11) % 10
+    stage(3, q2, s1);    // (4t + 11) % 10
     NRSE_WAIT();
     NRSE_BAR();
     NRSE_QUAD(1, 0, fbl)
@@ -256,6 +293,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
 #undef NRSE_READ_B
 #undef NRSE_QUAD
 #undef NRSE_WAIT
+#undef NRSE_FRAG
+#undef NRSE_MFMA
 
   // ---------------------------------------------------------------- epilogue: 4 x 64-row passes
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing zero-fill DMAs
@@ -335,7 +374,9 @@ long long nrse_gemm256_tiles(const nrse_gemm_params* p) {
 }
 
 bool nrse_gemm256_ok(const nrse_gemm_params* p) {
-  return p->M >= 128 && p->N >= 128 && dma_layout_ok(p, 256) && nrse_gemm256_tiles(p) < (1LL << 31);
+  return p->M >= 128 && p->N >= 128 && p->a.chunk_shift == 0 && p->b.chunk_shift == 0 &&
+         p->a.seg_stride >= 0 && p->b.seg_stride >= 0 && dma_layout_ok(p, 256) &&
+         nrse_gemm256_tiles(p) < (1LL << 31);
 }
 
 int nrse_gemm256(const nrse_gemm_params* p, hipStream_t st) {

@@ -9,7 +9,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libnrse_hip.so")
+# NRSE_LIB_PATH: load a differently built copy of the same library (diagnostic builds)
+LIB_PATH = os.environ.get("NRSE_LIB_PATH") or os.path.join(_HERE, "libnrse_hip.so")
 
 F32 = 0
 BF16 = 1
