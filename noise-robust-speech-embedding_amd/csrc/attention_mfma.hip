@@ -15,11 +15,19 @@
 // image stay (nearly) conflict-free.
 #include "common.h"
 
+// Diagnostic builds only (NRSE_ATT_ABLATE, tools/build_diag.sh): in attn_bwd_kv,
+// 1 = no diagonal LDS atomics, 2 = no dropout hash, 3 = no Q/dO/bias re-staging after the first
+// query block. Outputs of those builds are wrong; only their time matters.
+#ifndef NRSE_ATT_ABLATE
+#define NRSE_ATT_ABLATE 0
+#endif
+
 namespace {
 
 constexpr int D = 64;
 constexpr int TILE_B = 64 * 128;  // bytes per 64x64 bf16 tile
 constexpr int BT_LD = 68;         // f32 bias tile row stride (dK/dV kernel)
+constexpr int DPAD = 80;          // low-side margin of the LDS diagonal arrays (dK/dV kernel)
 typedef short short8v __attribute__((ext_vector_type(8)));
 
 NRSE_DEV int loff(int row, int chunk) { return row * 128 + ((chunk ^ (((row >> 1) & 3) << 1)) << 4); }
@@ -44,6 +52,17 @@ NRSE_DEV bf16x8 rd_tr(const char* t, int r0, int r1, int c0, int lane) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// Register r of a 16x16 MFMA C block rotated left by r lanes within each 16-lane row (DPP
+// row_ror:(16 - r): lane x receives lane (x + r) mod 16), added to the accumulator of its
+// diagonal: lo if the rotation did not wrap, hi (16 further down) if it did.
+template <int R>
+NRSE_DEV void diag_rot(float v, int x, float& lo, float& hi) {
+  const float u = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x120 + 16 - R, 0xF, 0xF, false));
+  const bool wrap = x >= 16 - R;
+  lo += wrap ? 0.f : u;
+  hi += wrap ? u : 0.f;
+}
+
 NRSE_DEV bf16x8 pack8(const float* a, const float* b) {
   bf16x8 v;
 #pragma unroll
@@ -51,19 +70,28 @@ NRSE_DEV bf16x8 pack8(const float* a, const float* b) {
   return v;
 }
 
-// Stage a 64-row x 64-d bf16 tile (rows row0.., column offset col_off in a row of ld elements)
-// with 256 threads: each thread two 16-byte chunks.
-NRSE_DEV void stage_tile(char* t, const bf16_t* base, long long ld, int row0, int nrows, int tid) {
+// A 64-row x 64-d bf16 tile (rows row0.. of a matrix with row stride ld) moved by 256 threads,
+// two 16-byte chunks each: tile_load issues the global loads into registers (the prefetch of the
+// next tile, in flight while the current one is computed), tile_store writes them to LDS.
+struct TileRegs {
+  uint4 a, b;
+};
+NRSE_DEV TileRegs tile_load(const bf16_t* base, long long ld, int row0, int nrows, int tid) {
   const int row = tid >> 2;
   const int c0 = (tid & 3) * 2;
-  uint4 a = make_uint4(0, 0, 0, 0), b = make_uint4(0, 0, 0, 0);
+  TileRegs r{make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
   if (row0 + row < nrows) {
     const bf16_t* src = base + (long long)(row0 + row) * ld + c0 * 8;
-    a = *reinterpret_cast<const uint4*>(src);
-    b = *reinterpret_cast<const uint4*>(src + 8);
+    r.a = *reinterpret_cast<const uint4*>(src);
+    r.b = *reinterpret_cast<const uint4*>(src + 8);
   }
-  *reinterpret_cast<uint4*>(t + loff(row, c0)) = a;
-  *reinterpret_cast<uint4*>(t + loff(row, c0 + 1)) = b;
+  return r;
+}
+NRSE_DEV void tile_store(char* t, const TileRegs& r, int tid) {
+  const int row = tid >> 2;
+  const int c0 = (tid & 3) * 2;
+  *reinterpret_cast<uint4*>(t + loff(row, c0)) = r.a;
+  *reinterpret_cast<uint4*>(t + loff(row, c0 + 1)) = r.b;
 }
 
 // ------------------------------------------------------------------------------ forward
@@ -101,10 +129,12 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // (no register prefetch here: at 95 VGPRs the kernel runs 5 waves per SIMD, which hides the
+  // staging latency better than a prefetch that costs a wave)
   for (int kb = 0; kb < T; kb += 64) {
     __syncthreads();
-    stage_tile(Kt, qkv + Hd + h * D, ld3, kb, T, tid);
-    stage_tile(Vt, qkv + 2 * Hd + h * D, ld3, kb, T, tid);
+    tile_store(Kt, tile_load(qkv + Hd + h * D, ld3, kb, T, tid), tid);
+    tile_store(Vt, tile_load(qkv + 2 * Hd + h * D, ld3, kb, T, tid), tid);
     __syncthreads();
     f32x4 s[4];
 #pragma unroll
@@ -226,11 +256,17 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
   f32x4 dq[4];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  TileRegs kn = tile_load(qkv + Hd + h * D, ld3, 0, T, tid);
+  TileRegs vn = tile_load(qkv + 2 * Hd + h * D, ld3, 0, T, tid);
   for (int kb = 0; kb < T; kb += 64) {
     __syncthreads();
-    stage_tile(Kt, qkv + Hd + h * D, ld3, kb, T, tid);
-    stage_tile(Vt, qkv + 2 * Hd + h * D, ld3, kb, T, tid);
+    tile_store(Kt, kn, tid);
+    tile_store(Vt, vn, tid);
     __syncthreads();
+    if (kb + 64 < T) {
+      kn = tile_load(qkv + Hd + h * D, ld3, kb + 64, T, tid);
+      vn = tile_load(qkv + 2 * Hd + h * D, ld3, kb + 64, T, tid);
+    }
     f32x4 s[4], dp[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -315,11 +351,16 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(const nrse_attn_bwd_pa
     kf[s] = __builtin_bit_cast(bf16x8, a);
     vf[s] = __builtin_bit_cast(bf16x8, c);
   }
-  // one diagonal accumulator per lane group g: the 16 lanes of a group hit distinct diagonals,
-  // so an LDS atomic wave instruction never serialises on one address
-  const int ndiag = T + 64;
+  // rel_attn_embed gradient: sum over (q, k) of gate[q] * dS[q, k] per diagonal k - q. Lane
+  // (g, i16) holds keys i16 and queries 16t + 4g + r; rotating register r left by r lanes
+  // within each 16-lane row (DPP) puts diagonal (i16 - 4g - 16t) or (i16 - 4g - 16t - 16) in
+  // lane i16 of row g, so 5 per-lane register accumulators (dacc[j], diagonal x - 4g - 16j
+  // relative to the block) collect a 64x64 tile; 4 of them are final after each query block
+  // and go to a per-row LDS array (rows of one wave never share a diagonal within a row array).
+  const int ndiag = T + 64 + DPAD;
   for (int e = tid; e < 4 * ndiag; e += 256) diag[e] = 0.f;
   float* mydiag = diag + g * ndiag;
+  float dacc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
   const long long bh = (long long)b * H + h;
   const uint32_t key = site_key(p.seed);
   const uint32_t thr = dropout_threshold(p.dropout_p);
@@ -330,28 +371,54 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(const nrse_attn_bwd_pa
   f32x4 dk[4], dv[4];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) dk[dt] = dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // diag index of (query qi, key kj): (kj - qi) - (kb0 - T + 1)
-  const int dbase = kb0 - T + 1;
-  for (int qb = 0; qb < T; qb += 64) {
-    __syncthreads();
-    stage_tile(Qt, qkv + h * D, ld3, qb, T, tid);
-    stage_tile(Ot, dctx + h * D, Hd, qb, T, tid);
+  // LDS index of diagonal kj - qi: (kj - qi) - (kb0 - T + 1) + DPAD
+  const int dbase = kb0 - T + 1 - DPAD;
+  // next query block in registers: Q and dO tiles, lse/delta/gate, bias[h, qb:qb+64, kb0:kb0+64]
+  TileRegs qn, on;
+  float4 bn[4];
+  float rn[3];
+  auto prefetch = [&](int qb) {
+    qn = tile_load(qkv + h * D, ld3, qb, T, tid);
+    on = tile_load(dctx + h * D, Hd, qb, T, tid);
     if (tid < 64) {
       const int q = qb + tid;
       const bool ok = q < T;
-      rowc[tid] = ok ? p.lse[bh * T + q] : 0.f;
-      rowc[64 + tid] = ok ? p.delta[bh * T + q] : 0.f;
-      rowc[128 + tid] = ok ? p.gate[bh * T + q] : 0.f;
+      rn[0] = ok ? p.lse[bh * T + q] : 0.f;
+      rn[1] = ok ? p.delta[bh * T + q] : 0.f;
+      rn[2] = ok ? p.gate[bh * T + q] : 0.f;
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {  // bias[h, qb:qb+64, kb0:kb0+64] -> LDS (rows padded in the table)
+    for (int u = 0; u < 4; ++u) {
       const int e = tid + 256 * u;
       const int row = e >> 4, c4 = (e & 15) * 4;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (qb + row < T) v = *reinterpret_cast<const float4*>(bsrc + (long long)(qb + row) * Tb + c4);
-      *reinterpret_cast<float4*>(btile + row * BT_LD + c4) = v;
+      bn[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (qb + row < T) bn[u] = *reinterpret_cast<const float4*>(bsrc + (long long)(qb + row) * Tb + c4);
     }
+  };
+  prefetch(0);
+  for (int qb = 0; qb < T; qb += 64) {
     __syncthreads();
+#if NRSE_ATT_ABLATE == 3
+    if (qb == 0) {
+#endif
+    tile_store(Qt, qn, tid);
+    tile_store(Ot, on, tid);
+    if (tid < 64) {
+      rowc[tid] = rn[0];
+      rowc[64 + tid] = rn[1];
+      rowc[128 + tid] = rn[2];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + 256 * u;
+      const int row = e >> 4, c4 = (e & 15) * 4;
+      *reinterpret_cast<float4*>(btile + row * BT_LD + c4) = bn[u];
+    }
+#if NRSE_ATT_ABLATE == 3
+    }
+#endif
+    __syncthreads();
+    if (qb + 64 < T) prefetch(qb + 64);
     f32x4 s[4], dp[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -364,31 +431,51 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(const nrse_attn_bwd_pa
       }
     }
     // element (query qb + 16t + 4g + r, key kj)
-    float pd[4][4], ds[4][4];
+    float pd[4][4], ds[4][4], gv[4][4];
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int ql = 16 * t + 4 * g + r;
         const int q = qb + ql;
-        float pv = 0.f, d = 0.f;
+        float pv = 0.f, d = 0.f, gdv = 0.f;
         if (q < T && kv) {
           const float gq = rowc[128 + ql];
           const float x = s[t][r] * p.scale + gq * btile[ql * BT_LD + kl];
           const float pr = __expf(x - rowc[ql]);
           float dpv = dp[t][r];
           pv = pr * dsc;
+#if NRSE_ATT_ABLATE != 2
           if (drop) {
             const bool keep = dropout_keep(key, (uint32_t)((bh * T + q) * T + kj), thr);
             if (!keep) { pv = 0.f; dpv = 0.f; }
             else dpv *= dsc;
           }
+#endif
           d = pr * (dpv - rowc[64 + ql]);
-          if (p.diag) atomicAdd(&mydiag[kj - q - dbase], d * gq);
+          gdv = d * gq;
         }
         pd[t][r] = pv;
         ds[t][r] = d;
+        gv[t][r] = gdv;
       }
+#if NRSE_ATT_ABLATE != 1
+    if (p.diag) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        dacc[t] += gv[t][0];
+        diag_rot<1>(gv[t][1], i16, dacc[t], dacc[t + 1]);
+        diag_rot<2>(gv[t][2], i16, dacc[t], dacc[t + 1]);
+        diag_rot<3>(gv[t][3], i16, dacc[t], dacc[t + 1]);
+      }
+      // diagonals x - 4g - 16j (j < 4) relative to kb0 + 16w - qb are complete
+      const int c0 = kb0 + 16 * w - qb + i16 - 4 * g - dbase;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) atomicAdd(&mydiag[c0 - 16 * j], dacc[j]);
+      dacc[0] = dacc[4];
+      dacc[1] = dacc[2] = dacc[3] = dacc[4] = 0.f;
+    }
+#endif
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       const bf16x8 pa = pack8(pd[2 * c], pd[2 * c + 1]);
@@ -413,6 +500,10 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(const nrse_attn_bwd_pa
       }
     }
   }
+  if (p.diag) {  // the carried accumulator: diagonals x - 4g relative to kb0 + 16w - (last qb + 64)
+    const int qend = ((T + 63) / 64) * 64;
+    atomicAdd(&mydiag[kb0 + 16 * w - qend + i16 - 4 * g - dbase], dacc[0]);
+  }
   __syncthreads();
   if (p.diag) {
     const int nd = 2 * T - 1;
@@ -436,7 +527,7 @@ int nrse_attn_fwd_mfma(const nrse_attn_fwd_params* p, hipStream_t st) {
 
 int nrse_attn_bwd_mfma(const nrse_attn_bwd_params* p, hipStream_t st) {
   dim3 grid((p->T + 63) / 64, p->H, p->batch);
-  const size_t lds_kv = 2 * TILE_B + (192 + 64 * BT_LD + 4 * (p->T + 64)) * sizeof(float);
+  const size_t lds_kv = 2 * TILE_B + (192 + 64 * BT_LD + 4 * (p->T + 64 + DPAD)) * sizeof(float);
   if (lds_kv > 160 * 1024) {
     nrse_set_error("nrse_attn_bwd: T=%d too long for the LDS diagonal accumulator", p->T);
     return NRSE_ERR_UNSUPPORTED;
