@@ -70,7 +70,7 @@ int nrse_abi_version(void);
  * C + s*c_split.
  * ------------------------------------------------------------------------------------------ */
 enum {
-  NRSE_EPI_BIAS = 1 << 0,         /* v += bias[n] (f32) */
+  NRSE_EPI_BIAS = 1 << 0,         /* v += bias[n] (f32); with splits > 1 only split 0 adds it */
   NRSE_EPI_GELU = 1 << 1,         /* aux <- v (if aux); v = gelu_erf(v) */
   NRSE_EPI_GELU_BWD = 1 << 2,     /* v *= gelu_erf'(aux[m,n]) */
   NRSE_EPI_DROPOUT = 1 << 3,      /* v = keep ? v/(1-p) : 0   (before residual) */
@@ -183,11 +183,11 @@ int nrse_rel_bias_bwd(const float* diag, const int* bucket, float* dE, int H, in
  * ([TF]modeling_wavlm.py:164-176). x1 [B*T, Hd] (the LN1 output), W [8, 64], bias [8], c [H]. */
 int nrse_gate_fwd(const void* x1, int x_dtype, const float* W, const float* bvec, const float* c, float* gate,
                   int batch, int T, int H, void* stream);
-/* Gate backward, one wave per (row, head): dx1 (f32) += W^T dproj; writes dproj [B*T*H, 8]
- * (x dtype; row n = row*H + h, so d(gru_rel_pos_linear.weight) = dproj^T x1.view(-1, 64) is a
- * GEMM and d(bias) a column sum) and dcterm [B*T, H] f32 (d(gru_rel_pos_const) = its column sum). */
+/* Gate backward, fused: dx1 (f32 [B*T, Hd]) += the gate-path gradient, and the parameter
+ * gradients accumulated (f32 atomics): dW [8, 64] (gru_rel_pos_linear.weight), db [8] (its
+ * bias), dc [H] (gru_rel_pos_const). x1, dx1 16-byte aligned. */
 int nrse_gate_bwd(const void* x1, int x_dtype, const float* W, const float* bvec, const float* c, const float* dgate,
-                  float* dx1, void* dproj, float* dcterm, int batch, int T, int H, void* stream);
+                  float* dx1, float* dW, float* db, float* dc, int batch, int T, int H, void* stream);
 
 typedef struct {
   const void* qkv; int dtype;     /* q/k/v (bf16 or f32) */
@@ -263,6 +263,11 @@ int nrse_specaug_bwd(const float* dh, const unsigned char* mask, float* dembed, 
 /* out[i] = in[i] * dropout_mask(seed, p)[i] (cast); in f32, out f32/bf16 */
 int nrse_dropout_cast(const float* in, void* out, int out_dtype, long long n, float dropout_p, uint32_t seed,
                       void* stream);
+/* out[r, c] = in[r, c] * dropout_mask(seed, p)[r*C + c] (cast) and colsum[c] += sum_r out[r, c]
+ * in one pass (the nn.Dropout backward feeding a Linear: its input gradient and bias gradient,
+ * [TF]modeling_wavlm.py:294, 482). C % 8 == 0, 16-byte aligned. */
+int nrse_dropout_cast_colsum(const float* in, void* out, int out_dtype, long long rows, int C, float dropout_p,
+                             uint32_t seed, float* colsum, void* stream);
 /* colsum[c] += sum_r x[r, c] (f32 atomics) */
 int nrse_colsum(const void* x, int dtype, float* colsum, long long rows, int C, void* stream);
 /* y = x cast (f32 <-> bf16), n elements */

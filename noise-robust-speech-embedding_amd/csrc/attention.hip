@@ -33,68 +33,154 @@ __global__ void rel_bias_bwd_kernel(const float* __restrict__ diag, const int* _
   if (d < nd) atomicAdd(dE + bucket[d] * H + h, diag[(long long)h * nd + d]);
 }
 
-// gate: one thread per (row, head)
-template <typename T>
-__global__ void gate_fwd_kernel(const void* __restrict__ x1, const float* __restrict__ W, const float* __restrict__ bv,
-                                const float* __restrict__ c, float* __restrict__ gate, int batch, int Tn, int H) {
-  __shared__ float w[8 * HD];
-  for (int i = threadIdx.x; i < 8 * HD; i += blockDim.x) w[i] = W[i];
-  __syncthreads();
-  const long long n = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long total = (long long)batch * Tn * H;
-  if (n >= total) return;
-  const long long row = n / H;
-  const int h = (int)(n % H);
-  float pr[8];
+// Gate projections. gru_rel_pos_linear is Linear(64 -> 8) shared by all heads, and only the
+// pair sums of its outputs are used (view(.., 2, 4).sum(-1), [TF]modeling_wavlm.py:168-176),
+// so the 8 rows of W fold into two 64-vectors wa = sum_{r<4} W[r], wb = sum_{r>=4} W[r]:
+// a = sigmoid(x.wa + sum_{r<4} b[r]), b = sigmoid(x.wb + sum_{r>=4} b[r]).
+// Item n = row * H + h is the head-h slice x1[row, 64h : 64h + 64] (64 contiguous values);
+// one 8-lane group per item, lane sub holds dims 8*sub .. 8*sub + 7 (one 16-byte bf16 load).
+template <typename T> NRSE_DEV void ld8v(const void* p, long long i, float* o);
+template <> NRSE_DEV void ld8v<bf16_t>(const void* p, long long i, float* o) {
+  const uint4 u = *reinterpret_cast<const uint4*>((const bf16_t*)p + i);
+  const unsigned w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
-  for (int r = 0; r < 8; ++r) pr[r] = bv[r];
-  const long long base = row * (long long)H * HD + h * HD;
-  for (int i = 0; i < HD; ++i) {
-    const float x = ld<T>(x1, base + i);
-#pragma unroll
-    for (int r = 0; r < 8; ++r) pr[r] += x * w[r * HD + i];
+  for (int e = 0; e < 4; ++e) {
+    o[2 * e] = __uint_as_float(w[e] << 16);
+    o[2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
   }
-  const float a = 1.f / (1.f + __expf(-(pr[0] + pr[1] + pr[2] + pr[3])));
-  const float b = 1.f / (1.f + __expf(-(pr[4] + pr[5] + pr[6] + pr[7])));
-  const long long bi = row / Tn, t = row % Tn;
-  gate[(bi * H + h) * Tn + t] = a * (b * c[h] - 1.f) + 2.f;
+}
+template <> NRSE_DEV void ld8v<float>(const void* p, long long i, float* o) {
+  const float4 a = *reinterpret_cast<const float4*>((const float*)p + i);
+  const float4 b = *reinterpret_cast<const float4*>((const float*)p + i + 4);
+  o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
 }
 
-// gate backward: one wave per (row, head), lane = head dim i. Recomputes the 8 projections
-// with wave reductions, then dx1[i] += sum_r dproj[r] W[r][i] (coalesced read-modify-write),
-// dproj [n][8] and dcterm [n] out for the GEMM / column-sum reductions done by the caller.
+struct GateW {
+  float wa[8], wb[8], ba, bb;
+  NRSE_DEV GateW(const float* W, const float* bv, int sub) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int i = 8 * sub + e;
+      wa[e] = W[i] + W[HD + i] + W[2 * HD + i] + W[3 * HD + i];
+      wb[e] = W[4 * HD + i] + W[5 * HD + i] + W[6 * HD + i] + W[7 * HD + i];
+    }
+    ba = bv[0] + bv[1] + bv[2] + bv[3];
+    bb = bv[4] + bv[5] + bv[6] + bv[7];
+  }
+  // (a, b) of the item whose 8 values this lane holds (sums over the 8-lane group)
+  NRSE_DEV void ab(const float* x, float& a, float& b) const {
+    float sa = 0.f, sb = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { sa += x[e] * wa[e]; sb += x[e] * wb[e]; }
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) { sa += __shfl_xor(sa, o, 64); sb += __shfl_xor(sb, o, 64); }
+    a = 1.f / (1.f + __expf(-(sa + ba)));
+    b = 1.f / (1.f + __expf(-(sb + bb)));
+  }
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void gate_fwd_kernel(const void* __restrict__ x1, const float* __restrict__ W,
+                                                       const float* __restrict__ bv, const float* __restrict__ c,
+                                                       float* __restrict__ gate, int batch, int Tn, int H) {
+  const int lane = threadIdx.x & 63, sub = lane & 7, ig = lane >> 3;
+  const GateW gw(W, bv, sub);
+  const long long total = (long long)batch * Tn * H;
+  const long long wave = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long long nwave = (long long)gridDim.x * (blockDim.x >> 6);
+  for (long long n0 = wave * 8; n0 < total; n0 += nwave * 8) {
+    const long long n = n0 + ig;
+    float x[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (n < total) ld8v<T>(x1, n * HD + 8 * sub, x);
+    float a, b;
+    gw.ab(x, a, b);
+    if (sub == 0 && n < total) {
+      const long long row = n / H;
+      const int h = (int)(n % H);
+      const long long bi = row / Tn, t = row % Tn;
+      gate[(bi * H + h) * Tn + t] = a * (b * c[h] - 1.f) + 2.f;
+    }
+  }
+}
+
+// Gate backward, fully fused: dx1 += dpa * wa + dpb * wb (f32 read-modify-write), and the
+// parameter gradients reduced in registers -> LDS -> one set of atomics per workgroup:
+//   dW[r < 4] += sum_n dpa_n x_n,  dW[r >= 4] += sum_n dpb_n x_n,  db likewise,
+//   dc[h] += sum_{n of head h} dgate * a * b.
+// The grid is a multiple of H workgroups, so the item stride (8 per wave per step) is a
+// multiple of H and every 8-lane group keeps one head for the whole loop.
+constexpr int GATE_BWD_BLOCKS_PER_HEAD = 16;
 template <typename T>
 __global__ __launch_bounds__(256) void gate_bwd_kernel(const void* __restrict__ x1, const float* __restrict__ W,
                                                        const float* __restrict__ bv, const float* __restrict__ c,
                                                        const float* __restrict__ dgate, float* __restrict__ dx1,
-                                                       T* __restrict__ dproj, float* __restrict__ dcterm, int batch,
-                                                       int Tn, int H) {
-  const int lane = threadIdx.x & 63;
-  const long long n = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+                                                       float* __restrict__ dW, float* __restrict__ db,
+                                                       float* __restrict__ dc, int batch, int Tn, int H) {
+  __shared__ float red[4][2][HD];
+  __shared__ float reds[4][2];
+  const int lane = threadIdx.x & 63, sub = lane & 7, ig = lane >> 3, w = threadIdx.x >> 6;
+  const GateW gw(W, bv, sub);
   const long long total = (long long)batch * Tn * H;
-  if (n >= total) return;
-  const long long row = n / H;
-  const int h = (int)(n % H);
-  const long long base = row * (long long)H * HD + h * HD;
-  const float x = ld<T>(x1, base + lane);
-  float w[8];
-#pragma unroll
-  for (int r = 0; r < 8; ++r) w[r] = W[r * HD + lane];
-  float sa = 0.f, sb = 0.f;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) { sa += x * w[r]; sb += x * w[4 + r]; }
-  sa = wave_sum(sa) + bv[0] + bv[1] + bv[2] + bv[3];
-  sb = wave_sum(sb) + bv[4] + bv[5] + bv[6] + bv[7];
-  const float a = 1.f / (1.f + __expf(-sa));
-  const float b = 1.f / (1.f + __expf(-sb));
-  const long long bi = row / Tn, t = row % Tn;
-  const float dg = dgate[(bi * H + h) * Tn + t];
+  const long long wave = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long long nwave = (long long)gridDim.x * (blockDim.x >> 6);
+  const int h = (int)((wave * 8 + ig) % H);
   const float ch = c[h];
-  const float dpa = dg * (b * ch - 1.f) * a * (1.f - a);
-  const float dpb = dg * a * ch * b * (1.f - b);
-  dx1[base + lane] += dpa * (w[0] + w[1] + w[2] + w[3]) + dpb * (w[4] + w[5] + w[6] + w[7]);
-  if (lane < 8) dproj[n * 8 + lane] = from_f<T>(lane < 4 ? dpa : dpb);
-  if (lane == 8) dcterm[n] = dg * a * b;
+  float accA[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, accB[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float sdpa = 0.f, sdpb = 0.f, sdc = 0.f;
+  for (long long n0 = wave * 8; n0 < total; n0 += nwave * 8) {
+    const long long n = n0 + ig;
+    const bool ok = n < total;
+    float x[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (ok) ld8v<T>(x1, n * HD + 8 * sub, x);
+    float a, b;
+    gw.ab(x, a, b);
+    float dg = 0.f;
+    if (ok) {
+      const long long row = n / H;
+      const long long bi = row / Tn, t = row % Tn;
+      dg = dgate[(bi * H + h) * Tn + t];
+    }
+    const float dpa = dg * (b * ch - 1.f) * a * (1.f - a);
+    const float dpb = dg * a * ch * b * (1.f - b);
+    if (ok) {
+      float4* d = reinterpret_cast<float4*>(dx1 + n * HD + 8 * sub);
+      float4 u = d[0], v = d[1];
+      u.x += dpa * gw.wa[0] + dpb * gw.wb[0]; u.y += dpa * gw.wa[1] + dpb * gw.wb[1];
+      u.z += dpa * gw.wa[2] + dpb * gw.wb[2]; u.w += dpa * gw.wa[3] + dpb * gw.wb[3];
+      v.x += dpa * gw.wa[4] + dpb * gw.wb[4]; v.y += dpa * gw.wa[5] + dpb * gw.wb[5];
+      v.z += dpa * gw.wa[6] + dpb * gw.wb[6]; v.w += dpa * gw.wa[7] + dpb * gw.wb[7];
+      d[0] = u; d[1] = v;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { accA[e] += dpa * x[e]; accB[e] += dpb * x[e]; }
+    sdpa += dpa; sdpb += dpb; sdc += dg * a * b;
+  }
+  // per-head term: one atomic per 8-lane group
+  if (sub == 0 && sdc != 0.f) atomicAdd(dc + h, sdc);
+  // sum over the 8 groups of the wave (lanes with equal sub hold the same dims)
+#pragma unroll
+  for (int o = 8; o < 64; o <<= 1) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { accA[e] += __shfl_xor(accA[e], o, 64); accB[e] += __shfl_xor(accB[e], o, 64); }
+    sdpa += __shfl_xor(sdpa, o, 64);
+    sdpb += __shfl_xor(sdpb, o, 64);
+  }
+  if (ig == 0) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { red[w][0][8 * sub + e] = accA[e]; red[w][1][8 * sub + e] = accB[e]; }
+    if (sub == 0) { reds[w][0] = sdpa; reds[w][1] = sdpb; }
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 * HD) {
+    const int j = threadIdx.x / HD, i = threadIdx.x % HD;
+    const float v = red[0][j][i] + red[1][j][i] + red[2][j][i] + red[3][j][i];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) atomicAdd(dW + (4 * j + r) * HD + i, v);
+  } else if (threadIdx.x < 2 * HD + 8) {
+    const int r = threadIdx.x - 2 * HD;
+    const int j = r >> 2;
+    atomicAdd(db + r, reds[0][j] + reds[1][j] + reds[2][j] + reds[3][j]);
+  }
 }
 
 // ---------------------------------------------------------------- f32 attention (row per lane)
@@ -352,8 +438,10 @@ extern "C" int nrse_rel_bias_bwd(const float* diag, const int* bucket, float* dE
 extern "C" int nrse_gate_fwd(const void* x1, int x_dtype, const float* W, const float* bvec, const float* c,
                              float* gate, int batch, int T, int H, void* stream) {
   NRSE_REQUIRE(x1 && W && bvec && c && gate && batch > 0 && T > 0 && H > 0, "nrse_gate_fwd: bad args");
+  NRSE_REQUIRE(((uintptr_t)x1 & 15) == 0, "nrse_gate_fwd: x1 not 16-byte aligned");
   const long long total = (long long)batch * T * H;
-  dim3 grid((unsigned)((total + 255) / 256));
+  const long long blocks = (total + 31) / 32;  // 8 items per wave, 4 waves per block
+  dim3 grid((unsigned)(blocks < 4096 ? blocks : 4096));
   hipStream_t st = (hipStream_t)stream;
   if (x_dtype == NRSE_BF16) hipLaunchKernelGGL(gate_fwd_kernel<bf16_t>, grid, dim3(256), 0, st, x1, W, bvec, c, gate, batch, T, H);
   else hipLaunchKernelGGL(gate_fwd_kernel<float>, grid, dim3(256), 0, st, x1, W, bvec, c, gate, batch, T, H);
@@ -361,19 +449,20 @@ extern "C" int nrse_gate_fwd(const void* x1, int x_dtype, const float* W, const 
 }
 
 extern "C" int nrse_gate_bwd(const void* x1, int x_dtype, const float* W, const float* bvec, const float* c,
-                             const float* dgate, float* dx1, void* dproj, float* dcterm, int batch, int T, int H,
+                             const float* dgate, float* dx1, float* dW, float* db, float* dc, int batch, int T, int H,
                              void* stream) {
-  NRSE_REQUIRE(x1 && W && bvec && c && dgate && dx1 && dproj && dcterm && batch > 0 && T > 0 && H > 0,
+  NRSE_REQUIRE(x1 && W && bvec && c && dgate && dx1 && dW && db && dc && batch > 0 && T > 0 && H > 0,
                "nrse_gate_bwd: bad args");
-  const long long total = (long long)batch * T * H;
+  NRSE_REQUIRE(((uintptr_t)x1 & 15) == 0 && ((uintptr_t)dx1 & 15) == 0, "nrse_gate_bwd: x1/dx1 not 16-byte aligned");
   hipStream_t st = (hipStream_t)stream;
-  dim3 grid((unsigned)((total + 3) / 4));
+  // a multiple of H workgroups: each 8-lane item group then keeps one head (see the kernel)
+  dim3 grid((unsigned)(GATE_BWD_BLOCKS_PER_HEAD * H));
   if (x_dtype == NRSE_BF16)
-    hipLaunchKernelGGL(gate_bwd_kernel<bf16_t>, grid, dim3(256), 0, st, x1, W, bvec, c, dgate, dx1, (bf16_t*)dproj,
-                       dcterm, batch, T, H);
+    hipLaunchKernelGGL(gate_bwd_kernel<bf16_t>, grid, dim3(256), 0, st, x1, W, bvec, c, dgate, dx1, dW, db, dc, batch,
+                       T, H);
   else
-    hipLaunchKernelGGL(gate_bwd_kernel<float>, grid, dim3(256), 0, st, x1, W, bvec, c, dgate, dx1, (float*)dproj,
-                       dcterm, batch, T, H);
+    hipLaunchKernelGGL(gate_bwd_kernel<float>, grid, dim3(256), 0, st, x1, W, bvec, c, dgate, dx1, dW, db, dc, batch,
+                       T, H);
   return nrse_check_launch("nrse_gate_bwd");
 }
 

@@ -290,7 +290,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const nrse_gemm_params p)
   for (int tn = 0; tn < 4; ++tn) {
     const int n = n0 + wn * 64 + tn * 16 + li;
     const bool nok = n < p.N;
-    const float bias = ((flags & NRSE_EPI_BIAS) && nok) ? p.bias[zq * p.bias_z1 + zr * p.bias_z2 + n] : 0.f;
+    const float bias = ((flags & NRSE_EPI_BIAS) && nok && split == 0) ? p.bias[zq * p.bias_z1 + zr * p.bias_z2 + n] : 0.f;
     float csum = 0.f;
 #pragma unroll
     for (int tm = 0; tm < 4; ++tm) {

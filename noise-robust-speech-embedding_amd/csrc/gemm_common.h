@@ -89,6 +89,7 @@ struct Epi {
   long long cbase, abase, rbase, bbase;
   uint32_t key, thresh;
   float dscale;
+  bool bias_on;  // split-K: the bias joins the sum once (split 0)
   NRSE_DEV Epi(const nrse_gemm_params& p, long long zq, long long zr, int split) {
     cbase = zq * p.c_z1 + zr * p.c_z2 + (long long)split * p.c_split;
     abase = zq * p.aux_z1 + zr * p.aux_z2;
@@ -97,6 +98,7 @@ struct Epi {
     key = site_key(p.seed);
     thresh = dropout_threshold(p.dropout_p);
     dscale = p.dropout_p < 1.f ? 1.f / (1.f - p.dropout_p) : 0.f;
+    bias_on = split == 0;
   }
 };
 
@@ -114,7 +116,7 @@ NRSE_DEV void epi8(const nrse_gemm_params& p, const Epi& e, int m, int n, float*
   }
 #pragma unroll
   for (int i = 0; i < 8; ++i) v[i] *= p.alpha;
-  if (flags & NRSE_EPI_BIAS) {
+  if ((flags & NRSE_EPI_BIAS) && e.bias_on) {
     const float4 a = *reinterpret_cast<const float4*>(p.bias + e.bbase + n);
     const float4 b = *reinterpret_cast<const float4*>(p.bias + e.bbase + n + 4);
     v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;

@@ -108,7 +108,112 @@ __global__ void dropout_cast_kernel(const float* __restrict__ in, void* __restri
   }
 }
 
-// colsum: grid (ceil(C/256), row chunks)
+// colsum, vector form (C % 8 == 0): a block covers 512 columns (64 lanes x 8 columns, one
+// 16-byte bf16 / 32-byte f32 load per lane per row) x 4 row lanes (the 4 waves) over a chunk of
+// rows; the 4 partial sums meet in LDS and leave as 256-byte atomic wave-instructions (lane i on
+// column i: the full memory-side atomic rate, MI355X_MICROARCH.md "Global float atomics").
+template <typename T>
+__global__ __launch_bounds__(256) void colsum8_kernel(const void* __restrict__ x, float* __restrict__ out,
+                                                      long long rows, int C, int chunk) {
+  __shared__ float part[4][512];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int cb0 = blockIdx.x * 512;
+  const int c0 = cb0 + lane * 8;
+  const long long r0 = (long long)blockIdx.y * chunk;
+  const long long r1 = min(rows, r0 + chunk);
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c0 < C) {
+#pragma unroll 4
+    for (long long r = r0 + w; r < r1; r += 4) {
+      if constexpr (sizeof(T) == 2) {
+        const uint4 u = *reinterpret_cast<const uint4*>((const bf16_t*)x + r * C + c0);
+        const unsigned v[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          a[2 * e] += __uint_as_float(v[e] << 16);
+          a[2 * e + 1] += __uint_as_float(v[e] & 0xffff0000u);
+        }
+      } else {
+        const float4 u = *reinterpret_cast<const float4*>((const float*)x + r * C + c0);
+        const float4 v = *reinterpret_cast<const float4*>((const float*)x + r * C + c0 + 4);
+        a[0] += u.x; a[1] += u.y; a[2] += u.z; a[3] += u.w; a[4] += v.x; a[5] += v.y; a[6] += v.z; a[7] += v.w;
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) part[w][lane * 8 + e] = a[e];
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int col = threadIdx.x + 256 * h;
+    if (cb0 + col < C) {
+      const float s = part[0][col] + part[1][col] + part[2][col] + part[3][col];
+      atomicAdd(out + cb0 + col, s);
+    }
+  }
+}
+
+// Dropout backward + cast + bias gradient in one pass over [rows, C] f32 rows (C % 8 == 0):
+// out = dropout(in) in the output dtype, colsum[c] += sum_r out[r, c] (the f32 value before the
+// cast). Same block geometry and atomic shape as colsum8_kernel.
+template <typename TO>
+__global__ __launch_bounds__(256) void dropout_cast_colsum_kernel(const float* __restrict__ in, TO* __restrict__ out,
+                                                                  float* __restrict__ colsum, long long rows, int C,
+                                                                  int chunk, float p, uint32_t seed) {
+  __shared__ float part[4][512];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int cb0 = blockIdx.x * 512;
+  const int c0 = cb0 + lane * 8;
+  const long long r0 = (long long)blockIdx.y * chunk;
+  const long long r1 = min(rows, r0 + chunk);
+  const uint32_t key = site_key(seed);
+  const uint32_t thr = dropout_threshold(p);
+  const float sc = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c0 < C) {
+#pragma unroll 2
+    for (long long r = r0 + w; r < r1; r += 4) {
+      const long long i = r * C + c0;
+      const float4 u = *reinterpret_cast<const float4*>(in + i);
+      const float4 v = *reinterpret_cast<const float4*>(in + i + 4);
+      float o[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+      if (p > 0.f) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = dropout_keep(key, (uint32_t)(i + e), thr) ? o[e] * sc : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[e] += o[e];
+      if constexpr (sizeof(TO) == 2) {
+        uint4 q;
+        q.x = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
+        q.y = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
+        q.z = (uint32_t)f2bf(o[4]) | ((uint32_t)f2bf(o[5]) << 16);
+        q.w = (uint32_t)f2bf(o[6]) | ((uint32_t)f2bf(o[7]) << 16);
+        *reinterpret_cast<uint4*>(out + i) = q;
+      } else {
+        *reinterpret_cast<float4*>(out + i) = make_float4(o[0], o[1], o[2], o[3]);
+        *reinterpret_cast<float4*>(out + i + 4) = make_float4(o[4], o[5], o[6], o[7]);
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) part[w][lane * 8 + e] = a[e];
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int col = threadIdx.x + 256 * h;
+    if (cb0 + col < C) atomicAdd(colsum + cb0 + col, part[0][col] + part[1][col] + part[2][col] + part[3][col]);
+  }
+}
+
+// rows per block of the row-sweep kernels above: ~1024 blocks, a multiple of 16 rows
+long long sweep_chunk(long long rows, int C) {
+  const int cb = (C + 511) / 512;
+  long long chunk = (rows * cb + 1023) / 1024;
+  return ((chunk + 15) / 16) * 16;
+}
+
+// colsum, scalar form: grid (ceil(C/256), row chunks)
 __global__ void colsum_kernel(const void* __restrict__ x, int dt, float* __restrict__ out, long long rows, int C,
                               int chunk) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -208,8 +313,37 @@ extern "C" int nrse_dropout_cast(const float* in, void* out, int odt, long long 
   return nrse_check_launch("nrse_dropout_cast");
 }
 
+extern "C" int nrse_dropout_cast_colsum(const float* in, void* out, int out_dtype, long long rows, int C, float p,
+                                        uint32_t seed, float* colsum, void* stream) {
+  NRSE_REQUIRE(in && out && colsum && rows > 0 && C > 0 && C % 8 == 0, "nrse_dropout_cast_colsum: bad args");
+  NRSE_REQUIRE(((uintptr_t)in & 15) == 0 && ((uintptr_t)out & 15) == 0, "nrse_dropout_cast_colsum: unaligned");
+  const int cb = (C + 511) / 512;
+  const long long chunk = sweep_chunk(rows, C);
+  const dim3 grid(cb, (unsigned)((rows + chunk - 1) / chunk));
+  if (out_dtype == NRSE_BF16)
+    hipLaunchKernelGGL(dropout_cast_colsum_kernel<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, in, (bf16_t*)out,
+                       colsum, rows, C, (int)chunk, p, seed);
+  else
+    hipLaunchKernelGGL(dropout_cast_colsum_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, in, (float*)out,
+                       colsum, rows, C, (int)chunk, p, seed);
+  return nrse_check_launch("nrse_dropout_cast_colsum");
+}
+
 extern "C" int nrse_colsum(const void* x, int dt, float* colsum, long long rows, int C, void* stream) {
   NRSE_REQUIRE(x && colsum && rows > 0 && C > 0, "nrse_colsum: bad args");
+  if (C % 8 == 0 && ((uintptr_t)x & 15) == 0) {
+    // ~1024 blocks; each row lane reads >= 4 rows
+    const int cb = (C + 511) / 512;
+    const long long chunk = sweep_chunk(rows, C);
+    const long long nchunks = (rows + chunk - 1) / chunk;
+    if (dt == NRSE_BF16)
+      hipLaunchKernelGGL(colsum8_kernel<bf16_t>, dim3(cb, (unsigned)nchunks), dim3(256), 0, (hipStream_t)stream, x,
+                         colsum, rows, C, (int)chunk);
+    else
+      hipLaunchKernelGGL(colsum8_kernel<float>, dim3(cb, (unsigned)nchunks), dim3(256), 0, (hipStream_t)stream, x,
+                         colsum, rows, C, (int)chunk);
+    return nrse_check_launch("nrse_colsum");
+  }
   int chunk = 64;
   long long nchunks = (rows + chunk - 1) / chunk;
   while (nchunks > 4096) { chunk *= 2; nchunks = (rows + chunk - 1) / chunk; }

@@ -116,7 +116,8 @@ _SIGNATURES = {
     "nrse_rel_bias_fwd": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp], c_int),
     "nrse_rel_bias_bwd": ([c_vp, c_vp, c_vp, c_int, c_int, c_vp], c_int),
     "nrse_gate_fwd": ([c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp], c_int),
-    "nrse_gate_bwd": ([c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp], c_int),
+    "nrse_gate_bwd": ([c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp],
+                      c_int),
     "nrse_attn_fwd": ([_P(AttnFwdParams), c_vp], c_int),
     "nrse_attn_bwd": ([_P(AttnBwdParams), c_vp], c_int),
     "nrse_conv0_fwd": ([_P(Conv0Params), c_vp], c_int),
@@ -127,6 +128,7 @@ _SIGNATURES = {
     "nrse_pad_rows": ([c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
     "nrse_specaug_bwd": ([c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_f, c_u32, c_vp], c_int),
     "nrse_dropout_cast": ([c_vp, c_vp, c_int, c_ll, c_f, c_u32, c_vp], c_int),
+    "nrse_dropout_cast_colsum": ([c_vp, c_vp, c_int, c_ll, c_int, c_f, c_u32, c_vp, c_vp], c_int),
     "nrse_colsum": ([c_vp, c_int, c_vp, c_ll, c_int, c_vp], c_int),
     "nrse_cast": ([c_vp, c_int, c_vp, c_int, c_ll, c_vp], c_int),
     "nrse_swap12": ([c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),

@@ -16,6 +16,7 @@ kernel sequences (no autograd), mirroring:
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -29,6 +30,9 @@ from .arch import WavLMArch
 from .hostside import bucket_vector, compute_mask_indices, layerdrop_decisions
 
 F32 = torch.float32
+# NRSE_SERIAL_TARGET=1 runs the target view on the main stream (profiling: kernel durations
+# without the concurrent view's interference)
+_SERIAL_TARGET = os.environ.get("NRSE_SERIAL_TARGET", "0") == "1"
 
 
 def _divisor_at_most(n: int, cap: int) -> int:
@@ -341,13 +345,13 @@ class ByolEngine:
             at = p + "attention."
             # FFN branch
             dv2 = torch.empty(BT, H, device=dev, dtype=cdt)
-            K.dropout_cast(dh, dv2, php, R.site_seed(fseed, R.site_ffn_out(li)))
+            K.dropout_cast_colsum(dh, dv2, Gv[p + "feed_forward.output_dense.bias"], php,
+                                  R.site_seed(fseed, R.site_ffn_out(li)))
             df1 = torch.empty(BT, F_, device=dev, dtype=cdt)
             K.linear_dgrad(dv2, Ps[p + "feed_forward.output_dense.weight"], df1, flags=_lib.EPI_GELU_BWD,
                            aux=L_["f1pre"], ldaux=F_, dropout_p=pact, seed=R.site_seed(fseed, R.site_act(li)),
                            colsum=Gv[p + "feed_forward.intermediate_dense.bias"])
             K.linear_wgrad(dv2, L_["g1"], Gv[p + "feed_forward.output_dense.weight"])
-            K.colsum(dv2, Gv[p + "feed_forward.output_dense.bias"])
             K.linear_wgrad(df1, L_["x2"], Gv[p + "feed_forward.intermediate_dense.weight"])
             dx2 = torch.empty(BT, H, device=dev, dtype=F32)
             K.linear_dgrad(df1, Ps[p + "feed_forward.intermediate_dense.weight"], dx2)
@@ -358,11 +362,10 @@ class ByolEngine:
             del dx2
             # attention branch
             dv1 = torch.empty(BT, H, device=dev, dtype=cdt)
-            K.dropout_cast(dhmid, dv1, php, R.site_seed(fseed, R.site_attn_out(li)))
+            K.dropout_cast_colsum(dhmid, dv1, Gv[at + "out_proj.bias"], php, R.site_seed(fseed, R.site_attn_out(li)))
             dctx = torch.empty(BT, H, device=dev, dtype=cdt)
             K.linear_dgrad(dv1, Ps[at + "out_proj.weight"], dctx)
             K.linear_wgrad(dv1, L_["ctx"], Gv[at + "out_proj.weight"])
-            K.colsum(dv1, Gv[at + "out_proj.bias"])
             del dv1
             dqkv = torch.empty(BT, 3 * H, device=dev, dtype=cdt)
             dgate = torch.empty(B, nh, T, device=dev, dtype=F32)
@@ -476,7 +479,7 @@ class ByolEngine:
     # ------------------------------------------------------------------ heads
     def _linear(self, x, w, b, out_dim):
         y = torch.empty(x.shape[0], out_dim, device=self.dev, dtype=F32)
-        K.linear_fwd(x, w, y, bias=b)
+        K.linear_fwd_small(x, w, y, bias=b)
         return y
 
     def _bn(self, x, P, name, bn_key, train, relu):
@@ -510,7 +513,7 @@ class ByolEngine:
         K.linear_wgrad(dy, x, Gw)
         K.colsum(dy, Gb)
         dx = torch.empty(dy.shape[0], w.shape[1], device=self.dev, dtype=F32)
-        K.linear_dgrad(dy, w, dx)
+        K.linear_dgrad_small(dy, w, dx)
         return dx
 
     def _bn_bwd(self, dy, cache, P, G, name, relu):
@@ -571,7 +574,7 @@ class ByolEngine:
         # view: the two encoders are independent until the loss, and each one's small kernels and
         # GEMM tail waves leave CUs idle that the other fills.
         main = torch.cuda.current_stream(self.dev)
-        side = self._side_stream()
+        side = main if _SERIAL_TARGET else self._side_stream()
         side.wait_stream(main)
         noisy.record_stream(side)
         with torch.cuda.stream(side):

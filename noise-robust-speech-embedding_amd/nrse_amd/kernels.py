@@ -143,6 +143,46 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, dx: torch.Tensor, *, flags: 
          flags=flags, **kw)
 
 
+def _small_m_splits(M: int, N: int, K: int) -> int:
+    """K splits for a GEMM with few output tiles (the [32, *] head layers): one 128x128 tile
+    column per N/128, so without a split a 1024-wide layer runs 8 workgroups on 256 CUs."""
+    if M > 128 or K < 512:
+        return 1
+    tiles = (N + 127) // 128
+    s = 1
+    while s * 2 * tiles <= 256 and K % (s * 2) == 0 and (K // (s * 2)) % 128 == 0:
+        s *= 2
+    return s
+
+
+def linear_fwd_small(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, *, bias=None) -> None:
+    """out[M,N] = x @ w^T (+ bias) for small M: split-K with f32 atomics (out is overwritten)."""
+    M, K = x.shape
+    N = w.shape[0]
+    S = _small_m_splits(M, N, K)
+    if S == 1 or out.dtype != torch.float32:
+        linear_fwd(x, w, out, bias=bias)
+        return
+    out.zero_()
+    ks = K // S
+    gemm(Operand(x, True, x.stride(0), seg_stride=ks), Operand(w, True, w.stride(0), seg_stride=ks), out, M, N, ks,
+         ldc=out.stride(0), splits=S, bias=bias, flags=_lib.EPI_ATOMIC)
+
+
+def linear_dgrad_small(dy: torch.Tensor, w: torch.Tensor, dx: torch.Tensor) -> None:
+    """dx[M,K] = dy[M,N] @ w[N,K] for small M: split over N with f32 atomics (dx is overwritten)."""
+    M, N = dy.shape
+    K = w.shape[1]
+    S = _small_m_splits(M, K, N)
+    if S == 1 or dx.dtype != torch.float32:
+        linear_dgrad(dy, w, dx)
+        return
+    dx.zero_()
+    ns = N // S
+    gemm(Operand(dy, True, dy.stride(0), seg_stride=ns), Operand(w, False, w.stride(0), seg_stride=ns * w.stride(0)),
+         dx, M, K, ns, ldc=dx.stride(0), splits=S, flags=_lib.EPI_ATOMIC)
+
+
 def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, *, splits: int = 0) -> None:
     """dw[N,K] += dy[M,N]^T @ x[M,K]  (f32 dw, atomics)."""
     M, N = dy.shape
@@ -220,15 +260,10 @@ def gate_fwd(x1, W, b, c, gate, batch, T, H):
 
 
 def gate_bwd(x1, W, b, c, dgate, dx1, dW, db, dc, batch, T, H):
-    """dx1 += gate-path gradient; dW/db/dc accumulated (dW via an MFMA GEMM over B*T*H rows)."""
-    n = batch * T * H
-    dproj = torch.empty(n, 8, device=x1.device, dtype=x1.dtype)
-    dcterm = torch.empty(batch * T, H, device=x1.device, dtype=torch.float32)
-    _call("nrse_gate_bwd", ptr(x1), dtype_code(x1), ptr(W), ptr(b), ptr(c), ptr(dgate), ptr(dx1), ptr(dproj),
-          ptr(dcterm), batch, T, H, stream_ptr())
-    linear_wgrad(dproj, x1.view(n, 64), dW, splits=256)
-    colsum(dproj, db)
-    colsum(dcterm, dc.view(-1))
+    """dx1 += gate-path gradient; dW/db/dc accumulated (one fused kernel)."""
+    assert dx1.dtype == torch.float32 and dW.dtype == db.dtype == dc.dtype == torch.float32
+    _call("nrse_gate_bwd", ptr(x1), dtype_code(x1), ptr(W), ptr(b), ptr(c), ptr(dgate), ptr(dx1), ptr(dW), ptr(db),
+          ptr(dc), batch, T, H, stream_ptr())
 
 
 def attn_fwd(qkv, gate, bias, ctx, lse, batch, T, H, dropout_p=0.0, seed=0):
@@ -299,6 +334,14 @@ def specaug_bwd(dh, mask, dembed, out, batch, T, C, p, seed):
 def dropout_cast(x, out, p=0.0, seed=0):
     assert x.dtype == torch.float32 and x.numel() == out.numel()
     _call("nrse_dropout_cast", ptr(x), ptr(out), dtype_code(out), x.numel(), p, seed & 0xFFFFFFFF, stream_ptr())
+
+
+def dropout_cast_colsum(x, out, colsum, p=0.0, seed=0):
+    """out = dropout(x) (cast), colsum += column sums of out: one pass."""
+    assert x.dtype == torch.float32 and x.numel() == out.numel() and colsum.dtype == torch.float32
+    C = x.shape[-1]
+    _call("nrse_dropout_cast_colsum", ptr(x), ptr(out), dtype_code(out), x.numel() // C, C, p, seed & 0xFFFFFFFF,
+          ptr(colsum), stream_ptr())
 
 
 def colsum(x, out):

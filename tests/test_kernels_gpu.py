@@ -202,3 +202,77 @@ def test_health_flags(nrse_device):
     y = x.clone(); y[5] = 0; y[7] = 0
     assert abs(float(st[2]) - float(y.abs().sum())) / float(y.abs().sum()) < 1e-5
     assert float(st[3]) == float(y.abs().max())
+
+
+def _gate_reference(x1, W, b, c, B, T, H):
+    """WavLMAttention gate, [TF]modeling_wavlm.py:168-176 (float64)."""
+    xh = x1.double().view(B, T, H, 64).permute(0, 2, 1, 3)                     # [B, H, T, 64]
+    pr = F.linear(xh, W, b).view(B, H, T, 2, 4).sum(-1)
+    ga, gb = torch.sigmoid(pr).chunk(2, dim=-1)
+    return (ga * (gb * c.view(1, H, 1, 1) - 1.0) + 2.0).squeeze(-1)            # [B, H, T]
+
+
+@pytest.mark.parametrize("xdt", [torch.float32, torch.bfloat16])
+def test_gate_fwd_bwd(nrse_device, xdt):
+    from nrse_amd import kernels as K
+    dev = nrse_device
+    B, T, H = 3, 77, 16
+    x1 = torch.randn(B * T, H * 64, device=dev).to(xdt)
+    W = torch.randn(8, 64, device=dev) * 0.2
+    bv = torch.randn(8, device=dev) * 0.2
+    c = torch.randn(H, device=dev)
+    gate = torch.empty(B, H, T, device=dev)
+    K.gate_fwd(x1, W, bv, c, gate, B, T, H)
+    Wr, br, cr = (t.double().requires_grad_(True) for t in (W, bv, c))
+    xr = x1.double().requires_grad_(True)
+    ref = _gate_reference(xr, Wr, br, cr.view(1, H, 1, 1), B, T, H)
+    assert rel(gate, ref) < 1e-6
+    dgate = torch.randn(B, H, T, device=dev)
+    dx1 = torch.randn(B * T, H * 64, device=dev)
+    dx1_0 = dx1.clone()
+    dW = torch.zeros(8, 64, device=dev); db = torch.zeros(8, device=dev); dc = torch.zeros(1, H, 1, 1, device=dev)
+    K.gate_bwd(x1, W, bv, c.view(1, H, 1, 1), dgate, dx1, dW, db, dc, B, T, H)
+    ref.backward(dgate.double())
+    assert rel(dx1 - dx1_0, xr.grad) < 1e-5
+    assert rel(dW, Wr.grad) < 1e-5 and rel(db, br.grad) < 1e-5 and rel(dc.view(-1), cr.grad) < 1e-5
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("rows,C", [(12768, 1024), (333, 3072), (1000, 8), (77, 520)])
+def test_colsum(nrse_device, dt, rows, C):
+    from nrse_amd import kernels as K
+    x = torch.randn(rows, C, device=nrse_device).to(dt)
+    out = torch.full((C,), 0.5, device=nrse_device)
+    K.colsum(x, out)
+    assert rel(out, x.double().sum(0) + 0.5) < 1e-5
+
+
+@pytest.mark.parametrize("M,N,Kd", [(32, 1024, 1024), (32, 2048, 2048), (32, 1024, 2048), (5, 256, 512)])
+def test_small_m_split_k_linears(nrse_device, M, N, Kd):
+    from nrse_amd import kernels as K
+    dev = nrse_device
+    x = torch.randn(M, Kd, device=dev); w = torch.randn(N, Kd, device=dev); b = torch.randn(N, device=dev)
+    y = torch.full((M, N), 7.0, device=dev)
+    K.linear_fwd_small(x, w, y, bias=b)
+    assert rel(y, x.double() @ w.double().t() + b.double()) < 1e-5
+    dy = torch.randn(M, N, device=dev)
+    dx = torch.full((M, Kd), 7.0, device=dev)
+    K.linear_dgrad_small(dy, w, dx)
+    assert rel(dx, dy.double() @ w.double()) < 1e-5
+
+
+@pytest.mark.parametrize("odt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_dropout_cast_colsum(nrse_device, odt, p):
+    from nrse_amd import kernels as K
+    dev = nrse_device
+    x = torch.randn(1000, 1024, device=dev)
+    ref = torch.empty(1000, 1024, device=dev, dtype=odt)
+    K.dropout_cast(x, ref, p, 1234)                      # the standalone kernel defines the mask
+    out = torch.empty_like(ref)
+    cs = torch.zeros(1024, device=dev)
+    K.dropout_cast_colsum(x, out, cs, p, 1234)
+    assert torch.equal(out, ref)
+    keep = (ref != 0) | (x == 0)
+    exact = torch.where(keep, x.double() / (1 - p), torch.zeros_like(x, dtype=torch.float64))
+    assert rel(cs, exact.sum(0)) < 1e-5
