@@ -40,6 +40,32 @@ NRSE_DEV float gelu_grad_f(float x) {
   return cdf + x * pdf;
 }
 
+// Fast erf for the GEMM epilogues: odd/even rational minimax approximation on [-4, 4] (the
+// single-precision coefficient set used by XLA / Eigen), |error| < 7e-8 in exact arithmetic and
+// < 5e-7 evaluated in f32 (erff: ~35 VALU instructions with both branches taken in a divergent
+// wave; this: 14). Used where the result is rounded to bf16 anyway (bf16 GEMM epilogues).
+NRSE_DEV float erf_fast(float x) {
+  x = fminf(fmaxf(x, -4.f), 4.f);
+  const float x2 = x * x;
+  float p = fmaf(x2, -2.72614225801306e-10f, 2.77068142495902e-08f);
+  p = fmaf(x2, p, -2.10102402082508e-06f);
+  p = fmaf(x2, p, -5.69250639462346e-05f);
+  p = fmaf(x2, p, -7.34990630326855e-04f);
+  p = fmaf(x2, p, -2.95459980854025e-03f);
+  p = fmaf(x2, p, -1.60960333262415e-02f);
+  float q = fmaf(x2, -1.45660718464996e-05f, -2.13374055278905e-04f);
+  q = fmaf(x2, q, -1.68282697438203e-03f);
+  q = fmaf(x2, q, -7.37332916720468e-03f);
+  q = fmaf(x2, q, -1.42647390514189e-02f);
+  return x * p * __builtin_amdgcn_rcpf(q);
+}
+NRSE_DEV float gelu_fast(float x) { return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f)); }
+NRSE_DEV float gelu_grad_fast(float x) {
+  const float cdf = 0.5f * (1.0f + erf_fast(x * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
 // Counter-based dropout hash (bijective 32-bit mixer, "lowbias32"). The mask of element i at
 // a dropout site seeded with `seed` is keep = hash(i ^ mix(seed)) >= p * 2^32. Deterministic
 // and stateless, so backward regenerates the forward mask from (seed, i).

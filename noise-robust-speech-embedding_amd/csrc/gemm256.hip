@@ -301,7 +301,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
   __syncthreads();
   float* ct = reinterpret_cast<float*>(smem);
   const int flags = p.flags;
-  const Epi epi(p, zq, zr, split);
+  Epi epi(p, zq, zr, split);
+  epi.load_bias(p, n0 + (tid & 31) * 8);  // the epilogue columns of this thread (see the loop)
   const bool colsum = (flags & NRSE_EPI_COLSUM) != 0;
   const int ccol = tid & 255, chalf = tid >> 8;
   float csum = 0.f;
@@ -333,7 +334,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
         }
       }
     } else {
-#pragma unroll 1
+#pragma unroll
       for (int it = 0; it < 4; ++it) {
         const int sgi = tid + NTHR * it;
         const int row = sgi >> 5;

@@ -90,6 +90,7 @@ struct Epi {
   uint32_t key, thresh;
   float dscale;
   bool bias_on;  // split-K: the bias joins the sum once (split 0)
+  float bias8[8];  // this thread's 8 bias values (its epilogue columns are fixed per thread)
   NRSE_DEV Epi(const nrse_gemm_params& p, long long zq, long long zr, int split) {
     cbase = zq * p.c_z1 + zr * p.c_z2 + (long long)split * p.c_split;
     abase = zq * p.aux_z1 + zr * p.aux_z2;
@@ -99,6 +100,18 @@ struct Epi {
     thresh = dropout_threshold(p.dropout_p);
     dscale = p.dropout_p < 1.f ? 1.f / (1.f - p.dropout_p) : 0.f;
     bias_on = split == 0;
+  }
+  // bias of output columns n..n+7 (call once: every epilogue iteration of a thread has the same n)
+  NRSE_DEV void load_bias(const nrse_gemm_params& p, int n) {
+    if ((p.flags & NRSE_EPI_BIAS) && bias_on && n < p.N) {
+      const float4 a = *reinterpret_cast<const float4*>(p.bias + bbase + n);
+      const float4 b = *reinterpret_cast<const float4*>(p.bias + bbase + n + 4);
+      bias8[0] = a.x; bias8[1] = a.y; bias8[2] = a.z; bias8[3] = a.w;
+      bias8[4] = b.x; bias8[5] = b.y; bias8[6] = b.z; bias8[7] = b.w;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) bias8[i] = 0.f;
+    }
   }
 };
 
@@ -116,21 +129,20 @@ NRSE_DEV void epi8(const nrse_gemm_params& p, const Epi& e, int m, int n, float*
   }
 #pragma unroll
   for (int i = 0; i < 8; ++i) v[i] *= p.alpha;
-  if ((flags & NRSE_EPI_BIAS) && e.bias_on) {
-    const float4 a = *reinterpret_cast<const float4*>(p.bias + e.bbase + n);
-    const float4 b = *reinterpret_cast<const float4*>(p.bias + e.bbase + n + 4);
-    v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+  if (flags & NRSE_EPI_BIAS) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] += e.bias8[i];
   }
   if (flags & NRSE_EPI_GELU) {
     if (p.aux) st8((void*)p.aux, p.aux_dtype, e.abase + (long long)m * p.ldaux + n, v);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = gelu_f(v[i]);
+    for (int i = 0; i < 8; ++i) v[i] = gelu_fast(v[i]);
   }
   if (flags & NRSE_EPI_GELU_BWD) {
     float a[8];
     ld8(p.aux, p.aux_dtype, e.abase + (long long)m * p.ldaux + n, a);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] *= gelu_grad_f(a[i]);
+    for (int i = 0; i < 8; ++i) v[i] *= gelu_grad_fast(a[i]);
   }
   if (flags & NRSE_EPI_RELU) {
 #pragma unroll

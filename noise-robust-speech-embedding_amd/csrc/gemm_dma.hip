@@ -167,9 +167,10 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_dma_kernel(const nrse_gemm_param
     }
     return;
   }
-  const Epi epi(p, zq, zr, split);
+  Epi epi(p, zq, zr, split);
+  epi.load_bias(p, n0 + (tid & 15) * 8);  // the epilogue columns of this thread (see the loop)
   const bool colsum = (flags & NRSE_EPI_COLSUM) != 0;
-#pragma unroll 1
+#pragma unroll
   for (int it = 0; it < 8; ++it) {
     const int sgi = tid + NTHR * it;
     const int row = sgi >> 4;

@@ -15,6 +15,7 @@ kernel sequences (no autograd), mirroring:
 """
 from __future__ import annotations
 
+import contextlib
 import math
 import os
 from dataclasses import dataclass, field
@@ -30,8 +31,8 @@ from .arch import WavLMArch
 from .hostside import bucket_vector, compute_mask_indices, layerdrop_decisions
 
 F32 = torch.float32
-# NRSE_SERIAL_TARGET=1 runs the target view on the main stream (profiling: kernel durations
-# without the concurrent view's interference)
+# NRSE_SERIAL_TARGET=1 runs the target view and the backward weight gradients on the main
+# stream (profiling: kernel durations without the concurrent streams' interference)
 _SERIAL_TARGET = os.environ.get("NRSE_SERIAL_TARGET", "0") == "1"
 
 
@@ -339,6 +340,8 @@ class ByolEngine:
         tape.final = None
         diag = torch.zeros(nh, 2 * T - 1, device=dev, dtype=F32)
         delta = torch.empty(B, nh, T, device=dev, dtype=F32)
+        # the transformer layers' weight gradients (off the dX critical path) run on a side stream
+        main = torch.cuda.current_stream(dev)
         for L_ in reversed(tape.layers):
             li = L_["li"]
             p = f"encoder.layers.{li}."
@@ -351,8 +354,9 @@ class ByolEngine:
             K.linear_dgrad(dv2, Ps[p + "feed_forward.output_dense.weight"], df1, flags=_lib.EPI_GELU_BWD,
                            aux=L_["f1pre"], ldaux=F_, dropout_p=pact, seed=R.site_seed(fseed, R.site_act(li)),
                            colsum=Gv[p + "feed_forward.intermediate_dense.bias"])
-            K.linear_wgrad(dv2, L_["g1"], Gv[p + "feed_forward.output_dense.weight"])
-            K.linear_wgrad(df1, L_["x2"], Gv[p + "feed_forward.intermediate_dense.weight"])
+            with self._wgrad_stream(main, dv2, df1, L_["g1"], L_["x2"]):
+                K.linear_wgrad(dv2, L_["g1"], Gv[p + "feed_forward.output_dense.weight"])
+                K.linear_wgrad(df1, L_["x2"], Gv[p + "feed_forward.intermediate_dense.weight"])
             dx2 = torch.empty(BT, H, device=dev, dtype=F32)
             K.linear_dgrad(df1, Ps[p + "feed_forward.intermediate_dense.weight"], dx2)
             del df1, dv2
@@ -365,15 +369,17 @@ class ByolEngine:
             K.dropout_cast_colsum(dhmid, dv1, Gv[at + "out_proj.bias"], php, R.site_seed(fseed, R.site_attn_out(li)))
             dctx = torch.empty(BT, H, device=dev, dtype=cdt)
             K.linear_dgrad(dv1, Ps[at + "out_proj.weight"], dctx)
-            K.linear_wgrad(dv1, L_["ctx"], Gv[at + "out_proj.weight"])
+            with self._wgrad_stream(main, dv1, L_["ctx"]):
+                K.linear_wgrad(dv1, L_["ctx"], Gv[at + "out_proj.weight"])
             del dv1
             dqkv = torch.empty(BT, 3 * H, device=dev, dtype=cdt)
             dgate = torch.empty(B, nh, T, device=dev, dtype=F32)
             K.attn_bwd(L_["qkv"], L_["gate"], tape.bias_tab, L_["ctx"], dctx, L_["lse"], delta, dqkv, dgate, diag, B,
                        T, nh, pat, R.site_seed(fseed, R.site_attn_probs(li)))
             del dctx
-            K.linear_wgrad(dqkv, L_["x1"], self.fused(self.grad_flat_for(Gv), li, "qkv_w"))
-            K.colsum(dqkv, self.fused(self.grad_flat_for(Gv), li, "qkv_b"))
+            with self._wgrad_stream(main, dqkv, L_["x1"]):
+                K.linear_wgrad(dqkv, L_["x1"], self.fused(self.grad_flat_for(Gv), li, "qkv_w"))
+                K.colsum(dqkv, self.fused(self.grad_flat_for(Gv), li, "qkv_b"))
             dx1 = torch.empty(BT, H, device=dev, dtype=F32)
             K.linear_dgrad(dqkv, self.fused(W.s_flat, li, "qkv_w"), dx1)
             del dqkv
@@ -387,6 +393,7 @@ class ByolEngine:
             L_.clear()
             dh = dhin
         tape.layers = []
+        main.wait_stream(self._bwd_side_stream())
         K.rel_bias_bwd(diag, self.buckets(T), Gv["encoder.layers.0.attention.rel_attn_embed.weight"], nh, T)
         # positional conv block: h0 = drop(h + gelu(conv(hpad) + b))
         pk, G = a.pos_kernel, a.pos_groups
@@ -544,6 +551,26 @@ class ByolEngine:
             W = EncoderWeights(self, self.target, self.target_sh)
             W.m_flat, W.s_flat = self.target, (self.target_sh if self.target_sh is not None else self.target)
         return W
+
+    def _bwd_side_stream(self) -> torch.cuda.Stream:
+        if getattr(self, "_bwd_side", None) is None:
+            self._bwd_side = torch.cuda.Stream(self.dev)
+        return self._bwd_side
+
+    @contextlib.contextmanager
+    def _wgrad_stream(self, main: torch.cuda.Stream, *used: torch.Tensor):
+        """Enqueue the enclosed weight-gradient GEMMs on the backward side stream, after all work
+        issued so far on `main` (their inputs); `used` tensors are kept alive for that stream.
+        The wgrads fill the CUs the dX chain's partial GEMM waves and small kernels leave idle."""
+        if _SERIAL_TARGET:
+            yield
+            return
+        side = self._bwd_side_stream()
+        side.wait_stream(main)
+        for t in used:
+            t.record_stream(side)
+        with torch.cuda.stream(side):
+            yield
 
     def _side_stream(self) -> torch.cuda.Stream:
         if getattr(self, "_side", None) is None:
