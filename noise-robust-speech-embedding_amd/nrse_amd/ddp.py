@@ -22,8 +22,12 @@ def init_from_env(backend: str | None = None):
         return 0, 1, int(os.environ.get("LOCAL_RANK", "0"))
     rank = int(os.environ["RANK"])
     local = int(os.environ.get("LOCAL_RANK", rank))
+    # NRSE_SHARE_DEVICE=1: every rank on device 0 (a rehearsal of the N-rank path on a one-GPU
+    # box, with NRSE_DDP_BACKEND=gloo since RCCL refuses two ranks on one device)
+    if os.environ.get("NRSE_SHARE_DEVICE", "0") == "1":
+        local = 0
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        backend = os.environ.get("NRSE_DDP_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     if backend == "nccl":
         torch.cuda.set_device(local)
     if not dist.is_initialized():
@@ -32,27 +36,55 @@ def init_from_env(backend: str | None = None):
 
 
 class GradAllReduce:
-    """Sum all-reduce of a flat gradient buffer in fixed-size buckets, issued asynchronously
-    back to front and waited before the optimizer (64 MiB buckets by default: large enough to
-    run at link bandwidth on the point-to-point xGMI ring, small enough to pipeline)."""
+    """Sum all-reduce of a flat gradient buffer in buckets.
+
+    Two ways to drive it:
+      * `allreduce(flat)`: the whole buffer in fixed-size buckets (64 MiB by default: large
+        enough to run at link bandwidth on the point-to-point xGMI ring, small enough to
+        pipeline), issued asynchronously back to front and waited before returning;
+      * overlapped with backward: `start()`, then `issue(view)` for each contiguous gradient
+        range as soon as backward has finished writing it (the engine issues one transformer
+        layer, ~50 MB of f32, at a time, on the stream that produced it), then `finish()`
+        before the optimizer. `finish()` makes the current stream wait for every issued
+        all-reduce (a device-side dependency, no host sync under NCCL/RCCL).
+    """
 
     def __init__(self, group=None, bucket_bytes: int = 64 << 20):
         self.group = group
         self.bucket_bytes = bucket_bytes
+        self._works = []
+        self.issued_elems = 0
 
-    def __call__(self, flat: torch.Tensor) -> None:
-        if not dist.is_initialized() or dist.get_world_size(self.group) == 1:
+    def active(self) -> bool:
+        return dist.is_initialized() and dist.get_world_size(self.group) > 1
+
+    def start(self) -> None:
+        self._works = []
+        self.issued_elems = 0
+
+    def issue(self, view: torch.Tensor) -> None:
+        """Asynchronously all-reduce one contiguous gradient range (split into buckets)."""
+        if not self.active() or view.numel() == 0:
             return
-        n = flat.numel()
-        step = max(1, self.bucket_bytes // flat.element_size())
-        works = []
+        step = max(1, self.bucket_bytes // view.element_size())
+        n = view.numel()
         end = n
         while end > 0:
             start = max(0, end - step)
-            works.append(dist.all_reduce(flat[start:end], op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+            self._works.append(dist.all_reduce(view[start:end], op=dist.ReduceOp.SUM, group=self.group,
+                                               async_op=True))
             end = start
-        for w in works:
+        self.issued_elems += n
+
+    def finish(self) -> None:
+        for w in self._works:
             w.wait()
+        self._works = []
+
+    def __call__(self, flat: torch.Tensor) -> None:
+        self.start()
+        self.issue(flat)
+        self.finish()
 
 
 def world_size() -> int:

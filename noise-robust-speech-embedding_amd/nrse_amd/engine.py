@@ -320,8 +320,10 @@ class ByolEngine:
         return emb, tape, executed
 
     # ------------------------------------------------------------------ encoder backward
-    def encoder_backward(self, tape: Tape, demb: torch.Tensor, Gv: dict, W: EncoderWeights) -> None:
-        """Accumulate d(loss)/d(encoder params) into the grad views Gv given d(loss)/d(emb)."""
+    def encoder_backward(self, tape: Tape, demb: torch.Tensor, Gv: dict, W: EncoderWeights, on_layer=None) -> None:
+        """Accumulate d(loss)/d(encoder params) into the grad views Gv given d(loss)/d(emb).
+        on_layer(li), if given, is called once layer li's gradients are all enqueued (main and
+        side stream) and no later kernel writes them (layer 0 excepted: rel_attn_embed)."""
         a = self.arch
         cdt = self.cdt
         dev = self.dev
@@ -392,6 +394,8 @@ class ByolEngine:
             del dx1, dhmid
             L_.clear()
             dh = dhin
+            if on_layer is not None:
+                on_layer(li)
         tape.layers = []
         main.wait_stream(self._bwd_side_stream())
         K.rel_bias_bwd(diag, self.buckets(T), Gv["encoder.layers.0.attention.rel_attn_embed.weight"], nh, T)
@@ -623,14 +627,41 @@ class ByolEngine:
         ctx = dict(tape=tape, W=Wo, pc=pc, qc=qc, emb=emb, Pon=Pon, Ppr=Ppr)
         return pred, tproj, ctx
 
-    def backward(self, dpred: torch.Tensor, ctx: dict) -> None:
-        """Accumulate all online-parameter gradients into self.grad from d(loss)/d(pred)."""
+    def layer_range(self, li: int) -> tuple:
+        """[start, end) of transformer layer li's parameters in the flat buffers."""
+        return PR.layer_range(self.layout, self.arch, li)
+
+    def backward(self, dpred: torch.Tensor, ctx: dict, allreduce=None) -> None:
+        """Accumulate all online-parameter gradients into self.grad from d(loss)/d(pred).
+        With a GradAllReduce, each transformer layer's gradient range (except layer 0's) is
+        all-reduced as soon as backward has finished it, overlapping the exchange with the
+        remaining layers; the rest of the buffer goes when backward ends. Layers LayerDrop
+        skipped hold zero gradient on every rank (rank-shared decisions) and are not sent."""
         Gp = self.group_views(self.grad, "predictor")
         Gj = self.group_views(self.grad, "projector")
         Ge = self.group_views(self.grad, "encoder")
         dproj = self.predictor_backward(dpred, ctx["qc"], ctx["Ppr"], Gp)
         demb = self.projector_backward(dproj, ctx["pc"], ctx["Pon"], Gj)
-        self.encoder_backward(ctx["tape"], demb, Ge, ctx["W"])
+        on_layer = None
+        if allreduce is not None and allreduce.active():
+            allreduce.start()
+            main = torch.cuda.current_stream(self.dev)
+
+            def on_layer(li):
+                if li == 0:
+                    return  # rel_attn_embed is written after the layer loop
+                s, e = self.layer_range(li)
+                side = main if _SERIAL_TARGET else self._bwd_side_stream()
+                side.wait_stream(main)  # the layer's main-stream gradients (LN, biases, gate)
+                with torch.cuda.stream(side):
+                    allreduce.issue(self.grad[s:e])
+        self.encoder_backward(ctx["tape"], demb, Ge, ctx["W"], on_layer=on_layer)
+        if on_layer is not None:
+            s1, _ = self.layer_range(1)
+            _, e_last = self.layer_range(self.arch.layers - 1)
+            allreduce.issue(self.grad[:s1])          # conv / projection / pos-conv / layer 0
+            allreduce.issue(self.grad[e_last:])      # final LN + heads
+            allreduce.finish()
 
     def optimizer_step(self, lr: float, grad_scale: float = 1.0) -> None:
         """clip_grad_norm_(1.0) + AdamW + target EMA (train_byol.py:67-71), no host sync."""
@@ -662,9 +693,7 @@ class ByolEngine:
         dpred = torch.empty_like(pred)
         K.byol_loss(pred, tproj, self.loss_buf, dpred, self.loss_stats)
         self.grad.zero_()
-        self.backward(dpred, ctx)
-        if allreduce is not None and world_size > 1:
-            allreduce(self.grad)
+        self.backward(dpred, ctx, allreduce=allreduce if world_size > 1 else None)
         self.optimizer_step(lr, grad_scale=1.0 / world_size)
         return self.loss_buf
 

@@ -229,3 +229,13 @@ def count_params(specs: list[PSpec]) -> int:
             n *= d
         t += n
     return t
+
+
+def layer_range(layout: ByolLayout, arch: WavLMArch, li: int) -> tuple:
+    """[start, end) of online transformer layer li's parameters in the flat buffer (the unit
+    of the overlapped gradient all-reduce, nrse_amd/ddp.py)."""
+    pre = GROUP_PREFIX["encoder"]
+    start = layout.offsets[pre + f"encoder.layers.{li}.attention.q_proj.weight"][0]
+    nxt = (f"encoder.layers.{li + 1}.attention.q_proj.weight" if li + 1 < arch.layers else "encoder.layer_norm.weight")
+    return start, layout.offsets[pre + nxt][0]
+

@@ -42,3 +42,46 @@ def test_bucketed_allreduce_world2():
     g1 = torch.randn(1_000_003, generator=torch.Generator().manual_seed(101))
     assert torch.allclose(out[0], g0 + g1, atol=1e-6)
     assert torch.equal(out[0], out[1])
+
+
+def _overlap_worker(rank, world, port, out):
+    """The overlapped schedule: layer ranges issued out of order while 'backward' continues,
+    the remainder issued last, finish() before use (nrse_amd/engine.py backward)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "noise-robust-speech-embedding_amd"))
+    from nrse_amd import arch as A, ddp, params as PR
+    ddp.init_from_env(backend="gloo")
+    arch = A.TINY
+    layout = PR.byol_layout(arch, 32, 64)
+    g = torch.Generator().manual_seed(7 + rank)
+    flat = torch.randn(layout.numel, generator=g)
+    ar = ddp.GradAllReduce(bucket_bytes=4096)
+    ar.start()
+    for li in reversed(range(1, arch.layers)):
+        s, e = PR.layer_range(layout, arch, li)
+        ar.issue(flat[s:e])
+    s1, _ = PR.layer_range(layout, arch, 1)
+    _, e_last = PR.layer_range(layout, arch, arch.layers - 1)
+    ar.issue(flat[:s1])
+    ar.issue(flat[e_last:])
+    ar.finish()
+    out[rank] = (flat.clone(), ar.issued_elems)
+    dist.destroy_process_group()
+
+
+def test_overlapped_layer_allreduce_world2():
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "noise-robust-speech-embedding_amd"))
+    from nrse_amd import arch as A, params as PR
+    layout = PR.byol_layout(A.TINY, 32, 64)
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_overlap_worker, args=(2, port, out), nprocs=2, join=True)
+    ref = sum(torch.randn(layout.numel, generator=torch.Generator().manual_seed(7 + r)) for r in range(2))
+    assert out[0][1] == layout.numel            # the ranges tile the whole buffer exactly once
+    assert torch.allclose(out[0][0], ref, atol=1e-6) and torch.equal(out[0][0], out[1][0])

@@ -1,0 +1,63 @@
+"""Data-parallel engine step on the GPU: two ranks sharing cuda:0 (gloo, since RCCL refuses two
+ranks on one device; NRSE_SHARE_DEVICE=1), each with its own pairs. The per-layer gradient
+all-reduce overlapped with backward (nrse_amd/engine.py backward) must produce the sum of the
+two ranks' local gradients, and both replicas must take the identical optimizer step."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), NRSE_SHARE_DEVICE="1", NRSE_DDP_BACKEND="gloo")
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "noise-robust-speech-embedding_amd"))
+    import torch.distributed as dist
+    from nrse_amd import arch as A, ddp, params as PR
+    from nrse_amd.engine import ByolEngine
+    r, w, local = ddp.init_from_env()
+    torch.cuda.set_device(local)
+    arch = A.TINY
+    layout = PR.byol_layout(arch, 256, 512)
+    flat = PR.init_byol_flat(layout, 1234)
+    g = torch.Generator().manual_seed(50 + r)
+    clean = (torch.randn(4, 16000, generator=g) * 0.1).cuda()
+    noisy = clean + 0.05 * torch.randn(4, 16000, generator=g).cuda()
+    loc = ByolEngine(arch, 256, 512, device="cuda:0", compute_dtype=torch.float32, init_flat=flat)
+    loc.train_step(clean, noisy, lr=1e-4, step_seed=3, rank=r)
+    g_local = loc.grad.cpu()
+    del loc
+    eng = ByolEngine(arch, 256, 512, device="cuda:0", compute_dtype=torch.float32, init_flat=flat)
+    ar = ddp.GradAllReduce(bucket_bytes=1 << 20)
+    eng.train_step(clean, noisy, lr=1e-4, step_seed=3, rank=r, allreduce=ar, world_size=w)
+    torch.cuda.synchronize()
+    out[r] = (g_local, eng.grad.cpu(), eng.online.cpu(), ar.issued_elems, layout.numel)
+    dist.destroy_process_group()
+
+
+def test_overlapped_allreduce_engine_two_ranks(nrse_device):
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(2, port, out), nprocs=2, join=True)
+    (gl0, gs0, p0, n0, numel), (gl1, gs1, p1, _, _) = out[0], out[1]
+    ref = gl0.double() + gl1.double()
+    err = float((gs0.double() - ref).norm() / ref.norm())
+    assert err < 1e-5, err
+    assert torch.equal(gs0, gs1)
+    assert torch.equal(p0, p1)
+    assert 0 < n0 <= numel
