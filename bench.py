@@ -77,6 +77,18 @@ def cpu_baseline(arch_large, seconds_hint=20.0):
                       f"os.cpu_count()={os.cpu_count()}"}
 
 
+def gemm_traffic():
+    """HBM bytes per nrse_gemm launch from the committed rocprofv3 PMC summary
+    (tools/pmc_gemm.sh -> profiles/r01_gemm_traffic.json: FETCH_SIZE x 2 (gfx950 correction) +
+    WRITE_SIZE, averaged over the GEMM launches of a bench step). None if absent."""
+    path = os.path.join(ROOT, "profiles", "r01_gemm_traffic.json")
+    try:
+        with open(path) as fh:
+            return float(json.load(fh)["family_hbm_bytes_per_launch"])
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -153,6 +165,7 @@ def main():
     st_ok = int((status == 0).sum())
     # live roofline of the dominant kernel family (nrse_gemm, MFMA-bound)
     gflops = sum(f for f, _, _, _ in probe)
+    gbytes = sum(b for b in K.gemm_probe_bytes())
     gms = sum(e0.elapsed_time(e1) for _, e0, e1, _ in probe)
     n_launch = len(probe)
     achieved_tfs = gflops / (gms * 1e-3) / 1e12 if gms > 0 else 0.0
@@ -183,7 +196,9 @@ def main():
                      F32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                      "frac": round(achieved_tfs / (BF16_DENSE_PEAK_TFS if cdt == torch.bfloat16 else F32_MFMA_PEAK_TFS),
                                    4),
-                     "traffic": None, "avg_launch_ms": round(gms / max(n_launch, 1), 4), "launches": n_launch,
+                     "traffic": gemm_traffic(), "traffic_unit": "HBM bytes per launch (PMC, profiles/r01_gemm_traffic.json)",
+                     "algorithmic_bytes_per_launch": round(gbytes / max(n_launch, 1)),
+                     "avg_launch_ms": round(gms / max(n_launch, 1), 4), "launches": n_launch,
                      "gemm_share_of_step": round(gms / (dt * 1e3), 3)},
         "step_tflops": round(fpp * value / world / 1e12, 1),
         "loss_last": round(loss, 5), "snr_mix_ok": st_ok,

@@ -219,8 +219,10 @@ int nrse_attn_bwd(const nrse_attn_bwd_params* p, void* stream);
  * Conv feature encoder front end and the positional-conv weight norm.
  * conv0 = Conv1d(1 -> C, k, stride s, no bias) + LN(C) + GELU ([TF]modeling_wavlm.py:712-720),
  * channels-last output [B, T0, C]. Backward recomputes conv0 from the waveform, applies the
- * LN+GELU backward and accumulates only dW (the waveform needs no gradient); dy may come
- * through col2im of conv1's dgrad GEMM (same geometry fields as nrse_ln_bwd_params).
+ * LN+GELU backward and accumulates only dW (the waveform needs no gradient), in TAP-MAJOR
+ * layout dw[k][C] (contiguous atomics; the caller transposes into the [C][1][k] parameter
+ * gradient); dy may come through col2im of conv1's dgrad GEMM (same geometry fields as
+ * nrse_ln_bwd_params).
  * ------------------------------------------------------------------------------------------ */
 typedef struct {
   const float* wav; int L;        /* [B, L] f32 */
@@ -229,7 +231,7 @@ typedef struct {
   void* out; int out_dtype;       /* [B, T0, C] = gelu(LN(conv)) */
   float* mean; float* rstd;       /* [B*T0] */
   const void* dy; int dy_dtype; int dy_mode; int col_k, col_s, col_tout;   /* bwd only */
-  float* dw; float* dgamma; float* dbeta;                                  /* bwd only */
+  float* dw; float* dgamma; float* dbeta;     /* bwd only; dw is [k][C] (tap-major) */
   int batch, T0, C, k, s; float eps;
 } nrse_conv0_params;
 int nrse_conv0_fwd(const nrse_conv0_params* p, void* stream);

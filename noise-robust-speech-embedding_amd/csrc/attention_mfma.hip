@@ -28,6 +28,12 @@ constexpr int D = 64;
 constexpr int TILE_B = 64 * 128;  // bytes per 64x64 bf16 tile
 constexpr int BT_LD = 68;         // f32 bias tile row stride (dK/dV kernel)
 constexpr int DPAD = 80;          // low-side margin of the LDS diagonal arrays (dK/dV kernel)
+// Softmax runs in the base-2 domain (v_exp_f32 is 2^x): scores are formed as
+// log2(e) * (q.k / 8 + gate * bias) with the log2(e) folded into the per-row constants, so each
+// element costs one fma + one exp; lse is stored in natural-log units.
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+NRSE_DEV float exp2_(float x) { return __builtin_amdgcn_exp2f(x); }
 typedef short short8v __attribute__((ext_vector_type(8)));
 
 NRSE_DEV int loff(int row, int chunk) { return row * 128 + ((chunk ^ (((row >> 1) & 3) << 1)) << 4); }
@@ -54,13 +60,13 @@ NRSE_DEV bf16x8 rd_tr(const char* t, int r0, int r1, int c0, int lane) {
 
 // Register r of a 16x16 MFMA C block rotated left by r lanes within each 16-lane row (DPP
 // row_ror:(16 - r): lane x receives lane (x + r) mod 16), added to the accumulator of its
-// diagonal: lo if the rotation did not wrap, hi (16 further down) if it did.
+// diagonal: lo if the rotation did not wrap, hi (16 further down) if it did. The wrap test is a
+// per-lane constant, so it enters as 0/1 multipliers (mlo = 1 - mhi) and each half is one fma.
 template <int R>
-NRSE_DEV void diag_rot(float v, int x, float& lo, float& hi) {
+NRSE_DEV void diag_rot(float v, float mlo, float mhi, float& lo, float& hi) {
   const float u = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x120 + 16 - R, 0xF, 0xF, false));
-  const bool wrap = x >= 16 - R;
-  lo += wrap ? 0.f : u;
-  hi += wrap ? u : 0.f;
+  lo = fmaf(u, mlo, lo);
+  hi = fmaf(u, mhi, hi);
 }
 
 NRSE_DEV bf16x8 pack8(const float* a, const float* b) {
@@ -68,6 +74,24 @@ NRSE_DEV bf16x8 pack8(const float* a, const float* b) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) { v[j] = (__bf16)a[j]; v[4 + j] = (__bf16)b[j]; }
   return v;
+}
+
+// Workgroup -> (query/key block, head, utterance). The grid is 1-D; workgroup i runs on XCD
+// i % 8. With H % 8 == 0 each XCD gets H/8 heads for every utterance, so the [H, T, Tb] f32
+// relative-position bias rows of its heads (2 x 0.7 MB at T = 399) stay in that XCD's 4 MB L2
+// across all B utterances instead of streaming from the Infinity Cache per workgroup, and the
+// blocks of one (b, h) run back to back on one XCD (their K/V tiles shared in L2).
+struct BlockPos { int blk, h, b; };
+NRSE_DEV BlockPos block_pos(int nblk, int H) {
+  const int id = blockIdx.x;
+  if ((H & 7) == 0) {
+    const int hx = H >> 3;
+    const int xcd = id & 7, local = id >> 3;
+    const int blk = local % nblk;
+    const int r = local / nblk;
+    return BlockPos{blk, xcd * hx + r % hx, r / hx};
+  }
+  return BlockPos{id % nblk, (id / nblk) % H, id / (nblk * H)};
 }
 
 // A 64-row x 64-d bf16 tile (rows row0.. of a matrix with row stride ld) moved by 256 threads,
@@ -101,10 +125,11 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
   char* Vt = lds + TILE_B;
   const int T = p.T, H = p.H, Hd = H * D;
   const long long ld3 = 3LL * Hd;
-  const int b = blockIdx.z, h = blockIdx.y;
+  const BlockPos bp = block_pos((p.T + 63) / 64, p.H);
+  const int b = bp.b, h = bp.h;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, i16 = lane & 15;
-  const int qi = blockIdx.x * 64 + w * 16 + i16;
+  const int qi = bp.blk * 64 + w * 16 + i16;
   const bool qv = qi < T;
   const int Tb = (T + 63) & ~63;
   const bf16_t* qkv = (const bf16_t*)p.qkv + (long long)b * T * ld3;
@@ -118,6 +143,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
   }
   const long long bh = (long long)b * H + h;
   const float gi = qv ? p.gate[bh * T + qi] : 0.f;
+  const float c1 = p.scale * LOG2E, gl = gi * LOG2E;
   const float* brow = p.bias + ((long long)h * T + (qv ? qi : T - 1)) * Tb;
   const uint32_t key = site_key(p.seed);
   const uint32_t thr = dropout_threshold(p.dropout_p);
@@ -152,7 +178,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
       const float bb[4] = {bv.x, bv.y, bv.z, bv.w};
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float x = s[t][r] * p.scale + gi * bb[r];
+        const float x = fmaf(s[t][r], c1, gl * bb[r]);
         v[t][r] = (k0 + r < T) ? x : -INFINITY;
         mx = fmaxf(mx, v[t][r]);
       }
@@ -160,7 +186,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float mn = fmaxf(m, mx);
-    const float alpha = __expf(m - mn);
+    const float alpha = exp2_(m - mn);
     m = mn;
     float pd[4][4];
     float ps = 0.f;
@@ -168,7 +194,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float e = __expf(v[t][r] - mn);
+        const float e = exp2_(v[t][r] - mn);
         ps += e;
         const int kj = kb + 16 * t + 4 * g + r;
         pd[t][r] = (drop && !dropout_keep(key, rowidx + kj, thr)) ? 0.f : e * dsc;
@@ -191,7 +217,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
   float l = lpart + __shfl_xor(lpart, 16, 64);
   l += __shfl_xor(l, 32, 64);
   bf16_t* ctx = (bf16_t*)p.ctx;
-  const int qrow0 = blockIdx.x * 64 + w * 16;
+  const int qrow0 = bp.blk * 64 + w * 16;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const float lr = __shfl(l, 4 * g + r, 64);
@@ -202,7 +228,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
       for (int dt = 0; dt < 4; ++dt) ctx[((long long)b * T + q) * Hd + h * D + 16 * dt + i16] = f2bf(o[dt][r] * inv);
     }
   }
-  if (g == 0 && qv) p.lse[bh * T + qi] = m + __logf(l);
+  if (g == 0 && qv) p.lse[bh * T + qi] = (m + __builtin_amdgcn_logf(l)) * LN2;
 }
 
 // ------------------------------------------------------------------------------ bwd: dQ, dgate
@@ -212,10 +238,11 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
   char* Vt = lds + TILE_B;
   const int T = p.T, H = p.H, Hd = H * D;
   const long long ld3 = 3LL * Hd;
-  const int b = blockIdx.z, h = blockIdx.y;
+  const BlockPos bp = block_pos((p.T + 63) / 64, p.H);
+  const int b = bp.b, h = bp.h;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, i16 = lane & 15;
-  const int qi = blockIdx.x * 64 + w * 16 + i16;
+  const int qi = bp.blk * 64 + w * 16 + i16;
   const bool qv = qi < T;
   const int Tb = (T + 63) & ~63;
   const bf16_t* qkv = (const bf16_t*)p.qkv + (long long)b * T * ld3;
@@ -243,7 +270,9 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
   dsum += __shfl_xor(dsum, 32, 64);
   const long long bh = (long long)b * H + h;
   const float gi = qv ? p.gate[bh * T + qi] : 0.f;
+  const float c1 = p.scale * LOG2E, gl = gi * LOG2E;
   const float lse = qv ? p.lse[bh * T + qi] : 0.f;
+  const float lse2 = lse * LOG2E;
   const float delta = dsum;
   if (g == 0 && qv) p.delta[bh * T + qi] = delta;  // consumed by attn_bwd_kv_kernel (launched after)
   const float* brow = p.bias + ((long long)h * T + (qv ? qi : T - 1)) * Tb;
@@ -289,7 +318,7 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
         const int kj = k0 + r;
         float d = 0.f;
         if (kj < T && qv) {
-          const float pr = __expf(s[t][r] * p.scale + gi * bb[r] - lse);
+          const float pr = exp2_(fmaf(s[t][r], c1, gl * bb[r]) - lse2);
           float dpv = dp[t][r];
           if (drop) dpv = dropout_keep(key, rowidx + kj, thr) ? dpv * dsc : 0.f;
           d = pr * (dpv - delta);
@@ -310,7 +339,7 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
   dgate += __shfl_xor(dgate, 32, 64);
   if (g == 0 && qv) p.dgate[bh * T + qi] = dgate;
   bf16_t* dqkv = (bf16_t*)p.dqkv + (long long)b * T * ld3;
-  const int qrow0 = blockIdx.x * 64 + w * 16;
+  const int qrow0 = bp.blk * 64 + w * 16;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int q = qrow0 + 4 * g + r;
@@ -331,10 +360,11 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(const nrse_attn_bwd_pa
   float* diag = btile + 64 * BT_LD;                          // [4 lane groups][T + 64]
   const int T = p.T, H = p.H, Hd = H * D;
   const long long ld3 = 3LL * Hd;
-  const int b = blockIdx.z, h = blockIdx.y;
+  const BlockPos bp = block_pos((p.T + 63) / 64, p.H);
+  const int b = bp.b, h = bp.h;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, i16 = lane & 15;
-  const int kb0 = blockIdx.x * 64;
+  const int kb0 = bp.blk * 64;
   const int kj = kb0 + w * 16 + i16;
   const bool kv = kj < T;
   const int Tb = (T + 63) & ~63;
@@ -361,8 +391,12 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(const nrse_attn_bwd_pa
   for (int e = tid; e < 4 * ndiag; e += 256) diag[e] = 0.f;
   float* mydiag = diag + g * ndiag;
   float dacc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  // rotation by r wraps for lanes i16 >= 16 - r
+  const float whi[3] = {i16 >= 15 ? 1.f : 0.f, i16 >= 14 ? 1.f : 0.f, i16 >= 13 ? 1.f : 0.f};
+  const float wlo[3] = {1.f - whi[0], 1.f - whi[1], 1.f - whi[2]};
   const long long bh = (long long)b * H + h;
   const uint32_t key = site_key(p.seed);
+  const float c1 = p.scale * LOG2E;
   const uint32_t thr = dropout_threshold(p.dropout_p);
   const bool drop = p.dropout_p > 0.f;
   const float dsc = drop ? 1.f / (1.f - p.dropout_p) : 1.f;
@@ -383,7 +417,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(const nrse_attn_bwd_pa
     if (tid < 64) {
       const int q = qb + tid;
       const bool ok = q < T;
-      rn[0] = ok ? p.lse[bh * T + q] : 0.f;
+      rn[0] = ok ? p.lse[bh * T + q] * LOG2E : 0.f;
       rn[1] = ok ? p.delta[bh * T + q] : 0.f;
       rn[2] = ok ? p.gate[bh * T + q] : 0.f;
     }
@@ -412,7 +446,8 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(const nrse_attn_bwd_pa
     for (int u = 0; u < 4; ++u) {
       const int e = tid + 256 * u;
       const int row = e >> 4, c4 = (e & 15) * 4;
-      *reinterpret_cast<float4*>(btile + row * BT_LD + c4) = bn[u];
+      *reinterpret_cast<float4*>(btile + row * BT_LD + c4) =
+          make_float4(bn[u].x * LOG2E, bn[u].y * LOG2E, bn[u].z * LOG2E, bn[u].w * LOG2E);
     }
 #if NRSE_ATT_ABLATE == 3
     }
@@ -441,8 +476,8 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(const nrse_attn_bwd_pa
         float pv = 0.f, d = 0.f, gdv = 0.f;
         if (q < T && kv) {
           const float gq = rowc[128 + ql];
-          const float x = s[t][r] * p.scale + gq * btile[ql * BT_LD + kl];
-          const float pr = __expf(x - rowc[ql]);
+          const float x = fmaf(s[t][r], c1, gq * btile[ql * BT_LD + kl]);  // log2 domain
+          const float pr = exp2_(x - rowc[ql]);
           float dpv = dp[t][r];
           pv = pr * dsc;
 #if NRSE_ATT_ABLATE != 2
@@ -464,9 +499,9 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(const nrse_attn_bwd_pa
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         dacc[t] += gv[t][0];
-        diag_rot<1>(gv[t][1], i16, dacc[t], dacc[t + 1]);
-        diag_rot<2>(gv[t][2], i16, dacc[t], dacc[t + 1]);
-        diag_rot<3>(gv[t][3], i16, dacc[t], dacc[t + 1]);
+        diag_rot<1>(gv[t][1], wlo[0], whi[0], dacc[t], dacc[t + 1]);
+        diag_rot<2>(gv[t][2], wlo[1], whi[1], dacc[t], dacc[t + 1]);
+        diag_rot<3>(gv[t][3], wlo[2], whi[2], dacc[t], dacc[t + 1]);
       }
       // diagonals x - 4g - 16j (j < 4) relative to kb0 + 16w - qb are complete
       const int c0 = kb0 + 16 * w - qb + i16 - 4 * g - dbase;
@@ -520,13 +555,13 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(const nrse_attn_bwd_pa
 int nrse_attn_use_mfma(int dtype, int head_dim) { return dtype == NRSE_BF16 && head_dim == D; }
 
 int nrse_attn_fwd_mfma(const nrse_attn_fwd_params* p, hipStream_t st) {
-  dim3 grid((p->T + 63) / 64, p->H, p->batch);
+  const dim3 grid((unsigned)((p->T + 63) / 64 * p->H * p->batch));
   hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), 0, st, *p);
   return nrse_check_launch("nrse_attn_fwd(mfma)");
 }
 
 int nrse_attn_bwd_mfma(const nrse_attn_bwd_params* p, hipStream_t st) {
-  dim3 grid((p->T + 63) / 64, p->H, p->batch);
+  const dim3 grid((unsigned)((p->T + 63) / 64 * p->H * p->batch));
   const size_t lds_kv = 2 * TILE_B + (192 + 64 * BT_LD + 4 * (p->T + 64 + DPAD)) * sizeof(float);
   if (lds_kv > 160 * 1024) {
     nrse_set_error("nrse_attn_bwd: T=%d too long for the LDS diagonal accumulator", p->T);

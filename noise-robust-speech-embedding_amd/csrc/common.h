@@ -32,18 +32,10 @@ NRSE_DEV void store_from_f(void* p, int dtype, long long i, float v) {
   else ((float*)p)[i] = v;
 }
 
-// Exact (erf) GELU as ACT2FN["gelu"] ([TF] activations.GELUActivation -> F.gelu default).
-NRSE_DEV float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
-NRSE_DEV float gelu_grad_f(float x) {
-  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
-  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
-  return cdf + x * pdf;
-}
 
-// Fast erf for the GEMM epilogues: odd/even rational minimax approximation on [-4, 4] (the
-// single-precision coefficient set used by XLA / Eigen), |error| < 7e-8 in exact arithmetic and
-// < 5e-7 evaluated in f32 (erff: ~35 VALU instructions with both branches taken in a divergent
-// wave; this: 14). Used where the result is rounded to bf16 anyway (bf16 GEMM epilogues).
+// Fast erf: odd/even rational minimax approximation on [-4, 4] (the single-precision
+// coefficient set used by XLA / Eigen), |error| < 7e-8 in exact arithmetic and < 5e-7 evaluated
+// in f32 (erff: ~35 VALU instructions with both branches taken in a divergent wave; this: 14).
 NRSE_DEV float erf_fast(float x) {
   x = fminf(fmaxf(x, -4.f), 4.f);
   const float x2 = x * x;
@@ -65,6 +57,11 @@ NRSE_DEV float gelu_grad_fast(float x) {
   const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
   return cdf + x * pdf;
 }
+// erf GELU as ACT2FN["gelu"] ([TF] activations.GELUActivation -> F.gelu default), evaluated with
+// erf_fast everywhere (|error| ~5e-7, the order of f32 erff's own; the parity tolerances are
+// 1e-5 rel-L2 per kernel and 1e-3 on embeddings).
+NRSE_DEV float gelu_f(float x) { return gelu_fast(x); }
+NRSE_DEV float gelu_grad_f(float x) { return gelu_grad_fast(x); }
 
 // Counter-based dropout hash (bijective 32-bit mixer, "lowbias32"). The mask of element i at
 // a dropout site seeded with `seed` is keep = hash(i ^ mix(seed)) >= p * 2^32. Deterministic

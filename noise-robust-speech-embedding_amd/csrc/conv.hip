@@ -214,7 +214,7 @@ __global__ __launch_bounds__(256) void conv0_bwd_kernel(const nrse_conv0_params 
     __syncthreads();
     for (int c = threadIdx.x; c < C; c += 256) {
       const float v = red[0][c] + red[1][c] + red[2][c] + red[3][c];
-      if (j < p.k) atomicAdd(p.dw + c * p.k + j, v);
+      if (j < p.k) atomicAdd(p.dw + (long long)j * C + c, v);  // [k][C]: 256-B atomic wave-instructions
       else if (j == p.k) atomicAdd(p.dgamma + c, v);
       else atomicAdd(p.dbeta + c, v);
     }
@@ -320,7 +320,7 @@ extern "C" int nrse_conv0_bwd(const nrse_conv0_params* p, void* stream) {
   if (p->dy_mode == NRSE_DY_COL2IM) NRSE_REQUIRE(p->col_k > 0 && p->col_s > 0 && p->col_tout > 0, "nrse_conv0_bwd: col2im");
   const long long rows = (long long)p->batch * p->T0;
   long long blocks = (rows + 3) / 4;
-  if (blocks > 2048) blocks = 2048;
+  if (blocks > 1024) blocks = 1024;  // each block adds (k + 2) * C partial sums at the end
   hipStream_t st = (hipStream_t)stream;
   switch (p->C) {
     case 256: hipLaunchKernelGGL(conv0_bwd_kernel<1>, dim3(blocks), dim3(256), 0, st, *p); break;

@@ -84,9 +84,25 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_dma_kernel(const nrse_gemm_param
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int n0 = blockIdx.x * BN;
-  const int m0 = blockIdx.y * BM;
-  const int z = blockIdx.z;
+  // XCD-aware, M-grouped tile order (as gemm256.hip): workgroup i runs on XCD i % 8, so the
+  // ids are renumbered to give each XCD a contiguous run of tiles, walked GM M-tiles deep, and
+  // the tiles an XCD holds at once share their A and B panels in its L2. (Row-major grid order
+  // put one N column on each XCD: every XCD streamed all of A, 4x the algorithmic traffic on
+  // the weight-gradient GEMMs.)
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int mt = (p.M + BM - 1) / BM, nt = (p.N + BN - 1) / BN;
+  const int per_z = mt * nt;
+  const int z = wg / per_z;
+  const int tt = wg - z * per_z;
+  constexpr int GM = 8;
+  const int group = tt / (GM * nt);
+  const int first_m = group * GM;
+  const int gm = min(GM, mt - first_m);
+  const int in_g = tt - group * GM * nt;
+  const int m0 = (first_m + in_g % gm) * BM;
+  const int n0 = (in_g / gm) * BN;
   const int zb = z / p.splits;
   const int split = z % p.splits;
   const long long zq = zb / p.zdiv, zr = zb % p.zdiv;
@@ -199,14 +215,17 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_dma_kernel(const nrse_gemm_param
 
 template <bool AKC, bool BKC>
 int launch(const nrse_gemm_params* p, hipStream_t st) {
-  dim3 grid(nrse_cdiv(p->N, BN), nrse_cdiv(p->M, BM), p->batch * p->splits);
-  hipLaunchKernelGGL((gemm_dma_kernel<AKC, BKC>), grid, dim3(NTHR), 0, st, *p);
+  const long long total = (long long)nrse_cdiv(p->N, BN) * nrse_cdiv(p->M, BM) * p->batch * p->splits;
+  hipLaunchKernelGGL((gemm_dma_kernel<AKC, BKC>), dim3((unsigned)total), dim3(NTHR), 0, st, *p);
   return nrse_check_launch("nrse_gemm(dma)");
 }
 
 }  // namespace
 
-bool nrse_gemm_dma_ok(const nrse_gemm_params* p) { return p->M >= 64 && dma_layout_ok(p, 64); }
+bool nrse_gemm_dma_ok(const nrse_gemm_params* p) {
+  return p->M >= 64 && dma_layout_ok(p, 64) &&
+         (long long)nrse_cdiv(p->N, BN) * nrse_cdiv(p->M, BM) * p->batch * p->splits < (1LL << 31);
+}
 
 int nrse_gemm_dma(const nrse_gemm_params* p, hipStream_t st) {
   if (p->a.kcontig && p->b.kcontig) return launch<true, true>(p, st);

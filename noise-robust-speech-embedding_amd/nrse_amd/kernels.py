@@ -100,6 +100,17 @@ def gemm(A: Operand, B: Operand, C: torch.Tensor, M: int, N: int, K: int, *, ldc
     p.colsum = ptr(colsum)
     probe = _GEMM_PROBE
     if probe is not None:
+        # algorithmic HBM bytes: A and B read once, C written once (read too when accumulated),
+        # epilogue operands (bias, aux, residual) once
+        ea = A.t.element_size()
+        nb = (M * K * nseg * splits + N * K * nseg * splits) * ea * batch
+        cb = M * N * C.element_size() * batch * (splits if flags & _lib.EPI_ATOMIC else 1)
+        nb += cb * (2 if flags & (_lib.EPI_ACCUM | _lib.EPI_ATOMIC) else 1)
+        if aux is not None:
+            nb += M * N * aux.element_size() * batch
+        if resid is not None:
+            nb += M * N * resid.element_size() * batch
+        _GEMM_PROBE_BYTES.append(nb)
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record()
@@ -119,9 +130,18 @@ def gemm_select(generation: int) -> int:
     return int(_lib.lib().nrse_gemm_select(int(generation)))
 
 
+_GEMM_PROBE_BYTES = []
+
+
 def set_gemm_probe(lst):
     global _GEMM_PROBE
     _GEMM_PROBE = lst
+    if lst is not None:
+        _GEMM_PROBE_BYTES.clear()
+
+
+def gemm_probe_bytes():
+    return list(_GEMM_PROBE_BYTES)
 
 
 # ----------------------------------------------------------------------------- linear helpers
@@ -290,8 +310,11 @@ def conv0_fwd(wav, w, gamma, beta, out, mean, rstd, T0, k, s, eps):
 
 
 def conv0_bwd(wav, w, gamma, beta, mean, rstd, dy, dw, dgamma, dbeta, T0, k, s, col):
+    """dw ([C, k] or [C, 1, k] f32) += the conv0 weight gradient (the kernel accumulates a
+    tap-major [k, C] copy, transposed into dw here)."""
     B, L = wav.shape
     C = w.shape[0]
+    dwT = torch.zeros(k, C, device=wav.device, dtype=torch.float32)
     p = Conv0Params()
     p.wav, p.L, p.w, p.gamma, p.beta = ptr(wav), L, ptr(w), ptr(gamma), ptr(beta)
     p.mean, p.rstd = ptr(mean), ptr(rstd)
@@ -301,9 +324,10 @@ def conv0_bwd(wav, w, gamma, beta, mean, rstd, dy, dw, dgamma, dbeta, T0, k, s, 
     else:
         p.dy_mode = _lib.DY_COL2IM
         p.col_k, p.col_s, p.col_tout = col
-    p.dw, p.dgamma, p.dbeta = ptr(dw), ptr(dgamma), ptr(dbeta)
+    p.dw, p.dgamma, p.dbeta = ptr(dwT), ptr(dgamma), ptr(dbeta)
     p.batch, p.T0, p.C, p.k, p.s = B, T0, C, k, s
     _call("nrse_conv0_bwd", ctypes.byref(p), stream_ptr())
+    swap12(dwT, dw, 1, k, C, accumulate=True)
 
 
 def weight_norm_fwd(g, v, wf, wd, norms, H, cpg, K):
