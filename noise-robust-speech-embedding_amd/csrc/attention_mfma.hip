@@ -169,20 +169,26 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss) s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rd_row(Kt, 16 * t + i16, 4 * ss + g), qf[ss], s[t], 0, 0, 0);
     }
+    // Wave-uniform branches keep the per-element work straight-line: the key mask only on the
+    // last (partial) tile, the dropout hash only when dropout is on (its 1/(1-p) scale is folded
+    // into the final 1/l).
     float v[4][4];
-    float mx = -INFINITY;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const int k0 = kb + 16 * t + 4 * g;
-      const float4 bv = *reinterpret_cast<const float4*>(brow + k0);
+      const float4 bv = *reinterpret_cast<const float4*>(brow + kb + 16 * t + 4 * g);
       const float bb[4] = {bv.x, bv.y, bv.z, bv.w};
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float x = fmaf(s[t][r], c1, gl * bb[r]);
-        v[t][r] = (k0 + r < T) ? x : -INFINITY;
-        mx = fmaxf(mx, v[t][r]);
-      }
+      for (int r = 0; r < 4; ++r) v[t][r] = fmaf(s[t][r], c1, gl * bb[r]);
     }
+    if (kb + 64 > T) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[t][r] = (kb + 16 * t + 4 * g + r < T) ? v[t][r] : -INFINITY;
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) mx = fmaxf(fmaxf(mx, fmaxf(v[t][0], v[t][1])), fmaxf(v[t][2], v[t][3]));
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float mn = fmaxf(m, mx);
@@ -194,11 +200,16 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float e = exp2_(v[t][r] - mn);
-        ps += e;
-        const int kj = kb + 16 * t + 4 * g + r;
-        pd[t][r] = (drop && !dropout_keep(key, rowidx + kj, thr)) ? 0.f : e * dsc;
+        pd[t][r] = exp2_(v[t][r] - mn);
+        ps += pd[t][r];
       }
+    if (drop) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          pd[t][r] = dropout_keep(key, rowidx + (uint32_t)(kb + 16 * t + 4 * g + r), thr) ? pd[t][r] : 0.f;
+    }
     lpart = lpart * alpha + ps;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -221,7 +232,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const float lr = __shfl(l, 4 * g + r, 64);
-    const float inv = 1.f / lr;
+    const float inv = dsc / lr;
     const int q = qrow0 + 4 * g + r;
     if (q < T) {
 #pragma unroll
@@ -307,25 +318,36 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
         dp[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rd_row(Vt, 16 * t + i16, 4 * ss + g), dof[ss], dp[t], 0, 0, 0);
       }
     }
-    float ds[4][4];
+    // Straight-line per element; wave-uniform branches for dropout and for the last (partial)
+    // key tile. Rows of invalid queries need no mask: their Q, dO, gate, lse and delta are zero,
+    // so d = 1 * (0 - 0) = 0.
+    float ds[4][4], bb[4][4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const int k0 = kb + 16 * t + 4 * g;
-      const float4 bv = *reinterpret_cast<const float4*>(brow + k0);
-      const float bb[4] = {bv.x, bv.y, bv.z, bv.w};
+      const float4 bv = *reinterpret_cast<const float4*>(brow + kb + 16 * t + 4 * g);
+      bb[t][0] = bv.x; bb[t][1] = bv.y; bb[t][2] = bv.z; bb[t][3] = bv.w;
+    }
+    if (drop) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int kj = k0 + r;
-        float d = 0.f;
-        if (kj < T && qv) {
-          const float pr = exp2_(fmaf(s[t][r], c1, gl * bb[r]) - lse2);
-          float dpv = dp[t][r];
-          if (drop) dpv = dropout_keep(key, rowidx + kj, thr) ? dpv * dsc : 0.f;
-          d = pr * (dpv - delta);
-        }
-        ds[t][r] = d;
-        dgate += d * bb[r];
-      }
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          dp[t][r] = dropout_keep(key, rowidx + (uint32_t)(kb + 16 * t + 4 * g + r), thr) ? dp[t][r] * dsc : 0.f;
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ds[t][r] = exp2_(fmaf(s[t][r], c1, gl * bb[t][r]) - lse2) * (dp[t][r] - delta);
+    if (kb + 64 > T) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ds[t][r] = (kb + 16 * t + 4 * g + r < T) ? ds[t][r] : 0.f;
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dgate += ds[t][r] * bb[t][r];
     }
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
@@ -367,6 +389,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(const nrse_attn_bwd_pa
   const int kb0 = bp.blk * 64;
   const int kj = kb0 + w * 16 + i16;
   const bool kv = kj < T;
+  const float kvf = kv ? 1.f : 0.f;
   const int Tb = (T + 63) & ~63;
   const bf16_t* qkv = (const bf16_t*)p.qkv + (long long)b * T * ld3;
   const bf16_t* dctx = (const bf16_t*)p.dctx + (long long)b * T * Hd;
@@ -465,34 +488,44 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(const nrse_attn_bwd_pa
         dp[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rd_row(Ot, 16 * t + i16, 4 * ss + g), vf[ss], dp[t], 0, 0, 0);
       }
     }
-    // element (query qb + 16t + 4g + r, key kj)
+    // element (query qb + 16t + 4g + r, key kj). Straight-line per element; the dropout hash
+    // behind one wave-uniform branch, its 1/(1-p) on P folded into the final dV scale. Rows of
+    // invalid queries contribute zero by construction (zero Q, dO, lse, delta, gate, bias rows);
+    // lanes of invalid keys produce dK/dV rows that are never stored, and kvf keeps them out of
+    // the diagonal sums.
     float pd[4][4], ds[4][4], gv[4][4];
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int ql = 16 * t + 4 * g + r;
-        const int q = qb + ql;
-        float pv = 0.f, d = 0.f, gdv = 0.f;
-        if (q < T && kv) {
-          const float gq = rowc[128 + ql];
-          const float x = fmaf(s[t][r], c1, gq * btile[ql * BT_LD + kl]);  // log2 domain
-          const float pr = exp2_(x - rowc[ql]);
-          float dpv = dp[t][r];
-          pv = pr * dsc;
+        ds[t][r] = exp2_(fmaf(s[t][r], c1, rowc[128 + ql] * btile[ql * BT_LD + kl]) - rowc[ql]);  // P (log2 domain)
+      }
 #if NRSE_ATT_ABLATE != 2
-          if (drop) {
-            const bool keep = dropout_keep(key, (uint32_t)((bh * T + q) * T + kj), thr);
-            if (!keep) { pv = 0.f; dpv = 0.f; }
-            else dpv *= dsc;
-          }
-#endif
-          d = pr * (dpv - rowc[64 + ql]);
-          gdv = d * gq;
+    if (drop) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool keep = dropout_keep(key, (uint32_t)((bh * T + qb + 16 * t + 4 * g + r) * T + kj), thr);
+          pd[t][r] = keep ? ds[t][r] : 0.f;
+          dp[t][r] = keep ? dp[t][r] * dsc : 0.f;
         }
-        pd[t][r] = pv;
-        ds[t][r] = d;
-        gv[t][r] = gdv;
+    } else
+#endif
+    {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pd[t][r] = ds[t][r];
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ql = 16 * t + 4 * g + r;
+        ds[t][r] *= dp[t][r] - rowc[64 + ql];
+        gv[t][r] = ds[t][r] * (rowc[128 + ql] * kvf);
       }
 #if NRSE_ATT_ABLATE != 1
     if (p.diag) {
@@ -531,7 +564,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(const nrse_attn_bwd_pa
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         dqkv[(long long)k * ld3 + Hd + h * D + 16 * dt + i16] = f2bf(dk[dt][r] * p.scale);
-        dqkv[(long long)k * ld3 + 2 * Hd + h * D + 16 * dt + i16] = f2bf(dv[dt][r]);
+        dqkv[(long long)k * ld3 + 2 * Hd + h * D + 16 * dt + i16] = f2bf(dv[dt][r] * dsc);
       }
     }
   }
