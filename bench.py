@@ -99,6 +99,9 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--detail", default=None, help="write per-shape GEMM timings here (json)")
+    ap.add_argument("--workload", default="fixed", choices=["fixed", "varlen"],
+                    help="fixed: configs[1] (8 s pairs, the metric); varlen: configs[4] (3-12 s length-bucketed "
+                         "pairs, MUSAN-style noise of its own length, SNR {4, 8})")
     args = ap.parse_args()
 
     from nrse_amd import arch as A, ddp, kernels as K
@@ -137,6 +140,30 @@ def main():
         K.snr_mix(clean_raw, noise_raw, noise_len, snr, clean_iv, noisy_iv, status, kscale, K.SNR_PEAK_ZMUV)
         return eng.train_step(clean_iv, noisy_iv, lr=lr_at(i), step_seed=i, rank=rank, allreduce=allreduce,
                               world_size=world)
+
+    varlen_batches = None
+    if args.workload == "varlen":
+        # configs[4]: every step a different length-bucketed batch of 3-12 s pairs, all staged in
+        # HBM before the timed region (the raw mix inputs; the SNR mix runs inside the step)
+        from nrse_amd import data as D
+        n_items = max(64, (args.steps + args.warmup) * B * world * 2)
+        ds = D.SyntheticVarLenPairs(n_items, 16000, 3.0, 12.0, [4, 8], seed=1234)
+        dl = D.create_varlen_loader(ds, B, seed=1234, rank=rank, world=world, num_workers=0)
+        varlen_batches = []
+        for raw in dl:
+            varlen_batches.append({k: v.to(dev) for k, v in raw.items()})
+            if len(varlen_batches) == args.steps + args.warmup:
+                break
+        if len(varlen_batches) < args.steps + args.warmup:
+            raise SystemExit("varlen: not enough bucketed batches for the requested steps")
+
+        def step(i):  # noqa: F811
+            r = varlen_batches[i]
+            Lb = r["clean"].shape[1]
+            c = torch.empty(B, Lb, device=dev)
+            n = torch.empty(B, Lb, device=dev)
+            K.snr_mix(r["clean"], r["noise"], r["noise_len"], r["snr"].float(), c, n, status, kscale, K.SNR_PEAK_ZMUV)
+            return eng.train_step(c, n, lr=lr_at(i), step_seed=i, rank=rank, allreduce=allreduce, world_size=world)
 
     for i in range(args.warmup):
         step(i)
@@ -179,18 +206,30 @@ def main():
             json.dump({k: {"tflops": v[0] / (v[1] * 1e-3) / 1e12, "ms_total": v[1], "launches": v[2]}
                        for k, v in sorted(per.items(), key=lambda kv: -kv[1][1])}, fh, indent=1)
     avg_exec = (executed[0] / args.steps, executed[1] / args.steps)
-    fpp, _ = flops_per_pair(arch, L, avg_exec)
+    if varlen_batches is None:
+        fpp, _ = flops_per_pair(arch, L, avg_exec)
+        audio_s = B * L / 16000.0 * args.steps
+    else:
+        lens = [varlen_batches[args.warmup + i]["clean"].shape[1] for i in range(args.steps)]
+        fpp = sum(flops_per_pair(arch, Lb, avg_exec)[0] for Lb in lens) / len(lens)
+        audio_s = sum(float(varlen_batches[args.warmup + i]["lengths"].sum()) for i in range(args.steps)) / 16000.0
     pairs = B * world * args.steps
     value = pairs / dt
     result = {
-        "metric": "BYOL utterance-pairs/sec, WavLM-large, 8s@16kHz, batch=32 per GPU",
+        "metric": ("BYOL utterance-pairs/sec, WavLM-large, 8s@16kHz, batch=32 per GPU" if varlen_batches is None else
+                   "BYOL utterance-pairs/sec, WavLM-large, 3-12s@16kHz length-bucketed, batch=32 per GPU"),
         "value": round(value, 3), "unit": "pairs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(dt / args.steps * 1e3, 2), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (N(0,0.1^2) speech, N(0,1) noise, on-GPU SNR "
                                                          "mix), random-init WavLM-Large weights",
-        "config": {"workload": "configs[1]: WavLM-large BYOL train step, synthetic 8s@16kHz clean/noisy pairs, "
-                               "batch=32 per GPU", "global_batch": B * world, "seq_len": L, "frames": arch.frames(L),
-                   "parallelism": f"dp{world}", "layerdrop_executed_layers": avg_exec},
+        "config": ({"workload": "configs[1]: WavLM-large BYOL train step, synthetic 8s@16kHz clean/noisy pairs, "
+                                "batch=32 per GPU", "global_batch": B * world, "seq_len": L, "frames": arch.frames(L),
+                    "parallelism": f"dp{world}", "layerdrop_executed_layers": avg_exec}
+                   if varlen_batches is None else
+                   {"workload": "configs[4]: WavLM-large BYOL, synthetic 3-12 s pairs in 1 s length buckets (padded "
+                                "to 0.5 s), noise of independent length tiled on GPU, SNR {4,8} dB, batch=32 per GPU",
+                    "global_batch": B * world, "parallelism": f"dp{world}", "layerdrop_executed_layers": avg_exec,
+                    "audio_seconds_per_s_per_rank": round(audio_s / dt, 1)}),
         "roofline": {"bound": "mfma", "kernel": "nrse_gemm (all launches in the timed region)",
                      "achieved": round(achieved_tfs, 1), "peak": BF16_DENSE_PEAK_TFS if cdt == torch.bfloat16 else
                      F32_MFMA_PEAK_TFS, "unit": "TFLOP/s",

@@ -12,6 +12,7 @@ compressed formats and resampling are not supported (files must be at the config
 """
 from __future__ import annotations
 
+import functools
 import os
 import random
 import wave
@@ -166,3 +167,147 @@ def create_dataloaders(config: dict, feature_extractor=None, *, synthetic_items:
     train = torch.utils.data.DataLoader(train_ds, shuffle=True, **kw)
     val = torch.utils.data.DataLoader(val_ds, shuffle=False, **kw) if val_size >= int(t["batch_size"]) else None
     return train, val
+
+
+# ----------------------------------------------------------------------------- variable length
+# BASELINE config 5: variable-length 3-12 s utterances in length-bucketed batches. The reference
+# crops/pads every item to one fixed length (audio_utils.py:38-49) and its encoder takes no
+# attention mask (src/models/encoder.py:23-25); bucketing keeps those semantics per batch (zero
+# padding at the end, to the batch's padded length) while cutting the padding work.
+def padded_length(n: int, multiple: int) -> int:
+    return ((n + multiple - 1) // multiple) * multiple
+
+
+class LengthBucketBatchSampler(torch.utils.data.Sampler):
+    """Batches of indices whose lengths fall in the same bucket (`boundaries`, in samples,
+    ascending; bucket i holds lengths in (boundaries[i-1], boundaries[i]]). Seeded per epoch:
+    items are shuffled inside buckets, cut into batches, the batch order shuffled, and with
+    world > 1 every rank takes an equal, disjoint share of the batches (rank-strided)."""
+
+    def __init__(self, lengths, batch_size: int, boundaries, *, seed: int = 42, rank: int = 0, world: int = 1,
+                 drop_last: bool = True):
+        self.lengths = [int(n) for n in lengths]
+        self.batch_size = int(batch_size)
+        self.boundaries = [int(b) for b in boundaries]
+        self.seed, self.rank, self.world, self.drop_last = seed, rank, world, drop_last
+        self.epoch = 0
+
+    def set_epoch(self, epoch: int) -> None:
+        self.epoch = int(epoch)
+
+    def bucket_of(self, n: int) -> int:
+        for i, b in enumerate(self.boundaries):
+            if n <= b:
+                return i
+        return len(self.boundaries)
+
+    def _batches(self) -> list:
+        rng = random.Random(self.seed * 1000003 + self.epoch)
+        buckets = {}
+        for i, n in enumerate(self.lengths):
+            buckets.setdefault(self.bucket_of(n), []).append(i)
+        batches = []
+        for k in sorted(buckets):
+            idx = buckets[k]
+            rng.shuffle(idx)
+            for s in range(0, len(idx), self.batch_size):
+                b = idx[s:s + self.batch_size]
+                if len(b) == self.batch_size or not self.drop_last:
+                    batches.append(b)
+        rng.shuffle(batches)
+        n = (len(batches) // self.world) * self.world
+        return batches[:n][self.rank::self.world]
+
+    def __iter__(self):
+        return iter(self._batches())
+
+    def __len__(self) -> int:
+        return len(self._batches())
+
+
+def collate_varlen(items: list, pad_multiple: int = 8000) -> dict:
+    """Raw varlen items -> {clean [B, Lp], noise [B, Ln], noise_len [B], snr [B], lengths [B]}:
+    clean zero-padded at the end to the batch maximum rounded up to `pad_multiple` samples (a
+    bounded set of step shapes), noise zero-padded to its batch maximum (the on-GPU mix tiles
+    each noise by its own noise_len, augment.py:10-15)."""
+    lens = [int(it["clean"].shape[0]) for it in items]
+    Lp = padded_length(max(lens), pad_multiple)
+    Ln = max(int(it["noise"].shape[0]) for it in items)
+    B = len(items)
+    clean = torch.zeros(B, Lp)
+    noise = torch.zeros(B, Ln)
+    for i, it in enumerate(items):
+        clean[i, :lens[i]] = it["clean"]
+        noise[i, :it["noise"].shape[0]] = it["noise"]
+    return {"clean": clean, "noise": noise,
+            "noise_len": torch.tensor([int(it["noise"].shape[0]) for it in items], dtype=torch.int32),
+            "snr": torch.stack([it["snr"] for it in items]), "lengths": torch.tensor(lens, dtype=torch.int64)}
+
+
+class SyntheticVarLenPairs(torch.utils.data.Dataset):
+    """Synthetic raw pairs with seeded lengths U[min_s, max_s] seconds (speech ~ N(0, 0.1^2),
+    noise ~ N(0, 1) of an independent random length: the MUSAN-style noise pool of config 5)."""
+
+    def __init__(self, n_items, sample_rate, min_s, max_s, snr_range, seed=1234):
+        self.n_items, self.sr, self.snr_range, self.seed = n_items, sample_rate, list(snr_range), seed
+        g = np.random.default_rng(seed)
+        self.lengths = g.integers(int(min_s * sample_rate), int(max_s * sample_rate) + 1, n_items)
+        self.noise_lengths = g.integers(int(min_s * sample_rate), int(max_s * sample_rate) + 1, n_items)
+
+    def __len__(self):
+        return self.n_items
+
+    def __getitem__(self, idx):
+        g = torch.Generator().manual_seed(self.seed * 1000003 + idx)
+        return {"clean": torch.randn(int(self.lengths[idx]), generator=g) * 0.1,
+                "noise": torch.randn(int(self.noise_lengths[idx]), generator=g),
+                "noise_len": torch.tensor(int(self.noise_lengths[idx]), dtype=torch.int32),
+                "snr": torch.tensor(self.snr_range[idx % len(self.snr_range)], dtype=torch.int64)}
+
+
+def wav_num_samples(path: str) -> int:
+    with wave.open(path, "rb") as w:
+        return w.getnframes()
+
+
+class WavVarLenPairs(torch.utils.data.Dataset):
+    """PCM WAV clean files at their own length (cropped to max_s), noise from a pool (MUSAN)."""
+
+    def __init__(self, clean_files, noise_files, sample_rate, max_s, snr_range, seed=42):
+        self.clean_files, self.noise_files = clean_files, noise_files
+        self.sr, self.nmax = sample_rate, int(max_s * sample_rate)
+        self.snr_range = list(snr_range)
+        self.rng = random.Random(seed)
+        self.lengths = [min(wav_num_samples(f), self.nmax) for f in clean_files]
+
+    def __len__(self):
+        return len(self.clean_files)
+
+    def _load(self, path, crop: bool):
+        x, sr = read_wav(path)
+        if sr != self.sr:
+            raise ValueError(f"{path}: sample rate {sr} != {self.sr} (no resampler in this build)")
+        return crop_or_pad(x, self.nmax, self.rng) if (crop and x.shape[0] > self.nmax) else x
+
+    def __getitem__(self, idx):
+        clean = self._load(self.clean_files[idx], True)
+        noise = self._load(self.noise_files[self.rng.randint(0, len(self.noise_files) - 1)], True)
+        return {"clean": torch.from_numpy(np.ascontiguousarray(clean)), "noise": torch.from_numpy(np.ascontiguousarray(noise)),
+                "noise_len": torch.tensor(noise.shape[0], dtype=torch.int32),
+                "snr": torch.tensor(self.rng.choice(self.snr_range), dtype=torch.int64)}
+
+
+def create_varlen_loader(dataset, batch_size: int, *, sample_rate: int = 16000, min_s: float = 3.0,
+                         max_s: float = 12.0, bucket_s: float = 1.0, pad_s: float = 0.5, seed: int = 42,
+                         rank: int = 0, world: int = 1, num_workers: int = 4):
+    """DataLoader of length-bucketed raw batches for a dataset exposing `.lengths` (samples)."""
+    edges = []
+    e = min_s + bucket_s
+    while e < max_s + 1e-9:
+        edges.append(int(round(e * sample_rate)))
+        e += bucket_s
+    sampler = LengthBucketBatchSampler(dataset.lengths, batch_size, edges, seed=seed, rank=rank, world=world)
+    pad = int(pad_s * sample_rate)
+    return torch.utils.data.DataLoader(dataset, batch_sampler=sampler, num_workers=num_workers,
+                                       collate_fn=functools.partial(collate_varlen, pad_multiple=pad),
+                                       pin_memory=True)

@@ -103,3 +103,19 @@ def test_stochastic_step_matches_oracle_with_same_masks(nrse_device):
                      layer_skip=skips, mask_time=masks)
     assert abs(float(loss) - r["loss"]) < 1e-4
     assert abs(eng.grad_norm() - r["grad_norm"]) / r["grad_norm"] < 1e-3
+
+
+def test_varlen_steps_match_oracle(nrse_device):
+    """Consecutive steps on different utterance lengths (config 5's bucketed batches): the
+    engine re-derives T, the rel-pos bucket table and every launch shape per step."""
+    arch = A.TINY.deterministic()
+    eng, st, _, _ = make(arch, torch.float32, B=4)
+    eng.cfg.ema_decay = 0.99
+    for i, L in enumerate((24000, 16000, 40000)):
+        g = torch.Generator().manual_seed(20 + i)
+        clean = torch.randn(4, L, generator=g)
+        noisy = clean + 0.3 * torch.randn(4, L, generator=g)
+        loss = eng.train_step(clean.cuda(), noisy.cuda(), lr=1e-4, step_seed=i)
+        r = O.train_step(st, clean, noisy, lr=1e-4, weight_decay=eng.cfg.weight_decay, ema_decay=0.99, step_seed=i)
+        assert abs(float(loss) - r["loss"]) < 1e-4, (L, float(loss), r["loss"])
+        assert abs(eng.grad_norm() - r["grad_norm"]) / r["grad_norm"] < 1e-3
