@@ -89,6 +89,56 @@ def gemm_traffic():
         return None
 
 
+def bench_emotion(args):
+    """configs[3]: one dimensional-emotion fine-tune iteration over the frozen WavLM-Large encoder
+    (default_wavlm-large_emotion_dim_ft.yaml: batch 36, 5 s, hidden 1024, dropout 0.3, AdamW
+    lr 1e-5 / wd 1e-4): encoder forward in train mode (no tape), head forward, CCC loss, head
+    backward, clip + AdamW. Synthetic audio and A/V/D labels; 1 GPU."""
+    from nrse_amd import arch as A, kernels as K
+    from nrse_amd.emotion import EmotionDimTrainer, EmotionHead
+    from nrse_amd.engine import ByolEngine
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    B = 36 if args.batch == 32 else args.batch
+    L = int(5.0 * 16000)
+    cdt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    eng = ByolEngine(A.LARGE, 1024, 2048, device=dev, compute_dtype=cdt, seed=1234)
+    head = EmotionHead(1024, 1024, 8, dropout=0.3, device=dev, compute_dtype=cdt, seed=42)
+    tr = EmotionDimTrainer(eng, head, lr=1e-5, weight_decay=1e-4)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(99)
+    wav = torch.randn(B, L, device=dev, generator=gen) * 0.1
+    labels = torch.rand(B, 3, device=dev, generator=gen) * 6 + 1
+    lengths = torch.full((B,), L, dtype=torch.int64)
+    for i in range(args.warmup):
+        tr.train_step(wav, labels, lengths, step_seed=i)
+    torch.cuda.synchronize()
+    probe = []
+    t0 = time.perf_counter()
+    K.set_gemm_probe(probe)
+    for i in range(args.steps):
+        tr.train_step(wav, labels, lengths, step_seed=args.warmup + i)
+    K.set_gemm_probe(None)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    gflops = sum(f for f, _, _, _ in probe)
+    gms = sum(e0.elapsed_time(e1) for _, e0, e1, _ in probe)
+    tfs = gflops / (gms * 1e-3) / 1e12 if gms > 0 else 0.0
+    result = {"metric": "emotion-dim fine-tune utterances/sec, frozen WavLM-large encoder, 5s@16kHz, batch=36",
+              "value": round(B * args.steps / dt, 3), "unit": "utterances/s", "n_gpus": 1, "steps": args.steps,
+              "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 2), "higher_is_better": True,
+              "scaling": "none", "vs_baseline": None, "dtype": args.dtype,
+              "data": "synthetic 5 s audio and A/V/D labels, random-init encoder and head",
+              "config": {"workload": "configs[3]: dimensional emotion head (attentive statistics pooling, shared + "
+                                     "dimensional FC, CCC loss) over the frozen encoder", "global_batch": B,
+                         "seq_len": L, "frames": A.LARGE.frames(L)},
+              "roofline": {"bound": "mfma", "kernel": "nrse_gemm (all launches in the timed region)",
+                           "achieved": round(tfs, 1), "peak": BF16_DENSE_PEAK_TFS, "unit": "TFLOP/s",
+                           "frac": round(tfs / BF16_DENSE_PEAK_TFS, 4), "launches": len(probe)},
+              "loss_last": round(float(head.loss_buf), 5)}
+    print(json.dumps(result), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -99,14 +149,17 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--detail", default=None, help="write per-shape GEMM timings here (json)")
-    ap.add_argument("--workload", default="fixed", choices=["fixed", "varlen"],
+    ap.add_argument("--workload", default="fixed", choices=["fixed", "varlen", "emotion"],
                     help="fixed: configs[1] (8 s pairs, the metric); varlen: configs[4] (3-12 s length-bucketed "
-                         "pairs, MUSAN-style noise of its own length, SNR {4, 8})")
+                         "pairs, MUSAN-style noise of its own length, SNR {4, 8}); emotion: configs[3] (dimensional "
+                         "emotion head over the frozen encoder, 36 x 5 s)")
     args = ap.parse_args()
 
     from nrse_amd import arch as A, ddp, kernels as K
     from nrse_amd.engine import ByolEngine, StepConfig
 
+    if args.workload == "emotion":
+        return bench_emotion(args)
     rank, world, local = ddp.init_from_env()
     if world != args.gpus and not (world == 1 and args.gpus == 1):
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)

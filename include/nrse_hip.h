@@ -79,7 +79,8 @@ enum {
   NRSE_EPI_ACCUM = 1 << 6,        /* v += C[m,n] (read-modify-write) */
   NRSE_EPI_ATOMIC = 1 << 7,       /* atomicAdd into f32 C */
   NRSE_EPI_COLSUM = 1 << 8,       /* colsum[n] += sum over rows of v (f32 atomics) */
-  NRSE_EPI_RELU = 1 << 9          /* v = max(v, 0) */
+  NRSE_EPI_RELU = 1 << 9,         /* v = max(v, 0) */
+  NRSE_EPI_TANH = 1 << 10         /* v = tanh(v) (attentive statistics pooling, src/models/pool.py:43) */
 };
 
 typedef struct {
@@ -133,7 +134,7 @@ int nrse_gemm_select(int generation);
  *      broadcast per utterance (NRSE_DY_BCAST: dy[b, t] = dy_vec[b] * dy_scale, the time-mean
  *      shim). dx = resid + LN'(...) (resid optional, f32). dgamma/dbeta accumulate (f32 atomics).
  * ------------------------------------------------------------------------------------------ */
-enum { NRSE_LN_GELU = 1 };
+enum { NRSE_LN_GELU = 1, NRSE_LN_RELU = 2 };   /* RELU: emotion heads, src/models/emotion.py:34-58 */
 enum { NRSE_DY_DIRECT = 0, NRSE_DY_COL2IM = 1, NRSE_DY_BCAST = 2 };
 
 typedef struct {
@@ -295,6 +296,26 @@ int nrse_bn_bwd(const float* dy, const float* x, const float* y, const float* w,
  * dp = dloss/dp (scaled by grad_scale); stats[0..1] = NaN flags before/after normalisation. */
 int nrse_byol_loss(const float* p, const float* z, float* loss, float* dp, float* stats, int rows, int D,
                    float grad_scale, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Downstream emotion head (BASELINE configs[3]; src/models/emotion.py over the frozen encoder).
+ * Attentive statistics pooling (src/models/pool.py:25-58) per utterance b over its first
+ * lens[b] frames (feat_len = (wav_len - 1) // 320 + 1, pool.py:11-19):
+ *   x [B, T, C] encoder output (f32/bf16), h [B, T, C] f32 = tanh(sap_linear(x)) (nrse_gemm with
+ *   NRSE_EPI_TANH), att [C]; w = softmax_t(h . att); pooled [B, 2C] = [sum w x,
+ *   sqrt(max(sum w x^2 - mu^2, 1e-5))]; w_out [B, T] and var_out [B, C] are saved for backward.
+ * Backward: dpre [B, T, C] = d(sap pre-activation) (zero past lens[b]; dtype dpre_dtype),
+ *   datt [C] accumulated; the encoder is frozen (no dx). C % 256 == 0, C <= 2048.
+ * CCC loss (src/train/dimentional_emotions.py:427-450): loss[0] = mean_d (1 - CCC_d) over pred,
+ *   target [rows, D]; dpred (optional) = dloss/dpred; 0 when rows <= 1.
+ * ------------------------------------------------------------------------------------------ */
+int nrse_asp_fwd(const void* x, int x_dtype, const float* h, const float* att, const int* lens, int batch, int T,
+                 int C, float* w_out, float* var_out, float* pooled, void* stream);
+int nrse_asp_bwd(const void* x, int x_dtype, const float* h, const float* att, const int* lens, int batch, int T,
+                 int C, const float* w_in, const float* var_in, const float* pooled, const float* dpooled, void* dpre,
+                 int dpre_dtype, float* datt, void* stream);
+int nrse_ccc_loss(const float* pred, int ld, const float* target, float* loss, float* dpred, int rows, int D,
+                  void* stream);   /* pred / dpred rows of stride ld >= D, target [rows, D] */
 
 /* ------------------------------------------------------------------------------------------
  * Optimiser tail over the flat f32 parameter / gradient buffers (train_byol.py:67-71,

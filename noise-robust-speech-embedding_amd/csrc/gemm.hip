@@ -305,6 +305,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const nrse_gemm_params p)
         }
         if (flags & NRSE_EPI_GELU_BWD) v *= gelu_grad_f(load_as_f(p.aux, p.aux_dtype, abase + (long long)m * p.ldaux + n));
         if (flags & NRSE_EPI_RELU) v = fmaxf(v, 0.f);
+        if (flags & NRSE_EPI_TANH) v = tanhf(v);
         const long long ci = cbase + (long long)m * p.ldc + n;
         const uint32_t eidx = (uint32_t)ci;
         if ((flags & NRSE_EPI_DROPOUT) && !(flags & NRSE_EPI_DROP_AFTER))

@@ -148,6 +148,10 @@ NRSE_DEV void epi8(const nrse_gemm_params& p, const Epi& e, int m, int n, float*
 #pragma unroll
     for (int i = 0; i < 8; ++i) v[i] = fmaxf(v[i], 0.f);
   }
+  if (flags & NRSE_EPI_TANH) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = tanhf(v[i]);
+  }
   const long long ci = e.cbase + (long long)m * p.ldc + n;
   if ((flags & NRSE_EPI_DROPOUT) && !(flags & NRSE_EPI_DROP_AFTER)) {
 #pragma unroll

@@ -78,6 +78,9 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const nrse_ln_fwd_params p)
     if (p.flags & NRSE_LN_GELU) {
 #pragma unroll
       for (int e = 0; e < CH; ++e) o[e] = gelu_f(o[e]);
+    } else if (p.flags & NRSE_LN_RELU) {
+#pragma unroll
+      for (int e = 0; e < CH; ++e) o[e] = fmaxf(o[e], 0.f);
     }
     store4(p.y, p.y_dtype, base + c0, o);
   }
@@ -140,7 +143,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const nrse_ln_bwd_params p)
       float4 ga = *reinterpret_cast<const float4*>(p.gamma + c0);
       const float gam[CH] = {ga.x, ga.y, ga.z, ga.w};
       float be[CH] = {0.f, 0.f, 0.f, 0.f};
-      if (p.flags & NRSE_LN_GELU) {
+      if (p.flags & (NRSE_LN_GELU | NRSE_LN_RELU)) {
         float4 bb = *reinterpret_cast<const float4*>(p.beta + c0);
         be[0] = bb.x; be[1] = bb.y; be[2] = bb.z; be[3] = bb.w;
       }
@@ -149,6 +152,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const nrse_ln_bwd_params p)
         xh[k][e] = (xv[e] - mean) * rstd;
         float gg = dy[e];
         if (p.flags & NRSE_LN_GELU) gg *= gelu_grad_f(xh[k][e] * gam[e] + be[e]);
+        else if (p.flags & NRSE_LN_RELU) gg = (xh[k][e] * gam[e] + be[e] > 0.f) ? gg : 0.f;
         dg[k][e] += gg * xh[k][e];
         db[k][e] += gg;
         g[k][e] = gg * gam[e];
@@ -264,7 +268,7 @@ extern "C" int nrse_layernorm_fwd(const nrse_ln_fwd_params* p, void* stream) {
 extern "C" int nrse_layernorm_bwd(const nrse_ln_bwd_params* p, void* stream) {
   NRSE_REQUIRE(p && p->dy && p->x && p->gamma && p->mean && p->rstd && p->dx && p->rows > 0,
                "nrse_layernorm_bwd: bad args");
-  NRSE_REQUIRE(!(p->flags & NRSE_LN_GELU) || p->beta, "nrse_layernorm_bwd: GELU needs beta");
+  NRSE_REQUIRE(!(p->flags & (NRSE_LN_GELU | NRSE_LN_RELU)) || p->beta, "nrse_layernorm_bwd: GELU/ReLU need beta");
   NRSE_REQUIRE((p->dgamma == nullptr) == (p->dbeta == nullptr), "nrse_layernorm_bwd: dgamma/dbeta together");
   if (p->dy_mode == NRSE_DY_COL2IM)
     NRSE_REQUIRE(p->col_k > 0 && p->col_s > 0 && p->col_tin > 0 && p->col_tout > 0 && p->rows % p->col_tin == 0,

@@ -25,8 +25,10 @@ EPI_ACCUM = 1 << 6
 EPI_ATOMIC = 1 << 7
 EPI_COLSUM = 1 << 8
 EPI_RELU = 1 << 9
+EPI_TANH = 1 << 10
 
 LN_GELU = 1
+LN_RELU = 2
 DY_DIRECT, DY_COL2IM, DY_BCAST = 0, 1, 2
 
 c_ll = ctypes.c_longlong
@@ -140,6 +142,10 @@ _SIGNATURES = {
     "nrse_adamw": ([_P(AdamWParams), c_vp], c_int),
     "nrse_ema": ([c_vp, c_vp, c_vp, c_int, c_ll, c_f, c_vp], c_int),
     "nrse_health": ([c_vp, c_int, c_ll, c_vp, c_vp], c_int),
+    "nrse_asp_fwd": ([c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp], c_int),
+    "nrse_asp_bwd": ([c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp,
+                      c_vp], c_int),
+    "nrse_ccc_loss": ([c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp], c_int),
     "nrse_snr_mix": ([c_vp, c_vp, c_vp, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp], c_int),
 }
 

@@ -188,8 +188,10 @@ class ByolEngine:
 
     # ------------------------------------------------------------------ encoder forward
     def encoder_forward(self, W: EncoderWeights, wav: torch.Tensor, *, train: bool, fseed: int = 0, skip=None,
-                        mask_np=None, need_grad: bool = False):
-        """WavLMModel.forward -> time-mean embedding [B, H] (f32) and the backward tape."""
+                        mask_np=None, need_grad: bool = False, hidden_dtype=None):
+        """WavLMModel.forward -> time-mean embedding [B, H] (f32) and the backward tape; with
+        hidden_dtype, the last_hidden_state [B, T, H] in that dtype instead of the embedding
+        (src/models/encoder.py:25-32, the emotion head's input; no tape)."""
         a = self.arch
         cdt = self.cdt
         dev = self.dev
@@ -309,6 +311,13 @@ class ByolEngine:
                 tape.layers.append(dict(li=li, h_in=hcur, x1=x1, m1=m1, r1=r1, qkv=qkv, gate=gate, ctx=ctx, lse=lse,
                                         hmid=hmid, x2=x2, m2=m2, r2=r2, f1pre=f1pre, g1=g1))
             hcur = hout
+        if hidden_dtype is not None:
+            # -------- final LN -> last_hidden_state ([TF]modeling_wavlm.py:513)
+            y = torch.empty(BT, H, device=dev, dtype=hidden_dtype)
+            mf = torch.empty(BT, device=dev, dtype=F32)
+            rf = torch.empty(BT, device=dev, dtype=F32)
+            K.ln_fwd(hcur, Pm["encoder.layer_norm.weight"], Pm["encoder.layer_norm.bias"], y, mf, rf, a.eps)
+            return y.view(B, T, H), None, executed
         # -------- final LN + time-mean shim
         emb = torch.zeros(B, H, device=dev, dtype=F32)
         mf = torch.empty(BT, device=dev, dtype=F32)

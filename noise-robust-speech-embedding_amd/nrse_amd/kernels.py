@@ -231,14 +231,14 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, *, splits:
 
 
 # ----------------------------------------------------------------------------- layernorm
-def ln_fwd(x, gamma, beta, y, mean, rstd, eps, gelu=False):
+def ln_fwd(x, gamma, beta, y, mean, rstd, eps, gelu=False, relu=False):
     rows, C = x.shape[0] if x.dim() == 2 else x.numel() // x.shape[-1], x.shape[-1]
     p = LnFwdParams(ptr(x), dtype_code(x), ptr(gamma), ptr(beta), ptr(y), dtype_code(y), ptr(mean), ptr(rstd),
-                    rows, C, eps, _lib.LN_GELU if gelu else 0)
+                    rows, C, eps, (_lib.LN_GELU if gelu else 0) | (_lib.LN_RELU if relu else 0))
     _call("nrse_layernorm_fwd", ctypes.byref(p), stream_ptr())
 
 
-def ln_bwd(dy, x, gamma, mean, rstd, dx, *, beta=None, gelu=False, resid=None, dgamma=None, dbeta=None,
+def ln_bwd(dy, x, gamma, mean, rstd, dx, *, beta=None, gelu=False, relu=False, resid=None, dgamma=None, dbeta=None,
            mode=_lib.DY_DIRECT, col=(0, 0, 0, 0), bcast_t=0, dy_scale=1.0, rows=None):
     C = x.shape[-1]
     rows = rows if rows is not None else x.numel() // C
@@ -251,7 +251,7 @@ def ln_bwd(dy, x, gamma, mean, rstd, dx, *, beta=None, gelu=False, resid=None, d
     p.dx, p.dx_dtype = ptr(dx), dtype_code(dx)
     p.resid = ptr(resid)
     p.dgamma, p.dbeta = ptr(dgamma), ptr(dbeta)
-    p.rows, p.C, p.flags = rows, C, (_lib.LN_GELU if gelu else 0)
+    p.rows, p.C, p.flags = rows, C, (_lib.LN_GELU if gelu else 0) | (_lib.LN_RELU if relu else 0)
     _call("nrse_layernorm_bwd", ctypes.byref(p), stream_ptr())
 
 
@@ -435,3 +435,26 @@ def snr_mix(clean, noise, noise_len, snr_db, clean_out, noisy_out, status, kscal
     assert noise.dim() == 2 and noise.shape[0] == B and clean.is_contiguous() and noise.stride(1) == 1
     _call("nrse_snr_mix", ptr(clean), ptr(noise), ptr(noise_len), noise.stride(0), ptr(snr_db), ptr(clean_out),
           ptr(noisy_out), ptr(status), ptr(kscale), None, B, L, int(mode), stream_ptr())
+
+
+# ----------------------------------------------------------------------------- emotion head
+def asp_fwd(x, h, att, lens, w_out, var_out, pooled):
+    """Attentive statistics pooling (src/models/pool.py:25-58); x [B, T, C], h f32 [B, T, C]."""
+    B, T, C = x.shape
+    assert h.dtype == torch.float32 and lens.dtype == torch.int32
+    _call("nrse_asp_fwd", ptr(x), dtype_code(x), ptr(h), ptr(att), ptr(lens), B, T, C, ptr(w_out), ptr(var_out),
+          ptr(pooled), stream_ptr())
+
+
+def asp_bwd(x, h, att, lens, w_in, var_in, pooled, dpooled, dpre, datt):
+    B, T, C = x.shape
+    _call("nrse_asp_bwd", ptr(x), dtype_code(x), ptr(h), ptr(att), ptr(lens), B, T, C, ptr(w_in), ptr(var_in),
+          ptr(pooled), ptr(dpooled), ptr(dpre), dtype_code(dpre), ptr(datt), stream_ptr())
+
+
+def ccc_loss(pred, target, loss, dpred=None):
+    """pred (and dpred) may be a column slice of a wider row-major buffer (row stride >= D)."""
+    rows, D = target.shape
+    assert pred.shape == (rows, D) and pred.stride(1) == 1 and (dpred is None or dpred.stride(0) == pred.stride(0))
+    _call("nrse_ccc_loss", ptr(pred), pred.stride(0), ptr(target), ptr(loss), ptr(dpred), rows, D, stream_ptr())
+

@@ -1,0 +1,138 @@
+"""Emotion head (BASELINE configs[3]) on the GPU: pooling / CCC kernels vs float64 torch, and the
+whole head (forward, CCC loss, backward) vs the reference's own EmotionClassifier outputs and
+gradients (tests/golden/emotion_head.npz, from tests/golden/make_golden_emotion.py)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def rel(a, b):
+    a = torch.as_tensor(a).detach().double().cpu(); b = torch.as_tensor(b).detach().double().cpu()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def _asp_ref(x, h, att, lens):
+    out, ws = [], []
+    for b, n in enumerate(lens):
+        xb, hb = x[b, :n], h[b, :n]
+        w = torch.softmax(hb @ att[:, 0], dim=0)
+        mu = (xb * w[:, None]).sum(0)
+        rh = torch.sqrt(((xb ** 2) * w[:, None]).sum(0).sub(mu ** 2).clamp(min=1e-5))
+        out.append(torch.cat([mu, rh]))
+    return torch.stack(out)
+
+
+@pytest.mark.parametrize("xdt", [torch.float32, torch.bfloat16])
+def test_asp_fwd_bwd(nrse_device, xdt):
+    from nrse_amd import kernels as K
+    dev = nrse_device
+    B, T, C = 3, 41, 512
+    x = (torch.randn(B, T, C, device=dev) * 0.5).to(xdt)
+    h = torch.tanh(torch.randn(B, T, C, device=dev))
+    att = torch.randn(C, 1, device=dev)
+    lens_l = [41, 17, 1]
+    lens = torch.tensor(lens_l, device=dev, dtype=torch.int32)
+    w = torch.empty(B, T, device=dev); var = torch.empty(B, C, device=dev); pooled = torch.empty(B, 2 * C, device=dev)
+    K.asp_fwd(x, h, att, lens, w, var, pooled)
+    xr = x.double(); hr = h.double().requires_grad_(True); ar = att.double().requires_grad_(True)
+    ref = _asp_ref(xr, hr, ar, lens_l)
+    assert rel(pooled, ref) < 1e-5
+    dp = torch.randn(B, 2 * C, device=dev)
+    dpre = torch.empty(B * T, C, device=dev)
+    datt = torch.zeros(C, 1, device=dev)
+    K.asp_bwd(x, h, att, lens, w, var, pooled, dp, dpre, datt)
+    ref.backward(dp.double())
+    dpre_ref = hr.grad * (1 - hr.detach() ** 2)            # through tanh
+    assert rel(dpre.view(B, T, C), dpre_ref) < 1e-4
+    assert rel(datt, ar.grad) < 1e-4
+
+
+def test_ccc_loss(nrse_device):
+    from nrse_amd import kernels as K
+    dev = nrse_device
+    p4 = torch.randn(9, 4, device=dev)
+    t = torch.rand(9, 3, device=dev) * 5
+    loss = torch.zeros(1, device=dev)
+    dp4 = torch.zeros(9, 4, device=dev)
+    K.ccc_loss(p4[:, :3], t, loss, dp4[:, :3])
+    pr = p4[:, :3].double().requires_grad_(True)
+    tr = t.double()
+    l = 0
+    for i in range(3):
+        a, b = pr[:, i], tr[:, i]
+        cov = ((a - a.mean()) * (b - b.mean())).mean()
+        l = l + 1 - 2 * cov / (a.var(unbiased=False) + b.var(unbiased=False) + (a.mean() - b.mean()) ** 2 + 1e-10)
+    l = l / 3
+    l.backward()
+    assert abs(float(loss) - float(l)) < 1e-5
+    assert rel(dp4[:, :3], pr.grad) < 1e-5 and float(dp4[:, 3].abs().sum()) == 0.0
+
+
+def _head_from_fixture(z, dtype):
+    from nrse_amd.emotion import EmotionHead
+    C = z["hidden"].shape[2]
+    hidden = z["param/shared_fc.0.weight"].shape[0]
+    head = EmotionHead(C, hidden, 8, dropout=0.0, device="cuda:0", compute_dtype=dtype)
+    flat = torch.zeros(head.numel)
+    for name, shp, _ in head.specs:
+        off, n = head.offsets[name]
+        flat[off:off + n] = torch.from_numpy(z["param/" + name]).reshape(-1)
+    return EmotionHead(C, hidden, 8, dropout=0.0, device="cuda:0", compute_dtype=dtype, init_flat=flat)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-4), (torch.bfloat16, 3e-2)])
+def test_head_matches_reference_fixture(nrse_device, dtype, tol):
+    from nrse_amd import kernels as K
+    z = np.load(os.path.join(GOLD, "emotion_head.npz"))
+    head = _head_from_fixture(z, dtype)
+    hid = torch.from_numpy(z["hidden"]).to(nrse_device, dtype).contiguous()
+    flens = torch.from_numpy(z["feat_lens"]).to(nrse_device)
+    _, dim, tape = head.forward(hid, flens, train=False)
+    assert rel(dim, z["dim"]) < tol
+    labels = torch.from_numpy(z["labels"]).to(nrse_device)
+    dout4 = torch.zeros(hid.shape[0], 4, device=nrse_device)
+    K.ccc_loss(dim, labels, head.loss_buf, dout4[:, :3])
+    assert abs(float(head.loss_buf) - float(z["loss"])) < 5 * tol
+    head.grad.zero_()
+    head.backward(dout4, tape, train=False)
+    for name, _, _ in head.specs:
+        key = "grad/" + name
+        if key in z.files:
+            g = head.view(head.grad, name)
+            assert rel(g, z[key]) < 20 * tol, (name, rel(g, z[key]))
+        else:
+            assert float(head.view(head.grad, name).abs().sum()) == 0.0, name
+
+
+def test_dim_trainer_step_tiny(nrse_device):
+    """Frozen tiny WavLM + head: one config-4 iteration runs, updates only the head's
+    pooling/shared/dimensional ranges, leaves the encoder untouched."""
+    from nrse_amd import arch as A
+    from nrse_amd.emotion import EmotionDimTrainer, EmotionHead
+    from nrse_amd.engine import ByolEngine
+    eng = ByolEngine(A.TINY, 256, 512, device="cuda:0", compute_dtype=torch.bfloat16)
+    enc0 = eng.online.clone()
+    head = EmotionHead(A.TINY.hidden, 256, 8, dropout=0.3, device="cuda:0", compute_dtype=torch.bfloat16)
+    p0 = head.params.clone()
+    tr = EmotionDimTrainer(eng, head, lr=1e-3, weight_decay=1e-4)
+    g = torch.Generator().manual_seed(0)
+    wav = torch.randn(6, 24000, generator=g).cuda()
+    labels = (torch.rand(6, 3, generator=g) * 6 + 1).cuda()
+    lengths = torch.tensor([24000, 20000, 16000, 24000, 9000, 12345])
+    loss = tr.train_step(wav, labels, lengths, step_seed=1)
+    torch.cuda.synchronize()
+    assert 0.0 <= float(loss) <= 4.0
+    assert torch.equal(eng.online, enc0)
+    d = (head.params - p0).abs()
+    for name, _, _ in head.specs:
+        moved = float(head.view(d, name).max())
+        if name.startswith("categorical"):
+            assert moved == 0.0, name
+        elif name.endswith(".1.bias") or name.endswith("bias") or "weight" in name or name == "pooling.attention":
+            assert moved > 0.0, name

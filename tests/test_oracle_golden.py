@@ -106,3 +106,24 @@ def test_oracle_train_step(tag):
     tidx = z["target_idx"]
     dt = (st.target - flat0[:layout.ema_numel])[tidx].numpy()
     assert np.max(np.abs(dt - z["target_delta_sample"])) < 0.05 * lr
+
+
+def test_emotion_head_oracle_matches_reference_fixture():
+    """oracle/emotion_head.py vs the reference EmotionClassifier (+ its pooling and ccc_loss) on
+    the same hidden states, ragged masks and parameters (tests/golden/make_golden_emotion.py)."""
+    from oracle import emotion_head as E
+    z = np.load(os.path.join(GOLD, "emotion_head.npz"))
+    P = {k[6:]: torch.from_numpy(z[k]).clone().requires_grad_(True) for k in z.files if k.startswith("param/")}
+    hidden = torch.from_numpy(z["hidden"])
+    lens = E.feat_lengths(torch.from_numpy(z["mask"]))
+    assert lens == z["feat_lens"].tolist()
+    out, _ = E.dimensional_forward(hidden, lens, P)
+    assert torch.allclose(out, torch.from_numpy(z["dim"]), rtol=1e-5, atol=1e-6)
+    loss = E.ccc_loss(out, torch.from_numpy(z["labels"]))
+    assert abs(float(loss) - float(z["loss"])) < 1e-6
+    loss.backward()
+    for k in z.files:
+        if k.startswith("grad/"):
+            g = P[k[5:]].grad
+            ref = torch.from_numpy(z[k])
+            assert torch.allclose(g, ref, rtol=1e-4, atol=1e-7), k
