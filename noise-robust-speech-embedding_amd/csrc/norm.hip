@@ -120,7 +120,9 @@ NRSE_DEV float load_dy(const nrse_ln_bwd_params& p, long long row, int c, float*
 
 template <int NK>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const nrse_ln_bwd_params p) {
-  __shared__ float red[2][4][NK * 64 * CH];
+  // one [4 waves][C] buffer, used for dgamma then dbeta: 16 KB at C = 1024, so a block fits on a
+  // CU beside two 128x128 GEMM workgroups of the concurrent weight-gradient stream
+  __shared__ float red[4][NK * 64 * CH];
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int C = p.C;
@@ -181,17 +183,16 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const nrse_ln_bwd_params p)
 #pragma unroll
   for (int k = 0; k < NK; ++k)
 #pragma unroll
-    for (int e = 0; e < CH; ++e) {
-      red[0][w][(k * 64 + lane) * CH + e] = dg[k][e];
-      red[1][w][(k * 64 + lane) * CH + e] = db[k][e];
-    }
+    for (int e = 0; e < CH; ++e) red[w][(k * 64 + lane) * CH + e] = dg[k][e];
   __syncthreads();
-  for (int c = threadIdx.x; c < C; c += 256) {
-    const float a = red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c];
-    const float b = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
-    atomicAdd(p.dgamma + c, a);
-    atomicAdd(p.dbeta + c, b);
-  }
+  for (int c = threadIdx.x; c < C; c += 256) atomicAdd(p.dgamma + c, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NK; ++k)
+#pragma unroll
+    for (int e = 0; e < CH; ++e) red[w][(k * 64 + lane) * CH + e] = db[k][e];
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) atomicAdd(p.dbeta + c, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
 }
 
 // Final LN + time-mean: grid (ceil(T / RPB), batch); 4 waves, each a row at a time.
