@@ -248,7 +248,18 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
     NRSE_MFMA(acc[(MH) * 4 + fi][(NH) * 2 + fj], fa[fi][s], FB[fj][s]);                  \
   __builtin_amdgcn_s_setprio(0);
 // the wait before each phase's first barrier retires every half-tile the NEXT phase reads
+#ifndef NRSE_G3_WAITMODE
+#define NRSE_G3_WAITMODE 0
+#endif
+#if NRSE_G3_WAITMODE == 1
+// one wait per K-tile (phase 3): retire K-tile t+1 (read in phases 0-2 of the next iteration),
+// leaving the 4 half-tiles of K-tile t+2 (8 DMAs) in flight
+#define NRSE_WAIT() ((void)0)
+#define NRSE_WAIT3() asm volatile("s_waitcnt vmcnt(8)" ::: "memory")
+#else
 #define NRSE_WAIT() asm volatile("s_waitcnt vmcnt(12)" ::: "memory")
+#define NRSE_WAIT3() NRSE_WAIT()
+#endif
 
   // ping-pong start: group 1 falls one barrier behind (schedule and hand-off rules: header)
   if (wm == 1) __builtin_amdgcn_s_barrier();
@@ -282,7 +293,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
     NRSE_BAR();
     // phase 3: (1, 0) from registers
     stage(3, q2, s1);    // (4t + 11) % 10
-    NRSE_WAIT();
+    NRSE_WAIT3();
     NRSE_BAR();
     NRSE_QUAD(1, 0, fbl)
     NRSE_BAR();
@@ -293,6 +304,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
 #undef NRSE_READ_B
 #undef NRSE_QUAD
 #undef NRSE_WAIT
+#undef NRSE_WAIT3
 #undef NRSE_FRAG
 #undef NRSE_MFMA
 
