@@ -292,6 +292,20 @@ int nrse_bn_fwd(const float* x, const float* w, const float* b, float* y, float*
                 void* stream);
 int nrse_bn_bwd(const float* dy, const float* x, const float* y, const float* w, const float* save_mean,
                 const float* save_invstd, float* dx, float* dw, float* db, int rows, int C, int relu, void* stream);
+/* SyncBatchNorm for data-parallel heads (torch.nn.SyncBatchNorm semantics over the reference's
+ * BatchNorm1d, src/models/multi_layer_heads.py:16-20, 39-45): phase 1 per-column local sums
+ * (f64 sum x, sum x^2 -> sums[2C]), the caller all-reduces them, phase 2 normalises with the global
+ * statistics over nglobal rows; backward: local (sum dy, sum dy*xhat) -> sums[2C], all-reduced by
+ * the caller into global_sums; dw/db accumulate the local share. */
+int nrse_bn_stats(const float* x, double* sums, int rows, int C, void* stream);
+int nrse_bn_fwd_global(const float* x, const float* w, const float* b, float* y, float* run_mean, float* run_var,
+                       float* save_mean, float* save_invstd, const double* global_sums, long long nglobal, int rows,
+                       int C, float momentum, float eps, int relu, void* stream);
+int nrse_bn_bwd_sums(const float* dy, const float* x, const float* y, const float* save_mean,
+                     const float* save_invstd, float* sums, int rows, int C, int relu, void* stream);
+int nrse_bn_bwd_global(const float* dy, const float* x, const float* y, const float* w, const float* save_mean,
+                       const float* save_invstd, const float* local_sums, const float* global_sums, long long nglobal,
+                       float* dx, float* dw, float* db, int rows, int C, int relu, void* stream);
 /* loss[0] = 2 - 2 mean_b clamp(<p_b/|p_b|, z_b/|z_b|>, -1, 1) (+1e-10 offsets, eps 1e-10);
  * dp = dloss/dp (scaled by grad_scale); stats[0..1] = NaN flags before/after normalisation. */
 int nrse_byol_loss(const float* p, const float* z, float* loss, float* dp, float* stats, int rows, int D,
@@ -332,8 +346,9 @@ typedef struct {
 int nrse_adamw(const nrse_adamw_params* p, void* stream);
 int nrse_ema(float* target, const float* online, void* t_shadow, int shadow_dtype, long long n, float decay,
              void* stream);
-/* health check (train_byol.py:52-59 / debugging_utils.py:4-30): flags[0..3] |= nan, inf,
- * sum|x| (f32 accumulated into stats[0]), max|x| (stats[1]) */
+/* health check (train_byol.py:52-59 / debugging_utils.py:4-30): accumulates into the caller-zeroed
+ * stats[0..3] = NaN count, Inf count, sum|x| over finite x, max|x| over finite x (decisions on the
+ * host, nrse_amd/health.py, in check_audio_tensor's order) */
 int nrse_health(const void* x, int dtype, long long n, float* stats, void* stream);
 
 /* ------------------------------------------------------------------------------------------

@@ -1,2 +1,2 @@
-"""Import-path mirror of the reference package layout (src.models / src.data / src.utils) over
-nrse_amd: `from src.models.byol import BYOLSpeechModel, byol_loss` works unchanged."""
+"""Import-path mirror of the reference `config` package: `from config.config_utils import
+get_config` works unchanged (reference config/config_utils.py:21-65)."""

@@ -137,6 +137,12 @@ _SIGNATURES = {
     "nrse_gelu_bwd_pad": ([c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
     "nrse_bn_fwd": ([c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_f, c_f, c_int, c_int, c_vp], c_int),
     "nrse_bn_bwd": ([c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp], c_int),
+    "nrse_bn_stats": ([c_vp, c_vp, c_int, c_int, c_vp], c_int),
+    "nrse_bn_fwd_global": ([c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_int, c_int, c_f, c_f, c_int,
+                            c_vp], c_int),
+    "nrse_bn_bwd_sums": ([c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp], c_int),
+    "nrse_bn_bwd_global": ([c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_vp, c_vp, c_vp, c_int, c_int,
+                            c_int, c_vp], c_int),
     "nrse_byol_loss": ([c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_f, c_vp], c_int),
     "nrse_sumsq": ([c_vp, c_ll, c_vp, c_vp], c_int),
     "nrse_adamw": ([_P(AdamWParams), c_vp], c_int),

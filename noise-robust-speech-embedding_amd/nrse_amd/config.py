@@ -26,6 +26,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--dtype", type=str, default="bf16", choices=["bf16", "f32"],
                    help="compute dtype of GEMM/attention operands (f32 = exact parity mode)")
     p.add_argument("--max_steps", type=int, default=None, help="stop after this many optimizer steps")
+    p.add_argument("--mock_items", type=int, default=None,
+                   help="train on test/create_mock_dataset.py-style mock pairs (configs[0] plumbing)")
+    p.add_argument("--sync_bn", action="store_true", help="DDP: SyncBatchNorm in the heads")
+    p.add_argument("--bf16_allreduce", action="store_true", help="DDP: gradient all-reduce in bf16 on the wire")
     return p
 
 
@@ -45,6 +49,10 @@ def apply_overrides(config: Dict[str, Any], args) -> Dict[str, Any]:
     config.setdefault("runtime", {})
     config["runtime"]["dtype"] = getattr(args, "dtype", "bf16")
     config["runtime"]["max_steps"] = getattr(args, "max_steps", None)
+    config["runtime"]["sync_bn"] = bool(getattr(args, "sync_bn", False))
+    config["runtime"]["bf16_allreduce"] = bool(getattr(args, "bf16_allreduce", False))
+    if getattr(args, "mock_items", None):
+        config["data"]["mock_items"] = args.mock_items
     return config
 
 

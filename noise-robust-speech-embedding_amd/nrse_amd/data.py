@@ -17,11 +17,14 @@ import os
 import random
 import wave
 
+import logging
+
 import numpy as np
 import torch
 
 from . import kernels as K
 
+logger = logging.getLogger("nrse")
 STATUS_OK = 0
 
 
@@ -90,8 +93,10 @@ def read_wav(path: str) -> tuple:
     return x, sr
 
 
-def crop_or_pad(x: np.ndarray, n: int, rng: random.Random, random_crop: bool = True) -> np.ndarray:
-    """Random crop if longer, zero-pad at the end if shorter (audio_utils.py:38-49)."""
+def crop_or_pad(x: np.ndarray, n: int, rng=random, random_crop: bool = True) -> np.ndarray:
+    """Random crop if longer, zero-pad at the end if shorter (audio_utils.py:38-49). `rng` is the
+    global `random` module by default, as in the reference (torch's DataLoader reseeds it per
+    worker and per epoch)."""
     if x.shape[0] > n:
         start = rng.randint(0, x.shape[0] - n) if random_crop else 0
         return x[start:start + n]
@@ -100,36 +105,80 @@ def crop_or_pad(x: np.ndarray, n: int, rng: random.Random, random_crop: bool = T
     return x
 
 
-class WavPairs(torch.utils.data.Dataset):
-    """Raw (clean, noise, snr) items from directories of PCM WAV files."""
+def audio_valid(x) -> bool:
+    """load_and_process_audio's output checks (audio_utils.py:51-58): no NaN, max|x| >= 1e-8."""
+    return x is not None and not bool(np.isnan(x).any()) and float(np.max(np.abs(x))) >= 1e-8
 
-    def __init__(self, clean_files, noise_files, sample_rate, max_audio_length, snr_range, seed=42):
+
+MAX_ATTEMPTS = 5   # noisy_speech_dataset.py:56
+
+
+class WavPairs(torch.utils.data.Dataset):
+    """Raw (clean, noise, snr) items from directories of PCM WAV files, with the reference's
+    retry rules for invalid audio (noisy_speech_dataset.py:56-76): an invalid clean file moves on
+    to the next file, an invalid noise file draws another. Mix failures are detected on the GPU
+    (nrse_snr_mix status) and re-drawn by MixedLoader through `redraw` (:80-86, 94-100)."""
+
+    def __init__(self, clean_files, noise_files, sample_rate, max_audio_length, snr_range):
         self.clean_files = clean_files
         self.noise_files = noise_files
         self.sr = sample_rate
         self.n = int(max_audio_length * sample_rate)
         self.snr_range = list(snr_range)
-        self.rng = random.Random(seed)
 
     def __len__(self):
         return len(self.clean_files)
 
     def _load(self, path):
-        x, sr = read_wav(path)
+        try:
+            x, sr = read_wav(path)
+        except Exception as e:   # audio_utils.py:62-64: load errors -> None
+            logger.error(f"Error loading audio file {path}: {e}")
+            return None
         if sr != self.sr:
             raise ValueError(f"{path}: sample rate {sr} != {self.sr} (no resampler in this build)")
-        return crop_or_pad(x, self.n, self.rng)
+        x = crop_or_pad(x, self.n)
+        return x if audio_valid(x) else None
+
+    def _noise(self):
+        return self._load(self.noise_files[random.randint(0, len(self.noise_files) - 1)])
 
     def __getitem__(self, idx):
+        for attempt in range(MAX_ATTEMPTS):
+            clean = self._load(self.clean_files[idx])
+            if clean is None:
+                logger.warning(f"Invalid clean speech file, trying next (attempt {attempt + 1})")
+                idx = (idx + 1) % len(self.clean_files)
+                continue
+            noise = self._noise()
+            if noise is None:
+                logger.warning(f"Invalid noise file, trying another (attempt {attempt + 1})")
+                continue
+            return _raw_item(clean, noise, random.choice(self.snr_range), idx, attempt + 1)
+        raise RuntimeError(f"no valid pair for item {idx} after {MAX_ATTEMPTS} attempts")
+
+    def redraw(self, idx: int):
+        """A fresh noise file and SNR for clean item idx (the reference's `continue` after a
+        failed mix keeps idx), or None if the noise file is invalid."""
         clean = self._load(self.clean_files[idx])
-        noise = self._load(self.noise_files[self.rng.randint(0, len(self.noise_files) - 1)])
-        return {"clean": torch.from_numpy(clean), "noise": torch.from_numpy(noise),
-                "noise_len": torch.tensor(noise.shape[0], dtype=torch.int32),
-                "snr": torch.tensor(self.rng.choice(self.snr_range), dtype=torch.int64)}
+        noise = self._noise()
+        if clean is None or noise is None:
+            return None
+        return _raw_item(clean, noise, random.choice(self.snr_range), idx, 0)
+
+
+def _raw_item(clean, noise, snr, idx, attempts):
+    clean = torch.as_tensor(np.ascontiguousarray(clean), dtype=torch.float32)
+    noise = torch.as_tensor(np.ascontiguousarray(noise), dtype=torch.float32)
+    return {"clean": clean, "noise": noise, "noise_len": torch.tensor(noise.shape[0], dtype=torch.int32),
+            "snr": torch.tensor(int(snr), dtype=torch.int64), "index": torch.tensor(idx, dtype=torch.int64),
+            "attempts": torch.tensor(attempts, dtype=torch.int32)}
 
 
 class SyntheticPairs(torch.utils.data.Dataset):
-    """Synthetic raw pairs (speech ~ N(0, 0.1^2), noise ~ N(0, 1)), used offline and by bench."""
+    """Synthetic raw pairs (speech ~ N(0, 0.1^2), noise ~ N(0, 1)), used offline and by bench;
+    item idx is a pure function of (seed, idx). `redraw` draws a fresh noise and SNR from the
+    global `random` stream."""
 
     def __init__(self, n_items, samples, snr_range, seed=1234):
         self.n_items, self.samples, self.snr_range, self.seed = n_items, samples, list(snr_range), seed
@@ -137,36 +186,181 @@ class SyntheticPairs(torch.utils.data.Dataset):
     def __len__(self):
         return self.n_items
 
-    def __getitem__(self, idx):
+    def _clean(self, idx):
         g = torch.Generator().manual_seed(self.seed * 1000003 + idx)
-        return {"clean": torch.randn(self.samples, generator=g) * 0.1, "noise": torch.randn(self.samples, generator=g),
-                "noise_len": torch.tensor(self.samples, dtype=torch.int32),
-                "snr": torch.tensor(self.snr_range[idx % len(self.snr_range)], dtype=torch.int64)}
+        return torch.randn(self.samples, generator=g) * 0.1, g
+
+    def __getitem__(self, idx):
+        clean, g = self._clean(idx)
+        return _raw_item(clean, torch.randn(self.samples, generator=g), self.snr_range[idx % len(self.snr_range)],
+                         idx, 1)
+
+    def redraw(self, idx: int):
+        clean, _ = self._clean(idx)
+        g = torch.Generator().manual_seed(random.getrandbits(62))
+        return _raw_item(clean, torch.randn(self.samples, generator=g), random.choice(self.snr_range), idx, 0)
 
 
-def create_dataloaders(config: dict, feature_extractor=None, *, synthetic_items: int | None = None,
-                       rank: int = 0, world: int = 1):
-    """(train_loader, val_loader) of RAW batches, split 85/15 with the seeded generator like
-    create_dataloaders (noisy_speech_dataset.py:163-175); feed them through GpuMixer."""
+class MockPairs(torch.utils.data.Dataset):
+    """configs[0]'s mock data (test/create_mock_dataset.py:4-25) at waveform length: clean ~ N(0, 1),
+    SNR cycling through snr_range by index, noisy = clean + N(0, 1) / (snr + 1). Items are already
+    the reference's dict batch entries (no mix), as the mock dataset's pairs are."""
+
+    def __init__(self, n_items, samples, snr_range, seed=42):
+        g = torch.Generator().manual_seed(seed)
+        self.clean = torch.randn(n_items, samples, generator=g)
+        self.snrs = torch.tensor([snr_range[i % len(snr_range)] for i in range(n_items)])
+        self.noisy = self.clean + torch.randn(n_items, samples, generator=g) / (self.snrs[:, None].float() + 1.0)
+
+    def __len__(self):
+        return self.clean.shape[0]
+
+    def __getitem__(self, idx):
+        return {"clean_input_values": self.clean[idx][None], "noisy_input_values": self.noisy[idx][None],
+                "snr": self.snrs[idx]}
+
+
+class MixedLoader:
+    """Iterable over a DataLoader of raw batches that yields the reference's dict batches
+    {clean_input_values [B, 1, L], noisy_input_values [B, 1, L], snr [B]} (noisy_speech_dataset.py:
+    140-144, collated), the mix done on the GPU for the whole batch (nrse_snr_mix).
+
+    Failed mixes (the reference's None / `continue` cases, status != 0) are re-drawn with a fresh
+    noise and SNR for the same clean item, up to MAX_ATTEMPTS attempts in total per item as in
+    the reference, and the batch rows replaced. The status check needs the status on the host:
+    batch i+1's mix is enqueued before batch i is handed out, and batch i's status read then, so
+    the host waits only for batch i's mix kernel, never for the training step in flight."""
+
+    def __init__(self, raw_loader, dataset, device, do_normalize: bool = True):
+        self.raw = raw_loader
+        self.dataset = dataset
+        self.mixer = GpuMixer(device, do_normalize)
+        self.redraws = 0
+
+    def __len__(self):
+        return len(self.raw)
+
+    @property
+    def sampler(self):
+        return self.raw.sampler
+
+    def _enqueue(self, raw):
+        batch = self.mixer(raw)
+        host = torch.empty(batch["status"].shape, dtype=torch.int32, pin_memory=True)
+        host.copy_(batch["status"], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return raw, batch, host, ev
+
+    def _finalize(self, pending):
+        raw, batch, host, ev = pending
+        ev.synchronize()
+        bad = [i for i, st in enumerate(host.tolist()) if st != STATUS_OK]
+        attempts = raw.get("attempts", torch.ones(len(host), dtype=torch.int32)).tolist()
+        snr = batch["snr"].clone()
+        while bad:
+            items, rows = [], []
+            for i in bad:
+                if attempts[i] >= MAX_ATTEMPTS:
+                    raise RuntimeError(f"noise mix failed {MAX_ATTEMPTS} times for item "
+                                       f"{int(raw['index'][i]) if 'index' in raw else i} (status {int(host[i])})")
+                logger.warning(f"Noise addition failed (status {int(host[i])}), trying again "
+                               f"(attempt {attempts[i] + 1})")
+                it = self.dataset.redraw(int(raw["index"][i]))
+                attempts[i] += 1
+                if it is None:
+                    continue
+                items.append(it)
+                rows.append(i)
+            if not items:
+                continue
+            L = batch["clean_input_values"].shape[-1]
+            Ln = max(int(it["noise"].shape[0]) for it in items)
+            sub = {"clean": torch.stack([torch.nn.functional.pad(it["clean"][:L], (0, L - min(L, it["clean"].shape[0])))
+                                         for it in items]),
+                   "noise": torch.stack([torch.nn.functional.pad(it["noise"], (0, Ln - it["noise"].shape[0]))
+                                         for it in items]),
+                   "noise_len": torch.stack([it["noise_len"] for it in items]),
+                   "snr": torch.stack([it["snr"] for it in items])}
+            mixed = self.mixer(sub)
+            st = mixed["status"].tolist()
+            self.redraws += len(items)
+            idx = torch.tensor(rows, device=batch["clean_input_values"].device)
+            batch["clean_input_values"].index_copy_(0, idx, mixed["clean_input_values"])
+            batch["noisy_input_values"].index_copy_(0, idx, mixed["noisy_input_values"])
+            for r, s_, it in zip(rows, st, items):
+                snr[r] = it["snr"]
+            bad = [r for r, s_ in zip(rows, st) if s_ != STATUS_OK] + [i for i in bad if i not in rows]
+        return {"clean_input_values": batch["clean_input_values"], "noisy_input_values": batch["noisy_input_values"],
+                "snr": snr}
+
+    def __iter__(self):
+        pending = None
+        for raw in self.raw:
+            cur = self._enqueue(raw)
+            if pending is not None:
+                yield self._finalize(pending)
+            pending = cur
+        if pending is not None:
+            yield self._finalize(pending)
+
+
+def _rank_share(ds, rank: int, world: int):
+    """Equal, disjoint per-rank shares: truncate to world * floor(N / world), then stride, so
+    every rank sees the same number of batches (no rank blocks in an all-reduce another rank
+    never issues) and the same LR schedule length."""
+    if world <= 1:
+        return ds
+    n = (len(ds) // world) * world
+    return torch.utils.data.Subset(ds, list(range(rank, n, world)))
+
+
+def create_raw_dataloaders(config: dict, *, synthetic_items: int | None = None, rank: int = 0, world: int = 1):
+    """(train_loader, val_loader, base dataset) of RAW batches, split 85/15 with the seeded
+    generator as in create_dataloaders (noisy_speech_dataset.py:163-175)."""
     d, t = config["data"], config["training"]
     sr, secs = int(d["sample_rate"]), float(d["max_audio_length"])
     clean_dir, noise_dir = d.get("clean_data_path", ""), d.get("noise_data_path", "")
     if os.path.isdir(clean_dir) and os.path.isdir(noise_dir):
-        ds = WavPairs(get_audio_files(clean_dir), get_audio_files(noise_dir), sr, secs, d["snr_range"],
-                      seed=t.get("seed", 42) + rank)
+        ds = WavPairs(get_audio_files(clean_dir), get_audio_files(noise_dir), sr, secs, d["snr_range"])
     else:
         n = synthetic_items or 64 * int(t["batch_size"])
         ds = SyntheticPairs(n, int(sr * secs), d["snr_range"], seed=t.get("seed", 42))
     val_size = int(len(ds) * d.get("validation_ratio", 0.1))
     train_ds, val_ds = torch.utils.data.random_split(
         ds, [len(ds) - val_size, val_size], generator=torch.Generator().manual_seed(t.get("seed", 42)))
-    if world > 1:
-        train_ds = torch.utils.data.Subset(train_ds, list(range(rank, len(train_ds), world)))
+    train_ds, val_ds = _rank_share(train_ds, rank, world), _rank_share(val_ds, rank, world)
     kw = dict(batch_size=int(t["batch_size"]), num_workers=min(int(t.get("num_workers", 4)), 8), pin_memory=True,
               drop_last=True)
     train = torch.utils.data.DataLoader(train_ds, shuffle=True, **kw)
-    val = torch.utils.data.DataLoader(val_ds, shuffle=False, **kw) if val_size >= int(t["batch_size"]) else None
-    return train, val
+    val = torch.utils.data.DataLoader(val_ds, shuffle=False, **kw) if len(val_ds) >= int(t["batch_size"]) else None
+    return train, val, ds
+
+
+def create_dataloaders(config: dict, feature_extractor=None, *, device=None, synthetic_items: int | None = None,
+                       rank: int = 0, world: int = 1):
+    """Drop-in for create_dataloaders (noisy_speech_dataset.py:151-194): (train_loader,
+    val_loader) yielding the reference's dict batches, mixed and normalised on the GPU.
+    `feature_extractor` is accepted for signature compatibility; its normalisation is
+    `config['data']['do_normalize']` (default True, Wav2Vec2FeatureExtractor's). The optional
+    `config['data']['mock_items']` selects configs[0]'s mock dataset (MockPairs)."""
+    d, t = config["data"], config["training"]
+    if d.get("mock_items"):
+        ds = MockPairs(int(d["mock_items"]), int(int(d["sample_rate"]) * float(d["max_audio_length"])),
+                       d["snr_range"], seed=t.get("seed", 42))
+        val_size = int(len(ds) * d.get("validation_ratio", 0.1))
+        tr, va = torch.utils.data.random_split(ds, [len(ds) - val_size, val_size],
+                                               generator=torch.Generator().manual_seed(t.get("seed", 42)))
+        tr, va = _rank_share(tr, rank, world), _rank_share(va, rank, world)
+        kw = dict(batch_size=int(t["batch_size"]), num_workers=0, drop_last=True)
+        return (torch.utils.data.DataLoader(tr, shuffle=True, **kw),
+                torch.utils.data.DataLoader(va, shuffle=False, **kw) if len(va) >= int(t["batch_size"]) else None)
+    if feature_extractor is not None and hasattr(feature_extractor, "do_normalize"):
+        d = {**d, "do_normalize": bool(feature_extractor.do_normalize)}
+    device = device or torch.device("cuda", torch.cuda.current_device())
+    train, val, base = create_raw_dataloaders(config, synthetic_items=synthetic_items, rank=rank, world=world)
+    norm = d.get("do_normalize", True)
+    return MixedLoader(train, base, device, norm), (MixedLoader(val, base, device, norm) if val is not None else None)
 
 
 # ----------------------------------------------------------------------------- variable length
@@ -241,7 +435,9 @@ def collate_varlen(items: list, pad_multiple: int = 8000) -> dict:
         noise[i, :it["noise"].shape[0]] = it["noise"]
     return {"clean": clean, "noise": noise,
             "noise_len": torch.tensor([int(it["noise"].shape[0]) for it in items], dtype=torch.int32),
-            "snr": torch.stack([it["snr"] for it in items]), "lengths": torch.tensor(lens, dtype=torch.int64)}
+            "snr": torch.stack([it["snr"] for it in items]), "lengths": torch.tensor(lens, dtype=torch.int64),
+            **({"index": torch.stack([it["index"] for it in items]),
+                "attempts": torch.stack([it["attempts"] for it in items])} if "index" in items[0] else {})}
 
 
 class SyntheticVarLenPairs(torch.utils.data.Dataset):
@@ -259,10 +455,16 @@ class SyntheticVarLenPairs(torch.utils.data.Dataset):
 
     def __getitem__(self, idx):
         g = torch.Generator().manual_seed(self.seed * 1000003 + idx)
-        return {"clean": torch.randn(int(self.lengths[idx]), generator=g) * 0.1,
-                "noise": torch.randn(int(self.noise_lengths[idx]), generator=g),
-                "noise_len": torch.tensor(int(self.noise_lengths[idx]), dtype=torch.int32),
-                "snr": torch.tensor(self.snr_range[idx % len(self.snr_range)], dtype=torch.int64)}
+        clean = torch.randn(int(self.lengths[idx]), generator=g) * 0.1
+        return _raw_item(clean, torch.randn(int(self.noise_lengths[idx]), generator=g),
+                         self.snr_range[idx % len(self.snr_range)], idx, 1)
+
+    def redraw(self, idx: int):
+        g = torch.Generator().manual_seed(self.seed * 1000003 + idx)
+        clean = torch.randn(int(self.lengths[idx]), generator=g) * 0.1
+        g2 = torch.Generator().manual_seed(random.getrandbits(62))
+        return _raw_item(clean, torch.randn(int(self.noise_lengths[idx]), generator=g2), random.choice(self.snr_range),
+                         idx, 0)
 
 
 def wav_num_samples(path: str) -> int:
@@ -273,11 +475,10 @@ def wav_num_samples(path: str) -> int:
 class WavVarLenPairs(torch.utils.data.Dataset):
     """PCM WAV clean files at their own length (cropped to max_s), noise from a pool (MUSAN)."""
 
-    def __init__(self, clean_files, noise_files, sample_rate, max_s, snr_range, seed=42):
+    def __init__(self, clean_files, noise_files, sample_rate, max_s, snr_range):
         self.clean_files, self.noise_files = clean_files, noise_files
         self.sr, self.nmax = sample_rate, int(max_s * sample_rate)
         self.snr_range = list(snr_range)
-        self.rng = random.Random(seed)
         self.lengths = [min(wav_num_samples(f), self.nmax) for f in clean_files]
 
     def __len__(self):
@@ -287,14 +488,13 @@ class WavVarLenPairs(torch.utils.data.Dataset):
         x, sr = read_wav(path)
         if sr != self.sr:
             raise ValueError(f"{path}: sample rate {sr} != {self.sr} (no resampler in this build)")
-        return crop_or_pad(x, self.nmax, self.rng) if (crop and x.shape[0] > self.nmax) else x
+        return crop_or_pad(x, self.nmax) if (crop and x.shape[0] > self.nmax) else x
 
     def __getitem__(self, idx):
+        # global `random`, as the reference: reseeded by torch per worker and per epoch
         clean = self._load(self.clean_files[idx], True)
-        noise = self._load(self.noise_files[self.rng.randint(0, len(self.noise_files) - 1)], True)
-        return {"clean": torch.from_numpy(np.ascontiguousarray(clean)), "noise": torch.from_numpy(np.ascontiguousarray(noise)),
-                "noise_len": torch.tensor(noise.shape[0], dtype=torch.int32),
-                "snr": torch.tensor(self.rng.choice(self.snr_range), dtype=torch.int64)}
+        noise = self._load(self.noise_files[random.randint(0, len(self.noise_files) - 1)], True)
+        return _raw_item(clean, noise, random.choice(self.snr_range), idx, 1)
 
 
 def create_varlen_loader(dataset, batch_size: int, *, sample_rate: int = 16000, min_s: float = 3.0,

@@ -153,6 +153,8 @@ class ByolEngine:
         self.health_buf = torch.zeros(4, 4, device=self.dev, dtype=F32)
         self.loss_stats = torch.zeros(2, device=self.dev, dtype=F32)
         self.executed_layers = [0, 0]
+        # DDP option (nrse_amd/ddp.SyncBN): head BatchNorm statistics over all ranks' rows
+        self.sync_bn = None
 
     # ------------------------------------------------------------------ views
     def group_views(self, flat: torch.Tensor, group: str) -> dict:
@@ -508,7 +510,15 @@ class ByolEngine:
         sm = torch.empty(C, device=self.dev, dtype=F32)
         si = torch.empty(C, device=self.dev, dtype=F32)
         rm, rv, nbt = self.bn[bn_key]
-        K.bn_fwd(x, P[name + ".weight"], P[name + ".bias"], y, rm, rv, sm, si, train, relu)
+        if train and self.sync_bn is not None:
+            # SyncBatchNorm: batch statistics over every rank's rows (one small all-reduce)
+            sums = torch.empty(2 * C, device=self.dev, dtype=torch.float64)
+            K.bn_stats(x, sums)
+            self.sync_bn.all_reduce(sums)
+            n = x.shape[0] * self.sync_bn.world()
+            K.bn_fwd_global(x, P[name + ".weight"], P[name + ".bias"], y, rm, rv, sm, si, sums, n, relu)
+        else:
+            K.bn_fwd(x, P[name + ".weight"], P[name + ".bias"], y, rm, rv, sm, si, train, relu)
         if train:
             nbt.add_(1)
         return y, (x, y, sm, si)
@@ -539,7 +549,16 @@ class ByolEngine:
     def _bn_bwd(self, dy, cache, P, G, name, relu):
         x, y, sm, si = cache
         dx = torch.empty_like(x)
-        K.bn_bwd(dy, x, y, P[name + ".weight"], sm, si, dx, G[name + ".weight"], G[name + ".bias"], relu)
+        if self.sync_bn is not None:
+            C = x.shape[1]
+            loc = torch.empty(2 * C, device=self.dev, dtype=F32)
+            K.bn_bwd_sums(dy, x, y, sm, si, loc, relu)
+            glob = loc.clone()
+            self.sync_bn.all_reduce(glob)
+            K.bn_bwd_global(dy, x, y, P[name + ".weight"], sm, si, loc, glob, x.shape[0] * self.sync_bn.world(), dx,
+                            G[name + ".weight"], G[name + ".bias"], relu)
+        else:
+            K.bn_bwd(dy, x, y, P[name + ".weight"], sm, si, dx, G[name + ".weight"], G[name + ".bias"], relu)
         return dx
 
     def predictor_backward(self, dpred, cache, P, G):
@@ -590,15 +609,19 @@ class ByolEngine:
             self._side = torch.cuda.Stream(self.dev)
         return self._side
 
-    def stochastic_inputs(self, step_seed: int, B: int, T: int, train: bool):
-        """LayerDrop decisions (rank-shared) and SpecAugment masks for both branches."""
+    def stochastic_inputs(self, step_seed: int, B: int, T: int, train: bool, rank: int = 0):
+        """LayerDrop decisions for both branches from a rank-SHARED stream (every replica skips
+        the same layers, so skipped layers carry zero gradient everywhere and are not sent), and
+        SpecAugment masks from a rank-DISTINCT stream (each rank masks its own utterances, as
+        dropout does through the rank in forward_seed)."""
         a = self.arch
         if not train:
             return (None, None), (None, None)
         g = np.random.default_rng([step_seed, 7])
         skips = (layerdrop_decisions(g, a.layers, a.layerdrop), layerdrop_decisions(g, a.layers, a.layerdrop))
-        masks = (compute_mask_indices(g, B, T, a.mask_time_prob, a.mask_time_length, a.mask_time_min_masks),
-                 compute_mask_indices(g, B, T, a.mask_time_prob, a.mask_time_length, a.mask_time_min_masks))
+        gm = np.random.default_rng([step_seed, 11, rank])
+        masks = (compute_mask_indices(gm, B, T, a.mask_time_prob, a.mask_time_length, a.mask_time_min_masks),
+                 compute_mask_indices(gm, B, T, a.mask_time_prob, a.mask_time_length, a.mask_time_min_masks))
         return skips, masks
 
     def forward(self, clean: torch.Tensor, noisy: torch.Tensor, *, train: bool, step_seed: int = 0, rank: int = 0,
@@ -607,7 +630,7 @@ class ByolEngine:
         B, L = clean.shape
         T = self.arch.frames(L)
         if skips is None or masks is None:
-            s2, m2 = self.stochastic_inputs(step_seed, B, T, train)
+            s2, m2 = self.stochastic_inputs(step_seed, B, T, train, rank)
             skips = skips if skips is not None else s2
             masks = masks if masks is not None else m2
         # The target view (no tape, no grad) runs on a side stream concurrently with the online
@@ -693,6 +716,7 @@ class ByolEngine:
         """One iteration of train_one_epoch (train_byol.py:47-77): forward, loss, backward,
         clip, AdamW, EMA. Returns the device-resident loss (no sync)."""
         B = clean.shape[0]
+        self.health_buf.zero_()   # rows: clean, noisy, online_pred, target_proj (nrse_amd/health.py)
         K.health(clean, self.health_buf[0])
         K.health(noisy, self.health_buf[1])
         pred, tproj, ctx = self.forward(clean, noisy, train=True, step_seed=step_seed, rank=rank, need_grad=True)

@@ -401,6 +401,28 @@ def bn_bwd(dy, x, y, w, sm, si, dx, dw, db, relu):
           int(relu), stream_ptr())
 
 
+def bn_stats(x, sums):
+    rows, C = x.shape
+    _call("nrse_bn_stats", ptr(x), ptr(sums), rows, C, stream_ptr())
+
+
+def bn_fwd_global(x, w, b, y, rm, rv, sm, si, gsums, nglobal, relu, momentum=0.1, eps=1e-5):
+    rows, C = x.shape
+    _call("nrse_bn_fwd_global", ptr(x), ptr(w), ptr(b), ptr(y), ptr(rm), ptr(rv), ptr(sm), ptr(si), ptr(gsums),
+          int(nglobal), rows, C, momentum, eps, int(relu), stream_ptr())
+
+
+def bn_bwd_sums(dy, x, y, sm, si, sums, relu):
+    rows, C = x.shape
+    _call("nrse_bn_bwd_sums", ptr(dy), ptr(x), ptr(y), ptr(sm), ptr(si), ptr(sums), rows, C, int(relu), stream_ptr())
+
+
+def bn_bwd_global(dy, x, y, w, sm, si, lsums, gsums, nglobal, dx, dw, db, relu):
+    rows, C = x.shape
+    _call("nrse_bn_bwd_global", ptr(dy), ptr(x), ptr(y), ptr(w), ptr(sm), ptr(si), ptr(lsums), ptr(gsums),
+          int(nglobal), ptr(dx), ptr(dw), ptr(db), rows, C, int(relu), stream_ptr())
+
+
 def byol_loss(p, z, loss, dp=None, stats=None, grad_scale=1.0):
     rows, D = p.shape
     _call("nrse_byol_loss", ptr(p), ptr(z), ptr(loss), ptr(dp), ptr(stats), rows, D, grad_scale, stream_ptr())

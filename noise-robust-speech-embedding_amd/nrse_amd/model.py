@@ -47,10 +47,17 @@ class _OnlineBranch(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dpred, dtproj):
         eng = ctx.model.engine
-        eng.grad.zero_()
-        eng.backward(dpred.contiguous().float(), ctx.c)
+        # the engine writes this backward's gradient into a fresh buffer that it then lets go of,
+        # so autograd adopts it as (or adds it into) online_flat.grad without a 1.3 GB copy
+        g = torch.zeros_like(eng.online)
+        home = eng.grad
+        eng.grad = g
+        try:
+            eng.backward(dpred.contiguous().float(), ctx.c)
+        finally:
+            eng.grad = home
         ctx.c = None
-        return None, None, eng.grad.clone(), None, None
+        return None, None, g, None, None
 
 
 class _Loss(torch.autograd.Function):
@@ -136,6 +143,7 @@ class BYOLSpeechModel(nn.Module):
         # the single trainable parameter: the flat online buffer (views carry the reference names)
         self.online_flat = nn.Parameter(self.engine.online, requires_grad=True)
         self._seed_counter = seed * 1000003
+        self._shadow_version = self.online_flat._version
 
     def _next_seed(self) -> int:
         self._seed_counter += 1
@@ -146,12 +154,25 @@ class BYOLSpeechModel(nn.Module):
             if x.dim() == 3:
                 x = x.squeeze(1)
             return x.to(self.engine.dev, torch.float32).contiguous()
+        self._sync_shadows()
         # grad mode is off inside Function.forward, so decide here whether to keep the tape
         need = torch.is_grad_enabled() and self.online_flat.requires_grad and self.training
         return _OnlineBranch.apply(prep(clean_input_values), prep(noisy_input_values), self.online_flat, self, need)
 
+    def _sync_shadows(self) -> None:
+        """Re-cast the bf16 GEMM-operand copy of the online weights if online_flat was modified
+        in place since the last cast (a torch optimizer's step(), a user's in-place edit). The
+        fused engine path (FusedAdamW / engine.train_step) writes the shadow itself."""
+        e = self.engine
+        v = self.online_flat._version
+        if v != self._shadow_version:
+            if e.online_sh is not None:
+                K.cast(e.online, e.online_sh)
+            self._shadow_version = v
+
     def _update_target_network(self) -> None:
         e = self.engine
+        self._sync_shadows()
         K.ema(e.target, e.online[:e.layout.ema_numel], e.target_sh, self.ema_decay)
 
     def _copy_weights(self, *args) -> None:
@@ -167,6 +188,7 @@ class BYOLSpeechModel(nn.Module):
         if e.online_sh is not None:
             K.cast(e.online, e.online_sh)
             K.cast(e.target, e.target_sh)
+        self._shadow_version = self.online_flat._version
 
     def get_encoder(self) -> WavLMEncoder:
         return WavLMEncoder(engine=self.engine, which="online")

@@ -20,7 +20,8 @@ import torch
 
 from . import ddp
 from .config import get_config
-from .data import GpuMixer, create_dataloaders
+from .data import create_dataloaders
+from .health import HealthMonitor
 from .model import BYOLSpeechModel
 
 logger = logging.getLogger("nrse")
@@ -66,55 +67,67 @@ class FusedAdamW(torch.optim.Optimizer):
         eng.optimizer_step(self.lr)
 
 
-def train_one_epoch(model, dataloader, optimizer, scheduler, device, config, mixer=None, allreduce=None,
-                    world=1, rank=0, step0=0, max_steps=None):
-    """train_byol.py:20-79 -> mean epoch loss."""
+def train_one_epoch(model, dataloader, optimizer, scheduler, device, config, allreduce=None, world=1, rank=0,
+                    step0=0, max_steps=None, health=None):
+    """train_byol.py:20-79 over the reference's dict batches -> (mean epoch loss, steps).
+    The step is the engine's fused one; the health checks of :52-59 are read back `health.lag`
+    steps late (nrse_amd/health.py), so no host sync happens inside the loop."""
     model.train()
     eng = model.engine
-    mixer = mixer or GpuMixer(device, config["data"].get("do_normalize", True))
     losses = []
     steps = 0
-    for raw in dataloader:
-        batch = mixer(raw)
-        loss = eng.train_step(batch["clean_input_values"].squeeze(1), batch["noisy_input_values"].squeeze(1),
+    for batch in dataloader:
+        clean = batch["clean_input_values"].to(device, non_blocking=True)
+        noisy = batch["noisy_input_values"].to(device, non_blocking=True)
+        loss = eng.train_step(clean.reshape(clean.shape[0], -1), noisy.reshape(noisy.shape[0], -1),
                               lr=optimizer.lr, step_seed=step0 + steps, rank=rank, allreduce=allreduce,
                               world_size=world)
+        if health is not None:
+            health.record(step0 + steps, eng.health_buf)
         losses.append(loss.clone())
         scheduler.step()
         steps += 1
         if max_steps is not None and step0 + steps >= max_steps:
             break
+    if health is not None:
+        health.flush()
     if not losses:
         return float("nan"), steps
     return float(torch.stack(losses).mean()), steps  # one host sync per epoch
 
 
 @torch.no_grad()
-def validate_model(model, val_loader, device, config, mixer=None):
+def validate_model(model, val_loader, device, config, world=1):
     """evaluate_byol.py:68-123: per-SNR cosine similarity of online-encoder embeddings of the
-    clean vs noisy views + validation BYOL loss, in eval mode."""
+    clean vs noisy views + validation BYOL loss, in eval mode. With world > 1 the sums are
+    all-reduced, so every rank gets the same metrics (and the same early-stopping decision)."""
     model.eval()
     eng = model.engine
-    mixer = mixer or GpuMixer(device, config["data"].get("do_normalize", True))
-    sims = {snr: [] for snr in config["data"]["snr_range"]}
-    vloss = []
-    for raw in val_loader or []:
-        batch = mixer(raw)
-        c, n = batch["clean_input_values"].squeeze(1), batch["noisy_input_values"].squeeze(1)
+    snrs = list(config["data"]["snr_range"])
+    sim_sum = torch.zeros(len(snrs), dtype=torch.float64, device=eng.dev)
+    sim_cnt = torch.zeros(len(snrs), dtype=torch.float64, device=eng.dev)
+    vl = torch.zeros(2, dtype=torch.float64, device=eng.dev)   # loss sum, batches
+    for batch in val_loader or []:
+        c = batch["clean_input_values"].to(device).reshape(batch["clean_input_values"].shape[0], -1)
+        n = batch["noisy_input_values"].to(device).reshape(c.shape[0], -1)
         ec = eng.embed(c)
         en = eng.embed(n)
-        s = torch.nn.functional.cosine_similarity(ec, en, dim=1)
-        for snr, v in zip(batch["snr"].tolist(), s.tolist()):
-            if snr in sims:
-                sims[snr].append(v)
+        s = torch.nn.functional.cosine_similarity(ec, en, dim=1).double()
+        for k, snr in enumerate(snrs):
+            m = (batch["snr"].to(eng.dev) == snr)
+            sim_sum[k] += (s * m).sum()
+            sim_cnt[k] += m.sum()
         _, _, loss = eng.eval_forward(c, n)
-        vloss.append(float(loss))
+        vl[0] += loss.double().sum()
+        vl[1] += 1
+    if world > 1:
+        for t in (sim_sum, sim_cnt, vl):
+            ddp.all_reduce_sum(t)
     model.train()
-    avg = {k: (sum(v) / len(v) if v else 0.0) for k, v in sims.items()}
-    return (sum(vloss) / len(vloss) if vloss else float("inf")), {
-        "val_loss": sum(vloss) / len(vloss) if vloss else float("inf"),
-        "val_avg_similarity": sum(avg.values()) / len(avg) if avg else 0.0,
-        "val_similarities": avg}
+    avg = {snr: (float(sim_sum[k] / sim_cnt[k]) if float(sim_cnt[k]) > 0 else 0.0) for k, snr in enumerate(snrs)}
+    val_loss = float(vl[0] / vl[1]) if float(vl[1]) > 0 else float("inf")
+    return val_loss, {"val_loss": val_loss, "val_avg_similarity": sum(avg.values()) / len(avg) if avg else 0.0,
+                      "val_similarities": avg}
 
 
 def main(argv=None):
@@ -129,23 +142,26 @@ def main(argv=None):
     os.makedirs(t["log_dir"], exist_ok=True)
     dtype = torch.float32 if config["runtime"]["dtype"] == "f32" else torch.bfloat16
     model = BYOLSpeechModel(config, device=device, compute_dtype=dtype)
-    train_loader, val_loader = create_dataloaders(config, rank=rank, world=world)
+    train_loader, val_loader = create_dataloaders(config, device=device, rank=rank, world=world)
     optimizer = FusedAdamW(model, lr=float(t["learning_rate"]), weight_decay=float(t["weight_decay"]))
     total_steps = max(1, len(train_loader) * int(t["num_epochs"]))
     scheduler = torch.optim.lr_scheduler.CosineAnnealingLR(optimizer, T_max=total_steps)
     metric = t.get("early_stopping_metric", "val_loss")
     stopper = EarlyStopping(t.get("early_stopping_patience", 5), t.get("early_stopping_min_delta", 0.0),
                             "min" if metric == "val_loss" else "max")
-    allreduce = ddp.GradAllReduce() if world > 1 else None
-    mixer = GpuMixer(device, config["data"].get("do_normalize", True))
+    allreduce = ddp.GradAllReduce(wire_dtype=torch.bfloat16 if config["runtime"].get("bf16_allreduce") else None) \
+        if world > 1 else None
+    if world > 1 and config["runtime"].get("sync_bn"):
+        model.engine.sync_bn = ddp.SyncBN()
+    health = HealthMonitor()
     best_loss, best_sim, step = float("inf"), 0.0, 0
     max_steps = config["runtime"].get("max_steps")
     for epoch in range(int(t["num_epochs"])):
         t0 = time.perf_counter()
-        ep_loss, n = train_one_epoch(model, train_loader, optimizer, scheduler, device, config, mixer, allreduce,
-                                     world, rank, step, max_steps)
+        ep_loss, n = train_one_epoch(model, train_loader, optimizer, scheduler, device, config, allreduce,
+                                     world, rank, step, max_steps, health)
         step += n
-        val_loss, vm = validate_model(model, val_loader, device, config, mixer)
+        val_loss, vm = validate_model(model, val_loader, device, config, world)
         if rank == 0:
             print(f"Epoch {epoch + 1}/{t['num_epochs']} - Train Loss: {ep_loss:.4f}, Val Loss: {val_loss:.4f}, "
                   f"Val Avg Similarity: {vm['val_avg_similarity']:.4f} ({n} steps, "

@@ -74,6 +74,64 @@ def position_bias(E: torch.Tensor, T: int, nb: int, md: int) -> torch.Tensor:
     return E[b].permute(2, 0, 1)
 
 
+# ------------------------------------------------------------------------- operand rounding
+# bf16-operand mode (set_operand_dtype(torch.bfloat16)) restates the numerics of the engine's bf16
+# mode (nrse_amd/engine.py): GEMM / attention operands and the activations the engine stores in
+# bf16 are rounded to bf16 (round-to-nearest-even), arithmetic and accumulation stay f32, the
+# residual stream, master weights, norms and softmax statistics stay f32. Two rounding points:
+#   _rf(x)  rounds in the forward pass (straight-through in backward): a bf16-stored activation or
+#           GEMM operand whose gradient the engine keeps in f32;
+#   _rg(x)  rounds the gradient in the backward pass: a tensor whose gradient the engine stores in
+#           bf16 as the dY operand of the dgrad / wgrad GEMMs (dv, df1, dqkv, dctx, dS, dpre ...).
+_OPERAND_DTYPE = None
+
+
+def set_operand_dtype(dtype) -> None:
+    global _OPERAND_DTYPE
+    _OPERAND_DTYPE = None if dtype in (None, torch.float32) else dtype
+
+
+def operand_dtype():
+    return _OPERAND_DTYPE
+
+
+class _RoundFwd(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, dt):
+        return x.to(dt).to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, None
+
+
+class _RoundGrad(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, dt):
+        ctx.dt = dt
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(ctx.dt).to(g.dtype), None
+
+
+def _rf(x: torch.Tensor) -> torch.Tensor:
+    return x if _OPERAND_DTYPE is None else _RoundFwd.apply(x, _OPERAND_DTYPE)
+
+
+def _rg(x: torch.Tensor) -> torch.Tensor:
+    return x if _OPERAND_DTYPE is None else _RoundGrad.apply(x, _OPERAND_DTYPE)
+
+
+def _lin(x, w, b=None, *, store=False):
+    """Linear on the GEMM path: rounded operands, f32 accumulate + bias epilogue, the output's
+    gradient rounded (it is the dY operand of this GEMM's dgrad / wgrad); store=True when the
+    engine also stores the output itself in bf16 (QKV, FFN-up pre-activation)."""
+    y = _rg(F.linear(_rf(x), _rf(w), b))
+    return _rf(y) if store else y
+
+
 # ------------------------------------------------------------------------- pieces
 def _drop(x: torch.Tensor, p: float, seed: int) -> torch.Tensor:
     if p <= 0:
@@ -87,10 +145,13 @@ def conv_stack(P: dict, a, wav: torch.Tensor) -> torch.Tensor:
     x = wav[:, None]
     for i, (k, s) in enumerate(zip(a.conv_kernel, a.conv_stride)):
         pre = f"feature_extractor.conv_layers.{i}."
-        x = F.conv1d(x, P[pre + "conv.weight"], stride=s)
+        if i == 0:   # direct conv from the f32 waveform (engine: conv0 kernel, f32 weights)
+            x = F.conv1d(x, P[pre + "conv.weight"], stride=s)
+        else:        # implicit GEMM, bf16 operands, pre-LN output stored in the compute dtype
+            x = _rf(_rg(F.conv1d(_rf(x), _rf(P[pre + "conv.weight"]), stride=s)))
         x = F.layer_norm(x.transpose(1, 2), (x.shape[1],), P[pre + "layer_norm.weight"], P[pre + "layer_norm.bias"],
                          a.eps).transpose(1, 2)
-        x = F.gelu(x)
+        x = _rg(_rf(F.gelu(x)))
     return x.transpose(1, 2)
 
 
@@ -110,23 +171,61 @@ def gate(P: dict, pre: str, x1: torch.Tensor, heads: int) -> torch.Tensor:
     return (ga * (gb * c - 1.0) + 2.0).squeeze(-1)
 
 
+class _FlashBf16(torch.autograd.Function):
+    """Gated rel-pos attention core in the engine's bf16 numerics (attention_mfma.hip): q, k, v
+    bf16; S = q k^T / 8 + gate * bias and the softmax in f32; P rounded for P V; the context stored
+    in bf16 and its incoming gradient dO in bf16. Backward as the flash kernels compute it:
+    delta = rowsum(dO * O) from the bf16-stored O, dS = P (dP - delta) in f32, dV = P_bf16^T dO,
+    dQ / dK from bf16 dS, the gate and rel-pos bias gradients from the f32 dS."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, g, pbias, dt):
+        hd = q.shape[-1]
+        s = (q @ k.transpose(-1, -2)) / math.sqrt(hd) + g[..., None] * pbias[None]
+        p = torch.softmax(s, dim=-1)
+        o = (p.to(dt).float() @ v).to(dt).float()
+        ctx.save_for_backward(q, k, v, g, pbias, p, o)
+        ctx.dt = dt
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, g, pbias, p, o = ctx.saved_tensors
+        dt = ctx.dt
+        hd = q.shape[-1]
+        do = do.to(dt).float()
+        dp = do @ v.transpose(-1, -2)
+        delta = (do * o).sum(-1, keepdim=True)
+        ds = p * (dp - delta)
+        dv = p.to(dt).float().transpose(-1, -2) @ do
+        ds16 = ds.to(dt).float()
+        dq = ds16 @ k / math.sqrt(hd)
+        dk = ds16.transpose(-1, -2) @ q / math.sqrt(hd)
+        dg = (ds * pbias[None]).sum(-1)
+        dbias = (ds * g[..., None]).sum(0)
+        return dq, dk, dv, dg, dbias, None
+
+
 def attention(P: dict, a, li: int, x1: torch.Tensor, pbias: torch.Tensor, fseed: int, train: bool):
     B, T, H = x1.shape
     nh, hd = a.heads, a.head_dim
     pre = f"encoder.layers.{li}.attention."
-    q = F.linear(x1, P[pre + "q_proj.weight"], P[pre + "q_proj.bias"])
-    k = F.linear(x1, P[pre + "k_proj.weight"], P[pre + "k_proj.bias"])
-    v = F.linear(x1, P[pre + "v_proj.weight"], P[pre + "v_proj.bias"])
+    q = _lin(x1, P[pre + "q_proj.weight"], P[pre + "q_proj.bias"], store=True)
+    k = _lin(x1, P[pre + "k_proj.weight"], P[pre + "k_proj.bias"], store=True)
+    v = _lin(x1, P[pre + "v_proj.weight"], P[pre + "v_proj.bias"], store=True)
     q = q.view(B, T, nh, hd).transpose(1, 2)
     k = k.view(B, T, nh, hd).transpose(1, 2)
     v = v.view(B, T, nh, hd).transpose(1, 2)
     g = gate(P, pre, x1, nh)                               # [B, nh, T]
+    if _OPERAND_DTYPE is not None and not (train and a.attention_dropout > 0):
+        ctx = _FlashBf16.apply(q, k, v, g, pbias, _OPERAND_DTYPE).transpose(1, 2).reshape(B, T, H)
+        return _lin(ctx, P[pre + "out_proj.weight"], P[pre + "out_proj.bias"])
     s = (q @ k.transpose(-1, -2)) / math.sqrt(hd) + g[..., None] * pbias[None]
     p = torch.softmax(s, dim=-1)
     if train:
         p = _drop(p, a.attention_dropout, rng.site_seed(fseed, rng.site_attn_probs(li)))
     ctx = (p @ v).transpose(1, 2).reshape(B, T, H)
-    return F.linear(ctx, P[pre + "out_proj.weight"], P[pre + "out_proj.bias"])
+    return _lin(ctx, P[pre + "out_proj.weight"], P[pre + "out_proj.bias"])
 
 
 def encoder_forward(P: dict, a, wav: torch.Tensor, *, train: bool = False, fseed: int = 0,
@@ -134,9 +233,9 @@ def encoder_forward(P: dict, a, wav: torch.Tensor, *, train: bool = False, fseed
     """WavLMModel.forward ([TF]modeling_wavlm.py:1032-1096) -> last_hidden_state [B, T, H]."""
     feats = conv_stack(P, a, wav)
     B, T, C = feats.shape
-    xn = F.layer_norm(feats, (C,), P["feature_projection.layer_norm.weight"], P["feature_projection.layer_norm.bias"],
-                      a.eps)
-    h = F.linear(xn, P["feature_projection.projection.weight"], P["feature_projection.projection.bias"])
+    xn = _rf(F.layer_norm(feats, (C,), P["feature_projection.layer_norm.weight"],
+                          P["feature_projection.layer_norm.bias"], a.eps))
+    h = _lin(xn, P["feature_projection.projection.weight"], P["feature_projection.projection.bias"])
     if train:
         h = _drop(h, a.feat_proj_dropout, rng.site_seed(fseed, rng.SITE_FEAT_PROJ))
     if train and mask_time is not None:
@@ -144,7 +243,8 @@ def encoder_forward(P: dict, a, wav: torch.Tensor, *, train: bool = False, fseed
         h = torch.where(m[..., None], P["masked_spec_embed"].view(1, 1, -1), h)
     pre = "encoder.pos_conv_embed.conv."
     w = weight_norm_w(P[pre + "parametrizations.weight.original0"], P[pre + "parametrizations.weight.original1"])
-    pc = F.conv1d(h.transpose(1, 2), w, P[pre + "bias"], padding=a.pos_kernel // 2, groups=a.pos_groups)
+    pc = _rg(F.conv1d(_rf(h).transpose(1, 2), _rf(w), P[pre + "bias"], padding=a.pos_kernel // 2,
+                      groups=a.pos_groups))
     if a.pos_kernel % 2 == 0:
         pc = pc[:, :, :-1]
     h = h + F.gelu(pc).transpose(1, 2)
@@ -155,18 +255,18 @@ def encoder_forward(P: dict, a, wav: torch.Tensor, *, train: bool = False, fseed
         if train and layer_skip is not None and layer_skip[li]:
             continue
         pre = f"encoder.layers.{li}."
-        x1 = F.layer_norm(h, (h.shape[-1],), P[pre + "layer_norm.weight"], P[pre + "layer_norm.bias"], a.eps)
+        x1 = _rf(F.layer_norm(h, (h.shape[-1],), P[pre + "layer_norm.weight"], P[pre + "layer_norm.bias"], a.eps))
         att = attention(P, a, li, x1, pbias, fseed, train)
         if train:
             att = _drop(att, a.hidden_dropout, rng.site_seed(fseed, rng.site_attn_out(li)))
         h = h + att
-        x2 = F.layer_norm(h, (h.shape[-1],), P[pre + "final_layer_norm.weight"], P[pre + "final_layer_norm.bias"],
-                          a.eps)
-        f = F.gelu(F.linear(x2, P[pre + "feed_forward.intermediate_dense.weight"],
-                            P[pre + "feed_forward.intermediate_dense.bias"]))
+        x2 = _rf(F.layer_norm(h, (h.shape[-1],), P[pre + "final_layer_norm.weight"],
+                              P[pre + "final_layer_norm.bias"], a.eps))
+        f = _rf(F.gelu(_rg(F.linear(x2, _rf(P[pre + "feed_forward.intermediate_dense.weight"]),
+                                    P[pre + "feed_forward.intermediate_dense.bias"]))))
         if train:
             f = _drop(f, a.activation_dropout, rng.site_seed(fseed, rng.site_act(li)))
-        f = F.linear(f, P[pre + "feed_forward.output_dense.weight"], P[pre + "feed_forward.output_dense.bias"])
+        f = _lin(f, P[pre + "feed_forward.output_dense.weight"], P[pre + "feed_forward.output_dense.bias"])
         if train:
             f = _drop(f, a.hidden_dropout, rng.site_seed(fseed, rng.site_ffn_out(li)))
         h = h + f

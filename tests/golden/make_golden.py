@@ -234,10 +234,28 @@ def make_buckets():
     print("buckets: ok")
 
 
+def make_configs():
+    """The reference's YAML configs as data fixtures (yaml.safe_load -> safe_dump), so the
+    configs[0] plumbing test runs the dev config on the GPU box, where /root/reference is absent."""
+    import yaml
+    out = os.path.join(HERE, "configs")
+    os.makedirs(out, exist_ok=True)
+    for name in ("dev_wavlm-large_byol.yaml", "default_wavlm-large_byol.yaml"):
+        with open(os.path.join(REF, "config", name)) as f:
+            cfg = yaml.safe_load(f)
+        with open(os.path.join(out, name), "w") as f:
+            yaml.safe_dump(cfg, f, sort_keys=False)
+    print("configs: ok")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-large", action="store_true")
+    ap.add_argument("--configs-only", action="store_true")
     args = ap.parse_args()
+    make_configs()
+    if args.configs_only:
+        return
     torch.set_num_threads(8)
     make_buckets()
     make_snr()

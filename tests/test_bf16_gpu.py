@@ -1,0 +1,98 @@
+"""bf16 mode of the HIP path against the oracle's bf16-operand mode (oracle/wavlm_byol.py
+set_operand_dtype: the same rounding points as the engine, f32 arithmetic).
+
+Why the check is on the ENCODER with a fixed upstream gradient: at random init the BYOL heads
+(Linear-BatchNorm-ReLU over a batch of near-identical embeddings, src/models/multi_layer_heads.py)
+are ill-conditioned -- a 1e-4 relative perturbation of the embedding moves d(loss)/d(emb) by ~8 %
+(tests/test_oracle_golden.py::test_head_gradient_conditioning) -- so any bf16 path, the oracle's
+own bf16 mode included, differs from f32 by O(0.3) on the end-to-end gradient. The encoder
+backward itself is well conditioned: given the same d(loss)/d(emb) the oracle's bf16 and f32
+gradients differ by ~5e-3. This test pins the HIP bf16 encoder forward + backward there, with no
+element-count exemptions (measured on the box: HIP vs oracle-bf16 ~1e-3 on embeddings and whole
+encoder gradient, against the oracle's own 5e-3 bf16-vs-f32 gap). The only tensors skipped are
+the k_proj biases, whose exact gradient is zero (softmax is invariant to a per-row shift of the
+scores) so any rounding is infinitely "relative". The end-to-end bf16 step is checked in tests/test_engine_gpu.py and, at
+WavLM-Large against the reference itself, in tests/test_large_gpu.py.
+"""
+import pytest
+import torch
+
+from oracle import wavlm_byol as O
+from nrse_amd import arch as A, params as PR
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a = torch.as_tensor(a).double().cpu(); b = torch.as_tensor(b).double().cpu()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def _hip_encoder(arch, flat, proj, pred, dtype, clean, R):
+    from nrse_amd.engine import ByolEngine
+    eng = ByolEngine(arch, proj, pred, compute_dtype=dtype, init_flat=flat)
+    W = eng.weights("online")
+    emb, tape, _ = eng.encoder_forward(W, clean.cuda(), train=True, need_grad=True)
+    eng.grad.zero_()
+    eng.encoder_backward(tape, R.cuda().contiguous(), eng.group_views(eng.grad, "encoder"), W)
+    torch.cuda.synchronize()
+    return emb.cpu(), eng.grad.cpu(), eng
+
+
+def _oracle_encoder(arch, layout, flat, dtype, clean, R):
+    O.set_operand_dtype(dtype)
+    try:
+        P = O.split_flat(layout, flat.clone(), leaves=True)
+        h = O.encoder_forward(P["encoder"], arch, clean, train=True)
+        emb = h.mean(1)
+        (emb * R).sum().backward()
+    finally:
+        O.set_operand_dtype(None)
+    return emb.detach(), O.gather_grad(layout, P)
+
+
+def _per_tensor(eng, g, gr, gf):
+    """Per tensor: (HIP-bf16 vs oracle-bf16 deviation / its bound, HIP deviation, intrinsic
+    deviation, name), worst first. The bound scales with the tensor's intrinsic bf16 sensitivity
+    d_int (the oracle's own bf16-vs-f32 deviation of that tensor):
+      matrices (>= 4096 elements, GEMM weight gradients):  max(2e-2, 2 d_int)
+      vectors (LN / bias / gate parameters: reductions over B*T rows, often of cancelling
+      terms -- gru_rel_pos_const sums dgate*sigmoid terms over every frame):  max(0.1, 4 d_int)"""
+    out = []
+    for gname, s in eng.layout.specs:
+        if gname != "encoder" or s.name.endswith("k_proj.bias"):
+            continue
+        off, cnt, _ = eng.layout.offsets[PR.GROUP_PREFIX[gname] + s.name]
+        d_hip = rel(g[off:off + cnt], gr[off:off + cnt])
+        d_int = rel(gr[off:off + cnt], gf[off:off + cnt])
+        bound = max(2e-2, 2 * d_int) if cnt >= 4096 else max(0.1, 4 * d_int)
+        out.append((d_hip / bound, d_hip, d_int, s.name))
+    out.sort(reverse=True)
+    return out
+
+
+@pytest.mark.parametrize("case", ["tiny", "large_3s"])
+def test_bf16_encoder_matches_bf16_oracle(nrse_device, case):
+    torch.set_num_threads(min(16, torch.get_num_threads()))
+    if case == "tiny":
+        arch, proj, pred, B, L = A.TINY.deterministic(), 256, 512, 8, 16000
+    else:
+        arch, proj, pred, B, L = A.LARGE.deterministic(), 1024, 2048, 2, 48000
+    layout = PR.byol_layout(arch, proj, pred)
+    flat = PR.init_byol_flat(layout, 1234)
+    g = torch.Generator().manual_seed(5)
+    clean = torch.randn(B, L, generator=g)
+    R = torch.randn(B, arch.hidden, generator=torch.Generator().manual_seed(9))
+    emb, grad, eng = _hip_encoder(arch, flat, proj, pred, torch.bfloat16, clean, R)
+    remb, rgrad = _oracle_encoder(arch, layout, flat, torch.bfloat16, clean, R)
+    femb, fgrad = _oracle_encoder(arch, layout, flat, None, clean, R)
+    ne = max(sum(eng.layout.offsets[PR.GROUP_PREFIX[gn] + s.name][:2]) for gn, s in eng.layout.specs
+             if gn == "encoder")
+    e_hip, e_o16 = rel(emb, remb), rel(remb, femb)
+    g_hip, g_o16 = rel(grad[:ne], rgrad[:ne]), rel(rgrad[:ne], fgrad[:ne])
+    worst = _per_tensor(eng, grad, rgrad, fgrad)
+    print(f"{case}: emb HIP-bf16 vs oracle-bf16 {e_hip:.2e} (oracle bf16 vs f32 {e_o16:.2e}); encoder grad "
+          f"{g_hip:.2e} (oracle bf16 vs f32 {g_o16:.2e}); worst tensors {worst[:3]}")
+    assert e_hip < 5e-3, (e_hip, e_o16)
+    assert g_hip < 2e-2, (g_hip, g_o16)
+    assert worst[0][0] < 1.0, worst[:5]

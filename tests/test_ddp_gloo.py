@@ -85,3 +85,74 @@ def test_overlapped_layer_allreduce_world2():
     ref = sum(torch.randn(layout.numel, generator=torch.Generator().manual_seed(7 + r)) for r in range(2))
     assert out[0][1] == layout.numel            # the ranges tile the whole buffer exactly once
     assert torch.allclose(out[0][0], ref, atol=1e-6) and torch.equal(out[0][0], out[1][0])
+
+
+def _bf16_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "noise-robust-speech-embedding_amd"))
+    from nrse_amd import ddp
+    ddp.init_from_env(backend="gloo")
+    flat = torch.randn(300_001, generator=torch.Generator().manual_seed(200 + rank))
+    ar = ddp.GradAllReduce(bucket_bytes=1 << 18, wire_dtype=torch.bfloat16)
+    ar.start()
+    ar.issue(flat[100_000:])
+    ar.issue(flat[:100_000])
+    ar.finish()
+    out[rank] = (flat.clone(), ar.issued_elems)
+    dist.destroy_process_group()
+
+
+def test_bf16_wire_allreduce_world2():
+    """GradAllReduce(wire_dtype=bf16): buckets cast to bf16 on the wire, summed, cast back into the
+    f32 gradient; equal on both ranks, within bf16 rounding of the f32 sum."""
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_bf16_worker, args=(2, port, out), nprocs=2, join=True)
+    ref = sum(torch.randn(300_001, generator=torch.Generator().manual_seed(200 + r)) for r in range(2))
+    got, n = out[0]
+    assert n == 300_001 and out[0][0].dtype == torch.float32
+    assert torch.equal(got, out[1][0])
+    assert float((got - ref).norm() / ref.norm()) < 8e-3
+    assert not torch.equal(got, ref)   # it really went over the wire in bf16
+
+
+def test_rank_shares_have_equal_batch_counts():
+    """ranks must see the same number of batches (else one blocks in an all-reduce
+    the other never issues) and the same LR-schedule length."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "noise-robust-speech-embedding_amd"))
+    from nrse_amd import data as D
+    cfg = {"data": {"clean_data_path": "", "noise_data_path": "", "sample_rate": 16000, "max_audio_length": 0.01,
+                    "snr_range": [0, 5], "validation_ratio": 0.15},
+           "training": {"batch_size": 4, "num_workers": 0, "seed": 1}}
+    for n_items in (127, 130, 64, 9):
+        for world in (2, 3, 8):
+            lens = set()
+            seen = []
+            for rank in range(world):
+                tr, va, _ = D.create_raw_dataloaders(cfg, synthetic_items=n_items, rank=rank, world=world)
+                lens.add((len(tr), len(tr.dataset), len(va) if va is not None else None))
+                seen += list(tr.dataset.indices)
+            assert len(lens) == 1, (n_items, world, lens)
+            assert len(seen) == len(set(seen))   # disjoint shares
+
+
+def test_stochastic_inputs_rank_distinct_masks_shared_layerdrop():
+    import sys
+    import types
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "noise-robust-speech-embedding_amd"))
+    from nrse_amd import arch as A
+    from nrse_amd.engine import ByolEngine
+    fake = types.SimpleNamespace(arch=A.LARGE)
+    s0, m0 = ByolEngine.stochastic_inputs(fake, 5, 32, 399, True, rank=0)
+    s1, m1 = ByolEngine.stochastic_inputs(fake, 5, 32, 399, True, rank=1)
+    assert list(map(list, s0)) == list(map(list, s1))
+    assert not (m0[0] == m1[0]).all()
+    s0b, m0b = ByolEngine.stochastic_inputs(fake, 5, 32, 399, True, rank=0)
+    assert (m0b[0] == m0[0]).all() and (m0b[1] == m0[1]).all()

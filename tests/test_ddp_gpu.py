@@ -61,3 +61,70 @@ def test_overlapped_allreduce_engine_two_ranks(nrse_device):
     assert torch.equal(gs0, gs1)
     assert torch.equal(p0, p1)
     assert 0 < n0 <= numel
+
+
+def _syncbn_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), NRSE_SHARE_DEVICE="1", NRSE_DDP_BACKEND="gloo")
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "noise-robust-speech-embedding_amd"))
+    import torch.distributed as dist
+    from nrse_amd import arch as A, ddp, params as PR
+    from nrse_amd.engine import ByolEngine
+    r, w, local = ddp.init_from_env()
+    torch.cuda.set_device(local)
+    arch = A.TINY.deterministic()
+    layout = PR.byol_layout(arch, 256, 512)
+    flat = PR.init_byol_flat(layout, 1234)
+    g = torch.Generator().manual_seed(60)
+    clean = torch.randn(8, 16000, generator=g) * 0.1
+    noisy = clean + 0.05 * torch.randn(8, 16000, generator=g)
+    sl = slice(4 * r, 4 * r + 4)
+    eng = ByolEngine(arch, 256, 512, device="cuda:0", compute_dtype=torch.float32, init_flat=flat)
+    eng.sync_bn = ddp.SyncBN()
+    with torch.no_grad():
+        pred, tproj, _ = eng.forward(clean[sl].cuda(), noisy[sl].cuda(), train=True)
+    loss = eng.train_step(clean[sl].cuda(), noisy[sl].cuda(), lr=1e-4, step_seed=0, rank=r,
+                          allreduce=ddp.GradAllReduce(), world_size=w)
+    lsum = loss.clone()
+    dist.all_reduce(lsum)
+    torch.cuda.synchronize()
+    out[r] = (pred.cpu(), tproj.cpu(), float(lsum) / w, eng.grad.cpu() / w, eng.online.cpu(),
+              eng.bn["online_projector.layers.1"][1].cpu())
+    dist.destroy_process_group()
+
+
+def test_sync_batchnorm_two_ranks_equal_one_rank_of_both(nrse_device):
+    """SyncBN (nrse_amd/ddp.SyncBN): 2 ranks x B/2 rows give the rows, loss, averaged gradient,
+    running statistics and parameter update of 1 rank x B (the two forwards per rank also update
+    the running stats twice, as on the single rank below)."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "noise-robust-speech-embedding_amd"))
+    from nrse_amd import arch as A, params as PR
+    from nrse_amd.engine import ByolEngine
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_syncbn_worker, args=(2, port, out), nprocs=2, join=True)
+    arch = A.TINY.deterministic()
+    layout = PR.byol_layout(arch, 256, 512)
+    flat = PR.init_byol_flat(layout, 1234)
+    g = torch.Generator().manual_seed(60)
+    clean = torch.randn(8, 16000, generator=g) * 0.1
+    noisy = clean + 0.05 * torch.randn(8, 16000, generator=g)
+    eng = ByolEngine(arch, 256, 512, device="cuda:0", compute_dtype=torch.float32, init_flat=flat)
+    with torch.no_grad():
+        pred, tproj, _ = eng.forward(clean.cuda(), noisy.cuda(), train=True)
+    loss = float(eng.train_step(clean.cuda(), noisy.cuda(), lr=1e-4, step_seed=0))
+
+    def rel(a, b):
+        return float((a.double() - b.double()).norm() / b.double().norm())
+    p2 = torch.cat([out[0][0], out[1][0]])
+    t2 = torch.cat([out[0][1], out[1][1]])
+    assert rel(p2, pred.cpu()) < 1e-4 and rel(t2, tproj.cpu()) < 1e-4
+    assert abs(out[0][2] - loss) < 1e-5 and abs(out[1][2] - loss) < 1e-5
+    assert rel(out[0][3], eng.grad.cpu()) < 1e-3
+    assert rel(out[0][5], eng.bn["online_projector.layers.1"][1].cpu()) < 1e-4
+    assert torch.equal(out[0][4], out[1][4])

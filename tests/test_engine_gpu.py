@@ -3,7 +3,8 @@ reference by tests/test_oracle_golden.py), on the tiny WavLM arch.
 
 Tolerances (stated per the north star): fp32 parity mode uses exact-f32 MFMA / f32 kernels,
 so embeddings and loss agree to ~1e-5 rel-L2; bf16 mode (bf16 GEMM operands, f32 accumulate,
-f32 residual stream) is checked at 2e-2 rel-L2 on embeddings.
+f32 residual stream) is checked at 2e-2 rel-L2 on embeddings against the f32 oracle and at 5e-3
+against the oracle's bf16-operand mode.
 """
 import numpy as np
 import pytest
@@ -47,10 +48,28 @@ def test_eval_forward_matches_oracle(nrse_device, dtype, tol):
     assert rel(pred, rp) < 5 * tol
     assert rel(tproj, rt) < 5 * tol
     assert abs(float(loss) - float(rl)) < 5 * tol
+    if dtype == torch.bfloat16:
+        # against the oracle's bf16-operand mode (same rounding points): 4x tighter
+        O.set_operand_dtype(dtype)
+        try:
+            with torch.no_grad():
+                rp16, rt16, remb16 = O.forward(st, clean, noisy, train=False)
+        finally:
+            O.set_operand_dtype(None)
+        assert rel(emb, remb16) < tol / 4, (rel(emb, remb16), rel(emb, remb))
+        assert rel(tproj, rt16) < 5 * tol / 4
 
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-4), (torch.bfloat16, 5e-2)])
 def test_train_step_matches_oracle(nrse_device, dtype, tol):
+    """One fused train step (forward, loss, backward, clip, AdamW, EMA) vs the oracle step.
+    bf16: the oracle runs in its bf16-operand mode (same rounding points). The end-to-end
+    gradient passes through the BYOL heads, whose BatchNorm over near-identical random-init
+    embeddings amplifies rounding ~800x (test_oracle_golden.py::test_head_gradient_conditioning;
+    the oracle's own bf16 and f32 modes differ by 0.27 rel-L2 here), so in bf16 only the loss,
+    the gradient norm and the whole-gradient direction are bounded end to end; the gradient is
+    pinned per tensor, with no exemptions but the zero-gradient k_proj biases, by
+    tests/test_bf16_gpu.py under a fixed upstream gradient."""
     arch = A.TINY.deterministic()
     eng, st, clean, noisy = make(arch, dtype, B=8)
     flat0 = st.online.clone()
@@ -58,27 +77,27 @@ def test_train_step_matches_oracle(nrse_device, dtype, tol):
     eng.cfg.ema_decay = ema
     eng.cfg.weight_decay = wd
     loss = eng.train_step(clean.cuda(), noisy.cuda(), lr=lr, step_seed=3)
-    r = O.train_step(st, clean, noisy, lr=lr, weight_decay=wd, ema_decay=ema, step_seed=3)
+    O.set_operand_dtype(dtype)
+    try:
+        r = O.train_step(st, clean, noisy, lr=lr, weight_decay=wd, ema_decay=ema, step_seed=3)
+    finally:
+        O.set_operand_dtype(None)
     assert abs(float(loss) - r["loss"]) < tol
     g = eng.grad.cpu()
     assert abs(eng.grad_norm() - r["grad_norm"]) / r["grad_norm"] < 10 * tol
-    # whole gradient vector, then per tensor. bf16 mode: the tiny arch at random init has a
-    # loss gradient dominated by near-cancelling terms (the BYOL cosine of two similar views), so
-    # bf16 operand rounding in the forward shows up at ~0.3 rel-L2 on the whole gradient (the
-    # same before and after every kernel change; the f32 path is at 1e-5), and tensors of a few
-    # elements whose gradient is a sum of cancelling terms (gru_rel_pos_const [1,H,1,1], conv LN
-    # biases) sit at O(1); those are checked in f32 mode only.
-    assert rel(g, r["grad"]) < (10 * tol if dtype == torch.float32 else 0.5)
-    min_numel = 1 if dtype == torch.float32 else 4096
-    worst = []
-    for gname, s in eng.layout.specs:
-        off, cnt, _ = eng.layout.offsets[PR.GROUP_PREFIX[gname] + s.name]
-        ref = r["grad"][off:off + cnt]
-        if ref.norm() < 1e-6 * r["grad_norm"] or cnt < min_numel:
-            continue
-        worst.append((rel(g[off:off + cnt], ref), s.name))
-    worst.sort(reverse=True)
-    assert worst[0][0] < 20 * tol, worst[:5]
+    if dtype == torch.float32:
+        assert rel(g, r["grad"]) < 10 * tol
+        worst = []
+        for gname, s in eng.layout.specs:
+            off, cnt, _ = eng.layout.offsets[PR.GROUP_PREFIX[gname] + s.name]
+            ref = r["grad"][off:off + cnt]
+            if ref.norm() < 1e-6 * r["grad_norm"]:
+                continue
+            worst.append((rel(g[off:off + cnt], ref), s.name))
+        worst.sort(reverse=True)
+        assert worst[0][0] < 20 * tol, worst[:5]
+    else:
+        assert rel(g, r["grad"]) < 0.5
     # AdamW + EMA: parameter deltas in units of lr. The first Adam step is ~lr*sign(g), so
     # entries with near-zero gradients flip sign under bf16 rounding of the operands.
     d = (eng.online.cpu() - flat0)

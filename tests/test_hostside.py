@@ -96,3 +96,12 @@ def test_config_schema_and_cli_overrides(tmp_path):
 
 def test_frames():
     assert A.LARGE.frames(128000) == 399 and A.LARGE.frames(80000) == 249
+
+
+def test_mock_pairs_follow_create_mock_dataset_rule():
+    from nrse_amd.data import MockPairs
+    ds = MockPairs(10, 800, [0, 5, 10, 15, 20], seed=1)
+    assert [int(ds[i]["snr"]) for i in range(10)] == [0, 5, 10, 15, 20] * 2
+    for i in range(10):
+        d = ds[i]["noisy_input_values"] - ds[i]["clean_input_values"]
+        assert abs(float(d.std()) * (int(ds[i]["snr"]) + 1) - 1.0) < 0.15

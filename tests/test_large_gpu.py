@@ -1,0 +1,158 @@
+"""WavLM-Large end to end on the HIP path against the REFERENCE's own outputs
+(tests/golden/byol_large.npz, written by tests/golden/make_golden.py from the reference
+BYOLSpeechModel / byol_loss / AdamW / _update_target_network on WavLM-Large, B = 4, 8 s).
+
+This is the north-star tolerance check: embeddings within 1e-3 rel-L2 of the reference
+(BASELINE.json north_star; reference src/models/byol.py:75-128, src/models/encoder.py:17-32,
+train_byol.py:56-74).
+
+* f32 parity mode (exact-f32 MFMA GEMMs, f32 attention / norms): the bound 1e-3 is asserted on
+  embeddings, online_pred, target_proj and the pre-clip gradient norm; the gradient sample, the
+  per-tensor gradient norms, the AdamW update and the EMA update are checked too.
+* bf16 mode (the benchmarked configs[1] path: bf16 GEMM / attention operands, f32 accumulation,
+  f32 residual stream and master weights): the deviation from the reference is measured,
+  printed and bounded (stated tolerances in DESIGN.md §6).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from nrse_amd import arch as A, params as PR
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FIX = os.path.join(ROOT, "tests", "golden", "byol_large.npz")
+OUT = os.path.join(ROOT, "gpurun_out")
+
+
+def rel(a, b):
+    a = torch.as_tensor(np.asarray(a) if not torch.is_tensor(a) else a).double().cpu()
+    b = torch.as_tensor(np.asarray(b) if not torch.is_tensor(b) else b).double().cpu()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def make_inputs(B, L, seed):
+    """Identical to tests/golden/make_golden.py:make_inputs (seed = SEED + 1 = 1235)."""
+    g = torch.Generator().manual_seed(seed)
+    clean = torch.randn(B, 1, L, generator=g)
+    noisy = clean + 0.3 * torch.randn(B, 1, L, generator=g)
+    return clean.squeeze(1), noisy.squeeze(1)
+
+
+@pytest.fixture(scope="module")
+def large():
+    z = np.load(FIX)
+    arch = A.LARGE.deterministic()
+    layout = PR.byol_layout(arch, int(z["proj_dim"]), int(z["pred_dim"]))
+    flat = PR.init_byol_flat(layout, int(z["seed"]))
+    clean, noisy = make_inputs(int(z["B"]), int(z["L"]), int(z["seed"]) + 1)
+    return dict(z=z, arch=arch, layout=layout, flat=flat, clean=clean, noisy=noisy)
+
+
+def _engine(large, dtype):
+    from nrse_amd.engine import ByolEngine
+    z = large["z"]
+    eng = ByolEngine(large["arch"], int(z["proj_dim"]), int(z["pred_dim"]), compute_dtype=dtype,
+                     init_flat=large["flat"])
+    eng.cfg.ema_decay = float(z["ema"])
+    eng.cfg.weight_decay = float(z["wd"])
+    return eng
+
+
+def _run(large, dtype):
+    """Eval forward, last_hidden_state, one det train step; returns the measured deviations."""
+    z = large["z"]
+    eng = _engine(large, dtype)
+    clean, noisy = large["clean"].cuda(), large["noisy"].cuda()
+    m = {}
+    pred, tproj, loss = eng.eval_forward(clean, noisy)
+    emb = eng.embed(clean)
+    hs, _, _ = eng.encoder_forward(eng.weights("online"), clean, train=False, hidden_dtype=torch.float32)
+    m["eval_emb"] = rel(emb, z["eval_emb"])
+    m["eval_pred"] = rel(pred, z["eval_pred"])
+    m["eval_tproj"] = rel(tproj, z["eval_tproj"])
+    m["eval_loss_abs"] = abs(float(loss) - float(z["eval_loss"]))
+    m["hidden_norms"] = rel(hs.norm(dim=-1), z["eval_hidden_norms"])
+    m["hidden_sample"] = rel(hs[:, ::37, ::13], z["eval_hidden_sample"])
+    del hs
+    lr = float(z["lr"])
+    l1 = eng.train_step(clean, noisy, lr=lr, step_seed=0)
+    torch.cuda.synchronize()
+    m["train_loss_abs"] = abs(float(l1) - float(z["train_loss"]))
+    m["grad_norm_rel"] = abs(eng.grad_norm() - float(z["train_grad_norm"])) / float(z["train_grad_norm"])
+    g = eng.grad.cpu()
+    idx = torch.from_numpy(z["grad_idx"])
+    m["grad_sample"] = rel(g[idx], z["grad_sample"])
+    # per-tensor gradient norms (505 tensors, layout order)
+    norms = []
+    for gname, s in eng.layout.specs:
+        off, cnt, _ = eng.layout.offsets[PR.GROUP_PREFIX[gname] + s.name]
+        norms.append(float(g[off:off + cnt].norm()))
+    ref_n = z["grad_tensor_norms"]
+    norms = np.array(norms)
+    sig = ref_n > 1e-4 * float(z["train_grad_norm"])
+    tn = np.abs(norms[sig] - ref_n[sig]) / ref_n[sig]
+    m["tensor_norm_worst"] = float(tn.max())
+    m["tensor_norm_median"] = float(np.median(tn))
+    m["tensor_norm_worst_name"] = [f"{gn}.{s.name}" for (gn, s), keep in zip(eng.layout.specs, sig) if keep][
+        int(tn.argmax())]
+    # AdamW update (first step ~ lr * sign(g)) and EMA of it, at the sampled indices
+    d = (eng.online.cpu()[idx] - large["flat"][idx]).numpy()
+    dr = z["online_delta_sample"]
+    m["online_delta"] = rel(d, dr)
+    m["online_delta_flip_frac"] = float((np.abs(d - dr) > 0.05 * lr).mean())
+    tidx = torch.from_numpy(z["target_idx"])
+    dt = (eng.target.cpu()[tidx] - large["flat"][tidx]).numpy()
+    m["target_delta"] = rel(dt, z["target_delta_sample"])
+    # BatchNorm running statistics after one train-mode forward of each view
+    bn = torch.cat([eng.bn["online_projector.layers.1"][0], eng.bn["online_projector.layers.1"][1],
+                    eng.bn["target_projector.layers.4"][1]]).cpu()
+    m["bn_running"] = rel(bn, z["bn_running"])
+    del eng
+    torch.cuda.empty_cache()
+    return m
+
+
+def _record(tag, m):
+    os.makedirs(OUT, exist_ok=True)
+    with open(os.path.join(OUT, f"large_parity_{tag}.json"), "w") as f:
+        json.dump(m, f, indent=1)
+    print(tag, json.dumps(m))
+
+
+def test_large_f32_matches_reference(nrse_device, large):
+    m = _run(large, torch.float32)
+    _record("f32", m)
+    tol = 1e-3   # north-star bound on embeddings
+    assert m["eval_emb"] < tol, m
+    assert m["eval_pred"] < tol and m["eval_tproj"] < tol, m
+    assert m["eval_loss_abs"] < 1e-4, m
+    assert m["hidden_norms"] < tol and m["hidden_sample"] < tol, m
+    assert m["train_loss_abs"] < 1e-4, m
+    assert m["grad_norm_rel"] < tol, m
+    assert m["grad_sample"] < 1e-2, m
+    assert m["tensor_norm_worst"] < 1e-2, m
+    assert m["online_delta_flip_frac"] < 0.01, m
+    assert m["online_delta"] < 0.05 and m["target_delta"] < 0.05, m
+    assert m["bn_running"] < tol, m
+
+
+def test_large_bf16_deviation(nrse_device, large):
+    """The benchmarked mode. Measured deviations are written to gpurun_out/large_parity_bf16.json
+    and quoted in DESIGN.md §6; the bounds below are the stated bf16 tolerances."""
+    m = _run(large, torch.bfloat16)
+    _record("bf16", m)
+    assert m["eval_emb"] < 1e-2, m
+    assert m["eval_pred"] < 3e-2 and m["eval_tproj"] < 3e-2, m
+    assert m["hidden_norms"] < 1e-2, m
+    assert m["train_loss_abs"] < 1e-2, m
+    # the end-to-end gradient goes through the heads' BatchNorm over 4 near-identical random-init
+    # embeddings (ill-conditioned: test_oracle_golden.py::test_head_gradient_conditioning), so a
+    # 5e-3 embedding deviation moves it by O(0.1-1); measured: norm 0.11, sample 0.71 rel-L2. The
+    # bf16 gradient is pinned under a fixed upstream gradient by tests/test_bf16_gpu.py.
+    assert m["grad_norm_rel"] < 0.25, m
+    assert m["grad_sample"] < 1.0, m
+    assert m["bn_running"] < 3e-2, m

@@ -102,3 +102,21 @@ def test_train_cli_synthetic(nrse_device, tmp_path):
     assert "Epoch 1/1" in out.stdout
     ck = torch.load(tmp_path / "ck" / "last_model.pt", weights_only=True, map_location="cpu")
     assert "online_encoder.model.encoder.layers.0.attention.rel_attn_embed.weight" in ck["model_state_dict"]
+
+
+def test_dev_yaml_cli_on_mock_dataset(nrse_device, tmp_path):
+    """configs[0]: the reference's dev YAML (config/dev_wavlm-large_byol.yaml, as a fixture) through
+    the train_byol CLI at batch 2 on test/create_mock_dataset.py-style pairs (SNR cycling through
+    snr_range, noise level 1/(snr+1)), WavLM-Large, one epoch capped at 3 steps."""
+    conf = os.path.join(ROOT, "tests", "golden", "configs", "dev_wavlm-large_byol.yaml")
+    out = subprocess.run([sys.executable, os.path.join(PKG, "train_byol.py"), "--config", conf, "--device", "cuda:0",
+                          "--batch_size", "2", "--epochs", "1", "--mock_items", "16", "--max_steps", "3"],
+                         capture_output=True, text=True, timeout=600, cwd=str(tmp_path))
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "Epoch 1/1" in out.stdout, out.stdout
+    ck = torch.load(tmp_path / "checkpoints/byol/wavlm_large-val_loss/last_model.pt", weights_only=True,
+                    map_location="cpu")
+    sd = ck["model_state_dict"]
+    assert sd["online_encoder.model.encoder.layers.23.feed_forward.output_dense.weight"].shape == (1024, 4096)
+    assert sd["online_predictor.layers.6.weight"].shape == (1024, 2048)
+    assert np.isfinite(ck["loss"])
