@@ -66,8 +66,9 @@ int nrse_abi_version(void);
  *   kcontig=1: o = m (resp. n), c = k      kcontig=0: o = k, c = m (resp. n)
  * K is split into `nseg` segments of `K` elements each (segment s adds s*seg_stride).
  * grid z = batch * splits; batch zb adds (zb / zdiv)*z1 + (zb % zdiv)*z2 to every pointer;
- * split s handles segments [s*nseg, (s+1)*nseg) and (with NRSE_EPI_SPLIT_SLAB) writes to
- * C + s*c_split.
+ * split s handles segments [s*nseg, (s+1)*nseg) and writes to C + s*c_split (c_split = 0: every
+ * split into C, with NRSE_EPI_ATOMIC; c_split > 0: per-split f32 slabs, summed afterwards by
+ * nrse_splitk_reduce).
  * ------------------------------------------------------------------------------------------ */
 enum {
   NRSE_EPI_BIAS = 1 << 0,         /* v += bias[n] (f32); with splits > 1 only split 0 adds it */
@@ -275,6 +276,10 @@ int nrse_dropout_cast_colsum(const float* in, void* out, int out_dtype, long lon
 int nrse_colsum(const void* x, int dtype, float* colsum, long long rows, int C, void* stream);
 /* y = x cast (f32 <-> bf16), n elements */
 int nrse_cast(const void* x, int x_dtype, void* y, int y_dtype, long long n, void* stream);
+/* Split-K reduction of a weight gradient (the Linear wgrads of the backward, train_byol.py:65):
+ * dst[i] (+)= sum_s slabs[s * n + i], s = 0 .. splits-1, in split order (deterministic); f32;
+ * accumulate = 0 overwrites dst. The partial slabs are written by nrse_gemm with c_split = n. */
+int nrse_splitk_reduce(float* dst, const float* slabs, int splits, long long n, int accumulate, void* stream);
 /* dst[a][c][b] (+)= src[a][b][c]  (conv weight [co][ci][k] <-> implicit-GEMM layout [co][k][ci]) */
 int nrse_swap12(const void* src, int src_dtype, void* dst, int dst_dtype, int d0, int d1, int d2, int accumulate,
                 void* stream);

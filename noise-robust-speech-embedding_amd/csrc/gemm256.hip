@@ -35,7 +35,25 @@
 
 // Diagnostic builds only (tools/build_diag.sh): 1 = global loads dropped (zero-record
 // descriptors), 2 = LDS fragment reads replaced by register values, 3 = MFMAs removed,
-// 4 = main-loop barriers removed, 5 = no LDS-DMA instructions, 6 = neither LDS-DMA nor MFMAs. Outputs of those builds are wrong; only their time matters.
+// 4 = main-loop barriers removed, 5 = no LDS-DMA instructions, 6 = neither LDS-DMA nor MFMAs,
+// 7 = epilogue without its global stores (LDS passes kept), 8 = epilogue without LDS reads or
+// stores. Outputs of those builds are wrong; only their time matters.
+// NRSE_G3_STAMPS (diagnostic builds only): workgroup 0-thread writes s_memtime at kernel entry,
+// after the prologue wait, after the main loop and at the end to ((u64*)p.colsum)[4 * wg + i]
+// when the COLSUM flag is off (tools/diag_stamps.py).
+#ifndef NRSE_G3_STAMPS
+#define NRSE_G3_STAMPS 0
+#endif
+#if NRSE_G3_STAMPS
+#define NRSE_STAMP(I)                                                                                 \
+  do {                                                                                                \
+    if (tid == 0 && p.colsum && !(p.flags & NRSE_EPI_COLSUM))                                         \
+      reinterpret_cast<unsigned long long*>(p.colsum)[4 * (long long)blockIdx.x + (I)] =              \
+          __builtin_amdgcn_s_memtime();                                                               \
+  } while (0)
+#else
+#define NRSE_STAMP(I) ((void)0)
+#endif
 #ifndef NRSE_G3_ABLATE
 #define NRSE_G3_ABLATE 0
 #endif
@@ -149,6 +167,7 @@ template <bool AKC, bool BKC>
 __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params p, int mt, int nt) {
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
   const int tid = threadIdx.x;
+  NRSE_STAMP(0);
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
@@ -220,6 +239,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
   }
   asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
   NRSE_BAR();
+  NRSE_STAMP(1);
 
   bf16x8 fa[4][2], fbl[2][2], fbh[2][2];
 #if NRSE_G3_ABLATE == 2
@@ -300,6 +320,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
     base = wrap(base + 4);
   }
   if (wm == 0) __builtin_amdgcn_s_barrier();
+  NRSE_STAMP(2);
 #undef NRSE_READ_A
 #undef NRSE_READ_B
 #undef NRSE_QUAD
@@ -360,7 +381,13 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
           }
           continue;
         }
+#if NRSE_G3_ABLATE == 7
+        if (cr[0] == 12345.f) epi8(p, epi, m, n, cr, colsum);  // never: keeps the LDS reads
+#elif NRSE_G3_ABLATE == 8
+        (void)cr;
+#else
         epi8(p, epi, m, n, cr, colsum);
+#endif
       }
       if (colsum) {
         __syncthreads();
@@ -370,6 +397,10 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
     __syncthreads();
   }
   if (colsum && n0 + ccol < p.N) atomicAdd(p.colsum + n0 + ccol, csum);
+#if NRSE_G3_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  NRSE_STAMP(3);
 }
 
 template <bool AKC, bool BKC>

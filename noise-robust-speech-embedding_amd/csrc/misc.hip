@@ -3,6 +3,8 @@
 //   SpecAugment apply/bwd  [TF]modeling_wavlm.py:1006-1011
 //   dropout backward       [TF]modeling_wavlm.py:99, 294, 482 (nn.Dropout)
 //   bias gradients         column sums of the output gradients of every nn.Linear
+#include <algorithm>
+
 #include "common.h"
 
 namespace {
@@ -357,6 +359,39 @@ extern "C" int nrse_cast(const void* x, int xdt, void* y, int ydt, long long n, 
   if (n == 0) return NRSE_OK;
   hipLaunchKernelGGL(cast_kernel, dim3(blocks_for(n)), dim3(256), 0, (hipStream_t)stream, x, xdt, y, ydt, n);
   return nrse_check_launch("nrse_cast");
+}
+
+// dst (+)= sum over splits of the f32 partial slabs, 16 B per lane, grid-stride; the slabs are
+// streamed once (HBM-bound: (splits + 1 or 2) * n * 4 bytes)
+static __global__ __launch_bounds__(256) void splitk_reduce_kernel(float* __restrict__ dst, const float* __restrict__ slabs,
+                                                            int splits, long long n4, long long n, int acc) {
+  const long long stride = (long long)gridDim.x * 256;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
+    float4 s = acc ? reinterpret_cast<const float4*>(dst)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 0; k < splits; ++k) {
+      const float4 v = reinterpret_cast<const float4*>(slabs + (long long)k * n)[i];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    reinterpret_cast<float4*>(dst)[i] = s;
+  }
+  // scalar tail (n % 4)
+  for (long long i = n4 * 4 + (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    float s = acc ? dst[i] : 0.f;
+    for (int k = 0; k < splits; ++k) s += slabs[(long long)k * n + i];
+    dst[i] = s;
+  }
+}
+
+extern "C" int nrse_splitk_reduce(float* dst, const float* slabs, int splits, long long n, int accumulate,
+                                  void* stream) {
+  NRSE_REQUIRE(dst && slabs && splits >= 1 && n > 0, "nrse_splitk_reduce: bad args");
+  NRSE_REQUIRE(((uintptr_t)dst & 15) == 0 && ((uintptr_t)slabs & 15) == 0 && (n % 4 == 0 || splits == 1),
+               "nrse_splitk_reduce: dst / slabs must be 16-byte aligned and n a multiple of 4");
+  const long long n4 = n / 4;
+  const long long blocks = std::min<long long>((n4 + 255) / 256, 2048);
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)std::max<long long>(blocks, 1)), dim3(256), 0,
+                     (hipStream_t)stream, dst, slabs, splits, n4, n, accumulate);
+  return nrse_check_launch("nrse_splitk_reduce");
 }
 
 extern "C" int nrse_swap12(const void* src, int sdt, void* dst, int ddt, int d0, int d1, int d2, int acc,

@@ -133,6 +133,7 @@ _SIGNATURES = {
     "nrse_dropout_cast_colsum": ([c_vp, c_vp, c_int, c_ll, c_int, c_f, c_u32, c_vp, c_vp], c_int),
     "nrse_colsum": ([c_vp, c_int, c_vp, c_ll, c_int, c_vp], c_int),
     "nrse_cast": ([c_vp, c_int, c_vp, c_int, c_ll, c_vp], c_int),
+    "nrse_splitk_reduce": ([c_vp, c_vp, c_int, c_ll, c_int, c_vp], c_int),
     "nrse_swap12": ([c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
     "nrse_gelu_bwd_pad": ([c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
     "nrse_bn_fwd": ([c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_f, c_f, c_int, c_int, c_vp], c_int),

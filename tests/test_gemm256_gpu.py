@@ -14,10 +14,12 @@ def rel(a, b):
     return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
 
 
-@pytest.fixture
-def gen3(nrse_device):
+@pytest.fixture(params=[3], ids=["gen3"])
+def gen3(nrse_device, request):
+    """The 256x256 kernel generation (gemm256.hip)."""
     from nrse_amd import kernels as K
-    old = K.gemm_select(3)
+    old = K.gemm_select(request.param)
+    K.current_gen = request.param
     yield K
     K.gemm_select(old)
 
@@ -83,13 +85,13 @@ def test_epilogue_dropout_matches_128_kernel(gen3, nrse_device, after):
     r = torch.randn(M, N, device=dev)
     flags = _lib.EPI_RESID | (_lib.EPI_DROP_AFTER if after else 0)
     outs = []
-    for g in (3, 2):
+    for g in (K.current_gen, 2):
         K.gemm_select(g)
         c = torch.empty(M, N, device=dev)
         K.gemm(K.Operand(x, True, Kd), K.Operand(w, True, Kd), c, M, N, Kd, ldc=N, flags=flags, resid=r, ldr=N,
                dropout_p=0.2, seed=1234)
         outs.append(c)
-    K.gemm_select(3)
+    K.gemm_select(K.current_gen)
     assert torch.equal(outs[0] == 0, outs[1] == 0)
     assert rel(outs[0], outs[1]) < 1e-6
     dropped = (outs[0] == 0) if after else (outs[0] - r == 0)
@@ -147,12 +149,32 @@ def test_step_shapes_agree_with_128_kernel(gen3, nrse_device):
     M, N, Kd = 12768, 4096, 1024
     x, w = bf(M, Kd, dev=dev), bf(N, Kd, dev=dev, scale=0.03)
     outs = []
-    for g in (3, 2):
+    for g in (K.current_gen, 2):
         K.gemm_select(g)
         c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
         K.gemm(K.Operand(x, True, Kd), K.Operand(w, True, Kd), c, M, N, Kd, ldc=N)
         outs.append(c.float())
-    K.gemm_select(3)
+    K.gemm_select(K.current_gen)
     assert rel(outs[0], outs[1]) < 5e-3
     idx = torch.randint(0, M, (64,), device=dev)
     assert rel(outs[0][idx], x[idx].double() @ w.double().t()) < 4e-3
+
+
+def test_many_tiles_per_workgroup_tails_batched(gen3, nrse_device):
+    """More tiles than CUs (several waves of workgroups), ragged M / N / K, a z-batch and the bias +
+    GELU + residual epilogue."""
+    K = gen3
+    from nrse_amd import _lib
+    dev = nrse_device
+    Z, M, N, Kd = 2, 2100, 4104, 200
+    x = bf(Z, M, Kd, dev=dev)
+    w = bf(Z, N, Kd, dev=dev, scale=0.1)
+    bias = torch.randn(N, device=dev)
+    r = torch.randn(Z, M, N, device=dev)
+    pre = torch.empty(Z, M, N, device=dev, dtype=torch.bfloat16)
+    c = torch.empty(Z, M, N, device=dev)
+    K.gemm(K.Operand(x, True, Kd, z1=M * Kd), K.Operand(w, True, Kd, z1=N * Kd), c, M, N, Kd, ldc=N, batch=Z,
+           c_z1=M * N, bias=bias, flags=_lib.EPI_GELU, aux=pre, ldaux=N, aux_z1=M * N, resid=r, ldr=N, r_z1=M * N)
+    ref_pre = torch.einsum("zmk,znk->zmn", x.double(), w.double()) + bias.double()
+    assert rel(pre, ref_pre) < 4e-3
+    assert rel(c, F.gelu(ref_pre) + r.double()) < 1e-5

@@ -73,3 +73,37 @@ def test_gemm_conv_implicit(nrse_device):
            ldc=C, batch=B, c_z1=Tout * C)
     ref = torch.nn.functional.conv1d(x.double().transpose(1, 2), w.double(), stride=s).transpose(1, 2)
     assert rel(y, ref) < 1e-6
+
+
+@pytest.mark.parametrize("shape", [(12768, 3072, 1024), (12768, 1024, 1024), (4096, 520, 264)])
+def test_linear_wgrad_slab_splitk(nrse_device, shape):
+    """linear_wgrad's split-K slab path (f32 partial slabs + nrse_splitk_reduce, accumulating into
+    an existing gradient) against float64, and identical to itself run to run (deterministic)."""
+    from nrse_amd import kernels as K
+    M, N, Kin = shape
+    dev = nrse_device
+    dy = (torch.randn(M, N, device=dev) * 0.1).to(torch.bfloat16)
+    x = torch.randn(M, Kin, device=dev).to(torch.bfloat16)
+    g0 = torch.randn(N, Kin, device=dev)
+    S = K._slab_splits(M, N, Kin)
+    dw = g0.clone()
+    K.linear_wgrad(dy, x, dw)
+    ref = g0.double() + dy.double().t() @ x.double()
+    assert rel(dw, ref) < 1e-5, (S, rel(dw, ref))
+    dw2 = g0.clone()
+    K.linear_wgrad(dy, x, dw2)
+    if S:
+        assert torch.equal(dw, dw2)
+
+
+def test_splitk_reduce(nrse_device):
+    from nrse_amd import kernels as K, _lib
+    dev = nrse_device
+    for n, S in ((4096, 3), (1000, 1), (12, 5)):
+        slabs = torch.randn(S, n, device=dev)
+        dst = torch.randn(n, device=dev)
+        ref = dst.double() + slabs.double().sum(0)
+        _lib.call("nrse_splitk_reduce", K.ptr(dst), K.ptr(slabs), S, n, 1, K.stream_ptr())
+        assert rel(dst, ref) < 1e-6
+        _lib.call("nrse_splitk_reduce", K.ptr(dst), K.ptr(slabs), S, n, 0, K.stream_ptr())
+        assert rel(dst, slabs.double().sum(0)) < 1e-6

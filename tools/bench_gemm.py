@@ -41,4 +41,9 @@ for name, M, N, Kd in shapes:
         t4 = timeit(lambda: K.linear_wgrad(dy, a, dw))
         line += f" g{g}: fwd {fl / t1 / 1e9:.0f} dgrad {fl / t3 / 1e9:.0f} wgrad {fl / t4 / 1e9:.0f} |"
     K.gemm_select(0)
+    for slab in (False, True):
+        K._SLAB_WGRAD = slab
+        t5 = timeit(lambda: K.linear_wgrad(dy, a, dw))
+        line += f" auto wgrad({'slab' if slab else 'atomic'}) {fl / t5 / 1e9:.0f} |"
+    K._SLAB_WGRAD = True
     print(line, flush=True)
