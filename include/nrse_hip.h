@@ -171,13 +171,18 @@ int nrse_ln_mean_fwd(const float* h, const float* gamma, const float* beta, floa
  * Gated relative-position attention, WavLMAttention ([TF]modeling_wavlm.py:147-271) with
  * F.multi_head_attention_forward / SDPA ([TORCH]functional.py:6206, 6629).
  * Layouts: qkv [B*T, 3*Hd] rows = (q | k | v), head h at columns h*64..h*64+63 (head_dim 64);
- * ctx [B*T, Hd]; gate, lse, delta [B, H, T] f32; bias [H, T, Tb] f32 with Tb = nrse_bias_ld(T)
- * (rows padded to a multiple of 64 with zeros; layer-0 table, reused by every layer as in
- * [TF]modeling_wavlm.py:505); bucket [2T-1] int32 = bucket(j - i) at j-i+T-1.
+ * ctx [B*T, Hd]; gate, lse, delta [B, H, T] f32; bucket [2T-1] int32 = bucket(j - i) at j-i+T-1.
+ * The relative-position bias (layer-0 table, reused by every layer as in [TF]modeling_wavlm.py:505)
+ * depends on j - i only: the bf16 MFMA kernels read it as a Toeplitz vector bias_vec [H, 2T-1]
+ * (bias_vec[h, j-i+T-1] = E[bucket(j-i), h], nrse_rel_bias_vec), staged per workgroup in LDS; the
+ * f32 parity-mode kernels read the expanded table bias [H, T, Tb], Tb = nrse_bias_ld(T) (rows
+ * padded to a multiple of 64 with zeros, nrse_rel_bias_fwd).
  * Dropout on the attention probabilities: keep(i) = hash(seed, ((b*H+h)*T+i)*T+j).
  * ------------------------------------------------------------------------------------------ */
 int nrse_bias_ld(int T);
 int nrse_rel_bias_fwd(const float* E, const int* bucket, float* bias, int H, int T, int nb, void* stream);
+/* bias_vec[h, e] = E[bucket[e], h], e in [0, 2T-1) */
+int nrse_rel_bias_vec(const float* E, const int* bucket, float* bias_vec, int H, int T, int nb, void* stream);
 /* dE[bucket[d], h] += diag[h, d] (compute_bias backward). */
 int nrse_rel_bias_bwd(const float* diag, const int* bucket, float* dE, int H, int T, void* stream);
 
@@ -199,6 +204,7 @@ typedef struct {
   int batch, T, H, head_dim;
   float scale;                    /* 1/sqrt(head_dim) */
   float dropout_p; uint32_t seed;
+  const float* bias_vec;          /* [H, 2T-1] (bf16 MFMA path); bias [H, T, Tb] is the f32 path's */
 } nrse_attn_fwd_params;
 
 typedef struct {
@@ -212,6 +218,7 @@ typedef struct {
   float* diag;                         /* [H, 2T-1] f32, accumulated: sum_b gate * dS along j-i */
   int batch, T, H, head_dim;
   float scale; float dropout_p; uint32_t seed;
+  const float* bias_vec;               /* [H, 2T-1] (bf16 MFMA path) */
 } nrse_attn_bwd_params;
 
 int nrse_attn_fwd(const nrse_attn_fwd_params* p, void* stream);

@@ -25,6 +25,15 @@ __global__ void rel_bias_kernel(const float* __restrict__ E, const int* __restri
   }
 }
 
+// Toeplitz form of the same table: vec[h, e] = E[bucket[e], h], e = j - i + T - 1
+__global__ void rel_bias_vec_kernel(const float* __restrict__ E, const int* __restrict__ bucket, float* __restrict__ vec,
+                                    int H, int T) {
+  const int nd = 2 * T - 1;
+  const int h = blockIdx.y;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < nd; e += gridDim.x * blockDim.x)
+    vec[(long long)h * nd + e] = E[bucket[e] * H + h];
+}
+
 __global__ void rel_bias_bwd_kernel(const float* __restrict__ diag, const int* __restrict__ bucket,
                                     float* __restrict__ dE, int H, int T) {
   const int nd = 2 * T - 1;
@@ -427,6 +436,14 @@ extern "C" int nrse_rel_bias_fwd(const float* E, const int* bucket, float* bias,
   return nrse_check_launch("nrse_rel_bias_fwd");
 }
 
+extern "C" int nrse_rel_bias_vec(const float* E, const int* bucket, float* vec, int H, int T, int nb, void* stream) {
+  NRSE_REQUIRE(E && bucket && vec && H > 0 && T > 0 && nb > 0, "nrse_rel_bias_vec: bad args");
+  const int nd = 2 * T - 1;
+  hipLaunchKernelGGL(rel_bias_vec_kernel, dim3((nd + 255) / 256, H), dim3(256), 0, (hipStream_t)stream, E, bucket, vec,
+                     H, T);
+  return nrse_check_launch("nrse_rel_bias_vec");
+}
+
 extern "C" int nrse_rel_bias_bwd(const float* diag, const int* bucket, float* dE, int H, int T, void* stream) {
   NRSE_REQUIRE(diag && bucket && dE && H > 0 && T > 0, "nrse_rel_bias_bwd: bad args");
   const int nd = 2 * T - 1;
@@ -471,11 +488,12 @@ int nrse_attn_bwd_mfma(const nrse_attn_bwd_params* p, hipStream_t st);
 int nrse_attn_use_mfma(int dtype, int head_dim);
 
 extern "C" int nrse_attn_fwd(const nrse_attn_fwd_params* p, void* stream) {
-  NRSE_REQUIRE(p && p->qkv && p->gate && p->bias && p->ctx && p->lse && p->batch > 0 && p->T > 0 && p->H > 0,
+  NRSE_REQUIRE(p && p->qkv && p->gate && (p->bias || p->bias_vec) && p->ctx && p->lse && p->batch > 0 && p->T > 0 && p->H > 0,
                "nrse_attn_fwd: bad args");
   if (p->head_dim != HD) { nrse_set_error("nrse_attn_fwd: head_dim %d != 64", p->head_dim); return NRSE_ERR_UNSUPPORTED; }
   hipStream_t st = (hipStream_t)stream;
   if (nrse_attn_use_mfma(p->dtype, p->head_dim)) return nrse_attn_fwd_mfma(p, st);
+  NRSE_REQUIRE(p->bias, "nrse_attn_fwd: the f32 path needs the [H, T, Tb] bias table");
   dim3 grid((p->T + 63) / 64, p->H, p->batch);
   if (p->dtype == NRSE_BF16) hipLaunchKernelGGL(attn_fwd_f32_kernel<bf16_t>, grid, dim3(64), 0, st, *p);
   else hipLaunchKernelGGL(attn_fwd_f32_kernel<float>, grid, dim3(64), 0, st, *p);
@@ -483,11 +501,12 @@ extern "C" int nrse_attn_fwd(const nrse_attn_fwd_params* p, void* stream) {
 }
 
 extern "C" int nrse_attn_bwd(const nrse_attn_bwd_params* p, void* stream) {
-  NRSE_REQUIRE(p && p->qkv && p->gate && p->bias && p->ctx && p->dctx && p->lse && p->delta && p->dqkv && p->dgate &&
+  NRSE_REQUIRE(p && p->qkv && p->gate && (p->bias || p->bias_vec) && p->ctx && p->dctx && p->lse && p->delta && p->dqkv && p->dgate &&
                p->batch > 0 && p->T > 0 && p->H > 0, "nrse_attn_bwd: bad args");
   if (p->head_dim != HD) { nrse_set_error("nrse_attn_bwd: head_dim %d != 64", p->head_dim); return NRSE_ERR_UNSUPPORTED; }
   hipStream_t st = (hipStream_t)stream;
   if (nrse_attn_use_mfma(p->dtype, p->head_dim)) return nrse_attn_bwd_mfma(p, st);  // computes delta itself
+  NRSE_REQUIRE(p->bias, "nrse_attn_bwd: the f32 path needs the [H, T, Tb] bias table");
   const long long total = (long long)p->batch * p->H * p->T;
   dim3 g1((unsigned)((total + 255) / 256));
   if (p->dtype == NRSE_BF16) hipLaunchKernelGGL(attn_delta_kernel<bf16_t>, g1, dim3(256), 0, st, *p);

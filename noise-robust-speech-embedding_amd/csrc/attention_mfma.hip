@@ -26,7 +26,6 @@ namespace {
 
 constexpr int D = 64;
 constexpr int TILE_B = 64 * 128;  // bytes per 64x64 bf16 tile
-constexpr int BT_LD = 68;         // f32 bias tile row stride (dK/dV kernel)
 constexpr int DPAD = 80;          // low-side margin of the LDS diagonal arrays (dK/dV kernel)
 // Softmax runs in the base-2 domain (v_exp_f32 is 2^x): scores are formed as
 // log2(e) * (q.k / 8 + gate * bias) with the log2(e) folded into the per-row constants, so each
@@ -94,45 +93,86 @@ NRSE_DEV BlockPos block_pos(int nblk, int H) {
   return BlockPos{id % nblk, (id / nblk) % H, id / (nblk * H)};
 }
 
-// A 64-row x 64-d bf16 tile (rows row0.. of a matrix with row stride ld) moved by 256 threads,
-// two 16-byte chunks each: tile_load issues the global loads into registers (the prefetch of the
-// next tile, in flight while the current one is computed), tile_store writes them to LDS.
-struct TileRegs {
-  uint4 a, b;
+// ------------------------------------------------------------------------------ shared staging
+// K / V tiles by LDS-DMA (buffer_load ... lds): a 64-row x 128-B tile is 8 wave-instructions of
+// 1 KiB (8 rows each); 4 waves issue 2 each. Lane l of instruction j of wave w writes LDS bytes
+// (2w+j)*1024 + 16 l = row (2w+j)*8 + l/8, 16-B position l%8, which in the swizzled image holds
+// logical chunk (l%8) ^ sw(row): the swizzle goes into the per-lane SOURCE address. Rows past the
+// utterance (>= T) are out of the descriptor's range and land as zeros.
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+struct KvDma {
+  __amdgpu_buffer_rsrc_t rs;
+  unsigned voff[2];  // row offset (tile row 0) + column offset of this lane's piece, per instruction
+  unsigned ld_b;     // row stride in bytes
 };
-NRSE_DEV TileRegs tile_load(const bf16_t* base, long long ld, int row0, int nrows, int tid) {
-  const int row = tid >> 2;
-  const int c0 = (tid & 3) * 2;
-  TileRegs r{make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
-  if (row0 + row < nrows) {
-    const bf16_t* src = base + (long long)(row0 + row) * ld + c0 * 8;
-    r.a = *reinterpret_cast<const uint4*>(src);
-    r.b = *reinterpret_cast<const uint4*>(src + 8);
+
+// col_b: byte offset of the 64-wide column block inside a row
+NRSE_DEV KvDma kv_dma_init(const bf16_t* utt_base, int T, long long ld, int col_b, int wave, int lane) {
+  KvDma d;
+  d.ld_b = (unsigned)(ld * 2);
+  d.rs = __builtin_amdgcn_make_buffer_rsrc((void*)utt_base, 0, (int)((long long)T * ld * 2), 0x00020000);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = (wave * 2 + j) * 8 + (lane >> 3);
+    const int chunk = (lane & 7) ^ (((row >> 1) & 3) << 1);
+    d.voff[j] = (unsigned)row * d.ld_b + (unsigned)col_b + (unsigned)chunk * 16;
   }
-  return r;
+  return d;
 }
-NRSE_DEV void tile_store(char* t, const TileRegs& r, int tid) {
-  const int row = tid >> 2;
-  const int c0 = (tid & 3) * 2;
-  *reinterpret_cast<uint4*>(t + loff(row, c0)) = r.a;
-  *reinterpret_cast<uint4*>(t + loff(row, c0 + 1)) = r.b;
+
+// stage rows row0 .. row0+63 into the tile at `tile` (wave-uniform LDS address)
+NRSE_DEV void kv_dma_issue(const KvDma& d, char* tile, int row0, int wave) {
+  const unsigned roff = (unsigned)row0 * d.ld_b;
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(d.rs, (lds_void_t*)(tile + (wave * 2 + j) * 1024), 16, d.voff[j] + roff,
+                                             0, 0, 0);
+}
+
+// The relative-position bias of a query block (64 queries from q0) over all keys, as 4 shifted
+// copies of the Toeplitz vector segment it touches: copy s holds vec[e_lo + j + s], e_lo =
+// T - 1 - q0 - 63 (values outside [0, 2T-1) are zero). A lane whose 4 consecutive elements start
+// at segment index u reads them with one aligned ds_read_b128 from copy (u & 3) at u - (u & 3).
+constexpr int BV_EXTRA = 136;  // 64 (last query offset) + 64 (padded key tile) + 8
+NRSE_DEV int bv_len(int T) { return ((T + BV_EXTRA) + 3) & ~3; }
+NRSE_DEV void bv_stage(float* bv, const float* vec, int T, int q0, int tid) {
+  const int len = bv_len(T), nd = 2 * T - 1;
+  const int e_lo = T - 1 - q0 - 63;
+  for (int j = tid; j < len; j += 256) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int e = e_lo + j + s;
+      bv[s * len + j] = (e >= 0 && e < nd) ? vec[e] : 0.f;
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------ forward
+// One workgroup = 64 queries (4 waves x 16) of one (b, h); K/V tiles double-buffered in LDS by
+// LDS-DMA, the next tile in flight while the current one is computed (one barrier per tile);
+// the gated bias gate[b,h,i] * vec[h, j-i+T-1] from the LDS Toeplitz copies.
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_params p) {
-  __shared__ __attribute__((aligned(16))) char lds[2 * TILE_B];
-  char* Kt = lds;
-  char* Vt = lds + TILE_B;
+  extern __shared__ __attribute__((aligned(16))) char dyn[];
+  char* const kv0 = dyn;                       // [2 buffers][K tile, V tile]
+  float* const bv = reinterpret_cast<float*>(dyn + 4 * TILE_B);
   const int T = p.T, H = p.H, Hd = H * D;
   const long long ld3 = 3LL * Hd;
   const BlockPos bp = block_pos((p.T + 63) / 64, p.H);
   const int b = bp.b, h = bp.h;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, i16 = lane & 15;
-  const int qi = bp.blk * 64 + w * 16 + i16;
+  const int q0 = bp.blk * 64;
+  const int qi = q0 + w * 16 + i16;
   const bool qv = qi < T;
-  const int Tb = (T + 63) & ~63;
   const bf16_t* qkv = (const bf16_t*)p.qkv + (long long)b * T * ld3;
+  const KvDma kd = kv_dma_init(qkv, T, ld3, (Hd + h * D) * 2, w, lane);
+  const KvDma vd = kv_dma_init(qkv, T, ld3, (2 * Hd + h * D) * 2, w, lane);
+  const int ntiles = (T + 63) / 64;
+  kv_dma_issue(kd, kv0, 0, w);
+  kv_dma_issue(vd, kv0 + TILE_B, 0, w);
+  bv_stage(bv, p.bias_vec + (long long)h * (2 * T - 1), T, q0, tid);
   // Q fragments (B operand of S^T = K Q^T): Q[qi][8g + 32s .. +8]
   bf16x8 qf[2];
 #pragma unroll
@@ -144,7 +184,11 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
   const long long bh = (long long)b * H + h;
   const float gi = qv ? p.gate[bh * T + qi] : 0.f;
   const float c1 = p.scale * LOG2E, gl = gi * LOG2E;
-  const float* brow = p.bias + ((long long)h * T + (qv ? qi : T - 1)) * Tb;
+  // bias copy and base for this lane: segment index u0 = kb + 4g + 63 - (qi - q0)
+  const int bvl = bv_len(T);
+  const int u00 = 4 * g + 63 - (w * 16 + i16);
+  const int bsel = u00 & 3;
+  const float* bvl_base = bv + bsel * bvl + (u00 - bsel);
   const uint32_t key = site_key(p.seed);
   const uint32_t thr = dropout_threshold(p.dropout_p);
   const bool drop = p.dropout_p > 0.f;
@@ -155,13 +199,20 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // (no register prefetch here: at 95 VGPRs the kernel runs 5 waves per SIMD, which hides the
-  // staging latency better than a prefetch that costs a wave)
-  for (int kb = 0; kb < T; kb += 64) {
-    __syncthreads();
-    tile_store(Kt, tile_load(qkv + Hd + h * D, ld3, kb, T, tid), tid);
-    tile_store(Vt, tile_load(qkv + 2 * Hd + h * D, ld3, kb, T, tid), tid);
-    __syncthreads();
+  for (int it = 0; it < ntiles; ++it) {
+    const int kb = it * 64;
+    char* const Kt = kv0 + (it & 1) * 2 * TILE_B;
+    char* const Vt = Kt + TILE_B;
+    // tile `it` landed (the only DMAs in flight) and, on the first tile, the bias copies written
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    // prefetch tile it+1 into the other buffer (its last readers finished before this barrier)
+    if (it + 1 < ntiles) {
+      char* const Kn = kv0 + ((it + 1) & 1) * 2 * TILE_B;
+      kv_dma_issue(kd, Kn, kb + 64, w);
+      kv_dma_issue(vd, Kn + TILE_B, kb + 64, w);
+    }
     f32x4 s[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -169,16 +220,14 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss) s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rd_row(Kt, 16 * t + i16, 4 * ss + g), qf[ss], s[t], 0, 0, 0);
     }
-    // Wave-uniform branches keep the per-element work straight-line: the key mask only on the
-    // last (partial) tile, the dropout hash only when dropout is on (its 1/(1-p) scale is folded
-    // into the final 1/l).
     float v[4][4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const float4 bv = *reinterpret_cast<const float4*>(brow + kb + 16 * t + 4 * g);
-      const float bb[4] = {bv.x, bv.y, bv.z, bv.w};
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[t][r] = fmaf(s[t][r], c1, gl * bb[r]);
+      const float4 bb = *reinterpret_cast<const float4*>(bvl_base + kb + 16 * t);
+      v[t][0] = fmaf(s[t][0], c1, gl * bb.x);
+      v[t][1] = fmaf(s[t][1], c1, gl * bb.y);
+      v[t][2] = fmaf(s[t][2], c1, gl * bb.z);
+      v[t][3] = fmaf(s[t][3], c1, gl * bb.w);
     }
     if (kb + 64 > T) {
 #pragma unroll
@@ -228,7 +277,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
   float l = lpart + __shfl_xor(lpart, 16, 64);
   l += __shfl_xor(l, 32, 64);
   bf16_t* ctx = (bf16_t*)p.ctx;
-  const int qrow0 = bp.blk * 64 + w * 16;
+  const int qrow0 = q0 + w * 16;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const float lr = __shfl(l, 4 * g + r, 64);
@@ -244,20 +293,27 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
 
 // ------------------------------------------------------------------------------ bwd: dQ, dgate
 __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_params p) {
-  __shared__ __attribute__((aligned(16))) char lds[2 * TILE_B];
-  char* Kt = lds;
-  char* Vt = lds + TILE_B;
+  extern __shared__ __attribute__((aligned(16))) char dyn[];
+  char* const kv0 = dyn;  // [2 buffers][K tile, V tile], LDS-DMA double buffer as in the forward
+  float* const bv = reinterpret_cast<float*>(dyn + 4 * TILE_B);
   const int T = p.T, H = p.H, Hd = H * D;
   const long long ld3 = 3LL * Hd;
   const BlockPos bp = block_pos((p.T + 63) / 64, p.H);
   const int b = bp.b, h = bp.h;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, i16 = lane & 15;
-  const int qi = bp.blk * 64 + w * 16 + i16;
+  const int q0 = bp.blk * 64;
+  const int qi = q0 + w * 16 + i16;
   const bool qv = qi < T;
-  const int Tb = (T + 63) & ~63;
   const bf16_t* qkv = (const bf16_t*)p.qkv + (long long)b * T * ld3;
   const bf16_t* dctx = (const bf16_t*)p.dctx + (long long)b * T * Hd;
+  const KvDma kd = kv_dma_init(qkv, T, ld3, (Hd + h * D) * 2, w, lane);
+  const KvDma vd = kv_dma_init(qkv, T, ld3, (2 * Hd + h * D) * 2, w, lane);
+  const int ntiles = (T + 63) / 64;
+  kv_dma_issue(kd, kv0, 0, w);
+  kv_dma_issue(vd, kv0 + TILE_B, 0, w);
+  bv_stage(bv, p.bias_vec + (long long)h * (2 * T - 1), T, q0, tid);
   bf16x8 qf[2], dof[2];
   const bf16_t* octx = (const bf16_t*)p.ctx + (long long)b * T * Hd;
   float dsum = 0.f;  // delta = rowsum(dO * O) for this lane's 16 of the 64 dims
@@ -286,7 +342,10 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
   const float lse2 = lse * LOG2E;
   const float delta = dsum;
   if (g == 0 && qv) p.delta[bh * T + qi] = delta;  // consumed by attn_bwd_kv_kernel (launched after)
-  const float* brow = p.bias + ((long long)h * T + (qv ? qi : T - 1)) * Tb;
+  const int bvl = bv_len(T);
+  const int u00 = 4 * g + 63 - (w * 16 + i16);
+  const int bsel = u00 & 3;
+  const float* bvl_base = bv + bsel * bvl + (u00 - bsel);
   const uint32_t key = site_key(p.seed);
   const uint32_t thr = dropout_threshold(p.dropout_p);
   const bool drop = p.dropout_p > 0.f;
@@ -296,16 +355,17 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
   f32x4 dq[4];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  TileRegs kn = tile_load(qkv + Hd + h * D, ld3, 0, T, tid);
-  TileRegs vn = tile_load(qkv + 2 * Hd + h * D, ld3, 0, T, tid);
-  for (int kb = 0; kb < T; kb += 64) {
-    __syncthreads();
-    tile_store(Kt, kn, tid);
-    tile_store(Vt, vn, tid);
-    __syncthreads();
-    if (kb + 64 < T) {
-      kn = tile_load(qkv + Hd + h * D, ld3, kb + 64, T, tid);
-      vn = tile_load(qkv + 2 * Hd + h * D, ld3, kb + 64, T, tid);
+  for (int it = 0; it < ntiles; ++it) {
+    const int kb = it * 64;
+    char* const Kt = kv0 + (it & 1) * 2 * TILE_B;
+    char* const Vt = Kt + TILE_B;
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (it + 1 < ntiles) {
+      char* const Kn = kv0 + ((it + 1) & 1) * 2 * TILE_B;
+      kv_dma_issue(kd, Kn, kb + 64, w);
+      kv_dma_issue(vd, Kn + TILE_B, kb + 64, w);
     }
     f32x4 s[4], dp[4];
 #pragma unroll
@@ -324,8 +384,8 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
     float ds[4][4], bb[4][4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const float4 bv = *reinterpret_cast<const float4*>(brow + kb + 16 * t + 4 * g);
-      bb[t][0] = bv.x; bb[t][1] = bv.y; bb[t][2] = bv.z; bb[t][3] = bv.w;
+      const float4 v4 = *reinterpret_cast<const float4*>(bvl_base + kb + 16 * t);
+      bb[t][0] = v4.x; bb[t][1] = v4.y; bb[t][2] = v4.z; bb[t][3] = v4.w;
     }
     if (drop) {
 #pragma unroll
@@ -361,7 +421,7 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
   dgate += __shfl_xor(dgate, 32, 64);
   if (g == 0 && qv) p.dgate[bh * T + qi] = dgate;
   bf16_t* dqkv = (bf16_t*)p.dqkv + (long long)b * T * ld3;
-  const int qrow0 = bp.blk * 64 + w * 16;
+  const int qrow0 = q0 + w * 16;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int q = qrow0 + 4 * g + r;
@@ -375,24 +435,51 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
 // ------------------------------------------------------------------------------ bwd: dK, dV, diag
 __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(const nrse_attn_bwd_params p) {
   extern __shared__ __attribute__((aligned(16))) char dyn[];
-  char* Qt = dyn;
-  char* Ot = dyn + TILE_B;
-  float* rowc = reinterpret_cast<float*>(dyn + 2 * TILE_B);  // lse[64], delta[64], gate[64]
-  float* btile = rowc + 192;                                 // bias tile [64 q][BT_LD]
-  float* diag = btile + 64 * BT_LD;                          // [4 lane groups][T + 64]
+  char* const qo0 = dyn;  // [2 buffers][Q tile, dO tile], LDS-DMA double buffer
   const int T = p.T, H = p.H, Hd = H * D;
+  const int Tp = (T + 63) & ~63;
+  float* const rowall = reinterpret_cast<float*>(dyn + 4 * TILE_B);  // lse*log2e [Tp], delta [Tp], gate [Tp]
+  float* const rbv = rowall + 3 * Tp;                                 // 4 reversed bias copies
+  const int bvl = bv_len(T);
+  float* const diag = rbv + 4 * bvl;                                  // [4 lane groups][T + 64 + DPAD]
   const long long ld3 = 3LL * Hd;
   const BlockPos bp = block_pos((p.T + 63) / 64, p.H);
   const int b = bp.b, h = bp.h;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, i16 = lane & 15;
   const int kb0 = bp.blk * 64;
   const int kj = kb0 + w * 16 + i16;
   const bool kv = kj < T;
   const float kvf = kv ? 1.f : 0.f;
-  const int Tb = (T + 63) & ~63;
   const bf16_t* qkv = (const bf16_t*)p.qkv + (long long)b * T * ld3;
   const bf16_t* dctx = (const bf16_t*)p.dctx + (long long)b * T * Hd;
+  const KvDma qd = kv_dma_init(qkv, T, ld3, h * D * 2, w, lane);
+  const KvDma od = kv_dma_init(dctx, T, Hd, h * D * 2, w, lane);
+  const int ntiles = (T + 63) / 64;
+  kv_dma_issue(qd, qo0, 0, w);
+  kv_dma_issue(od, qo0 + TILE_B, 0, w);
+  const long long bh = (long long)b * H + h;
+  for (int q = tid; q < Tp; q += 256) {
+    const bool ok = q < T;
+    rowall[q] = ok ? p.lse[bh * T + q] * LOG2E : 0.f;
+    rowall[Tp + q] = ok ? p.delta[bh * T + q] : 0.f;
+    rowall[2 * Tp + q] = ok ? p.gate[bh * T + q] : 0.f;
+  }
+  // bias of (query q, key kj) = vec[kj - q + T - 1]: reversed copies, copy s index j holds
+  // log2e * vec[e_hi - j - s], e_hi = kb0 + 63 + T - 1; element (q, kj) sits at segment index
+  // u = 63 - kl + q, so a lane's 4 consecutive queries are one aligned float4 of copy (u & 3).
+  {
+    const float* vec = p.bias_vec + (long long)h * (2 * T - 1);
+    const int nd = 2 * T - 1, e_hi = kb0 + 63 + T - 1;
+    for (int j = tid; j < bvl; j += 256) {
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const int e = e_hi - j - s4;
+        rbv[s4 * bvl + j] = (e >= 0 && e < nd) ? vec[e] * LOG2E : 0.f;
+      }
+    }
+  }
   bf16x8 kf[2], vf[2];
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
@@ -417,66 +504,32 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(const nrse_attn_bwd_pa
   // rotation by r wraps for lanes i16 >= 16 - r
   const float whi[3] = {i16 >= 15 ? 1.f : 0.f, i16 >= 14 ? 1.f : 0.f, i16 >= 13 ? 1.f : 0.f};
   const float wlo[3] = {1.f - whi[0], 1.f - whi[1], 1.f - whi[2]};
-  const long long bh = (long long)b * H + h;
   const uint32_t key = site_key(p.seed);
   const float c1 = p.scale * LOG2E;
   const uint32_t thr = dropout_threshold(p.dropout_p);
   const bool drop = p.dropout_p > 0.f;
   const float dsc = drop ? 1.f / (1.f - p.dropout_p) : 1.f;
-  const float* bsrc = p.bias + (long long)h * T * Tb + kb0;
   const int kl = w * 16 + i16;  // key within the 64-key block
+  const int u00 = 63 - kl + 4 * g;
+  const int bsel = u00 & 3;
+  const float* rb_base = rbv + bsel * bvl + (u00 - bsel);
   f32x4 dk[4], dv[4];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) dk[dt] = dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
   // LDS index of diagonal kj - qi: (kj - qi) - (kb0 - T + 1) + DPAD
   const int dbase = kb0 - T + 1 - DPAD;
-  // next query block in registers: Q and dO tiles, lse/delta/gate, bias[h, qb:qb+64, kb0:kb0+64]
-  TileRegs qn, on;
-  float4 bn[4];
-  float rn[3];
-  auto prefetch = [&](int qb) {
-    qn = tile_load(qkv + h * D, ld3, qb, T, tid);
-    on = tile_load(dctx + h * D, Hd, qb, T, tid);
-    if (tid < 64) {
-      const int q = qb + tid;
-      const bool ok = q < T;
-      rn[0] = ok ? p.lse[bh * T + q] * LOG2E : 0.f;
-      rn[1] = ok ? p.delta[bh * T + q] : 0.f;
-      rn[2] = ok ? p.gate[bh * T + q] : 0.f;
+  for (int it = 0; it < ntiles; ++it) {
+    const int qb = it * 64;
+    char* const Qt = qo0 + (it & 1) * 2 * TILE_B;
+    char* const Ot = Qt + TILE_B;
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (it + 1 < ntiles) {
+      char* const Qn = qo0 + ((it + 1) & 1) * 2 * TILE_B;
+      kv_dma_issue(qd, Qn, qb + 64, w);
+      kv_dma_issue(od, Qn + TILE_B, qb + 64, w);
     }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = tid + 256 * u;
-      const int row = e >> 4, c4 = (e & 15) * 4;
-      bn[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (qb + row < T) bn[u] = *reinterpret_cast<const float4*>(bsrc + (long long)(qb + row) * Tb + c4);
-    }
-  };
-  prefetch(0);
-  for (int qb = 0; qb < T; qb += 64) {
-    __syncthreads();
-#if NRSE_ATT_ABLATE == 3
-    if (qb == 0) {
-#endif
-    tile_store(Qt, qn, tid);
-    tile_store(Ot, on, tid);
-    if (tid < 64) {
-      rowc[tid] = rn[0];
-      rowc[64 + tid] = rn[1];
-      rowc[128 + tid] = rn[2];
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = tid + 256 * u;
-      const int row = e >> 4, c4 = (e & 15) * 4;
-      *reinterpret_cast<float4*>(btile + row * BT_LD + c4) =
-          make_float4(bn[u].x * LOG2E, bn[u].y * LOG2E, bn[u].z * LOG2E, bn[u].w * LOG2E);
-    }
-#if NRSE_ATT_ABLATE == 3
-    }
-#endif
-    __syncthreads();
-    if (qb + 64 < T) prefetch(qb + 64);
     f32x4 s[4], dp[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -490,17 +543,21 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(const nrse_attn_bwd_pa
     }
     // element (query qb + 16t + 4g + r, key kj). Straight-line per element; the dropout hash
     // behind one wave-uniform branch, its 1/(1-p) on P folded into the final dV scale. Rows of
-    // invalid queries contribute zero by construction (zero Q, dO, lse, delta, gate, bias rows);
+    // invalid queries contribute zero by construction (zero Q, dO, lse, delta, gate rows);
     // lanes of invalid keys produce dK/dV rows that are never stored, and kvf keeps them out of
     // the diagonal sums.
     float pd[4][4], ds[4][4], gv[4][4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int ql = 16 * t + 4 * g + r;
-        ds[t][r] = exp2_(fmaf(s[t][r], c1, rowc[128 + ql] * btile[ql * BT_LD + kl]) - rowc[ql]);  // P (log2 domain)
-      }
+    for (int t = 0; t < 4; ++t) {
+      const int ql = qb + 16 * t + 4 * g;
+      const float4 l4 = *reinterpret_cast<const float4*>(rowall + ql);
+      const float4 g4 = *reinterpret_cast<const float4*>(rowall + 2 * Tp + ql);
+      const float4 b4 = *reinterpret_cast<const float4*>(rb_base + qb + 16 * t);
+      ds[t][0] = exp2_(fmaf(s[t][0], c1, g4.x * b4.x) - l4.x);  // P (log2 domain)
+      ds[t][1] = exp2_(fmaf(s[t][1], c1, g4.y * b4.y) - l4.y);
+      ds[t][2] = exp2_(fmaf(s[t][2], c1, g4.z * b4.z) - l4.z);
+      ds[t][3] = exp2_(fmaf(s[t][3], c1, g4.w * b4.w) - l4.w);
+    }
 #if NRSE_ATT_ABLATE != 2
     if (drop) {
 #pragma unroll
@@ -520,13 +577,15 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(const nrse_attn_bwd_pa
         for (int r = 0; r < 4; ++r) pd[t][r] = ds[t][r];
     }
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int ql = 16 * t + 4 * g + r;
-        ds[t][r] *= dp[t][r] - rowc[64 + ql];
-        gv[t][r] = ds[t][r] * (rowc[128 + ql] * kvf);
-      }
+    for (int t = 0; t < 4; ++t) {
+      const int ql = qb + 16 * t + 4 * g;
+      const float4 d4 = *reinterpret_cast<const float4*>(rowall + Tp + ql);
+      const float4 g4 = *reinterpret_cast<const float4*>(rowall + 2 * Tp + ql);
+      ds[t][0] *= dp[t][0] - d4.x; gv[t][0] = ds[t][0] * (g4.x * kvf);
+      ds[t][1] *= dp[t][1] - d4.y; gv[t][1] = ds[t][1] * (g4.y * kvf);
+      ds[t][2] *= dp[t][2] - d4.z; gv[t][2] = ds[t][2] * (g4.z * kvf);
+      ds[t][3] *= dp[t][3] - d4.w; gv[t][3] = ds[t][3] * (g4.w * kvf);
+    }
 #if NRSE_ATT_ABLATE != 1
     if (p.diag) {
 #pragma unroll
@@ -588,20 +647,36 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(const nrse_attn_bwd_pa
 int nrse_attn_use_mfma(int dtype, int head_dim) { return dtype == NRSE_BF16 && head_dim == D; }
 
 int nrse_attn_fwd_mfma(const nrse_attn_fwd_params* p, hipStream_t st) {
+  if (!p->bias_vec) {
+    nrse_set_error("nrse_attn_fwd: the bf16 MFMA path needs bias_vec (nrse_rel_bias_vec)");
+    return NRSE_ERR_ARG;
+  }
   const dim3 grid((unsigned)((p->T + 63) / 64 * p->H * p->batch));
-  hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), 0, st, *p);
+  const size_t lds = 4 * TILE_B + 4 * (size_t)((p->T + BV_EXTRA + 3) & ~3) * sizeof(float);
+  if (lds > 160 * 1024) {
+    nrse_set_error("nrse_attn_fwd: T=%d too long for the LDS bias copies", p->T);
+    return NRSE_ERR_UNSUPPORTED;
+  }
+  hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), lds, st, *p);
   return nrse_check_launch("nrse_attn_fwd(mfma)");
 }
 
 int nrse_attn_bwd_mfma(const nrse_attn_bwd_params* p, hipStream_t st) {
+  if (!p->bias_vec) {
+    nrse_set_error("nrse_attn_bwd: the bf16 MFMA path needs bias_vec (nrse_rel_bias_vec)");
+    return NRSE_ERR_ARG;
+  }
   const dim3 grid((unsigned)((p->T + 63) / 64 * p->H * p->batch));
-  const size_t lds_kv = 2 * TILE_B + (192 + 64 * BT_LD + 4 * (p->T + 64 + DPAD)) * sizeof(float);
+  const size_t bvl = (size_t)((p->T + BV_EXTRA + 3) & ~3);
+  const size_t lds_q = 4 * TILE_B + 4 * bvl * sizeof(float);
+  const size_t lds_kv =
+      4 * TILE_B + (3 * (size_t)((p->T + 63) & ~63) + 4 * bvl + 4 * (size_t)(p->T + 64 + DPAD)) * sizeof(float);
   if (lds_kv > 160 * 1024) {
-    nrse_set_error("nrse_attn_bwd: T=%d too long for the LDS diagonal accumulator", p->T);
+    nrse_set_error("nrse_attn_bwd: T=%d too long for the LDS bias copies / diagonal accumulator", p->T);
     return NRSE_ERR_UNSUPPORTED;
   }
   // the dQ kernel also produces delta = rowsum(dO * O), which the dK/dV kernel reads
-  hipLaunchKernelGGL(attn_bwd_q_kernel, grid, dim3(256), 0, st, *p);
+  hipLaunchKernelGGL(attn_bwd_q_kernel, grid, dim3(256), lds_q, st, *p);
   hipLaunchKernelGGL(attn_bwd_kv_kernel, grid, dim3(256), lds_kv, st, *p);
   return nrse_check_launch("nrse_attn_bwd(mfma)");
 }

@@ -78,14 +78,14 @@ class LnBwdParams(ctypes.Structure):
 class AttnFwdParams(ctypes.Structure):
     _fields_ = [("qkv", c_vp), ("dtype", c_int), ("gate", c_vp), ("bias", c_vp), ("ctx", c_vp), ("lse", c_vp),
                 ("batch", c_int), ("T", c_int), ("H", c_int), ("head_dim", c_int), ("scale", c_f),
-                ("dropout_p", c_f), ("seed", c_u32)]
+                ("dropout_p", c_f), ("seed", c_u32), ("bias_vec", c_vp)]
 
 
 class AttnBwdParams(ctypes.Structure):
     _fields_ = [("qkv", c_vp), ("dtype", c_int), ("gate", c_vp), ("bias", c_vp), ("ctx", c_vp), ("dctx", c_vp),
                 ("lse", c_vp), ("delta", c_vp), ("dqkv", c_vp), ("dgate", c_vp), ("diag", c_vp),
                 ("batch", c_int), ("T", c_int), ("H", c_int), ("head_dim", c_int), ("scale", c_f),
-                ("dropout_p", c_f), ("seed", c_u32)]
+                ("dropout_p", c_f), ("seed", c_u32), ("bias_vec", c_vp)]
 
 
 class Conv0Params(ctypes.Structure):
@@ -116,6 +116,7 @@ _SIGNATURES = {
     "nrse_ln_mean_fwd": ([c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_f, c_vp], c_int),
     "nrse_bias_ld": ([c_int], c_int),
     "nrse_rel_bias_fwd": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp], c_int),
+    "nrse_rel_bias_vec": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp], c_int),
     "nrse_rel_bias_bwd": ([c_vp, c_vp, c_vp, c_int, c_int, c_vp], c_int),
     "nrse_gate_fwd": ([c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp], c_int),
     "nrse_gate_bwd": ([c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp],

@@ -70,6 +70,7 @@ class Tape:
     pos_pre: torch.Tensor | None = None
     pos: dict | None = None
     bias_tab: torch.Tensor | None = None
+    bias_vec: torch.Tensor | None = None
     layers: list = field(default_factory=list)
     final: tuple | None = None
     fseed: int = 0
@@ -261,12 +262,21 @@ class ByolEngine:
                resid=h, ldr=H, r_z1=T * H, r_z2=cpg, dropout_p=php, seed=R.site_seed(fseed, R.SITE_POS))
         # -------- relative position bias table (layer 0 computes it, every layer reuses it)
         nh = a.heads
-        bias_tab = torch.empty(nh, T, K.bias_ld(T), device=dev, dtype=F32)
-        K.rel_bias_fwd(Pm["encoder.layers.0.attention.rel_attn_embed.weight"], self.buckets(T), bias_tab, nh, T)
+        # bf16 (MFMA) attention reads the Toeplitz vector [nh, 2T-1] (the bias depends on j - i
+        # only); the f32 parity kernels read the [nh, T, Tb] table
+        E_rel = Pm["encoder.layers.0.attention.rel_attn_embed.weight"]
+        if cdt == torch.bfloat16:
+            bias_tab = None
+            bias_vec = torch.empty(nh, 2 * T - 1, device=dev, dtype=F32)
+            K.rel_bias_vec(E_rel, self.buckets(T), bias_vec, nh, T)
+        else:
+            bias_vec = None
+            bias_tab = torch.empty(nh, T, K.bias_ld(T), device=dev, dtype=F32)
+            K.rel_bias_fwd(E_rel, self.buckets(T), bias_tab, nh, T)
         if need_grad:
             tape.T = T
             tape.feats, tape.fp_mean, tape.fp_rstd, tape.xn = feats, fm, fr, xn
-            tape.mask, tape.hpad, tape.pos_pre, tape.bias_tab = mask, hpad, pos_pre, bias_tab
+            tape.mask, tape.hpad, tape.pos_pre, tape.bias_tab, tape.bias_vec = mask, hpad, pos_pre, bias_tab, bias_vec
             tape.pos = dict(W=W)
         del xn, feats
         # -------- transformer layers ([TF]modeling_wavlm.py:488-513, 355-373)
@@ -292,7 +302,8 @@ class ByolEngine:
                        Pm[at + "gru_rel_pos_const"], gate, B, T, nh)
             ctx = torch.empty(BT, H, device=dev, dtype=cdt)
             lse = torch.empty(B, nh, T, device=dev, dtype=F32)
-            K.attn_fwd(qkv, gate, bias_tab, ctx, lse, B, T, nh, pat, R.site_seed(fseed, R.site_attn_probs(li)))
+            K.attn_fwd(qkv, gate, bias_tab, ctx, lse, B, T, nh, pat, R.site_seed(fseed, R.site_attn_probs(li)),
+                       bias_vec=bias_vec)
             hmid = torch.empty(BT, H, device=dev, dtype=F32)
             K.linear_fwd(ctx, Ps[at + "out_proj.weight"], hmid, bias=Pm[at + "out_proj.bias"], resid=hcur, ldr=H,
                          dropout_p=php, seed=R.site_seed(fseed, R.site_attn_out(li)))
@@ -388,7 +399,7 @@ class ByolEngine:
             dqkv = torch.empty(BT, 3 * H, device=dev, dtype=cdt)
             dgate = torch.empty(B, nh, T, device=dev, dtype=F32)
             K.attn_bwd(L_["qkv"], L_["gate"], tape.bias_tab, L_["ctx"], dctx, L_["lse"], delta, dqkv, dgate, diag, B,
-                       T, nh, pat, R.site_seed(fseed, R.site_attn_probs(li)))
+                       T, nh, pat, R.site_seed(fseed, R.site_attn_probs(li)), bias_vec=tape.bias_vec)
             del dctx
             with self._wgrad_stream(main, dqkv, L_["x1"]):
                 K.linear_wgrad(dqkv, L_["x1"], self.fused(self.grad_flat_for(Gv), li, "qkv_w"))

@@ -303,6 +303,12 @@ def rel_bias_fwd(E, bucket, bias, H, T):
     _call("nrse_rel_bias_fwd", ptr(E), ptr(bucket), ptr(bias), H, T, E.shape[0], stream_ptr())
 
 
+def rel_bias_vec(E, bucket, vec, H, T):
+    """Toeplitz form of the rel-pos bias: vec [H, 2T-1], vec[h, j-i+T-1] = E[bucket(j-i), h]."""
+    assert vec.shape == (H, 2 * T - 1) and vec.is_contiguous()
+    _call("nrse_rel_bias_vec", ptr(E), ptr(bucket), ptr(vec), H, T, E.shape[0], stream_ptr())
+
+
 def rel_bias_bwd(diag, bucket, dE, H, T):
     _call("nrse_rel_bias_bwd", ptr(diag), ptr(bucket), ptr(dE), H, T, stream_ptr())
 
@@ -318,15 +324,18 @@ def gate_bwd(x1, W, b, c, dgate, dx1, dW, db, dc, batch, T, H):
           ptr(dc), batch, T, H, stream_ptr())
 
 
-def attn_fwd(qkv, gate, bias, ctx, lse, batch, T, H, dropout_p=0.0, seed=0):
+def attn_fwd(qkv, gate, bias, ctx, lse, batch, T, H, dropout_p=0.0, seed=0, bias_vec=None):
+    """bias: [H, T, Tb] table (f32 parity path), bias_vec: [H, 2T-1] Toeplitz vector (bf16 path)."""
     p = AttnFwdParams(ptr(qkv), dtype_code(qkv), ptr(gate), ptr(bias), ptr(ctx), ptr(lse), batch, T, H, 64,
-                      0.125, dropout_p, seed & 0xFFFFFFFF)
+                      0.125, dropout_p, seed & 0xFFFFFFFF, ptr(bias_vec))
     _call("nrse_attn_fwd", ctypes.byref(p), stream_ptr())
 
 
-def attn_bwd(qkv, gate, bias, ctx, dctx, lse, delta, dqkv, dgate, diag, batch, T, H, dropout_p=0.0, seed=0):
+def attn_bwd(qkv, gate, bias, ctx, dctx, lse, delta, dqkv, dgate, diag, batch, T, H, dropout_p=0.0, seed=0,
+             bias_vec=None):
     p = AttnBwdParams(ptr(qkv), dtype_code(qkv), ptr(gate), ptr(bias), ptr(ctx), ptr(dctx), ptr(lse), ptr(delta),
-                      ptr(dqkv), ptr(dgate), ptr(diag), batch, T, H, 64, 0.125, dropout_p, seed & 0xFFFFFFFF)
+                      ptr(dqkv), ptr(dgate), ptr(diag), batch, T, H, 64, 0.125, dropout_p, seed & 0xFFFFFFFF,
+                      ptr(bias_vec))
     _call("nrse_attn_bwd", ctypes.byref(p), stream_ptr())
 
 

@@ -9,7 +9,8 @@ dev = "cuda"
 B, T, H = 32, 399, 16
 qkv = (torch.randn(B * T, 3 * H * 64, device=dev) * 0.5).bfloat16()
 gate = torch.rand(B, H, T, device=dev) + 1
-bias = torch.randn(H, T, K.bias_ld(T), device=dev)
+bias = None
+bvec = torch.randn(H, 2 * T - 1, device=dev)
 ctx = torch.empty(B * T, H * 64, device=dev, dtype=torch.bfloat16)
 lse = torch.empty(B, H, T, device=dev)
 dctx = torch.randn_like(ctx)
@@ -29,8 +30,8 @@ def timeit(fn, iters=20):
     return s.elapsed_time(e) / iters
 
 for p in (0.0, 0.1):
-    tf = timeit(lambda: K.attn_fwd(qkv, gate, bias, ctx, lse, B, T, H, p, 1))
-    tb = timeit(lambda: K.attn_bwd(qkv, gate, bias, ctx, dctx, lse, delta, dqkv, dgate, diag, B, T, H, p, 1))
-    tbn = timeit(lambda: K.attn_bwd(qkv, gate, bias, ctx, dctx, lse, delta, dqkv, dgate, None, B, T, H, p, 1))
+    tf = timeit(lambda: K.attn_fwd(qkv, gate, bias, ctx, lse, B, T, H, p, 1, bias_vec=bvec))
+    tb = timeit(lambda: K.attn_bwd(qkv, gate, bias, ctx, dctx, lse, delta, dqkv, dgate, diag, B, T, H, p, 1, bias_vec=bvec))
+    tbn = timeit(lambda: K.attn_bwd(qkv, gate, bias, ctx, dctx, lse, delta, dqkv, dgate, None, B, T, H, p, 1, bias_vec=bvec))
     fl = 4.0 * B * H * T * T * 64
     print(f"p={p}: fwd {tf*1e3:.1f}us ({fl/tf/1e9:.0f} TF) | bwd {tb*1e3:.1f}us ({2.5*fl/tb/1e9:.0f} TF) | bwd no-diag {tbn*1e3:.1f}us", flush=True)
