@@ -157,6 +157,10 @@ typedef struct {
   const float* resid;                    /* optional f32 [rows, C] added to dx */
   float* dgamma; float* dbeta;
   long long rows; int C; int flags;
+  /* optional fused consumer of dx (the residual branch's dropout backward, replacing a separate
+   * nrse_dropout_cast_colsum pass over dx): dv = dropout(dx; dv_p, dv_seed) in dv_dtype,
+   * dv_colsum[c] += sum_r dv[r, c] (if dv_colsum) */
+  void* dv; int dv_dtype; float* dv_colsum; float dv_p; uint32_t dv_seed;
 } nrse_ln_bwd_params;
 
 int nrse_layernorm_fwd(const nrse_ln_fwd_params* p, void* stream);

@@ -250,7 +250,9 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
 #if NRSE_G3_ABLATE == 3 || NRSE_G3_ABLATE == 6
 #define NRSE_MFMA(C, A, B) asm volatile("" ::"v"(A), "v"(B))
 #else
-#define NRSE_MFMA(C, A, B) C = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B, C, 0, 0, 0)
+// transposed product (B fragment in the A slot): lane (g, i) of an accumulator holds output row i,
+// columns 4g..4g+3, so the epilogue stages each quad into LDS with one 16-byte write
+#define NRSE_MFMA(C, A, B) C = __builtin_amdgcn_mfma_f32_16x16x32_bf16(B, A, C, 0, 0, 0)
 #endif
 #define NRSE_READ_A(SLOT)                                                                \
   _Pragma("unroll") for (int fi = 0; fi < 4; ++fi)                                     \
@@ -348,9 +350,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
       for (int fi = 0; fi < 4; ++fi)
 #pragma unroll
         for (int fn = 0; fn < 4; ++fn)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            ct[(fi * 16 + 4 * g + r) * CT_LD + wn * 64 + fn * 16 + li] = acc[mh * 4 + fi][fn][r];
+          *reinterpret_cast<f32x4*>(ct + (fi * 16 + li) * CT_LD + wn * 64 + fn * 16 + 4 * g) = acc[mh * 4 + fi][fn];
     }
     __syncthreads();
     const int mrow0 = m0 + pass * 64;

@@ -118,41 +118,66 @@ NRSE_DEV float load_dy(const nrse_ln_bwd_params& p, long long row, int c, float*
   return 0.f;
 }
 
+// LayerNorm backward, one wave per row, grid-stride over rows with the next row's operands
+// (x, dy, residual, mean, rstd) loaded while the current row is reduced, so each wave keeps two
+// rows of loads in flight. Optional fused consumer (the residual branch's dropout backward that
+// feeds the next GEMM, misc.hip dropout_cast_colsum): dv = dropout(dx) cast to dv_dtype and
+// dv_colsum[c] += sum_r dv[r, c], with the same counter-hash mask (element index r*C + c), so dx
+// is not read back. gamma / beta / dv column sums: per-lane accumulators across the rows of a
+// wave, reduced over the block's 4 waves in one 16 KB LDS buffer, one f32 atomic per column and
+// block.
+template <int NK>
+struct LnRow {
+  float x[NK][CH], dy[NK][CH], r[NK][CH];
+  float mean, rstd;
+};
+
+template <int NK>
+NRSE_DEV void ln_bwd_load(const nrse_ln_bwd_params& p, long long row, int lane, LnRow<NK>& b) {
+  b.mean = p.mean[row];
+  b.rstd = p.rstd[row];
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const int c0 = (k * 64 + lane) * CH;
+    load4(p.x, p.x_dtype, row * p.C + c0, b.x[k]);
+    load_dy(p, row, c0, b.dy[k]);
+    if (p.resid) V4<float>::load(p.resid + row * p.C + c0, b.r[k]);
+  }
+}
+
 template <int NK>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const nrse_ln_bwd_params p) {
-  // one [4 waves][C] buffer, used for dgamma then dbeta: 16 KB at C = 1024, so a block fits on a
-  // CU beside two 128x128 GEMM workgroups of the concurrent weight-gradient stream
   __shared__ float red[4][NK * 64 * CH];
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int C = p.C;
-  float dg[NK][CH], db[NK][CH];
+  const bool fuse = p.dv != nullptr;
+  const uint32_t key = site_key(p.dv_seed);
+  const uint32_t thr = dropout_threshold(p.dv_p);
+  const float dsc = p.dv_p > 0.f ? 1.f / (1.f - p.dv_p) : 1.f;
+  float dg[NK][CH], db[NK][CH], dc[NK][CH];
 #pragma unroll
   for (int k = 0; k < NK; ++k)
 #pragma unroll
-    for (int e = 0; e < CH; ++e) dg[k][e] = db[k][e] = 0.f;
-  const long long nw = (long long)gridDim.x * 4;
-  for (long long row = (long long)blockIdx.x * 4 + w; row < p.rows; row += nw) {
-    const float mean = p.mean[row], rstd = p.rstd[row];
+    for (int e = 0; e < CH; ++e) dg[k][e] = db[k][e] = dc[k][e] = 0.f;
+
+  auto compute = [&](const LnRow<NK>& b, long long row) {
     float xh[NK][CH], g[NK][CH];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int k = 0; k < NK; ++k) {
       const int c0 = (k * 64 + lane) * CH;
-      float xv[CH], dy[CH];
-      load4(p.x, p.x_dtype, row * C + c0, xv);
-      load_dy(p, row, c0, dy);
-      float4 ga = *reinterpret_cast<const float4*>(p.gamma + c0);
+      const float4 ga = *reinterpret_cast<const float4*>(p.gamma + c0);
       const float gam[CH] = {ga.x, ga.y, ga.z, ga.w};
       float be[CH] = {0.f, 0.f, 0.f, 0.f};
       if (p.flags & (NRSE_LN_GELU | NRSE_LN_RELU)) {
-        float4 bb = *reinterpret_cast<const float4*>(p.beta + c0);
+        const float4 bb = *reinterpret_cast<const float4*>(p.beta + c0);
         be[0] = bb.x; be[1] = bb.y; be[2] = bb.z; be[3] = bb.w;
       }
 #pragma unroll
       for (int e = 0; e < CH; ++e) {
-        xh[k][e] = (xv[e] - mean) * rstd;
-        float gg = dy[e];
+        xh[k][e] = (b.x[k][e] - b.mean) * b.rstd;
+        float gg = b.dy[k][e];
         if (p.flags & NRSE_LN_GELU) gg *= gelu_grad_f(xh[k][e] * gam[e] + be[e]);
         else if (p.flags & NRSE_LN_RELU) gg = (xh[k][e] * gam[e] + be[e] > 0.f) ? gg : 0.f;
         dg[k][e] += gg * xh[k][e];
@@ -169,30 +194,51 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const nrse_ln_bwd_params p)
       const int c0 = (k * 64 + lane) * CH;
       float o[CH];
 #pragma unroll
-      for (int e = 0; e < CH; ++e) o[e] = rstd * (g[k][e] - s1 - xh[k][e] * s2);
-      if (p.resid) {
-        float r[CH];
-        V4<float>::load(p.resid + row * C + c0, r);
-#pragma unroll
-        for (int e = 0; e < CH; ++e) o[e] += r[e];
+      for (int e = 0; e < CH; ++e) {
+        o[e] = b.rstd * (g[k][e] - s1 - xh[k][e] * s2);
+        if (p.resid) o[e] += b.r[k][e];
       }
       store4(p.dx, p.dx_dtype, row * C + c0, o);
+      if (fuse) {
+        const long long i = row * C + c0;
+        if (p.dv_p > 0.f) {
+#pragma unroll
+          for (int e = 0; e < CH; ++e) o[e] = dropout_keep(key, (uint32_t)(i + e), thr) ? o[e] * dsc : 0.f;
+        }
+#pragma unroll
+        for (int e = 0; e < CH; ++e) dc[k][e] += o[e];
+        store4(p.dv, p.dv_dtype, i, o);
+      }
     }
+  };
+
+  const long long nw = (long long)gridDim.x * 4;
+  long long row = (long long)blockIdx.x * 4 + w;
+  LnRow<NK> ba, bb;
+  if (row < p.rows) ln_bwd_load(p, row, lane, ba);
+  for (; row < p.rows; row += 2 * nw) {
+    const long long rb = row + nw;
+    if (rb < p.rows) ln_bwd_load(p, rb, lane, bb);
+    compute(ba, row);
+    if (rb >= p.rows) break;
+    if (rb + nw < p.rows) ln_bwd_load(p, rb + nw, lane, ba);
+    compute(bb, rb);
   }
-  if (p.dgamma == nullptr) return;
+
+  auto reduce = [&](float (&acc)[NK][CH], float* dst) {
 #pragma unroll
-  for (int k = 0; k < NK; ++k)
+    for (int k = 0; k < NK; ++k)
 #pragma unroll
-    for (int e = 0; e < CH; ++e) red[w][(k * 64 + lane) * CH + e] = dg[k][e];
-  __syncthreads();
-  for (int c = threadIdx.x; c < C; c += 256) atomicAdd(p.dgamma + c, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < NK; ++k)
-#pragma unroll
-    for (int e = 0; e < CH; ++e) red[w][(k * 64 + lane) * CH + e] = db[k][e];
-  __syncthreads();
-  for (int c = threadIdx.x; c < C; c += 256) atomicAdd(p.dbeta + c, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
+      for (int e = 0; e < CH; ++e) red[w][(k * 64 + lane) * CH + e] = acc[k][e];
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += 256) atomicAdd(dst + c, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
+    __syncthreads();
+  };
+  if (p.dgamma) {
+    reduce(dg, p.dgamma);
+    reduce(db, p.dbeta);
+  }
+  if (fuse && p.dv_colsum) reduce(dc, p.dv_colsum);
 }
 
 // Final LN + time-mean: grid (ceil(T / RPB), batch); 4 waves, each a row at a time.
@@ -276,14 +322,12 @@ extern "C" int nrse_layernorm_bwd(const nrse_ln_bwd_params* p, void* stream) {
                  "nrse_layernorm_bwd: bad col2im geometry");
   if (p->dy_mode == NRSE_DY_BCAST) NRSE_REQUIRE(p->bcast_t > 0, "nrse_layernorm_bwd: bad bcast_t");
   if (!c_ok(p->C)) { nrse_set_error("nrse_layernorm_bwd: C=%d not in {256,512,1024}", p->C); return NRSE_ERR_UNSUPPORTED; }
-  // grid-stride: enough waves to stream the rows, few enough blocks that the per-block
-  // dgamma/dbeta atomics (2*C per block) stay small next to the row traffic
+  NRSE_REQUIRE(!p->dv || (p->dv_dtype == NRSE_BF16 || p->dv_dtype == NRSE_F32), "nrse_layernorm_bwd: bad dv dtype");
+  // grid-stride: 2 blocks per CU (8 waves, each with two rows of loads in flight) when the
+  // column sums are accumulated, so the per-block atomics stay ~3 * C * 512
   long long blocks = (p->rows + 3) / 4;
   long long cap = 8192;
-  if (p->dgamma) {
-    cap = p->rows / 256;
-    cap = cap < 512 ? 512 : (cap > 4096 ? 4096 : cap);
-  }
+  if (p->dgamma || p->dv_colsum) cap = 512;
   if (blocks > cap) blocks = cap;
   NRSE_DISPATCH_NK(ln_bwd_kernel, p->C, dim3((unsigned)blocks), (hipStream_t)stream, *p);
   return nrse_check_launch("nrse_layernorm_bwd");

@@ -72,7 +72,8 @@ class LnBwdParams(ctypes.Structure):
                 ("bcast_t", c_int), ("dy_scale", c_f),
                 ("x", c_vp), ("x_dtype", c_int), ("gamma", c_vp), ("beta", c_vp), ("mean", c_vp), ("rstd", c_vp),
                 ("dx", c_vp), ("dx_dtype", c_int), ("resid", c_vp), ("dgamma", c_vp), ("dbeta", c_vp),
-                ("rows", c_ll), ("C", c_int), ("flags", c_int)]
+                ("rows", c_ll), ("C", c_int), ("flags", c_int),
+                ("dv", c_vp), ("dv_dtype", c_int), ("dv_colsum", c_vp), ("dv_p", c_f), ("dv_seed", c_u32)]
 
 
 class AttnFwdParams(ctypes.Structure):

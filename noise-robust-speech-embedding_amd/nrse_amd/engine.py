@@ -359,21 +359,32 @@ class ByolEngine:
         # final LN (+ time-mean): dy[b,t] = demb[b] / T
         hfin, mf, rf = tape.final
         dh = torch.empty(BT, H, device=dev, dtype=F32)
+        order = list(reversed(tape.layers))
+
+        def ffn_out_dropout(j):
+            """The fused consumer of a layer-output gradient: layer order[j]'s FFN output-dropout
+            backward + output_dense bias gradient (kwargs of K.ln_bwd), and its bf16/f32 result."""
+            if j >= len(order):
+                return None, {}
+            lj = order[j]["li"]
+            dv = torch.empty(BT, H, device=dev, dtype=cdt)
+            return dv, dict(dv=dv, dv_colsum=Gv[f"encoder.layers.{lj}.feed_forward.output_dense.bias"], dv_p=php,
+                            dv_seed=R.site_seed(fseed, R.site_ffn_out(lj)))
+
+        dv2_next, kw = ffn_out_dropout(0)
         K.ln_bwd(demb, hfin, Pm["encoder.layer_norm.weight"], mf, rf, dh, dgamma=Gv["encoder.layer_norm.weight"],
-                 dbeta=Gv["encoder.layer_norm.bias"], mode=_lib.DY_BCAST, bcast_t=T, dy_scale=1.0 / T, rows=BT)
+                 dbeta=Gv["encoder.layer_norm.bias"], mode=_lib.DY_BCAST, bcast_t=T, dy_scale=1.0 / T, rows=BT, **kw)
         tape.final = None
         diag = torch.zeros(nh, 2 * T - 1, device=dev, dtype=F32)
         delta = torch.empty(B, nh, T, device=dev, dtype=F32)
         # the transformer layers' weight gradients (off the dX critical path) run on a side stream
         main = torch.cuda.current_stream(dev)
-        for L_ in reversed(tape.layers):
+        for j, L_ in enumerate(order):
             li = L_["li"]
             p = f"encoder.layers.{li}."
             at = p + "attention."
-            # FFN branch
-            dv2 = torch.empty(BT, H, device=dev, dtype=cdt)
-            K.dropout_cast_colsum(dh, dv2, Gv[p + "feed_forward.output_dense.bias"], php,
-                                  R.site_seed(fseed, R.site_ffn_out(li)))
+            # FFN branch (its output-dropout backward was fused into the LN backward that made dh)
+            dv2 = dv2_next
             df1 = torch.empty(BT, F_, device=dev, dtype=cdt)
             K.linear_dgrad(dv2, Ps[p + "feed_forward.output_dense.weight"], df1, flags=_lib.EPI_GELU_BWD,
                            aux=L_["f1pre"], ldaux=F_, dropout_p=pact, seed=R.site_seed(fseed, R.site_act(li)),
@@ -385,12 +396,14 @@ class ByolEngine:
             K.linear_dgrad(df1, Ps[p + "feed_forward.intermediate_dense.weight"], dx2)
             del df1, dv2
             dhmid = torch.empty(BT, H, device=dev, dtype=F32)
+            dv1 = torch.empty(BT, H, device=dev, dtype=cdt)
+            # + the attention output-dropout backward and out_proj bias gradient, fused
             K.ln_bwd(dx2, L_["hmid"], Pm[p + "final_layer_norm.weight"], L_["m2"], L_["r2"], dhmid, resid=dh,
-                     dgamma=Gv[p + "final_layer_norm.weight"], dbeta=Gv[p + "final_layer_norm.bias"])
+                     dgamma=Gv[p + "final_layer_norm.weight"], dbeta=Gv[p + "final_layer_norm.bias"],
+                     dv=dv1, dv_colsum=Gv[at + "out_proj.bias"], dv_p=php,
+                     dv_seed=R.site_seed(fseed, R.site_attn_out(li)))
             del dx2
             # attention branch
-            dv1 = torch.empty(BT, H, device=dev, dtype=cdt)
-            K.dropout_cast_colsum(dhmid, dv1, Gv[at + "out_proj.bias"], php, R.site_seed(fseed, R.site_attn_out(li)))
             dctx = torch.empty(BT, H, device=dev, dtype=cdt)
             K.linear_dgrad(dv1, Ps[at + "out_proj.weight"], dctx)
             with self._wgrad_stream(main, dv1, L_["ctx"]):
@@ -411,8 +424,10 @@ class ByolEngine:
                        Pm[at + "gru_rel_pos_const"], dgate, dx1, Gv[at + "gru_rel_pos_linear.weight"],
                        Gv[at + "gru_rel_pos_linear.bias"], Gv[at + "gru_rel_pos_const"], B, T, nh)
             dhin = torch.empty(BT, H, device=dev, dtype=F32)
+            # + the next (lower) layer's FFN output-dropout backward, fused
+            dv2_next, kw = ffn_out_dropout(j + 1)
             K.ln_bwd(dx1, L_["h_in"], Pm[p + "layer_norm.weight"], L_["m1"], L_["r1"], dhin, resid=dhmid,
-                     dgamma=Gv[p + "layer_norm.weight"], dbeta=Gv[p + "layer_norm.bias"])
+                     dgamma=Gv[p + "layer_norm.weight"], dbeta=Gv[p + "layer_norm.bias"], **kw)
             del dx1, dhmid
             L_.clear()
             dh = dhin

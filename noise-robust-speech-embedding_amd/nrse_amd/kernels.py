@@ -271,7 +271,10 @@ def ln_fwd(x, gamma, beta, y, mean, rstd, eps, gelu=False, relu=False):
 
 
 def ln_bwd(dy, x, gamma, mean, rstd, dx, *, beta=None, gelu=False, relu=False, resid=None, dgamma=None, dbeta=None,
-           mode=_lib.DY_DIRECT, col=(0, 0, 0, 0), bcast_t=0, dy_scale=1.0, rows=None):
+           mode=_lib.DY_DIRECT, col=(0, 0, 0, 0), bcast_t=0, dy_scale=1.0, rows=None,
+           dv=None, dv_colsum=None, dv_p=0.0, dv_seed=0):
+    """LayerNorm backward; with `dv`, also the fused dropout_cast_colsum of dx: dv = dropout(dx)
+    (cast to dv's dtype), dv_colsum += column sums of dv."""
     C = x.shape[-1]
     rows = rows if rows is not None else x.numel() // C
     p = LnBwdParams()
@@ -284,6 +287,10 @@ def ln_bwd(dy, x, gamma, mean, rstd, dx, *, beta=None, gelu=False, relu=False, r
     p.resid = ptr(resid)
     p.dgamma, p.dbeta = ptr(dgamma), ptr(dbeta)
     p.rows, p.C, p.flags = rows, C, (_lib.LN_GELU if gelu else 0) | (_lib.LN_RELU if relu else 0)
+    if dv is not None:
+        assert dv.numel() == rows * C and (dv_colsum is None or dv_colsum.dtype == torch.float32)
+        p.dv, p.dv_dtype, p.dv_colsum = ptr(dv), dtype_code(dv), ptr(dv_colsum)
+        p.dv_p, p.dv_seed = dv_p, dv_seed & 0xFFFFFFFF
     _call("nrse_layernorm_bwd", ctypes.byref(p), stream_ptr())
 
 

@@ -45,6 +45,43 @@ def test_layernorm_fwd_bwd(nrse_device, C, xdt, gelu):
     assert rel(dg, gr.grad) < 1e-5 and rel(db, br.grad) < 1e-5
 
 
+@pytest.mark.parametrize("rows", [12768, 333, 5])
+@pytest.mark.parametrize("dvdt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_layernorm_bwd_fused_dropout_colsum(nrse_device, rows, dvdt, p):
+    """The LN backward's fused consumer equals the separate dropout_cast_colsum pass over dx
+    (same mask, same cast, same column sums), and dx / dgamma / dbeta are unchanged by it."""
+    from nrse_amd import kernels as K
+    dev = nrse_device
+    C = 1024
+    x = torch.randn(rows, C, device=dev) * 2 + 0.5
+    g = torch.randn(C, device=dev) * 0.1 + 1
+    b = torch.randn(C, device=dev) * 0.1
+    y = torch.empty(rows, C, device=dev)
+    mean = torch.empty(rows, device=dev); rstd = torch.empty(rows, device=dev)
+    K.ln_fwd(x, g, b, y, mean, rstd, 1e-5)
+    dy = torch.randn(rows, C, device=dev)
+    resid = torch.randn(rows, C, device=dev)
+    outs = []
+    for fused in (False, True):
+        dx = torch.empty(rows, C, device=dev)
+        dg = torch.zeros(C, device=dev); db = torch.zeros(C, device=dev)
+        dv = torch.empty(rows, C, device=dev, dtype=dvdt); cs = torch.zeros(C, device=dev)
+        if fused:
+            K.ln_bwd(dy, x, g, mean, rstd, dx, resid=resid, dgamma=dg, dbeta=db, dv=dv, dv_colsum=cs, dv_p=p,
+                     dv_seed=4321)
+        else:
+            K.ln_bwd(dy, x, g, mean, rstd, dx, resid=resid, dgamma=dg, dbeta=db)
+            K.dropout_cast_colsum(dx, dv, cs, p, 4321)
+        outs.append((dx, dg, db, dv, cs))
+    (dx0, dg0, db0, dv0, cs0), (dx1, dg1, db1, dv1, cs1) = outs
+    assert torch.equal(dx0, dx1) and torch.equal(dv0, dv1)
+    assert rel(dg1, dg0) < 1e-6 and rel(db1, db0) < 1e-6 and rel(cs1, cs0) < 1e-6
+    if p > 0:
+        frac = float((dv1 == 0).float().mean())
+        assert abs(frac - p) < (0.01 if rows > 1000 else 0.05)
+
+
 def test_layernorm_bwd_col2im_and_bcast(nrse_device):
     from nrse_amd import kernels as K, _lib
     dev = nrse_device
