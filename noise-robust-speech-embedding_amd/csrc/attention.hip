@@ -212,9 +212,10 @@ __global__ __launch_bounds__(64) void attn_fwd_f32_kernel(const nrse_attn_fwd_pa
   const float g = valid ? p.gate[((long long)b * H + h) * Tn + i] : 0.f;
   const float* brow = p.bias + ((long long)h * Tn + (valid ? i : 0)) * bias_ld_dev(Tn);
   const uint32_t key = site_key(p.seed);
-  const uint32_t thr = dropout_threshold(p.dropout_p);
+  const uint32_t thr = dropout_threshold16(p.dropout_p);
+  const uint32_t tp2 = (uint32_t)((Tn + 1) >> 1);
   const float dsc = p.dropout_p > 0.f ? 1.f / (1.f - p.dropout_p) : 1.f;
-  const uint32_t rowidx = (uint32_t)((((long long)b * H + h) * Tn + i) * Tn);
+  const uint32_t arow = (uint32_t)(((long long)b * H + h) * Tn + i);
   float m = -INFINITY, l = 0.f;
   for (int j0 = 0; j0 < Tn; j0 += 64) {
     __syncthreads();
@@ -247,7 +248,7 @@ __global__ __launch_bounds__(64) void attn_fwd_f32_kernel(const nrse_attn_fwd_pa
       const float pj = __expf(s[jj] - m);
       l += pj;
       float pd = pj;
-      if (p.dropout_p > 0.f) pd = dropout_keep(key, rowidx + j0 + jj, thr) ? pj * dsc : 0.f;
+      if (p.dropout_p > 0.f) pd = attn_keep(key, arow, tp2, j0 + jj, thr) ? pj * dsc : 0.f;
 #pragma unroll
       for (int d = 0; d < HD; ++d) o[d] += pd * Vs[jj][d];
     }
@@ -296,7 +297,7 @@ __global__ __launch_bounds__(64) void attn_bwd_kv_f32_kernel(const nrse_attn_bwd
     dk[d] = dv[d] = 0.f;
   }
   const uint32_t key = site_key(p.seed);
-  const uint32_t thr = dropout_threshold(p.dropout_p);
+  const uint32_t thr = dropout_threshold16(p.dropout_p);
   const float dsc = p.dropout_p > 0.f ? 1.f / (1.f - p.dropout_p) : 1.f;
   const int nd = 2 * Tn - 1;
   for (int i0 = 0; i0 < Tn; i0 += 64) {
@@ -332,7 +333,7 @@ __global__ __launch_bounds__(64) void attn_bwd_kv_f32_kernel(const nrse_attn_bwd
         const float pr = __expf(s - rowc[0][ii]);
         float pd = pr, dp = dpd;
         if (p.dropout_p > 0.f) {
-          const bool keep = dropout_keep(key, (uint32_t)((((long long)b * H + h) * Tn + i) * Tn + j), thr);
+          const bool keep = attn_keep(key, (uint32_t)(((long long)b * H + h) * Tn + i), (uint32_t)((Tn + 1) >> 1), j, thr);
           pd = keep ? pr * dsc : 0.f;
           dp = keep ? dpd * dsc : 0.f;
         }
@@ -383,7 +384,7 @@ __global__ __launch_bounds__(64) void attn_bwd_q_f32_kernel(const nrse_attn_bwd_
   const float g = valid ? p.gate[ri] : 0.f;
   const float* brow = p.bias + ((long long)h * Tn + (valid ? i : 0)) * bias_ld_dev(Tn);
   const uint32_t key = site_key(p.seed);
-  const uint32_t thr = dropout_threshold(p.dropout_p);
+  const uint32_t thr = dropout_threshold16(p.dropout_p);
   const float dsc = p.dropout_p > 0.f ? 1.f / (1.f - p.dropout_p) : 1.f;
   float dgate = 0.f;
   for (int j0 = 0; j0 < Tn; j0 += 64) {
@@ -408,7 +409,7 @@ __global__ __launch_bounds__(64) void attn_bwd_q_f32_kernel(const nrse_attn_bwd_
       const float pr = __expf(s - lse);
       float dp = dpd;
       if (p.dropout_p > 0.f) {
-        const bool keep = dropout_keep(key, (uint32_t)((((long long)b * H + h) * Tn + i) * Tn + j), thr);
+        const bool keep = attn_keep(key, (uint32_t)(((long long)b * H + h) * Tn + i), (uint32_t)((Tn + 1) >> 1), j, thr);
         dp = keep ? dpd * dsc : 0.f;
       }
       const float ds = pr * (dp - delta);

@@ -190,10 +190,11 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
   const int bsel = u00 & 3;
   const float* bvl_base = bv + bsel * bvl + (u00 - bsel);
   const uint32_t key = site_key(p.seed);
-  const uint32_t thr = dropout_threshold(p.dropout_p);
+  const uint32_t thr = dropout_threshold16(p.dropout_p);
   const bool drop = p.dropout_p > 0.f;
   const float dsc = drop ? 1.f / (1.f - p.dropout_p) : 1.f;
-  const uint32_t rowidx = (uint32_t)((bh * T + qi) * T);
+  // this lane's query row: key pair (kb + 16t + 4g)/2 + rp holds elements r = 2rp, 2rp + 1
+  const uint32_t rowpair = (uint32_t)(bh * T + qi) * (uint32_t)((T + 1) >> 1) + (uint32_t)(2 * g);
   float m = -INFINITY, lpart = 0.f;
   f32x4 o[4];
 #pragma unroll
@@ -256,8 +257,11 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          pd[t][r] = dropout_keep(key, rowidx + (uint32_t)(kb + 16 * t + 4 * g + r), thr) ? pd[t][r] : 0.f;
+        for (int rp = 0; rp < 2; ++rp) {
+          const uint32_t hh = mix32((rowpair + (uint32_t)((kb >> 1) + 8 * t + rp)) ^ key);
+          pd[t][2 * rp] = attn_half_keep(hh, 0, thr) ? pd[t][2 * rp] : 0.f;
+          pd[t][2 * rp + 1] = attn_half_keep(hh, 1, thr) ? pd[t][2 * rp + 1] : 0.f;
+        }
     }
     lpart = lpart * alpha + ps;
 #pragma unroll
@@ -347,10 +351,10 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
   const int bsel = u00 & 3;
   const float* bvl_base = bv + bsel * bvl + (u00 - bsel);
   const uint32_t key = site_key(p.seed);
-  const uint32_t thr = dropout_threshold(p.dropout_p);
+  const uint32_t thr = dropout_threshold16(p.dropout_p);
   const bool drop = p.dropout_p > 0.f;
   const float dsc = drop ? 1.f / (1.f - p.dropout_p) : 1.f;
-  const uint32_t rowidx = (uint32_t)((bh * T + qi) * T);
+  const uint32_t rowpair = (uint32_t)(bh * T + qi) * (uint32_t)((T + 1) >> 1) + (uint32_t)(2 * g);  // as fwd
   float dgate = 0.f;
   f32x4 dq[4];
 #pragma unroll
@@ -391,8 +395,11 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          dp[t][r] = dropout_keep(key, rowidx + (uint32_t)(kb + 16 * t + 4 * g + r), thr) ? dp[t][r] * dsc : 0.f;
+        for (int rp = 0; rp < 2; ++rp) {
+          const uint32_t hh = mix32((rowpair + (uint32_t)((kb >> 1) + 8 * t + rp)) ^ key);
+          dp[t][2 * rp] = attn_half_keep(hh, 0, thr) ? dp[t][2 * rp] * dsc : 0.f;
+          dp[t][2 * rp + 1] = attn_half_keep(hh, 1, thr) ? dp[t][2 * rp + 1] * dsc : 0.f;
+        }
     }
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -506,7 +513,13 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(const nrse_attn_bwd_pa
   const float wlo[3] = {1.f - whi[0], 1.f - whi[1], 1.f - whi[2]};
   const uint32_t key = site_key(p.seed);
   const float c1 = p.scale * LOG2E;
-  const uint32_t thr = dropout_threshold(p.dropout_p);
+  const uint32_t thr = dropout_threshold16(p.dropout_p);
+  // dropout: this lane's key kj and its neighbour kj ^ 1 share every pair hash (row q, kj / 2);
+  // the even lane hashes rows r = 0, 1 of each 4-row group, the odd lane rows 2, 3, and they swap
+  // the results (DPP quad_perm [1,0,3,2])
+  const int par = kj & 1;
+  const uint32_t tp2 = (uint32_t)((T + 1) >> 1);
+  const uint32_t colpair = (uint32_t)(kj >> 1);
   const bool drop = p.dropout_p > 0.f;
   const float dsc = drop ? 1.f / (1.f - p.dropout_p) : 1.f;
   const int kl = w * 16 + i16;  // key within the 64-key block
@@ -561,13 +574,20 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(const nrse_attn_bwd_pa
 #if NRSE_ATT_ABLATE != 2
     if (drop) {
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
+      for (int t = 0; t < 4; ++t) {
+        const uint32_t qa = (uint32_t)(bh * T + qb + 16 * t + 4 * g + 2 * par);
+        const uint32_t ha = mix32((qa * tp2 + colpair) ^ key);
+        const uint32_t hb = mix32(((qa + 1) * tp2 + colpair) ^ key);
+        const uint32_t xa = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ha, 0xB1, 0xF, 0xF, false);
+        const uint32_t xb = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hb, 0xB1, 0xF, 0xF, false);
+        const uint32_t hr[4] = {par ? xa : ha, par ? xb : hb, par ? ha : xa, par ? hb : xb};
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const bool keep = dropout_keep(key, (uint32_t)((bh * T + qb + 16 * t + 4 * g + r) * T + kj), thr);
+          const bool keep = attn_half_keep(hr[r], par, thr);
           pd[t][r] = keep ? ds[t][r] : 0.f;
           dp[t][r] = keep ? dp[t][r] * dsc : 0.f;
         }
+      }
     } else
 #endif
     {

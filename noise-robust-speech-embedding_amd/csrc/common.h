@@ -80,6 +80,25 @@ __host__ __device__ inline uint32_t dropout_threshold(float p) {
   return (uint32_t)t;
 }
 
+// Attention-probability dropout (the [B, H, T, T] site, the largest): one mixer hash per PAIR of
+// keys of a query row, 16 bits per element, so the two 32-bit multiplies of mix32 (quarter-rate
+// VALU) are paid once per two elements. Element (row, k), row = (b*H + h)*T + q:
+//   hash = mix32((row * ((T + 1) / 2) + k / 2) ^ key), half = k odd ? hash >> 16 : hash & 0xffff,
+//   keep = half >= thr16, thr16 = round(p * 65536) (P(drop) within 8e-6 of p).
+__host__ __device__ inline uint32_t dropout_threshold16(float p) {
+  const double t = (double)p * 65536.0 + 0.5;
+  return t >= 65536.0 ? 65536u : (uint32_t)t;
+}
+NRSE_DEV uint32_t attn_pair_hash(uint32_t key, uint32_t row, uint32_t tp2, int k) {
+  return mix32((row * tp2 + (uint32_t)(k >> 1)) ^ key);
+}
+NRSE_DEV bool attn_half_keep(uint32_t hash, int odd, uint32_t thr16) {
+  return (odd ? (hash >> 16) : (hash & 0xffffu)) >= thr16;
+}
+NRSE_DEV bool attn_keep(uint32_t key, uint32_t row, uint32_t tp2, int k, uint32_t thr16) {
+  return attn_half_keep(attn_pair_hash(key, row, tp2, k), k & 1, thr16);
+}
+
 // Wave-wide reductions (wave64).
 NRSE_DEV float wave_sum(float v) {
 #pragma unroll

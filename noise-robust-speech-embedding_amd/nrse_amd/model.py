@@ -194,37 +194,48 @@ class BYOLSpeechModel(nn.Module):
         return WavLMEncoder(engine=self.engine, which="online")
 
     # ---------------------------------------------------------------- checkpoints
-    def state_dict(self, *args, **kwargs):
+    def _state_items(self):
+        """(key, tensor) of the checkpoint: the reference BYOLSpeechModel.state_dict() key set,
+        shapes and dtypes (pinned by tests/golden/state_manifest.json): online encoder / projector
+        / predictor, target encoder / projector, each BatchNorm's buffers after its bias. Within
+        the encoder the order is the flat layout's, not transformers' module order (consumers
+        match by key)."""
         e = self.engine
-        sd = {}
-        sd.update({k: v.detach().clone() for k, v in PR.named_views(e.layout, e.online).items()})
-        sd.update({k: v.detach().clone() for k, v in PR.named_views(e.layout, e.target, target=True).items()})
-        for key, (rm, rv, nbt) in e.bn.items():
-            sd[key + ".running_mean"] = rm.clone()
-            sd[key + ".running_var"] = rv.clone()
-            sd[key + ".num_batches_tracked"] = nbt.clone()
-        return sd
+        for views in (PR.named_views(e.layout, e.online), PR.named_views(e.layout, e.target, target=True)):
+            for k, v in views.items():
+                yield k, v
+                if k.endswith(".bias") and k[:-5] in e.bn:
+                    rm, rv, nbt = e.bn[k[:-5]]
+                    yield k[:-5] + ".running_mean", rm
+                    yield k[:-5] + ".running_var", rv
+                    yield k[:-5] + ".num_batches_tracked", nbt
+
+    def state_dict(self, *args, **kwargs):
+        return {k: v.detach().clone() for k, v in self._state_items()}
 
     def load_state_dict(self, sd: dict, strict: bool = True):
-        e = self.engine
-        on = PR.named_views(e.layout, e.online)
-        tg = PR.named_views(e.layout, e.target, target=True)
-        missing = []
+        """torch.nn.Module.load_state_dict semantics over the reference key layout: shape
+        mismatches always raise; with strict, missing or unexpected keys raise; returns
+        (missing_keys, unexpected_keys)."""
+        from torch.nn.modules.module import _IncompatibleKeys
+        own = dict(self._state_items())
+        missing = [k for k in own if k not in sd]
+        unexpected = [k for k in sd if k not in own]
+        bad = [f"{k}: checkpoint {tuple(sd[k].shape)} vs model {tuple(v.shape)}" for k, v in own.items()
+               if k in sd and tuple(sd[k].shape) != tuple(v.shape)]
+        if bad or (strict and (missing or unexpected)):
+            msg = [f"size mismatch for {b}" for b in bad]
+            if strict and missing:
+                msg.append(f"Missing key(s): {missing[:8]}{'...' if len(missing) > 8 else ''}")
+            if strict and unexpected:
+                msg.append(f"Unexpected key(s): {unexpected[:8]}{'...' if len(unexpected) > 8 else ''}")
+            raise RuntimeError("Error(s) in loading state_dict for BYOLSpeechModel:\n\t" + "\n\t".join(msg))
         with torch.no_grad():
-            for views in (on, tg):
-                for k, v in views.items():
-                    if k in sd:
-                        v.copy_(sd[k].to(v.device, v.dtype).view_as(v))
-                    else:
-                        missing.append(k)
-            for key, (rm, rv, nbt) in e.bn.items():
-                for suffix, t in ((".running_mean", rm), (".running_var", rv), (".num_batches_tracked", nbt)):
-                    if key + suffix in sd:
-                        t.copy_(sd[key + suffix])
-        if strict and missing:
-            raise KeyError(f"missing keys: {missing[:8]}{'...' if len(missing) > 8 else ''}")
+            for k, v in own.items():
+                if k in sd:
+                    v.copy_(sd[k].to(v.device, v.dtype))
         self.refresh_shadows()
-        return missing
+        return _IncompatibleKeys(missing, unexpected)
 
     def train(self, mode: bool = True):
         self.training = mode

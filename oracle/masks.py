@@ -46,3 +46,27 @@ def dropout_mask(seed: int, p: float, shape) -> np.ndarray:
     n = int(np.prod(shape))
     k = keep_mask(seed, p, n).reshape(shape)
     return k.astype(np.float32) * np.float32(1.0 / (1.0 - p)) if p < 1 else np.zeros(shape, np.float32)
+
+
+def threshold16(p: float) -> int:
+    t = p * 65536.0 + 0.5
+    return 65536 if t >= 65536.0 else int(t)
+
+
+def attn_keep_mask(seed: int, p: float, rows: int, T: int) -> np.ndarray:
+    """keep[row, k] of the attention-probability site (csrc/common.h attn_keep): one mix32 hash per
+    pair of keys of a query row, 16 bits per element; row = (b*H + h)*T + q."""
+    r = np.arange(rows, dtype=np.uint64)[:, None]
+    kk = np.arange(T, dtype=np.uint64)[None, :]
+    tp2 = np.uint64((T + 1) // 2)
+    h = mix32(((r * tp2 + (kk >> np.uint64(1))) & M32) ^ site_key(seed))
+    half = np.where((kk & np.uint64(1)) == 1, h >> np.uint64(16), h & np.uint64(0xFFFF))
+    return half >= np.uint64(threshold16(p))
+
+
+def attn_dropout_mask(seed: int, p: float, shape) -> np.ndarray:
+    """Multiplicative mask (0 or 1/(1-p)) over attention probabilities of shape [..., T, T]."""
+    T = int(shape[-1])
+    rows = int(np.prod(shape[:-1]))
+    k = attn_keep_mask(seed, p, rows, T).reshape(shape)
+    return k.astype(np.float32) * np.float32(1.0 / (1.0 - p)) if p < 1 else np.zeros(shape, np.float32)

@@ -223,7 +223,9 @@ def attention(P: dict, a, li: int, x1: torch.Tensor, pbias: torch.Tensor, fseed:
     s = (q @ k.transpose(-1, -2)) / math.sqrt(hd) + g[..., None] * pbias[None]
     p = torch.softmax(s, dim=-1)
     if train:
-        p = _drop(p, a.attention_dropout, rng.site_seed(fseed, rng.site_attn_probs(li)))
+        if a.attention_dropout > 0:  # the pair-hash mask of the attention kernels (masks.attn_keep_mask)
+            p = p * torch.from_numpy(masks.attn_dropout_mask(rng.site_seed(fseed, rng.site_attn_probs(li)),
+                                                             a.attention_dropout, tuple(p.shape)))
     ctx = (p @ v).transpose(1, 2).reshape(B, T, H)
     return _lin(ctx, P[pre + "out_proj.weight"], P[pre + "out_proj.bias"])
 

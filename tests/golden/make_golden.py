@@ -248,11 +248,31 @@ def make_configs():
     print("configs: ok")
 
 
+def make_state_manifest():
+    """state_manifest.json: the reference BYOLSpeechModel.state_dict() key / shape / dtype list, in
+    its order, for the tiny arch and WavLM-Large (the checkpoint format train_byol.py:207-240
+    saves as 'model_state_dict' and src/train/dimentional_emotions.py:43-45 and
+    baseline/train_ft_cat_ser_weighted_checkpoint.py:137-158 load)."""
+    import json
+    out = {}
+    for tag, arch, pp in (("tiny", A.TINY, (256, 512)), ("large", A.LARGE, (1024, 2048))):
+        with tempfile.TemporaryDirectory() as td:
+            model, _, _ = build_reference_model(arch.deterministic(), pp[0], pp[1], 0.99, td)
+            out[tag] = [[k, list(v.shape), str(v.dtype).replace("torch.", "")] for k, v in model.state_dict().items()]
+        print(f"state manifest {tag}: {len(out[tag])} entries")
+    with open(os.path.join(HERE, "state_manifest.json"), "w") as fh:
+        json.dump(out, fh, indent=0)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-large", action="store_true")
     ap.add_argument("--configs-only", action="store_true")
+    ap.add_argument("--manifest-only", action="store_true")
     args = ap.parse_args()
+    if args.manifest_only:
+        make_state_manifest()
+        return
     make_configs()
     if args.configs_only:
         return

@@ -23,7 +23,7 @@ def reference(qkv, gate, bias, B, T, H, p, seed):
     lse = torch.logsumexp(s, -1)
     pr = torch.softmax(s, -1)
     if p > 0:
-        m = torch.from_numpy(MK.dropout_mask(seed, p, (B, H, T, T))).double().to(qkv.device)
+        m = torch.from_numpy(MK.attn_dropout_mask(seed, p, (B, H, T, T))).double().to(qkv.device)
         pr = pr * m
     ctx = (pr @ v).transpose(1, 2).reshape(B * T, H * D)
     return x, g, bt, ctx, lse

@@ -105,3 +105,19 @@ def test_mock_pairs_follow_create_mock_dataset_rule():
     for i in range(10):
         d = ds[i]["noisy_input_values"] - ds[i]["clean_input_values"]
         assert abs(float(d.std()) * (int(ds[i]["snr"]) + 1) - 1.0) < 0.15
+
+
+def test_attention_pair_hash_mask_statistics():
+    """The attention-probability dropout mask (one hash per key pair, 16 bits per element): drop
+    rate p, and the two elements of a pair independent (joint drop rate p^2)."""
+    import numpy as np
+    from oracle import masks as MK
+    p, rows, T = 0.1, 600, 399
+    keep = MK.attn_keep_mask(1234, p, rows, T)
+    assert abs(1 - keep.mean() - p) < 0.004
+    pairs = keep[:, : T - 1].reshape(rows, -1, 2)
+    both = float((~pairs[..., 0] & ~pairs[..., 1]).mean())
+    assert abs(both - p * p) < 0.002
+    assert MK.threshold16(0.0) == 0 and MK.threshold16(1.0) == 65536
+    m = MK.attn_dropout_mask(7, p, (2, 3, T, T))
+    assert set(np.unique(m)).issubset({0.0, np.float32(1 / (1 - p))})

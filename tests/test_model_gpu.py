@@ -120,3 +120,107 @@ def test_dev_yaml_cli_on_mock_dataset(nrse_device, tmp_path):
     assert sd["online_encoder.model.encoder.layers.23.feed_forward.output_dense.weight"].shape == (1024, 4096)
     assert sd["online_predictor.layers.6.weight"].shape == (1024, 2048)
     assert np.isfinite(ck["loss"])
+
+
+def test_checkpoint_interop_reference_layout(nrse_device, tmp_path):
+    """f3: checkpoints in the reference format. (1) state_dict() has exactly the reference
+    BYOLSpeechModel's keys, shapes and dtypes (tests/golden/state_manifest.json, dumped from
+    the reference by make_golden.py --manifest-only). (2) A checkpoint written the way
+    train_byol.py:207-240 writes it ({'model_state_dict': ...}, the reference's weights of the
+    byol_tiny fixture) loads strictly, after torch.load(weights_only=True), and reproduces the
+    reference's eval outputs. (3) torch semantics: unexpected keys and shape mismatches raise."""
+    import json
+    from nrse_amd.model import BYOLSpeechModel
+    man = json.load(open(os.path.join(ROOT, "tests", "golden", "state_manifest.json")))["tiny"]
+    z = np.load(os.path.join(ROOT, "tests", "golden", "byol_tiny.npz"))
+    c = cfg()
+    c["model"].update(projection_dim=int(z["proj_dim"]), prediction_dim=int(z["pred_dim"]), ema_decay=float(z["ema"]))
+    m = BYOLSpeechModel(c, arch=A.TINY.deterministic(), compute_dtype=torch.float32)
+    sd = m.state_dict()
+    ours = {k: [list(v.shape), str(v.dtype).replace("torch.", "")] for k, v in sd.items()}
+    assert ours == {k: [shp, dt] for k, shp, dt in man}   # (load_state_dict matches by key, not order)
+    # the reference's weights of the fixture, keyed as its state_dict (target = online copy)
+    layout = PR.byol_layout(A.TINY.deterministic(), int(z["proj_dim"]), int(z["pred_dim"]))
+    views = PR.named_views(layout, PR.init_byol_flat(layout, int(z["seed"])))
+    ref_sd = {}
+    for k, shp, dt in man:
+        src = k.replace("target_", "online_", 1) if k.startswith("target_") else k
+        if src in views:
+            ref_sd[k] = views[src].clone().reshape(shp)
+        elif k.endswith("running_mean"):
+            ref_sd[k] = torch.zeros(shp)
+        elif k.endswith("running_var"):
+            ref_sd[k] = torch.ones(shp)
+        else:
+            ref_sd[k] = torch.zeros(shp, dtype=torch.long)
+    torch.save({"epoch": 0, "model_state_dict": ref_sd, "optimizer_state_dict": {}, "loss": 0.0, "similarity": 0.0},
+               tmp_path / "best_val_loss.pt")
+    ck = torch.load(tmp_path / "best_val_loss.pt", weights_only=True, map_location="cpu")
+    m2 = BYOLSpeechModel({**c, "training": {**c["training"], "seed": 77}}, arch=A.TINY.deterministic(),
+                         compute_dtype=torch.float32)
+    res = m2.load_state_dict(ck["model_state_dict"])
+    assert res.missing_keys == [] and res.unexpected_keys == []
+    m2.eval()
+    with torch.no_grad():
+        pred, tproj = m2(torch.from_numpy(z["clean"]).cuda()[:, None], torch.from_numpy(z["noisy"]).cuda()[:, None])
+    for got, key in ((pred, "eval_pred"), (tproj, "eval_tproj")):
+        ref = torch.from_numpy(z[key])
+        assert float((got.cpu() - ref).norm() / ref.norm()) < 1e-4, key
+    bad = dict(ck["model_state_dict"])
+    bad["online_projector.layers.9.weight"] = torch.zeros(3)
+    with pytest.raises(RuntimeError, match="Unexpected"):
+        m2.load_state_dict(bad)
+    assert m2.load_state_dict(bad, strict=False).unexpected_keys == ["online_projector.layers.9.weight"]
+    bad = dict(ck["model_state_dict"])
+    bad["online_predictor.layers.0.weight"] = bad["online_predictor.layers.0.weight"].t().contiguous()
+    with pytest.raises(RuntimeError, match="size mismatch"):
+        m2.load_state_dict(bad)
+
+
+def test_validate_model_matches_oracle(nrse_device):
+    """f2: train.validate_model (evaluate_byol.py:12-123: per-SNR mean cosine similarity of the
+    online encoder's clean vs noisy embeddings, mean eval-mode BYOL loss over batches) equals the
+    same computation on the oracle, for a model after one training step (non-trivial BN running
+    statistics), over ragged SNR groups and a short last batch."""
+    from nrse_amd import train as TR
+    from nrse_amd.model import BYOLSpeechModel
+    arch = A.TINY.deterministic()
+    c = cfg()
+    m = BYOLSpeechModel(c, arch=arch, compute_dtype=torch.float32, seed=5)
+    layout = PR.byol_layout(arch, 256, 512)
+    g = torch.Generator().manual_seed(11)
+    wav = torch.randn(9, 16000, generator=g) * 0.1
+    noise = torch.randn(9, 16000, generator=g) * 0.1
+    snr_range = [0, 5, 10, 15, 20]
+    snrs = torch.tensor([0, 5, 5, 10, 20, 20, 20, 0, 15])
+    noisy = wav + noise / (snrs[:, None].float() + 1)
+    # one fused step first, so the BN running buffers are not at their init values
+    m.engine.train_step(wav[:4].cuda(), noisy[:4].cuda(), lr=1e-4, step_seed=3)
+    batches = [dict(clean_input_values=wav[i:i + 4, None], noisy_input_values=noisy[i:i + 4, None], snr=snrs[i:i + 4])
+               for i in range(0, 9, 4)]
+    val_loss, met = TR.validate_model(m, batches, "cuda", {"data": {"snr_range": snr_range}})
+    # oracle: the same weights and BN buffers, eval mode
+    st = O.OracleState(layout, m.engine.online.detach().cpu())
+    st.target = m.engine.target.detach().cpu().clone()
+    sd = m.state_dict()
+    for key in sd:
+        if key.endswith("running_mean") or key.endswith("running_var"):
+            net, rest = key.split(".", 1)
+            st.buffers[net][rest].copy_(sd[key].cpu())
+    assert float(st.buffers["online_projector"]["layers.1.running_var"].sub(1).abs().max()) > 0
+    sims = {s: [] for s in snr_range}
+    losses = []
+    with torch.no_grad():
+        for b in batches:
+            cl, nz = b["clean_input_values"][:, 0], b["noisy_input_values"][:, 0]
+            pred, tproj, ec = O.forward(st, cl, nz, train=False)
+            _, _, en = O.forward(st, nz, cl, train=False)
+            s = torch.nn.functional.cosine_similarity(ec, en, dim=1)
+            for i, snr in enumerate(b["snr"].tolist()):
+                sims[snr].append(float(s[i]))
+            losses.append(float(O.byol_loss(pred, tproj)))
+    ref = {k: sum(v) / len(v) for k, v in sims.items()}
+    for k in snr_range:
+        assert abs(met["val_similarities"][k] - ref[k]) < 1e-5, (k, met["val_similarities"][k], ref[k])
+    assert abs(met["val_avg_similarity"] - sum(ref.values()) / len(ref)) < 1e-5
+    assert abs(val_loss - sum(losses) / len(losses)) < 1e-4 * max(1.0, abs(val_loss))
