@@ -499,12 +499,18 @@ class ByolEngine:
                          dbeta=Gv[p + "layer_norm.bias"], mode=_lib.DY_COL2IM, col=col)
             del dy_src
             # wgrad -> [co][k*ci] then into the [co][ci][k] grad layout
-            dWr = torch.zeros(Cc, k * Cin, device=dev, dtype=F32)
-            tiles = ((Cc + 127) // 128) * ((k * Cin + 127) // 128)
-            S = _divisor_at_most(B, max(1, 512 // tiles))
-            K.gemm(K.Operand(dpre, False, Cc, seg_stride=Tout * Cc), K.Operand(c["x"], False, s * Cin,
-                                                                               seg_stride=Tin * Cin),
-                   dWr, Cc, k * Cin, Tout, ldc=k * Cin, nseg=B // S, splits=S, flags=_lib.EPI_ATOMIC)
+            A_op = K.Operand(dpre, False, Cc, seg_stride=Tout * Cc)
+            B_op = K.Operand(c["x"], False, s * Cin, seg_stride=Tin * Cin)
+            if cdt == torch.bfloat16:
+                # split-K over utterances into f32 slabs on the 256x256 kernel + ordered reduce
+                dWr = torch.empty(Cc, k * Cin, device=dev, dtype=F32)
+                S = K.slab_splits_for(((Cc + 255) // 256) * ((k * Cin + 255) // 256), B)
+                K.gemm_slab(A_op, B_op, dWr, Cc, k * Cin, Tout, nseg=B // S, splits=S, accumulate=False)
+            else:
+                dWr = torch.zeros(Cc, k * Cin, device=dev, dtype=F32)
+                tiles = ((Cc + 127) // 128) * ((k * Cin + 127) // 128)
+                S = _divisor_at_most(B, max(1, 512 // tiles))
+                K.gemm(A_op, B_op, dWr, Cc, k * Cin, Tout, ldc=k * Cin, nseg=B // S, splits=S, flags=_lib.EPI_ATOMIC)
             K.swap12(dWr, Gv[p + "conv.weight"], Cc, k, Cin, accumulate=True)
             del dWr
             # dgrad -> G [B*Tout, k*Cin] (col2im folded into the next LN backward)

@@ -219,6 +219,26 @@ def _slab_splits(M: int, N: int, K: int) -> int:
 _SLAB_WGRAD = True
 
 
+def slab_splits_for(tiles256: int, n_units: int) -> int:
+    """Largest divisor S of n_units with tiles256 * S <= 256 (one wave of 256x256 workgroups)."""
+    best = 1
+    for s in range(1, n_units + 1):
+        if n_units % s == 0 and tiles256 * s <= 256:
+            best = s
+    return best
+
+
+def gemm_slab(A: "Operand", B: "Operand", out: torch.Tensor, M: int, N: int, K: int, *, nseg: int, splits: int,
+              accumulate: bool) -> None:
+    """out[M,N] (+)= sum over `splits` K-ranges of A B^T (each split: nseg segments of K), the
+    partials stored as f32 slabs by the 256x256 kernel and summed in split order by one streaming
+    nrse_splitk_reduce: the deterministic, atomic-free split-K of linear_wgrad, for any operands."""
+    assert out.dtype == torch.float32 and out.is_contiguous() and out.numel() == M * N
+    slab = torch.empty(splits, M, N, device=out.device, dtype=torch.float32)
+    gemm(A, B, slab, M, N, K, ldc=N, nseg=nseg, splits=splits, c_split=M * N)
+    _call("nrse_splitk_reduce", ptr(out), ptr(slab), splits, M * N, 1 if accumulate else 0, stream_ptr())
+
+
 def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, *, splits: int = 0) -> None:
     """dw[N,K] += dy[M,N]^T @ x[M,K]  (f32 dw).
 
