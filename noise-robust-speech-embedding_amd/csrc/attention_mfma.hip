@@ -17,7 +17,8 @@
 
 // Diagnostic builds only (NRSE_ATT_ABLATE, tools/build_diag.sh): in attn_bwd_kv,
 // 1 = no diagonal LDS atomics, 2 = no dropout hash, 3 = no Q/dO/bias re-staging after the first
-// query block. Outputs of those builds are wrong; only their time matters.
+// query block, 4 = no final global atomics of the diagonal sums, 5 = plain LDS stores instead of
+// the per-tile diagonal staging, 6 = no DPP diagonal rotations. Outputs of those builds are wrong; only their time matters.
 #ifndef NRSE_ATT_ABLATE
 #define NRSE_ATT_ABLATE 0
 #endif
@@ -26,7 +27,11 @@ namespace {
 
 constexpr int D = 64;
 constexpr int TILE_B = 64 * 128;  // bytes per 64x64 bf16 tile
-constexpr int DPAD = 80;          // low-side margin of the LDS diagonal arrays (dK/dV kernel)
+// dK/dV kernel: diagonal accumulator arrays of ndiag(T) = Tp + 80 floats, the diagonal d = kj - qi
+// of the block at index d - (kb0 - T + 1) + dpad(T); dpad >= Tp - T + 13 covers the lowest index
+// (the carried accumulator at qend = Tp), the top is T + 62 + dpad < ndiag
+NRSE_DEV int diag_pad(int T) { return ((T + 63) & ~63) - T + 16; }
+NRSE_DEV int diag_len(int T) { return ((T + 63) & ~63) + 80; }
 // Softmax runs in the base-2 domain (v_exp_f32 is 2^x): scores are formed as
 // log2(e) * (q.k / 8 + gate * bias) with the log2(e) folded into the per-row constants, so each
 // element costs one fma + one exp; lse is stored in natural-log units.
@@ -134,8 +139,10 @@ NRSE_DEV void kv_dma_issue(const KvDma& d, char* tile, int row0, int wave) {
 // copies of the Toeplitz vector segment it touches: copy s holds vec[e_lo + j + s], e_lo =
 // T - 1 - q0 - 63 (values outside [0, 2T-1) are zero). A lane whose 4 consecutive elements start
 // at segment index u reads them with one aligned ds_read_b128 from copy (u & 3) at u - (u & 3).
-constexpr int BV_EXTRA = 136;  // 64 (last query offset) + 64 (padded key tile) + 8
-NRSE_DEV int bv_len(int T) { return ((T + BV_EXTRA) + 3) & ~3; }
+// Copy length: a lane reads 4 floats at (u00 - (u00 & 3)) + kb + 16t <= 72 + (Tp - 64) + 48, so
+// Tp + 64 entries cover every read (Tp = T rounded up to the 64-key tile); the fwd kernel's LDS
+// is then 32 KB of K/V tiles + 4 (Tp + 64) floats = 40 KB at T = 399: 4 workgroups per CU.
+__host__ __device__ inline int bv_len(int T) { return ((T + 63) & ~63) + 64; }
 NRSE_DEV void bv_stage(float* bv, const float* vec, int T, int q0, int tid) {
   const int len = bv_len(T), nd = 2 * T - 1;
   const int e_lo = T - 1 - q0 - 63;
@@ -440,7 +447,10 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
 }
 
 // ------------------------------------------------------------------------------ bwd: dK, dV, diag
-__global__ __launch_bounds__(256) void attn_bwd_kv_kernel(const nrse_attn_bwd_params p) {
+// 3 waves per SIMD (<= 168 VGPRs; LDS ~50 KB at T = 399 -> 3 workgroups per CU): the element
+// loops are long dependency chains, latency-bound at 2 waves per SIMD
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void attn_bwd_kv_kernel(
+    const nrse_attn_bwd_params p) {
   extern __shared__ __attribute__((aligned(16))) char dyn[];
   char* const qo0 = dyn;  // [2 buffers][Q tile, dO tile], LDS-DMA double buffer
   const int T = p.T, H = p.H, Hd = H * D;
@@ -448,7 +458,8 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(const nrse_attn_bwd_pa
   float* const rowall = reinterpret_cast<float*>(dyn + 4 * TILE_B);  // lse*log2e [Tp], delta [Tp], gate [Tp]
   float* const rbv = rowall + 3 * Tp;                                 // 4 reversed bias copies
   const int bvl = bv_len(T);
-  float* const diag = rbv + 4 * bvl;                                  // [4 lane groups][T + 64 + DPAD]
+  float* const diag = rbv + 4 * bvl;                                  // [diag_len(T)]
+  float* const dtmp = diag + diag_len(T);                             // [4 waves][4 lane rows][64]
   const long long ld3 = 3LL * Hd;
   const BlockPos bp = block_pos((p.T + 63) / 64, p.H);
   const int b = bp.b, h = bp.h;
@@ -503,10 +514,30 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(const nrse_attn_bwd_pa
   // within each 16-lane row (DPP) puts diagonal (i16 - 4g - 16t) or (i16 - 4g - 16t - 16) in
   // lane i16 of row g, so 5 per-lane register accumulators (dacc[j], diagonal x - 4g - 16j
   // relative to the block) collect a 64x64 tile; 4 of them are final after each query block
-  // and go to a per-row LDS array (rows of one wave never share a diagonal within a row array).
-  const int ndiag = T + 64 + DPAD;
-  for (int e = tid; e < 4 * ndiag; e += 256) diag[e] = 0.f;
-  float* mydiag = diag + g * ndiag;
+  // and are folded into the workgroup's diagonal array without LDS atomics (ds_add_f32 cost the
+  // kernel ~100 of its 300 us): every lane stores its 4 sums to its own slots of a per-tile
+  // staging area, and after a barrier one thread per relative diagonal (124 of them) adds the
+  // <= 16 staged values that fall on it.
+  const int ndiag = diag_len(T);
+  const int DPAD = diag_pad(T);
+  for (int e = tid; e < ndiag; e += 256) diag[e] = 0.f;
+  float* const tw = dtmp + (w * 4 + g) * 64;
+  // fold the staged tile of relative diagonals r = 16 w + (slot - 48) - 4 g into diag[cb + r]
+  auto fold = [&](int cb) {
+    __syncthreads();
+    if (tid < 124) {
+      const int r = tid - 60;
+      float s = 0.f;
+#pragma unroll
+      for (int wv = 0; wv < 4; ++wv)
+#pragma unroll
+        for (int gg = 0; gg < 4; ++gg) {
+          const int slot = r - 16 * wv + 4 * gg + 48;
+          if (slot >= 0 && slot < 64) s += dtmp[(wv * 4 + gg) * 64 + slot];
+        }
+      diag[cb + r] += s;
+    }
+  };
   float dacc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
   // rotation by r wraps for lanes i16 >= 16 - r
   const float whi[3] = {i16 >= 15 ? 1.f : 0.f, i16 >= 14 ? 1.f : 0.f, i16 >= 13 ? 1.f : 0.f};
@@ -611,16 +642,20 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(const nrse_attn_bwd_pa
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         dacc[t] += gv[t][0];
+#if NRSE_ATT_ABLATE == 6
+        dacc[t] += gv[t][1] + gv[t][2] + gv[t][3];
+#else
         diag_rot<1>(gv[t][1], wlo[0], whi[0], dacc[t], dacc[t + 1]);
         diag_rot<2>(gv[t][2], wlo[1], whi[1], dacc[t], dacc[t + 1]);
         diag_rot<3>(gv[t][3], wlo[2], whi[2], dacc[t], dacc[t + 1]);
+#endif
       }
-      // diagonals x - 4g - 16j (j < 4) relative to kb0 + 16w - qb are complete
-      const int c0 = kb0 + 16 * w - qb + i16 - 4 * g - dbase;
+      // diagonals i16 - 4g - 16j + 16w (j < 4) relative to kb0 - qb are complete: stage, fold
 #pragma unroll
-      for (int j = 0; j < 4; ++j) atomicAdd(&mydiag[c0 - 16 * j], dacc[j]);
+      for (int j = 0; j < 4; ++j) tw[i16 - 16 * j + 48] = dacc[j];
       dacc[0] = dacc[4];
       dacc[1] = dacc[2] = dacc[3] = dacc[4] = 0.f;
+      fold(kb0 - qb - dbase);
     }
 #endif
 #pragma unroll
@@ -647,19 +682,24 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(const nrse_attn_bwd_pa
       }
     }
   }
-  if (p.diag) {  // the carried accumulator: diagonals x - 4g relative to kb0 + 16w - (last qb + 64)
+  if (p.diag) {  // the carried accumulator: diagonals i16 - 4g + 16w relative to kb0 - (last qb + 64)
     const int qend = ((T + 63) / 64) * 64;
-    atomicAdd(&mydiag[kb0 + 16 * w - qend + i16 - 4 * g - dbase], dacc[0]);
+    __syncthreads();  // the last tile's fold has read the staging area
+    tw[i16 + 48] = dacc[0];
+    tw[i16 + 32] = tw[i16 + 16] = tw[i16] = 0.f;
+    fold(kb0 - qend - dbase);
   }
   __syncthreads();
+#if NRSE_ATT_ABLATE != 4
   if (p.diag) {
     const int nd = 2 * T - 1;
     for (int e = tid; e < ndiag; e += 256) {
       const int dd = dbase + e + T - 1;  // index of d = kj - qi in [0, 2T-1)
-      const float v = diag[e] + diag[ndiag + e] + diag[2 * ndiag + e] + diag[3 * ndiag + e];
+      const float v = diag[e];
       if (dd >= 0 && dd < nd && v != 0.f) atomicAdd(p.diag + (long long)h * nd + dd, v);
     }
   }
+#endif
 }
 
 }  // namespace
@@ -672,7 +712,7 @@ int nrse_attn_fwd_mfma(const nrse_attn_fwd_params* p, hipStream_t st) {
     return NRSE_ERR_ARG;
   }
   const dim3 grid((unsigned)((p->T + 63) / 64 * p->H * p->batch));
-  const size_t lds = 4 * TILE_B + 4 * (size_t)((p->T + BV_EXTRA + 3) & ~3) * sizeof(float);
+  const size_t lds = 4 * TILE_B + 4 * (size_t)bv_len(p->T) * sizeof(float);
   if (lds > 160 * 1024) {
     nrse_set_error("nrse_attn_fwd: T=%d too long for the LDS bias copies", p->T);
     return NRSE_ERR_UNSUPPORTED;
@@ -687,10 +727,10 @@ int nrse_attn_bwd_mfma(const nrse_attn_bwd_params* p, hipStream_t st) {
     return NRSE_ERR_ARG;
   }
   const dim3 grid((unsigned)((p->T + 63) / 64 * p->H * p->batch));
-  const size_t bvl = (size_t)((p->T + BV_EXTRA + 3) & ~3);
+  const size_t bvl = (size_t)bv_len(p->T);
   const size_t lds_q = 4 * TILE_B + 4 * bvl * sizeof(float);
   const size_t lds_kv =
-      4 * TILE_B + (3 * (size_t)((p->T + 63) & ~63) + 4 * bvl + 4 * (size_t)(p->T + 64 + DPAD)) * sizeof(float);
+      4 * TILE_B + (3 * (size_t)((p->T + 63) & ~63) + 4 * bvl + (size_t)(((p->T + 63) & ~63) + 80) + 1024) * sizeof(float);
   if (lds_kv > 160 * 1024) {
     nrse_set_error("nrse_attn_bwd: T=%d too long for the LDS bias copies / diagonal accumulator", p->T);
     return NRSE_ERR_UNSUPPORTED;
@@ -700,3 +740,4 @@ int nrse_attn_bwd_mfma(const nrse_attn_bwd_params* p, hipStream_t st) {
   hipLaunchKernelGGL(attn_bwd_kv_kernel, grid, dim3(256), lds_kv, st, *p);
   return nrse_check_launch("nrse_attn_bwd(mfma)");
 }
+

@@ -327,7 +327,13 @@ extern "C" int nrse_layernorm_bwd(const nrse_ln_bwd_params* p, void* stream) {
   // column sums are accumulated, so the per-block atomics stay ~3 * C * 512
   long long blocks = (p->rows + 3) / 4;
   long long cap = 8192;
-  if (p->dgamma || p->dv_colsum) cap = 512;
+  if (p->dgamma || p->dv_colsum) {
+    // >= 2 blocks per CU; long row sweeps (the conv layers' 4e5 rows) get up to 8 per CU
+    cap = p->rows / 192;
+    cap = cap < 512 ? 512 : (cap > 2048 ? 2048 : cap);
+  }
+  static const long long cap_env = getenv("NRSE_LN_BWD_CAP") ? atoll(getenv("NRSE_LN_BWD_CAP")) : 0;
+  if (cap_env > 0) cap = cap_env;  // tuning experiments (tools/bench_ln.py)
   if (blocks > cap) blocks = cap;
   NRSE_DISPATCH_NK(ln_bwd_kernel, p->C, dim3((unsigned)blocks), (hipStream_t)stream, *p);
   return nrse_check_launch("nrse_layernorm_bwd");
