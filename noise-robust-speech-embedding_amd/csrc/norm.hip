@@ -49,7 +49,7 @@ NRSE_DEV void store4(void* p, int dt, long long i, const float* o) {
 template <int NK>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const nrse_ln_fwd_params p) {
   const int lane = threadIdx.x & 63;
-  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const long long row = (long long)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (row >= p.rows) return;
   const int C = p.C;
   float v[NK][CH];
@@ -126,14 +126,14 @@ NRSE_DEV float load_dy(const nrse_ln_bwd_params& p, long long row, int c, float*
 // is not read back. gamma / beta / dv column sums: per-lane accumulators across the rows of a
 // wave, reduced over the block's 4 waves in one 16 KB LDS buffer, one f32 atomic per column and
 // block.
-template <int NK>
+template <int NK, bool RES>
 struct LnRow {
-  float x[NK][CH], dy[NK][CH], r[NK][CH];
+  float x[NK][CH], dy[NK][CH], r[RES ? NK : 1][CH];
   float mean, rstd;
 };
 
-template <int NK>
-NRSE_DEV void ln_bwd_load(const nrse_ln_bwd_params& p, long long row, int lane, LnRow<NK>& b) {
+template <int NK, bool RES>
+NRSE_DEV void ln_bwd_load(const nrse_ln_bwd_params& p, long long row, int lane, LnRow<NK, RES>& b) {
   b.mean = p.mean[row];
   b.rstd = p.rstd[row];
 #pragma unroll
@@ -141,27 +141,35 @@ NRSE_DEV void ln_bwd_load(const nrse_ln_bwd_params& p, long long row, int lane, 
     const int c0 = (k * 64 + lane) * CH;
     load4(p.x, p.x_dtype, row * p.C + c0, b.x[k]);
     load_dy(p, row, c0, b.dy[k]);
-    if (p.resid) V4<float>::load(p.resid + row * p.C + c0, b.r[k]);
+    if constexpr (RES) {
+      if (p.resid) V4<float>::load(p.resid + row * p.C + c0, b.r[k]);
+    }
   }
 }
 
-template <int NK>
+// RES: the encoder-layer form (residual input, fused dropout-cast consumer); !RES (conv / feature
+// projection LNs) drops their registers: 137 -> fewer VGPRs, more waves for the long row sweeps
+template <int NK, bool RES>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const nrse_ln_bwd_params p) {
   __shared__ float red[4][NK * 64 * CH];
   const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: row math (col2im divisions) on the SALU
   const int C = p.C;
-  const bool fuse = p.dv != nullptr;
+  const bool fuse = RES && p.dv != nullptr;
   const uint32_t key = site_key(p.dv_seed);
   const uint32_t thr = dropout_threshold(p.dv_p);
   const float dsc = p.dv_p > 0.f ? 1.f / (1.f - p.dv_p) : 1.f;
-  float dg[NK][CH], db[NK][CH], dc[NK][CH];
+  float dg[NK][CH], db[NK][CH], dc[RES ? NK : 1][CH];
 #pragma unroll
   for (int k = 0; k < NK; ++k)
 #pragma unroll
-    for (int e = 0; e < CH; ++e) dg[k][e] = db[k][e] = dc[k][e] = 0.f;
+    for (int e = 0; e < CH; ++e) dg[k][e] = db[k][e] = 0.f;
+#pragma unroll
+  for (int k = 0; k < (RES ? NK : 1); ++k)
+#pragma unroll
+    for (int e = 0; e < CH; ++e) dc[k][e] = 0.f;
 
-  auto compute = [&](const LnRow<NK>& b, long long row) {
+  auto compute = [&](const LnRow<NK, RES>& b, long long row) {
     float xh[NK][CH], g[NK][CH];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -196,7 +204,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const nrse_ln_bwd_params p)
 #pragma unroll
       for (int e = 0; e < CH; ++e) {
         o[e] = b.rstd * (g[k][e] - s1 - xh[k][e] * s2);
-        if (p.resid) o[e] += b.r[k][e];
+        if constexpr (RES) {
+          if (p.resid) o[e] += b.r[RES ? k : 0][e];
+        }
       }
       store4(p.dx, p.dx_dtype, row * C + c0, o);
       if (fuse) {
@@ -206,7 +216,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const nrse_ln_bwd_params p)
           for (int e = 0; e < CH; ++e) o[e] = dropout_keep(key, (uint32_t)(i + e), thr) ? o[e] * dsc : 0.f;
         }
 #pragma unroll
-        for (int e = 0; e < CH; ++e) dc[k][e] += o[e];
+        for (int e = 0; e < CH; ++e) dc[RES ? k : 0][e] += o[e];
         store4(p.dv, p.dv_dtype, i, o);
       }
     }
@@ -214,7 +224,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const nrse_ln_bwd_params p)
 
   const long long nw = (long long)gridDim.x * 4;
   long long row = (long long)blockIdx.x * 4 + w;
-  LnRow<NK> ba, bb;
+  LnRow<NK, RES> ba, bb;
   if (row < p.rows) ln_bwd_load(p, row, lane, ba);
   for (; row < p.rows; row += 2 * nw) {
     const long long rb = row + nw;
@@ -225,7 +235,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const nrse_ln_bwd_params p)
     compute(bb, rb);
   }
 
-  auto reduce = [&](float (&acc)[NK][CH], float* dst) {
+  auto reduce = [&](auto& acc, float* dst) {
 #pragma unroll
     for (int k = 0; k < NK; ++k)
 #pragma unroll
@@ -238,7 +248,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const nrse_ln_bwd_params p)
     reduce(dg, p.dgamma);
     reduce(db, p.dbeta);
   }
-  if (fuse && p.dv_colsum) reduce(dc, p.dv_colsum);
+  if constexpr (RES) {
+    if (fuse && p.dv_colsum) reduce(dc, p.dv_colsum);
+  }
 }
 
 // Final LN + time-mean: grid (ceil(T / RPB), batch); 4 waves, each a row at a time.
@@ -335,7 +347,17 @@ extern "C" int nrse_layernorm_bwd(const nrse_ln_bwd_params* p, void* stream) {
   static const long long cap_env = getenv("NRSE_LN_BWD_CAP") ? atoll(getenv("NRSE_LN_BWD_CAP")) : 0;
   if (cap_env > 0) cap = cap_env;  // tuning experiments (tools/bench_ln.py)
   if (blocks > cap) blocks = cap;
-  NRSE_DISPATCH_NK(ln_bwd_kernel, p->C, dim3((unsigned)blocks), (hipStream_t)stream, *p);
+  const dim3 grid((unsigned)blocks);
+  hipStream_t st = (hipStream_t)stream;
+  const bool res = p->resid || p->dv;
+  switch (p->C / 256) {
+    case 1: if (res) hipLaunchKernelGGL((ln_bwd_kernel<1, true>), grid, dim3(256), 0, st, *p);
+            else hipLaunchKernelGGL((ln_bwd_kernel<1, false>), grid, dim3(256), 0, st, *p); break;
+    case 2: if (res) hipLaunchKernelGGL((ln_bwd_kernel<2, true>), grid, dim3(256), 0, st, *p);
+            else hipLaunchKernelGGL((ln_bwd_kernel<2, false>), grid, dim3(256), 0, st, *p); break;
+    default: if (res) hipLaunchKernelGGL((ln_bwd_kernel<4, true>), grid, dim3(256), 0, st, *p);
+             else hipLaunchKernelGGL((ln_bwd_kernel<4, false>), grid, dim3(256), 0, st, *p); break;
+  }
   return nrse_check_launch("nrse_layernorm_bwd");
 }
 

@@ -47,3 +47,12 @@ us = timeit(lambda: K.ln_bwd(G, xc, gc, mc, rc, dpre, beta=bc, gelu=True, dgamma
                              col=(k, s, Tout, Tin), rows=B * Tin), iters=10)
 byt = B * Tin * Cin * 2 * 2 + B * Tout * k * Cin * 2
 print(f"conv1 LN+GELU bwd col2im 409568x512: {us:.1f} us  {byt / us / 1e3:.0f} GB/s", flush=True)
+if os.environ.get("LN_VARIANTS"):
+    us = timeit(lambda: K.ln_bwd(G, xc, gc, mc, rc, dpre, beta=bc, gelu=False, dgamma=dgc, dbeta=dbc,
+                                 mode=_lib.DY_COL2IM, col=(k, s, Tout, Tin), rows=B * Tin), iters=10)
+    print(f"  variant no GELU: {us:.1f} us", flush=True)
+    dyd = torch.randn(B * Tin, Cin, device=dev).to(torch.bfloat16)
+    us = timeit(lambda: K.ln_bwd(dyd, xc, gc, mc, rc, dpre, beta=bc, gelu=True, dgamma=dgc, dbeta=dbc), iters=10)
+    print(f"  variant direct dy (bf16), GELU: {us:.1f} us", flush=True)
+    us = timeit(lambda: K.ln_bwd(dyd, xc, gc, mc, rc, dpre), iters=10)
+    print(f"  variant direct dy, no GELU, no dgamma: {us:.1f} us", flush=True)
