@@ -89,6 +89,25 @@ def gemm_traffic():
         return None
 
 
+def gemm_mfma_busy():
+    """Matrix-pipe busy fraction of the 256x256 GEMM kernels from the committed counter pass
+    (tools/pmc_sq.sh -> profiles/r02_pmc_sq_table.json): SQ_VALU_MFMA_BUSY_CYCLES over all
+    SIMD-cycles of the launch (GRBM_GUI_ACTIVE / 8 XCDs x 256 CUs x 4 SIMDs), per step shape,
+    isolated launches. None if absent."""
+    path = os.path.join(ROOT, "profiles", "r02_pmc_sq_table.json")
+    try:
+        with open(path) as fh:
+            t = json.load(fh)
+        out = {}
+        for k, v in t.items():
+            if k.startswith("gemm256_kernel") and "mfma_busy" in v:
+                name, grid, _ = k.rsplit(" ", 2)
+                out[f"{name} ({int(grid) // 512} workgroups)"] = round(v["mfma_busy"], 3)
+        return out
+    except (OSError, KeyError, ValueError, IndexError):
+        return None
+
+
 def bench_emotion(args):
     """configs[3]: one dimensional-emotion fine-tune iteration over the frozen WavLM-Large encoder
     (default_wavlm-large_emotion_dim_ft.yaml: batch 36, 5 s, hidden 1024, dropout 0.3, AdamW
@@ -289,6 +308,7 @@ def main():
                      "frac": round(achieved_tfs / (BF16_DENSE_PEAK_TFS if cdt == torch.bfloat16 else F32_MFMA_PEAK_TFS),
                                    4),
                      "traffic": gemm_traffic(), "traffic_unit": "HBM bytes per launch (PMC, profiles/r01_gemm_traffic.json)",
+                     "mfma_busy_pmc": gemm_mfma_busy(),
                      "algorithmic_bytes_per_launch": round(gbytes / max(n_launch, 1)),
                      "avg_launch_ms": round(gms / max(n_launch, 1), 4), "launches": n_launch,
                      "gemm_share_of_step": round(gms / (dt * 1e3), 3)},
