@@ -254,11 +254,13 @@ int nrse_conv0_bwd(const nrse_conv0_params* p, void* stream);
  * w[o, i, j] = g[j] * v[o, i, j] / ||v[:, :, j]||.  Writes the two GEMM weight layouts
  *   wf [G][cpg][K*cpg]: wf[g][o][j*cpg + i]        (forward:  B operand, n = o)
  *   wd [G][cpg][K*cpg]: wd[g][i][j'*cpg + o] = w[g*cpg+o][i][K-1-j']  (dgrad, flipped taps)
- * and norms[K]. Backward takes dWf in the wf layout (f32) and produces dg [K], dv [H, cpg, K]. */
+ * and norms[K]. Backward takes dWf in the wf layout (f32) and produces dg [K], dv [H, cpg, K].
+ * part: optional scratch of 256 * K doubles (K <= 256 dividing 256) for the coalesced two-stage
+ * per-tap reductions (ordered, deterministic); null -> one strided block per tap (slow). */
 int nrse_weight_norm_fwd(const float* g, const float* v, void* wf, void* wd, int w_dtype, float* norms, int H,
-                         int cpg, int K, void* stream);
+                         int cpg, int K, double* part, void* stream);
 int nrse_weight_norm_bwd(const float* dWf, const float* g, const float* v, const float* norms, float* dg, float* dv,
-                         float* scratch, int H, int cpg, int K, void* stream);
+                         float* scratch, int H, int cpg, int K, double* part, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Elementwise / data-movement kernels of the step.

@@ -252,6 +252,62 @@ __global__ __launch_bounds__(256) void wn_norm_kernel(const float* __restrict__ 
   }
 }
 
+// Coalesced form for K <= 256 dividing 256: thread (jj = tid % K, eo = tid / K) sums e = eo,
+// eo + 256/K, ... over this block's e range, the partials of one j reduced in LDS, one double per
+// (block, j) stored; wn_norm_final_kernel adds the blocks in order (deterministic). v is read in
+// full 512-B rows (the [H*cpg][K] layout's K-contiguous rows).
+__global__ __launch_bounds__(256) void wn_norm_part_kernel(const float* __restrict__ v, const float* __restrict__ dWf,
+                                                           double* __restrict__ part, int H, int cpg, int K,
+                                                           long long epb) {
+  __shared__ double red[256];
+  const int tid = threadIdx.x;
+  const int j = tid % K, eo = tid / K, es = 256 / K;
+  const long long n = (long long)H * cpg;
+  const long long e0 = (long long)blockIdx.x * epb, e1 = min(n, e0 + epb);
+  double a = 0.0;
+  for (long long e = e0 + eo; e < e1; e += es) {
+    const float x = v[e * K + j];
+    if (dWf) {
+      const long long go = e / cpg;
+      const int i = (int)(e - go * cpg);
+      a += (double)x * dWf[go * (long long)K * cpg + (long long)j * cpg + i];
+    } else {
+      a += (double)x * x;
+    }
+  }
+  red[tid] = a;
+  __syncthreads();
+  if (tid < K) {
+    double s = 0.0;
+    for (int q = 0; q < es; ++q) s += red[q * K + tid];
+    part[(long long)blockIdx.x * K + tid] = s;
+  }
+}
+
+__global__ void wn_norm_final_kernel(const double* __restrict__ part, int nb, int K, float* __restrict__ norms,
+                                     float* __restrict__ sdot) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= K) return;
+  double s = 0.0;
+  for (int b = 0; b < nb; ++b) s += part[(long long)b * K + j];
+  if (sdot) sdot[j] = (float)s;
+  else norms[j] = (float)sqrt(s);
+}
+
+// norms[j] = ||v[:, :, j]|| (dWf null) or sdot[j] = <v[:, :, j], dW[:, :, j]> (dWf layout [g][o][j*cpg + i])
+constexpr int WN_NB = 256;  // blocks of the two-stage reduction (part holds WN_NB * K doubles)
+void wn_norm(hipStream_t st, const float* v, float* norms, const float* dWf, float* sdot, int H, int cpg, int K,
+             double* part) {
+  if (part && K <= 256 && 256 % K == 0) {
+    const long long n = (long long)H * cpg;
+    const long long epb = (n + WN_NB - 1) / WN_NB;
+    hipLaunchKernelGGL(wn_norm_part_kernel, dim3(WN_NB), dim3(256), 0, st, v, dWf, part, H, cpg, K, epb);
+    hipLaunchKernelGGL(wn_norm_final_kernel, dim3((K + 255) / 256), dim3(256), 0, st, part, WN_NB, K, norms, sdot);
+    return;
+  }
+  hipLaunchKernelGGL(wn_norm_kernel, dim3(K), dim3(256), 0, st, v, norms, dWf, sdot, H, cpg, K);
+}
+
 template <typename T>
 __global__ void wn_apply_kernel(const float* __restrict__ g, const float* __restrict__ v,
                                 const float* __restrict__ norms, T* __restrict__ wf, T* __restrict__ wd, int H, int cpg,
@@ -331,11 +387,10 @@ extern "C" int nrse_conv0_bwd(const nrse_conv0_params* p, void* stream) {
 }
 
 extern "C" int nrse_weight_norm_fwd(const float* g, const float* v, void* wf, void* wd, int w_dtype, float* norms,
-                                    int H, int cpg, int K, void* stream) {
+                                    int H, int cpg, int K, double* part, void* stream) {
   NRSE_REQUIRE(g && v && wf && wd && norms && H > 0 && cpg > 0 && K > 0 && H % cpg == 0, "nrse_weight_norm_fwd: bad args");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(wn_norm_kernel, dim3(K), dim3(256), 0, st, v, norms, (const float*)nullptr, (float*)nullptr, H,
-                     cpg, K);
+  wn_norm(st, v, norms, nullptr, nullptr, H, cpg, K, part);
   const long long total = (long long)H * cpg * K;
   int blocks = (int)((total + 255) / 256);
   if (blocks > 4096) blocks = 4096;
@@ -349,10 +404,10 @@ extern "C" int nrse_weight_norm_fwd(const float* g, const float* v, void* wf, vo
 }
 
 extern "C" int nrse_weight_norm_bwd(const float* dWf, const float* g, const float* v, const float* norms, float* dg,
-                                    float* dv, float* scratch, int H, int cpg, int K, void* stream) {
+                                    float* dv, float* scratch, int H, int cpg, int K, double* part, void* stream) {
   NRSE_REQUIRE(dWf && g && v && norms && dg && dv && scratch, "nrse_weight_norm_bwd: bad args");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(wn_norm_kernel, dim3(K), dim3(256), 0, st, v, (float*)nullptr, dWf, scratch, H, cpg, K);
+  wn_norm(st, v, nullptr, dWf, scratch, H, cpg, K, part);
   const long long total = (long long)H * cpg * K;
   int blocks = (int)((total + 255) / 256);
   if (blocks > 4096) blocks = 4096;

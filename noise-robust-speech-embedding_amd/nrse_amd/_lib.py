@@ -126,8 +126,8 @@ _SIGNATURES = {
     "nrse_attn_bwd": ([_P(AttnBwdParams), c_vp], c_int),
     "nrse_conv0_fwd": ([_P(Conv0Params), c_vp], c_int),
     "nrse_conv0_bwd": ([_P(Conv0Params), c_vp], c_int),
-    "nrse_weight_norm_fwd": ([c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_vp], c_int),
-    "nrse_weight_norm_bwd": ([c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp], c_int),
+    "nrse_weight_norm_fwd": ([c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_vp, c_vp], c_int),
+    "nrse_weight_norm_bwd": ([c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp], c_int),
     "nrse_specaug_pad": ([c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
     "nrse_pad_rows": ([c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
     "nrse_specaug_bwd": ([c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_f, c_u32, c_vp], c_int),

@@ -398,14 +398,21 @@ def conv0_bwd(wav, w, gamma, beta, mean, rstd, dy, dw, dgamma, dbeta, T0, k, s, 
     swap12(dwT, dw, 1, k, C, accumulate=True)
 
 
+def _wn_part(v, K):
+    """Scratch of the coalesced two-stage per-tap reduction (256 * K doubles) or None."""
+    return torch.empty(256 * K, device=v.device, dtype=torch.float64) if K <= 256 and 256 % K == 0 else None
+
+
 def weight_norm_fwd(g, v, wf, wd, norms, H, cpg, K):
+    part = _wn_part(v, K)
     _call("nrse_weight_norm_fwd", ptr(g), ptr(v), ptr(wf), ptr(wd), dtype_code(wf), ptr(norms), H, cpg, K,
-          stream_ptr())
+          ptr(part), stream_ptr())
 
 
 def weight_norm_bwd(dWf, g, v, norms, dg, dv, scratch, H, cpg, K):
+    part = _wn_part(v, K)
     _call("nrse_weight_norm_bwd", ptr(dWf), ptr(g), ptr(v), ptr(norms), ptr(dg), ptr(dv), ptr(scratch), H, cpg, K,
-          stream_ptr())
+          ptr(part), stream_ptr())
 
 
 # ----------------------------------------------------------------------------- elementwise
