@@ -11,6 +11,18 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 #define NRSE_DEV __device__ __forceinline__
 
+// Load through an explicit global (addrspace 1) pointer: a generic pointer the compiler cannot
+// prove global becomes a flat load, which also counts in lgkmcnt, so every LDS / shuffle wait
+// after it (lgkmcnt(0)) waits for the memory load too.
+template <typename T>
+NRSE_DEV T ldg(const T* p) {  // scalars and ext-vector types
+  return *(const __attribute__((address_space(1))) T*)p;
+}
+NRSE_DEV uint2 ldg(const uint2* p) {  // HIP vector struct: load as an ext vector, bit-cast
+  typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint2, *(const __attribute__((address_space(1))) u32x2v*)p);
+}
+
 NRSE_DEV float bf2f(bf16_t x) { return __uint_as_float(((uint32_t)x) << 16); }
 NRSE_DEV bf16_t f2bf(float x) {
   __bf16 b = (__bf16)x;  // v_cvt_pk_bf16_f32: round-to-nearest-even, NaN stays NaN

@@ -115,105 +115,210 @@ NRSE_DEV void ld4(const void* p, int dt, long long i, float* o) {
   }
 }
 
-template <int NQ>
-__global__ __launch_bounds__(256) void conv0_bwd_kernel(const nrse_conv0_params p) {
+// conv0 backward: LN + GELU backward, the conv weight gradient dW[j][c] = sum_rows dc[c] * x[j],
+// dgamma, dbeta. VALU-bound (conv recompute, GELU', dW: ~50 operations per element), so:
+//  - a row is shared by C/256 waves (lane = 4 channels, 40 dW accumulators instead of 80), the
+//    two waves of a C = 512 row exchange their LN partial sums through LDS (one barrier per row,
+//    double-buffered slots), which keeps the kernel near 128 VGPRs (4 waves per SIMD);
+//  - the conv and dW FMAs run as packed fp32 (v_pk_fma_f32: two channels per instruction);
+//  - the next row's operands (10 samples, mean / rstd, up to two col2im taps of dy) are loaded
+//    while the current row computes, the two taps into separate registers (no load -> add chain).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// One row's operands. BF (bf16 dy, the bf16 step): raw 8-byte words, unpacked at use, so no
+// unpack (and no wait for the load) sits between the prefetch and the use. Every load is issued
+// on every row from a valid address (clamped row, dummy tap offset + flag): a load skipped on
+// some path leaves the wait-count pass no static count of the loads in flight.
+template <bool BF>
+struct C0Row {
+  float xs[KMAX];
+  float mean, rstd;
+  uint2 r0, r1;     // BF
+  f32x4 f0, f1;     // !BF
+  bool v0, v1;
+};
+
+template <bool BF>
+NRSE_DEV void c0_load(const nrse_conv0_params& p, long long row, int c0, bool col2, C0Row<BF>& r) {
+  const long long b = row / p.T0;
+  const int t = (int)(row - b * p.T0);
+  const float* x = p.wav + b * p.L + (long long)t * p.s;
+#pragma unroll
+  for (int j = 0; j < KMAX; ++j) r.xs[j] = j < p.k ? ldg(x + j) : 0.f;
+  r.mean = ldg(p.mean + row);
+  r.rstd = ldg(p.rstd + row);
+  long long o0 = row * p.C, o1 = 0;
+  bool v0 = true, v1 = false;
+  if (p.dy_mode == NRSE_DY_COL2IM) {
+    // taps j0 = t mod s and j0 + s (k <= 2s): col row (t - j) / s of tap j
+    const int j0 = t % p.col_s;
+    const int j1 = j0 + p.col_s;
+    const int t0 = (t - j0) / p.col_s, t1 = (t - j1) / p.col_s;
+    v0 = j0 < p.col_k && t0 < p.col_tout;
+    v1 = j1 < p.col_k && t >= j1 && t1 < p.col_tout;
+    o0 = v0 ? ((b * p.col_tout + t0) * p.col_k + j0) * (long long)p.C : 0;
+    o1 = v1 ? ((b * p.col_tout + t1) * p.col_k + j1) * (long long)p.C : 0;
+  }
+  r.v0 = v0;
+  r.v1 = v1;
+  if constexpr (BF) {
+    const bf16_t* dy = (const bf16_t*)p.dy;
+    r.r0 = ldg(reinterpret_cast<const uint2*>(dy + o0 + c0));
+    r.r1 = ldg(reinterpret_cast<const uint2*>(dy + o1 + c0));
+  } else {
+    const float* dy = (const float*)p.dy;
+    r.f0 = ldg(reinterpret_cast<const f32x4*>(dy + o0 + c0));
+    r.f1 = ldg(reinterpret_cast<const f32x4*>(dy + o1 + c0));
+  }
+}
+
+NRSE_DEV f32x4 unpack_bf4v(uint2 v) {
+  return f32x4{__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xffff0000u), __uint_as_float(v.y << 16),
+               __uint_as_float(v.y & 0xffff0000u)};
+}
+
+// generic col2im fold (k > 2s): the tap loop, dy summed into f0 (rare geometry; no prefetch)
+NRSE_DEV f32x4 c0_dy_generic(const nrse_conv0_params& p, long long row, int c0) {
+  const long long b = row / p.T0;
+  const int t = (int)(row - b * p.T0);
+  f32x4 d = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < p.col_k; ++j) {
+    const int dd = t - j;
+    if (dd < 0) break;
+    if (dd % p.col_s) continue;
+    const int tt = dd / p.col_s;
+    if (tt >= p.col_tout) continue;
+    const long long i = ((b * p.col_tout + tt) * p.col_k + j) * (long long)p.C + c0;
+    d += p.dy_dtype == NRSE_BF16 ? unpack_bf4v(*reinterpret_cast<const uint2*>((const bf16_t*)p.dy + i))
+                                 : *reinterpret_cast<const f32x4*>((const float*)p.dy + i);
+  }
+  return d;
+}
+
+template <int WPR, bool BF>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void conv0_bwd_kernel(const nrse_conv0_params p) {
+  constexpr int RPB = 4 / WPR;  // rows in flight per block
   __shared__ __attribute__((aligned(16))) float wT[KMAX * 512];
-  __shared__ float red[4][NQ * 256];
+  __shared__ float red[RPB][WPR * 256];
+  __shared__ f32x2 xch[2][4];  // [row parity][wave]: the wave's (sum g, sum g*xh)
   const int lane = threadIdx.x & 63;
-  const int wv = threadIdx.x >> 6;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int rg = w / WPR, half = w % WPR;
   const int C = p.C;
+  const int c0 = (half * 64 + lane) * 4;
   load_wT(wT, p.w, C, p.k);
   __syncthreads();
-  float dw[NQ][4][KMAX];
-  float ga[NQ][4], be[NQ][4], dga[NQ][4], dbe[NQ][4];
+  f32x2 dw[KMAX][2], dga[2], dbe[2], ga[2], be[2];
 #pragma unroll
-  for (int q = 0; q < NQ; ++q)
+  for (int h = 0; h < 2; ++h) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int c = (q * 64 + lane) * 4 + e;
-#pragma unroll
-      for (int j = 0; j < KMAX; ++j) dw[q][e][j] = 0.f;
-      ga[q][e] = p.gamma[c];
-      be[q][e] = p.beta[c];
-      dga[q][e] = dbe[q][e] = 0.f;
-    }
-  const long long rows = (long long)p.batch * p.T0;
-  const long long nw = (long long)gridDim.x * 4;
-  const bool s2 = p.col_s == 2;
-  for (long long r0 = (long long)blockIdx.x * 4 + wv; r0 < rows; r0 += nw) {
-    const long long row = uniform_ll(r0);
-    const long long b = row / p.T0;
-    const int t = (int)(row - b * p.T0);
-    const float* x = p.wav + b * p.L + (long long)t * p.s;
-    float xs[KMAX];
-#pragma unroll
-    for (int j = 0; j < KMAX; ++j) xs[j] = j < p.k ? x[j] : 0.f;
-    const float mean = p.mean[row], rstd = p.rstd[row];
-    float y[NQ][4];
-    conv_row<NQ>(wT, C, lane, xs, y);
-    float xh[NQ][4], g[NQ][4];
-    float s1 = 0.f, s2v = 0.f;
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const int c0 = (q * 64 + lane) * 4;
-      float dy[4] = {0.f, 0.f, 0.f, 0.f};
-      if (p.dy_mode == NRSE_DY_DIRECT) {
-        ld4(p.dy, p.dy_dtype, row * C + c0, dy);
-      } else {
-        const long long kc = (long long)p.col_k * C;
-        for (int j = 0; j < p.col_k; ++j) {
-          const int d = t - j;
-          if (d < 0) break;
-          if (s2 ? (d & 1) : (d % p.col_s)) continue;
-          const int tt = s2 ? (d >> 1) : d / p.col_s;
-          if (tt >= p.col_tout) continue;
-          float u[4];
-          ld4(p.dy, p.dy_dtype, (b * p.col_tout + tt) * kc + (long long)j * C + c0, u);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) dy[e] += u[e];
-        }
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        xh[q][e] = (y[q][e] - mean) * rstd;
-        const float gg = dy[e] * gelu_grad_f(xh[q][e] * ga[q][e] + be[q][e]);
-        dga[q][e] += gg * xh[q][e];
-        dbe[q][e] += gg;
-        g[q][e] = gg * ga[q][e];
-        s1 += g[q][e];
-        s2v += g[q][e] * xh[q][e];
-      }
-    }
-    s1 = wave_sum(s1) / C;
-    s2v = wave_sum(s2v) / C;
-#pragma unroll
-    for (int q = 0; q < NQ; ++q)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float dc = rstd * (g[q][e] - s1 - xh[q][e] * s2v);
-#pragma unroll
-        for (int j = 0; j < KMAX; ++j) dw[q][e][j] += dc * xs[j];
-      }
+    for (int j = 0; j < KMAX; ++j) dw[j][h] = f32x2{0.f, 0.f};
+    dga[h] = dbe[h] = f32x2{0.f, 0.f};
+    ga[h] = f32x2{p.gamma[c0 + 2 * h], p.gamma[c0 + 2 * h + 1]};
+    be[h] = f32x2{p.beta[c0 + 2 * h], p.beta[c0 + 2 * h + 1]};
   }
-  // block reduce: dw (C*k), dgamma, dbeta
+  const long long rows = (long long)p.batch * p.T0;
+  const long long last = rows - 1;
+  const long long stride = (long long)gridDim.x * RPB;
+  const long long first = (long long)blockIdx.x * RPB;
+  // uniform trip count over the block (the row exchange is a block barrier)
+  const long long iters = first < rows ? (rows - first + stride - 1) / stride : 0;
+  const bool generic = p.dy_mode == NRSE_DY_COL2IM && p.col_k > 2 * p.col_s;
+  const float invC = 1.f / C;
+
+  auto step = [&](const C0Row<BF>& cur, C0Row<BF>& nxt, long long it, long long row) {
+    const long long rn = row + stride;
+    c0_load<BF>(p, rn < last ? rn : last, c0, !generic, nxt);
+    __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this row's math
+    const bool live = row < rows;
+    f32x2 xh[2], g[2];
+    float s1 = 0.f, s2 = 0.f;
+    if (live) {
+      f32x4 dd;
+      if (generic) {
+        dd = c0_dy_generic(p, row, c0);
+      } else if constexpr (BF) {
+        const uint2 z = make_uint2(0u, 0u);
+        dd = unpack_bf4v(cur.v0 ? cur.r0 : z) + unpack_bf4v(cur.v1 ? cur.r1 : z);
+      } else {
+        const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+        dd = (cur.v0 ? cur.f0 : z) + (cur.v1 ? cur.f1 : z);
+      }
+      f32x2 y[2] = {f32x2{0.f, 0.f}, f32x2{0.f, 0.f}};
+#pragma unroll
+      for (int j = 0; j < KMAX; ++j) {  // weights from LDS: one ds_read_b128 per tap
+        const float4 q = *reinterpret_cast<const float4*>(wT + j * C + c0);
+        y[0] += f32x2{q.x, q.y} * cur.xs[j];
+        y[1] += f32x2{q.z, q.w} * cur.xs[j];
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        xh[h] = (y[h] - cur.mean) * cur.rstd;
+        const f32x2 z = xh[h] * ga[h] + be[h];
+        const f32x2 dy = h == 0 ? f32x2{dd.x, dd.y} : f32x2{dd.z, dd.w};
+        const f32x2 gg = dy * f32x2{gelu_grad_f(z.x), gelu_grad_f(z.y)};
+        dga[h] += gg * xh[h];
+        dbe[h] += gg;
+        g[h] = gg * ga[h];
+        s1 += g[h].x + g[h].y;
+        const f32x2 gx = g[h] * xh[h];
+        s2 += gx.x + gx.y;
+      }
+    }
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+    if constexpr (WPR > 1) {
+      const int par = (int)(it & 1);
+      if (lane == 0) xch[par][w] = f32x2{s1, s2};
+      __syncthreads();
+      s1 = 0.f;
+      s2 = 0.f;
+#pragma unroll
+      for (int q = 0; q < WPR; ++q) {  // fixed order: both waves of the row get identical sums
+        const f32x2 v = xch[par][rg * WPR + q];
+        s1 += v.x;
+        s2 += v.y;
+      }
+    }
+    if (live) {
+      s1 *= invC;
+      s2 *= invC;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x2 dc = (g[h] - s1 - xh[h] * s2) * cur.rstd;
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) dw[j][h] += dc * cur.xs[j];
+      }
+    }
+  };
+
+  C0Row<BF> ra, rb;
+  long long row = first + rg;
+  if (iters > 0) c0_load<BF>(p, row < last ? row : last, c0, !generic, ra);
+  for (long long it = 0; it < iters; it += 2) {  // two row buffers, alternated (no copies)
+    step(ra, rb, it, row);
+    row += stride;
+    if (it + 1 >= iters) break;
+    step(rb, ra, it + 1, row);
+    row += stride;
+  }
+  // block reduce: dw (k x C), dgamma, dbeta (the RPB row groups hold disjoint rows)
   for (int j = 0; j < p.k + 2; ++j) {
 #pragma unroll
-    for (int q = 0; q < NQ; ++q)
+    for (int h = 0; h < 2; ++h) {
+      f32x2 v = dbe[h];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float v;
-        if (j < p.k) {
-          v = 0.f;
-#pragma unroll
-          for (int jj = 0; jj < KMAX; ++jj) if (jj == j) v = dw[q][e][jj];
-        } else {
-          v = (j == p.k) ? dga[q][e] : dbe[q][e];
-        }
-        red[wv][(q * 64 + lane) * 4 + e] = v;
-      }
+      for (int jj = 0; jj < KMAX; ++jj)
+        if (jj == j) v = dw[jj][h];
+      if (j == p.k) v = dga[h];
+      red[rg][c0 + 2 * h] = v.x;
+      red[rg][c0 + 2 * h + 1] = v.y;
+    }
     __syncthreads();
     for (int c = threadIdx.x; c < C; c += 256) {
-      const float v = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+      float v = 0.f;
+#pragma unroll
+      for (int q = 0; q < RPB; ++q) v += red[q][c];
       if (j < p.k) atomicAdd(p.dw + (long long)j * C + c, v);  // [k][C]: 256-B atomic wave-instructions
       else if (j == p.k) atomicAdd(p.dgamma + c, v);
       else atomicAdd(p.dbeta + c, v);
@@ -265,6 +370,7 @@ __global__ __launch_bounds__(256) void wn_norm_part_kernel(const float* __restri
   const long long n = (long long)H * cpg;
   const long long e0 = (long long)blockIdx.x * epb, e1 = min(n, e0 + epb);
   double a = 0.0;
+#pragma unroll 8
   for (long long e = e0 + eo; e < e1; e += es) {
     const float x = v[e * K + j];
     if (dWf) {
@@ -284,14 +390,22 @@ __global__ __launch_bounds__(256) void wn_norm_part_kernel(const float* __restri
   }
 }
 
-__global__ void wn_norm_final_kernel(const double* __restrict__ part, int nb, int K, float* __restrict__ norms,
-                                     float* __restrict__ sdot) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= K) return;
+// one block per tap: thread b loads block b's partial, fixed-order tree (wave shuffles, then the
+// 4 wave sums in order): deterministic, one load latency instead of nb dependent ones
+__global__ __launch_bounds__(256) void wn_norm_final_kernel(const double* __restrict__ part, int nb, int K,
+                                                            float* __restrict__ norms, float* __restrict__ sdot) {
+  __shared__ double red[4];
+  const int j = blockIdx.x;
   double s = 0.0;
-  for (int b = 0; b < nb; ++b) s += part[(long long)b * K + j];
-  if (sdot) sdot[j] = (float)s;
-  else norms[j] = (float)sqrt(s);
+  for (int b = threadIdx.x; b < nb; b += 256) s += part[(long long)b * K + j];
+  s = wave_sum_d(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double t = red[0] + red[1] + red[2] + red[3];
+    if (sdot) sdot[j] = (float)t;
+    else norms[j] = (float)sqrt(t);
+  }
 }
 
 // norms[j] = ||v[:, :, j]|| (dWf null) or sdot[j] = <v[:, :, j], dW[:, :, j]> (dWf layout [g][o][j*cpg + i])
@@ -302,7 +416,7 @@ void wn_norm(hipStream_t st, const float* v, float* norms, const float* dWf, flo
     const long long n = (long long)H * cpg;
     const long long epb = (n + WN_NB - 1) / WN_NB;
     hipLaunchKernelGGL(wn_norm_part_kernel, dim3(WN_NB), dim3(256), 0, st, v, dWf, part, H, cpg, K, epb);
-    hipLaunchKernelGGL(wn_norm_final_kernel, dim3((K + 255) / 256), dim3(256), 0, st, part, WN_NB, K, norms, sdot);
+    hipLaunchKernelGGL(wn_norm_final_kernel, dim3(K), dim3(256), 0, st, part, WN_NB, K, norms, sdot);
     return;
   }
   hipLaunchKernelGGL(wn_norm_kernel, dim3(K), dim3(256), 0, st, v, norms, dWf, sdot, H, cpg, K);
@@ -375,12 +489,20 @@ extern "C" int nrse_conv0_bwd(const nrse_conv0_params* p, void* stream) {
   NRSE_REQUIRE(p->k > 0 && p->k <= KMAX, "nrse_conv0_bwd: bad k");
   if (p->dy_mode == NRSE_DY_COL2IM) NRSE_REQUIRE(p->col_k > 0 && p->col_s > 0 && p->col_tout > 0, "nrse_conv0_bwd: col2im");
   const long long rows = (long long)p->batch * p->T0;
-  long long blocks = (rows + 3) / 4;
+  const int rpb = p->C == 512 ? 2 : 4;
+  const bool bf = p->dy_dtype == NRSE_BF16;
+  long long blocks = (rows + rpb - 1) / rpb;
   if (blocks > 1024) blocks = 1024;  // each block adds (k + 2) * C partial sums at the end
   hipStream_t st = (hipStream_t)stream;
   switch (p->C) {
-    case 256: hipLaunchKernelGGL(conv0_bwd_kernel<1>, dim3(blocks), dim3(256), 0, st, *p); break;
-    case 512: hipLaunchKernelGGL(conv0_bwd_kernel<2>, dim3(blocks), dim3(256), 0, st, *p); break;
+    case 256:
+      if (bf) hipLaunchKernelGGL((conv0_bwd_kernel<1, true>), dim3(blocks), dim3(256), 0, st, *p);
+      else hipLaunchKernelGGL((conv0_bwd_kernel<1, false>), dim3(blocks), dim3(256), 0, st, *p);
+      break;
+    case 512:  // 2 waves per row
+      if (bf) hipLaunchKernelGGL((conv0_bwd_kernel<2, true>), dim3(blocks), dim3(256), 0, st, *p);
+      else hipLaunchKernelGGL((conv0_bwd_kernel<2, false>), dim3(blocks), dim3(256), 0, st, *p);
+      break;
     default: nrse_set_error("nrse_conv0_bwd: C=%d unsupported", p->C); return NRSE_ERR_UNSUPPORTED;
   }
   return nrse_check_launch("nrse_conv0_bwd");

@@ -126,21 +126,76 @@ NRSE_DEV float load_dy(const nrse_ln_bwd_params& p, long long row, int c, float*
 // is not read back. gamma / beta / dv column sums: per-lane accumulators across the rows of a
 // wave, reduced over the block's 4 waves in one 16 KB LDS buffer, one f32 atomic per column and
 // block.
-template <int NK, bool RES>
+// COL: col2im dy with at most two taps per row (k <= 2s, every conv layer of the feature
+// encoder): both taps are loaded into their own registers and summed in compute().
+// BF: x and dy are bf16 (the bf16 conv / feature-projection LNs): the row keeps the raw 8-byte
+// words and compute() unpacks them, so no unpack (and no wait for the load) sits between the
+// prefetch of the next row and its use; converting at load time put an s_waitcnt vmcnt(0)
+// after every dy / x load and serialised the prefetch away.
+template <int NK, bool RES, bool COL, bool BF>
 struct LnRow {
-  float x[NK][CH], dy[NK][CH], r[RES ? NK : 1][CH];
+  float x[BF ? 1 : NK][CH], dy[BF ? 1 : NK][CH], r[RES ? NK : 1][CH], dy2[COL && !BF ? NK : 1][CH];
+  uint2 xr[BF ? NK : 1], dyr[BF ? NK : 1], dy2r[COL && BF ? NK : 1];
   float mean, rstd;
+  bool v0, v1;  // BF: col2im taps present (their loads are issued regardless, from a valid address)
 };
 
-template <int NK, bool RES>
-NRSE_DEV void ln_bwd_load(const nrse_ln_bwd_params& p, long long row, int lane, LnRow<NK, RES>& b) {
+NRSE_DEV void unpack_bf4(uint2 v, float* o) {
+  o[0] = __uint_as_float(v.x << 16); o[1] = __uint_as_float(v.x & 0xffff0000u);
+  o[2] = __uint_as_float(v.y << 16); o[3] = __uint_as_float(v.y & 0xffff0000u);
+}
+
+// element offsets of the (up to) two col rows feeding LN row `row` (-1: no such tap)
+NRSE_DEV void col_taps(const nrse_ln_bwd_params& p, long long row, long long& o0, long long& o1) {
+  const long long b = row / p.col_tin;
+  const int tau = (int)(row - b * p.col_tin);
+  const int j0 = tau % p.col_s;
+  long long o[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int j = j0 + u * p.col_s;
+    const int t = (tau - j) / p.col_s;
+    o[u] = (j < p.col_k && tau >= j && t < p.col_tout)
+               ? ((b * p.col_tout + t) * p.col_k + j) * (long long)p.C : -1;
+  }
+  o0 = o[0];
+  o1 = o[1];
+}
+
+template <int NK, bool RES, bool COL, bool BF>
+NRSE_DEV void ln_bwd_load(const nrse_ln_bwd_params& p, long long row, int lane, LnRow<NK, RES, COL, BF>& b) {
   b.mean = p.mean[row];
   b.rstd = p.rstd[row];
+  long long o0 = -1, o1 = -1;
+  if constexpr (COL) col_taps(p, row, o0, o1);
+  else if constexpr (BF) o0 = row * p.C;  // direct dy
+  if constexpr (BF) {
+    // every load is issued on every row: a load skipped on some path leaves the wait-count pass
+    // no static count for the rows in flight, and it then waits for all of them
+    b.v0 = o0 >= 0;
+    b.v1 = o1 >= 0;
+    o0 = o0 < 0 ? 0 : o0;
+    o1 = o1 < 0 ? 0 : o1;
+  }
 #pragma unroll
   for (int k = 0; k < NK; ++k) {
     const int c0 = (k * 64 + lane) * CH;
-    load4(p.x, p.x_dtype, row * p.C + c0, b.x[k]);
-    load_dy(p, row, c0, b.dy[k]);
+    if constexpr (BF) {
+      const bf16_t* dyp = (const bf16_t*)p.dy;
+      b.xr[k] = ldg(reinterpret_cast<const uint2*>((const bf16_t*)p.x + row * p.C + c0));
+      b.dyr[k] = ldg(reinterpret_cast<const uint2*>(dyp + o0 + c0));
+      if constexpr (COL) b.dy2r[k] = ldg(reinterpret_cast<const uint2*>(dyp + o1 + c0));
+    } else {
+      load4(p.x, p.x_dtype, row * p.C + c0, b.x[k]);
+      if constexpr (COL) {
+        if (o0 >= 0) load4(p.dy, p.dy_dtype, o0 + c0, b.dy[k]);
+        else b.dy[k][0] = b.dy[k][1] = b.dy[k][2] = b.dy[k][3] = 0.f;
+        if (o1 >= 0) load4(p.dy, p.dy_dtype, o1 + c0, b.dy2[k]);
+        else b.dy2[k][0] = b.dy2[k][1] = b.dy2[k][2] = b.dy2[k][3] = 0.f;
+      } else {
+        load_dy(p, row, c0, b.dy[k]);
+      }
+    }
     if constexpr (RES) {
       if (p.resid) V4<float>::load(p.resid + row * p.C + c0, b.r[k]);
     }
@@ -149,9 +204,20 @@ NRSE_DEV void ln_bwd_load(const nrse_ln_bwd_params& p, long long row, int lane, 
 
 // RES: the encoder-layer form (residual input, fused dropout-cast consumer); !RES (conv / feature
 // projection LNs) drops their registers: 137 -> fewer VGPRs, more waves for the long row sweeps
-template <int NK, bool RES>
+template <int NK, bool RES, bool COL, bool BF>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const nrse_ln_bwd_params p) {
   __shared__ float red[4][NK * 64 * CH];
+  // gamma / beta staged once: read per row from LDS (lgkmcnt), not global memory, whose per-row
+  // loads were the youngest vmcnt entries and made every row wait for the prefetched next row
+  // (the encoder form keeps global reads: hoisted LDS copies would cost it 32 VGPRs)
+  __shared__ __attribute__((aligned(16))) float gb[RES ? 1 : 2][RES ? 4 : NK * 64 * CH];
+  if constexpr (!RES) {
+    for (int c = threadIdx.x; c < p.C; c += 256) {
+      gb[0][c] = p.gamma[c];
+      gb[1][c] = (p.flags & (NRSE_LN_GELU | NRSE_LN_RELU)) ? p.beta[c] : 0.f;
+    }
+    __syncthreads();
+  }
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: row math (col2im divisions) on the SALU
   const int C = p.C;
@@ -169,23 +235,45 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const nrse_ln_bwd_params p)
 #pragma unroll
     for (int e = 0; e < CH; ++e) dc[k][e] = 0.f;
 
-  auto compute = [&](const LnRow<NK, RES>& b, long long row) {
+  auto compute = [&](const LnRow<NK, RES, COL, BF>& b, long long row) {
     float xh[NK][CH], g[NK][CH];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int k = 0; k < NK; ++k) {
       const int c0 = (k * 64 + lane) * CH;
-      const float4 ga = *reinterpret_cast<const float4*>(p.gamma + c0);
-      const float gam[CH] = {ga.x, ga.y, ga.z, ga.w};
-      float be[CH] = {0.f, 0.f, 0.f, 0.f};
-      if (p.flags & (NRSE_LN_GELU | NRSE_LN_RELU)) {
-        const float4 bb = *reinterpret_cast<const float4*>(p.beta + c0);
+      float gam[CH], be[CH] = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (RES) {
+        const float4 ga = *reinterpret_cast<const float4*>(p.gamma + c0);
+        gam[0] = ga.x; gam[1] = ga.y; gam[2] = ga.z; gam[3] = ga.w;
+        if (p.flags & (NRSE_LN_GELU | NRSE_LN_RELU)) {
+          const float4 bb = *reinterpret_cast<const float4*>(p.beta + c0);
+          be[0] = bb.x; be[1] = bb.y; be[2] = bb.z; be[3] = bb.w;
+        }
+      } else {
+        const float4 ga = *reinterpret_cast<const float4*>(&gb[0][c0]);
+        gam[0] = ga.x; gam[1] = ga.y; gam[2] = ga.z; gam[3] = ga.w;
+        const float4 bb = *reinterpret_cast<const float4*>(&gb[RES ? 0 : 1][c0]);
         be[0] = bb.x; be[1] = bb.y; be[2] = bb.z; be[3] = bb.w;
+      }
+      float xv[CH], dv0[CH], dv1[CH] = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (BF) {
+        const uint2 z2 = make_uint2(0u, 0u);
+        unpack_bf4(b.xr[k], xv);
+        unpack_bf4(b.v0 ? b.dyr[k] : z2, dv0);
+        if constexpr (COL) unpack_bf4(b.v1 ? b.dy2r[k] : z2, dv1);
+      } else {
+#pragma unroll
+        for (int e = 0; e < CH; ++e) {
+          xv[e] = b.x[k][e];
+          dv0[e] = b.dy[k][e];
+          if constexpr (COL) dv1[e] = b.dy2[k][e];
+        }
       }
 #pragma unroll
       for (int e = 0; e < CH; ++e) {
-        xh[k][e] = (b.x[k][e] - b.mean) * b.rstd;
-        float gg = b.dy[k][e];
+        xh[k][e] = (xv[e] - b.mean) * b.rstd;
+        float gg = dv0[e];
+        if constexpr (COL) gg += dv1[e];
         if (p.flags & NRSE_LN_GELU) gg *= gelu_grad_f(xh[k][e] * gam[e] + be[e]);
         else if (p.flags & NRSE_LN_RELU) gg = (xh[k][e] * gam[e] + be[e] > 0.f) ? gg : 0.f;
         dg[k][e] += gg * xh[k][e];
@@ -224,14 +312,27 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const nrse_ln_bwd_params p)
 
   const long long nw = (long long)gridDim.x * 4;
   long long row = (long long)blockIdx.x * 4 + w;
-  LnRow<NK, RES> ba, bb;
+  LnRow<NK, RES, COL, BF> ba, bb;
+  const long long last = p.rows - 1;
   if (row < p.rows) ln_bwd_load(p, row, lane, ba);
   for (; row < p.rows; row += 2 * nw) {
     const long long rb = row + nw;
-    if (rb < p.rows) ln_bwd_load(p, rb, lane, bb);
+    // BF: unconditional (clamped) prefetch, fenced from the scheduler, which otherwise sinks the
+    // loads below part of the current row's math to save registers (and then waits for them)
+    if (BF) {
+      ln_bwd_load(p, rb < last ? rb : last, lane, bb);
+      __builtin_amdgcn_sched_barrier(0);
+    } else if (rb < p.rows) {
+      ln_bwd_load(p, rb, lane, bb);
+    }
     compute(ba, row);
     if (rb >= p.rows) break;
-    if (rb + nw < p.rows) ln_bwd_load(p, rb + nw, lane, ba);
+    if (BF) {
+      ln_bwd_load(p, rb + nw < last ? rb + nw : last, lane, ba);
+      __builtin_amdgcn_sched_barrier(0);
+    } else if (rb + nw < p.rows) {
+      ln_bwd_load(p, rb + nw, lane, ba);
+    }
     compute(bb, rb);
   }
 
@@ -350,14 +451,22 @@ extern "C" int nrse_layernorm_bwd(const nrse_ln_bwd_params* p, void* stream) {
   const dim3 grid((unsigned)blocks);
   hipStream_t st = (hipStream_t)stream;
   const bool res = p->resid || p->dv;
+  const bool col2 = !res && p->dy_mode == NRSE_DY_COL2IM && p->col_k <= 2 * p->col_s;
+  // bf16 x and dy (conv / feature-projection LNs of the bf16 step), direct or two-tap col2im dy
+  const bool bf = !res && p->x_dtype == NRSE_BF16 && p->dy_dtype == NRSE_BF16 &&
+                  (col2 || p->dy_mode == NRSE_DY_DIRECT);
+#define NRSE_LN_BWD_NK(NK)                                                                          \
+  if (res) hipLaunchKernelGGL((ln_bwd_kernel<NK, true, false, false>), grid, dim3(256), 0, st, *p);    \
+  else if (bf && col2) hipLaunchKernelGGL((ln_bwd_kernel<NK, false, true, true>), grid, dim3(256), 0, st, *p); \
+  else if (bf) hipLaunchKernelGGL((ln_bwd_kernel<NK, false, false, true>), grid, dim3(256), 0, st, *p); \
+  else if (col2) hipLaunchKernelGGL((ln_bwd_kernel<NK, false, true, false>), grid, dim3(256), 0, st, *p); \
+  else hipLaunchKernelGGL((ln_bwd_kernel<NK, false, false, false>), grid, dim3(256), 0, st, *p);
   switch (p->C / 256) {
-    case 1: if (res) hipLaunchKernelGGL((ln_bwd_kernel<1, true>), grid, dim3(256), 0, st, *p);
-            else hipLaunchKernelGGL((ln_bwd_kernel<1, false>), grid, dim3(256), 0, st, *p); break;
-    case 2: if (res) hipLaunchKernelGGL((ln_bwd_kernel<2, true>), grid, dim3(256), 0, st, *p);
-            else hipLaunchKernelGGL((ln_bwd_kernel<2, false>), grid, dim3(256), 0, st, *p); break;
-    default: if (res) hipLaunchKernelGGL((ln_bwd_kernel<4, true>), grid, dim3(256), 0, st, *p);
-             else hipLaunchKernelGGL((ln_bwd_kernel<4, false>), grid, dim3(256), 0, st, *p); break;
+    case 1: NRSE_LN_BWD_NK(1) break;
+    case 2: NRSE_LN_BWD_NK(2) break;
+    default: NRSE_LN_BWD_NK(4) break;
   }
+#undef NRSE_LN_BWD_NK
   return nrse_check_launch("nrse_layernorm_bwd");
 }
 

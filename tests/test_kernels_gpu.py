@@ -82,10 +82,12 @@ def test_layernorm_bwd_fused_dropout_colsum(nrse_device, rows, dvdt, p):
         assert abs(frac - p) < (0.01 if rows > 1000 else 0.05)
 
 
-def test_layernorm_bwd_col2im_and_bcast(nrse_device):
+@pytest.mark.parametrize("C,k,s", [(256, 3, 2), (512, 2, 2), (256, 5, 2), (512, 3, 1)])
+def test_layernorm_bwd_col2im_and_bcast(nrse_device, C, k, s):
+    """col2im dy: the two-tap path (k <= 2s: every feature-encoder conv) and the generic tap loop."""
     from nrse_amd import kernels as K, _lib
     dev = nrse_device
-    B, Tin, C, k, s = 3, 52, 256, 3, 2
+    B, Tin = 3, 52
     Tout = (Tin - k) // s + 1
     x = torch.randn(B * Tin, C, device=dev)
     g = torch.ones(C, device=dev); b = torch.zeros(C, device=dev)
@@ -129,6 +131,37 @@ def test_conv0_fwd_bwd(nrse_device, C):
     dw = torch.zeros(C, k, device=dev); dg = torch.zeros(C, device=dev); db = torch.zeros(C, device=dev)
     K.conv0_bwd(wav, w.view(C, k), g, b, mean, rstd, dy, dw, dg, db, T0, k, s, None)
     ref.backward(dy.double())
+    assert rel(dw, wr.grad.view(C, k)) < 1e-4
+    assert rel(dg, gr.grad) < 1e-5 and rel(db, br.grad) < 1e-5
+
+
+@pytest.mark.parametrize("C,ck,cs,dt", [(512, 3, 2, torch.bfloat16), (512, 2, 2, torch.float32),
+                                         (256, 3, 2, torch.float32), (512, 4, 1, torch.float32)])
+def test_conv0_bwd_col2im(nrse_device, C, ck, cs, dt):
+    """conv0 backward with dy as the col2im fold of the next conv's dgrad output [B, Tout, ck*C]
+    (the engine's form): two-tap path (ck <= 2cs) and the generic tap loop (ck = 4, cs = 1)."""
+    from nrse_amd import kernels as K
+    dev = nrse_device
+    B, L, k, s = 3, 3001, 10, 5
+    T0 = (L - k) // s + 1
+    Tout = (T0 - ck) // cs + 1
+    wav = torch.randn(B, L, device=dev)
+    w = torch.randn(C, 1, k, device=dev) * 0.3
+    g = torch.randn(C, device=dev) * 0.1 + 1; b = torch.randn(C, device=dev) * 0.1
+    out = torch.empty(B * T0, C, device=dev)
+    mean = torch.empty(B * T0, device=dev); rstd = torch.empty_like(mean)
+    K.conv0_fwd(wav, w.view(C, k), g, b, out, mean, rstd, T0, k, s, 1e-5)
+    col = (torch.randn(B * Tout, ck * C, device=dev)).to(dt)
+    dyf = torch.zeros(B, T0, C, device=dev, dtype=torch.float64)
+    cv = col.double().view(B, Tout, ck, C)
+    for j in range(ck):
+        dyf[:, j:j + cs * (Tout - 1) + 1:cs] += cv[:, :, j]
+    wr = w.double().requires_grad_(True); gr = g.double().requires_grad_(True); br = b.double().requires_grad_(True)
+    ref = F.conv1d(wav.double()[:, None], wr, stride=s)
+    ref = F.gelu(F.layer_norm(ref.transpose(1, 2), (C,), gr, br, 1e-5))
+    ref.backward(dyf)
+    dw = torch.zeros(C, k, device=dev); dg = torch.zeros(C, device=dev); db = torch.zeros(C, device=dev)
+    K.conv0_bwd(wav, w.view(C, k), g, b, mean, rstd, col, dw, dg, db, T0, k, s, (ck, cs, Tout))
     assert rel(dw, wr.grad.view(C, k)) < 1e-4
     assert rel(dg, gr.grad) < 1e-5 and rel(db, br.grad) < 1e-5
 

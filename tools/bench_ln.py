@@ -56,3 +56,16 @@ if os.environ.get("LN_VARIANTS"):
     print(f"  variant direct dy (bf16), GELU: {us:.1f} us", flush=True)
     us = timeit(lambda: K.ln_bwd(dyd, xc, gc, mc, rc, dpre), iters=10)
     print(f"  variant direct dy, no GELU, no dgamma: {us:.1f} us", flush=True)
+# conv0 (1 -> 512, k10 s5) + LN + GELU backward, dy = col2im of conv1's dgrad [32 x 12799, 3 x 512]
+L0, T0 = 128000, 25599
+wav = torch.randn(32, L0, device=dev) * 0.1
+w0 = torch.randn(512, 10, device=dev) * 0.3
+g0 = torch.ones(512, device=dev); b0 = torch.zeros(512, device=dev)
+o0 = torch.empty(32 * T0, 512, device=dev, dtype=torch.bfloat16)
+m0 = torch.empty(32 * T0, device=dev); r0 = torch.empty(32 * T0, device=dev)
+us = timeit(lambda: K.conv0_fwd(wav, w0, g0, b0, o0, m0, r0, T0, 10, 5, 1e-5), iters=10)
+print(f"conv0 fwd 819168x512 (bf16 out): {us:.1f} us  {32 * T0 * 512 * 2 / us / 1e3:.0f} GB/s", flush=True)
+col0 = torch.randn(32 * Tin, 3 * 512, device=dev).to(torch.bfloat16)
+dw0 = torch.zeros(512, 10, device=dev); dg0 = torch.zeros(512, device=dev); db0 = torch.zeros(512, device=dev)
+us = timeit(lambda: K.conv0_bwd(wav, w0, g0, b0, m0, r0, col0, dw0, dg0, db0, T0, 10, 5, (3, 2, Tin)), iters=10)
+print(f"conv0 bwd col2im 819168x512: {us:.1f} us  {32 * Tin * 3 * 512 * 2 / us / 1e3:.0f} GB/s (col read)", flush=True)
