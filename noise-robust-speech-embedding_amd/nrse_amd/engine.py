@@ -52,6 +52,10 @@ class StepConfig:
     eps: float = 1e-8
     max_norm: float = 1.0
     ema_decay: float = 0.997
+    # Run clip/AdamW/EMA on their own stream in per-layer segments and let the NEXT step's forward
+    # wait per layer (see ByolEngine.optimizer_step). Same kernels, same per-element arithmetic:
+    # parameters are bit-identical to the serial order (tests/test_engine_gpu.py).
+    overlap_optimizer: bool = False
 
 
 @dataclass
@@ -156,6 +160,36 @@ class ByolEngine:
         self.executed_layers = [0, 0]
         # DDP option (nrse_amd/ddp.SyncBN): head BatchNorm statistics over all ranks' rows
         self.sync_bn = None
+        # overlapped optimizer: per-segment "updated" events of the last step, and "done"
+        self._opt_stream = None
+        self._opt_events = None
+        self._opt_done = None
+        self._segments = self._param_segments()
+
+    # ------------------------------------------------------------------ overlapped optimizer
+    def _param_segments(self) -> list:
+        """Flat-buffer ranges in the order the forward consumes them: [front end .. layer 0],
+        layer 1, ..., layer L-1, [final LN + heads]. Boundaries are rounded UP to 4 elements
+        (the kernels' float4 alignment), which can only move an element into an EARLIER segment."""
+        a = self.arch
+        n = self.layout.numel
+        cuts = [0] + [PR.layer_range(self.layout, a, li)[0] for li in range(1, a.layers)]
+        cuts.append(PR.layer_range(self.layout, a, a.layers - 1)[1])
+        cuts = [min(n, (c + 3) // 4 * 4) for c in cuts] + [n]
+        return [(cuts[i], cuts[i + 1]) for i in range(len(cuts) - 1)]
+
+    def _param_wait(self, seg: int) -> None:
+        """The current stream waits until segment `seg` of the last optimizer step is updated
+        (no-op unless the optimizer step was overlapped)."""
+        if self._opt_events is not None:
+            torch.cuda.current_stream(self.dev).wait_event(self._opt_events[seg])
+
+    def sync_optimizer(self) -> None:
+        """The current stream waits for the whole last optimizer step (parameters, moments, EMA,
+        grad buffer reads). Called by every entry point that reads or writes the flat buffers
+        outside the overlapped forward."""
+        if self._opt_done is not None:
+            torch.cuda.current_stream(self.dev).wait_event(self._opt_done)
 
     # ------------------------------------------------------------------ views
     def group_views(self, flat: torch.Tensor, group: str) -> dict:
@@ -286,6 +320,8 @@ class ByolEngine:
         pact = a.activation_dropout if train else 0.0
         executed = 0
         for li in range(a.layers):
+            if li > 0:
+                self._param_wait(li)  # layer li's parameters of the overlapped optimizer step
             if train and skip is not None and skip[li]:
                 continue
             executed += 1
@@ -324,6 +360,7 @@ class ByolEngine:
                 tape.layers.append(dict(li=li, h_in=hcur, x1=x1, m1=m1, r1=r1, qkv=qkv, gate=gate, ctx=ctx, lse=lse,
                                         hmid=hmid, x2=x2, m2=m2, r2=r2, f1pre=f1pre, g1=g1))
             hcur = hout
+        self._param_wait(a.layers)  # final LN (+ the heads that follow)
         if hidden_dtype is not None:
             # -------- final LN -> last_hidden_state ([TF]modeling_wavlm.py:513)
             y = torch.empty(BT, H, device=dev, dtype=hidden_dtype)
@@ -608,6 +645,8 @@ class ByolEngine:
 
     # ------------------------------------------------------------------ public API
     def weights(self, which: str) -> EncoderWeights:
+        """Encoder weight views (+ the derived conv / pos-conv GEMM layouts, computed on the
+        current stream). Inside forward() the caller has waited for the front-end segment."""
         if which == "online":
             W = EncoderWeights(self, self.online, self.online_sh)
             W.m_flat, W.s_flat = self.online, (self.online_sh if self.online_sh is not None else self.online)
@@ -673,11 +712,13 @@ class ByolEngine:
         side.wait_stream(main)
         noisy.record_stream(side)
         with torch.cuda.stream(side):
+            self._param_wait(0)
             Wt = self.weights("target")
             temb, _, ex1 = self.encoder_forward(Wt, noisy, train=train, fseed=R.forward_seed(step_seed, 1, rank),
                                                 skip=skips[1], mask_np=masks[1], need_grad=False)
             Ptp = self.group_views(self.target, "projector")
             tproj, _ = self.projector_forward(temb, Ptp, "target_projector", train)
+        self._param_wait(0)
         Wo = self.weights("online")
         emb, tape, ex0 = self.encoder_forward(Wo, clean, train=train, fseed=R.forward_seed(step_seed, 0, rank),
                                               skip=skips[0], mask_np=masks[0], need_grad=need_grad)
@@ -728,16 +769,49 @@ class ByolEngine:
             allreduce.finish()
 
     def optimizer_step(self, lr: float, grad_scale: float = 1.0) -> None:
-        """clip_grad_norm_(1.0) + AdamW + target EMA (train_byol.py:67-71), no host sync."""
+        """clip_grad_norm_(1.0) + AdamW + target EMA (train_byol.py:67-71), no host sync.
+
+        With cfg.overlap_optimizer the HBM-bound AdamW + EMA (~3 ms at B = 32) leave the main
+        stream: after the global gradient norm (which every segment's clip coefficient needs), a
+        dedicated stream updates the parameters segment by segment in forward order and records
+        an event per segment; the next step's forward waits per layer, so the update streams
+        underneath the MFMA-bound GEMMs of the next step's first layers instead of running alone.
+        Per element the arithmetic is identical, so the parameters are bit-identical to the
+        serial order."""
         c = self.cfg
         self.step_count += 1
+        self.sync_optimizer()  # the previous step's update has read sumsq_buf
         self.sumsq_buf.zero_()
         K.sumsq(self.grad, self.sumsq_buf)
-        K.adamw(self.online, self.grad, self.m, self.v, self.online_sh, lr=lr, beta1=c.betas[0], beta2=c.betas[1],
-                eps=c.eps, weight_decay=c.weight_decay, step=self.step_count, max_norm=c.max_norm,
-                sumsq_buf=self.sumsq_buf, grad_scale=grad_scale)
+        kw = dict(lr=lr, beta1=c.betas[0], beta2=c.betas[1], eps=c.eps, weight_decay=c.weight_decay,
+                  step=self.step_count, max_norm=c.max_norm, sumsq_buf=self.sumsq_buf, grad_scale=grad_scale)
         ne = self.layout.ema_numel
-        K.ema(self.target, self.online[:ne], self.target_sh, c.ema_decay)
+        if not c.overlap_optimizer:
+            K.adamw(self.online, self.grad, self.m, self.v, self.online_sh, **kw)
+            K.ema(self.target, self.online[:ne], self.target_sh, c.ema_decay)
+            self._opt_events = self._opt_done = None
+            return
+        main = torch.cuda.current_stream(self.dev)
+        if self._opt_stream is None:
+            self._opt_stream = torch.cuda.Stream(self.dev)
+        st = self._opt_stream
+        st.wait_stream(main)
+        events = []
+        sh, tsh = self.online_sh, self.target_sh
+        with torch.cuda.stream(st):
+            for s, e in self._segments:
+                if e > s:
+                    K.adamw(self.online[s:e], self.grad[s:e], self.m[s:e], self.v[s:e],
+                            sh[s:e] if sh is not None else None, **kw)
+                    te = min(e, ne)
+                    if te > s:
+                        K.ema(self.target[s:te], self.online[s:te], tsh[s:te] if tsh is not None else None,
+                              c.ema_decay)
+                ev = torch.cuda.Event()
+                ev.record(st)
+                events.append(ev)
+        self._opt_events = events
+        self._opt_done = events[-1]
 
     def grad_norm(self, world_size: int = 1) -> float:
         """Pre-clip global gradient norm of the last step (host sync)."""
@@ -757,12 +831,14 @@ class ByolEngine:
         self.loss_buf.zero_()
         dpred = torch.empty_like(pred)
         K.byol_loss(pred, tproj, self.loss_buf, dpred, self.loss_stats)
+        self.sync_optimizer()  # the last update has read the gradient buffer
         self.grad.zero_()
         self.backward(dpred, ctx, allreduce=allreduce if world_size > 1 else None)
         self.optimizer_step(lr, grad_scale=1.0 / world_size)
         return self.loss_buf
 
     def eval_forward(self, clean, noisy):
+        self.sync_optimizer()
         with torch.no_grad():
             pred, tproj, _ = self.forward(clean, noisy, train=False, need_grad=False)
         loss = torch.zeros(1, device=self.dev, dtype=F32)
@@ -770,5 +846,6 @@ class ByolEngine:
         return pred, tproj, loss
 
     def embed(self, wav: torch.Tensor, which: str = "online") -> torch.Tensor:
+        self.sync_optimizer()
         emb, _, _ = self.encoder_forward(self.weights(which), wav, train=False)
         return emb

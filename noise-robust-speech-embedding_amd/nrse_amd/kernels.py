@@ -133,11 +133,17 @@ def gemm_select(generation: int) -> int:
 _GEMM_PROBE_BYTES = []
 
 
+_GEMM_PROBE_OWNER = None
+
+
 def set_gemm_probe(lst):
-    global _GEMM_PROBE
+    """Record (flops, start event, end event, shape) of every GEMM launch into `lst` while set
+    (None: off). Re-enabling with the same list keeps appending (bytes included)."""
+    global _GEMM_PROBE, _GEMM_PROBE_OWNER
     _GEMM_PROBE = lst
-    if lst is not None:
+    if lst is not None and lst is not _GEMM_PROBE_OWNER:
         _GEMM_PROBE_BYTES.clear()
+        _GEMM_PROBE_OWNER = lst
 
 
 def gemm_probe_bytes():

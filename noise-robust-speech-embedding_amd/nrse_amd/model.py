@@ -135,7 +135,7 @@ class BYOLSpeechModel(nn.Module):
         self.ema_decay = float(m["ema_decay"])
         tr = config.get("training", {})
         cfg = StepConfig(lr=float(tr.get("learning_rate", 1e-5)), weight_decay=float(tr.get("weight_decay", 1e-5)),
-                         ema_decay=self.ema_decay)
+                         ema_decay=self.ema_decay, overlap_optimizer=True)
         seed = seed if seed is not None else int(tr.get("seed", 42))
         self.engine = ByolEngine(arch, int(m["projection_dim"]), int(m["prediction_dim"]),
                                  device=device or _device_default(), compute_dtype=compute_dtype, seed=seed,
@@ -164,6 +164,7 @@ class BYOLSpeechModel(nn.Module):
         in place since the last cast (a torch optimizer's step(), a user's in-place edit). The
         fused engine path (FusedAdamW / engine.train_step) writes the shadow itself."""
         e = self.engine
+        e.sync_optimizer()
         v = self.online_flat._version
         if v != self._shadow_version:
             if e.online_sh is not None:
@@ -172,11 +173,13 @@ class BYOLSpeechModel(nn.Module):
 
     def _update_target_network(self) -> None:
         e = self.engine
+        e.sync_optimizer()
         self._sync_shadows()
         K.ema(e.target, e.online[:e.layout.ema_numel], e.target_sh, self.ema_decay)
 
     def _copy_weights(self, *args) -> None:
         e = self.engine
+        e.sync_optimizer()
         e.target.copy_(e.online[:e.layout.ema_numel])
         if e.target_sh is not None:
             K.cast(e.target, e.target_sh)
@@ -185,6 +188,7 @@ class BYOLSpeechModel(nn.Module):
         """Re-derive the bf16 operand copies after the f32 weights were changed outside the
         fused optimizer (e.g. by torch.optim or load_state_dict)."""
         e = self.engine
+        e.sync_optimizer()
         if e.online_sh is not None:
             K.cast(e.online, e.online_sh)
             K.cast(e.target, e.target_sh)
@@ -211,6 +215,7 @@ class BYOLSpeechModel(nn.Module):
                     yield k[:-5] + ".num_batches_tracked", nbt
 
     def state_dict(self, *args, **kwargs):
+        self.engine.sync_optimizer()
         return {k: v.detach().clone() for k, v in self._state_items()}
 
     def load_state_dict(self, sd: dict, strict: bool = True):
@@ -218,6 +223,7 @@ class BYOLSpeechModel(nn.Module):
         mismatches always raise; with strict, missing or unexpected keys raise; returns
         (missing_keys, unexpected_keys)."""
         from torch.nn.modules.module import _IncompatibleKeys
+        self.engine.sync_optimizer()
         own = dict(self._state_items())
         missing = [k for k in own if k not in sd]
         unexpected = [k for k in sd if k not in own]

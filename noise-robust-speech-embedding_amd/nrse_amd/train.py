@@ -63,6 +63,7 @@ class FusedAdamW(torch.optim.Optimizer):
 
     def step(self, closure=None):  # used by the unfused path (autograd backward)
         eng = self.model.engine
+        eng.sync_optimizer()
         eng.grad.copy_(self.model.online_flat.grad)
         eng.optimizer_step(self.lr)
 

@@ -14,7 +14,7 @@ from nrse_amd.engine import ByolEngine, StepConfig
 dev = torch.device("cuda", 0)
 B, L = 32, 128000
 eng = ByolEngine(A.LARGE, 1024, 2048, device=dev, compute_dtype=torch.bfloat16, seed=1234,
-                 step_cfg=StepConfig(ema_decay=0.997))
+                 step_cfg=StepConfig(ema_decay=0.997, overlap_optimizer=os.environ.get("SERIAL_OPT") is None))
 g = torch.Generator(device=dev); g.manual_seed(1)
 clean = torch.randn(B, L, device=dev, generator=g) * 0.1
 noisy = clean + torch.randn(B, L, device=dev, generator=g) * 0.1

@@ -23,13 +23,13 @@ def main():
         wg = int(r.get("Workgroup_Size_X", r.get("Workgroup_Size", 1)) or 1)
         ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]), r["Stream_Id"], grid // max(wg, 1)))
     ev.sort()
-    marks = [e[1] for e in ev if "adamw_kernel" in e[2]]
+    marks = [e[1] for e in ev if "sumsq_kernel" in e[2]]  # one gradient-norm launch per step
     lo, hi = marks[-2], marks[-1]
     ev = [e for e in ev if e[0] >= lo and e[1] <= hi]
     busy_until = lo
     gaps = defaultdict(lambda: [0, 0.0])
     groups = defaultdict(lambda: [0, 0.0])
-    prev = "adamw_kernel"
+    prev = "sumsq_kernel"
     idle_total = 0.0
     for s, e, n, st, nwg in ev:
         gap = max(0, s - busy_until)

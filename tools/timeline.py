@@ -9,7 +9,7 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 nsteps = int(sys.argv[2]) if len(sys.argv) > 2 else 4   # window: the last nsteps optimizer steps
 ev = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"][:70], r["Stream_Id"]) for r in rows]
 ev.sort()
-marks = [e[1] for e in ev if "adamw_kernel" in e[2]]
+marks = [e[1] for e in ev if "sumsq_kernel" in e[2]]  # one gradient-norm launch per step
 t_lo, t_hi = marks[-nsteps - 1], marks[-1]
 ev = [e for e in ev if e[0] >= t_lo and e[1] <= t_hi]
 span = ev[-1][1] - ev[0][0]
