@@ -26,22 +26,8 @@ NRSE_DEV void load_wT(float* wT, const float* w, int C, int k) {
   }
 }
 
-template <int NQ>
-NRSE_DEV void conv_row(const float* wT, int C, int lane, const float* xs, float (&y)[NQ][4]) {
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-    const int c0 = (q * 64 + lane) * 4;
-    float a[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int j = 0; j < KMAX; ++j) {
-      const float4 wv = *reinterpret_cast<const float4*>(wT + j * C + c0);
-      a[0] += wv.x * xs[j]; a[1] += wv.y * xs[j]; a[2] += wv.z * xs[j]; a[3] += wv.w * xs[j];
-    }
-#pragma unroll
-    for (int e = 0; e < 4; ++e) y[q][e] = a[e];
-  }
-}
-
+// conv0 forward: VALU-bound (10-tap conv, LN, GELU per element), so channel pairs run as
+// packed FP32 (v_pk_fma_f32 / v_pk_mul_f32): lane owns 4*NQ channels as 2*NQ pairs.
 template <int NQ>
 __global__ __launch_bounds__(256) void conv0_fwd_kernel(const nrse_conv0_params p) {
   __shared__ __attribute__((aligned(16))) float wT[KMAX * 512];
@@ -49,15 +35,16 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(const nrse_conv0_params 
   const int C = p.C;
   load_wT(wT, p.w, C, p.k);
   __syncthreads();
-  float ga[NQ][4], be[NQ][4];
+  f32x2 ga[NQ][2], be[NQ][2];
 #pragma unroll
   for (int q = 0; q < NQ; ++q)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int c = (q * 64 + lane) * 4 + e;
-      ga[q][e] = p.gamma[c];
-      be[q][e] = p.beta[c];
+    for (int h = 0; h < 2; ++h) {
+      const int c = (q * 64 + lane) * 4 + 2 * h;
+      ga[q][h] = f32x2{p.gamma[c], p.gamma[c + 1]};
+      be[q][h] = f32x2{p.beta[c], p.beta[c + 1]};
     }
+  const float invC = 1.f / C;
   const long long rows = (long long)p.batch * p.T0;
   const long long nw = (long long)gridDim.x * 4;
   for (long long r0 = (long long)blockIdx.x * 4 + (threadIdx.x >> 6); r0 < rows; r0 += nw) {
@@ -68,33 +55,44 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(const nrse_conv0_params 
     float xs[KMAX];
 #pragma unroll
     for (int j = 0; j < KMAX; ++j) xs[j] = j < p.k ? x[j] : 0.f;
-    float y[NQ][4];
-    conv_row<NQ>(wT, C, lane, xs, y);
-    float s = 0.f;
-#pragma unroll
-    for (int q = 0; q < NQ; ++q)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) s += y[q][e];
-    const float mean = wave_sum(s) / C;
-    float v = 0.f;
-#pragma unroll
-    for (int q = 0; q < NQ; ++q)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) { const float d = y[q][e] - mean; v += d * d; }
-    const float rstd = rsqrtf(wave_sum(v) / C + p.eps);
+    f32x2 y[NQ][2];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-      float o[4];
+      const int c0 = (q * 64 + lane) * 4;
+      y[q][0] = y[q][1] = f32x2{0.f, 0.f};
 #pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = gelu_f((y[q][e] - mean) * rstd * ga[q][e] + be[q][e]);
+      for (int j = 0; j < KMAX; ++j) {
+        const float4 wv = *reinterpret_cast<const float4*>(wT + j * C + c0);
+        y[q][0] = pk_fma(f32x2{wv.x, wv.y}, splat2(xs[j]), y[q][0]);
+        y[q][1] = pk_fma(f32x2{wv.z, wv.w}, splat2(xs[j]), y[q][1]);
+      }
+    }
+    f32x2 s2 = f32x2{0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) s2 += y[q][0] + y[q][1];
+    const float mean = wave_sum(s2.x + s2.y) * invC;
+    f32x2 v2 = f32x2{0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x2 d = y[q][h] - mean;
+        v2 = pk_fma(d, d, v2);
+      }
+    const float rstd = rsqrtf(wave_sum(v2.x + v2.y) * invC + p.eps);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      f32x2 o[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) o[h] = gelu2(pk_fma((y[q][h] - mean) * rstd, ga[q][h], be[q][h]));
       const long long off = row * C + (q * 64 + lane) * 4;
       if (p.out_dtype == NRSE_BF16) {
         uint2 u;
-        u.x = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
-        u.y = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
+        u.x = (uint32_t)f2bf(o[0].x) | ((uint32_t)f2bf(o[0].y) << 16);
+        u.y = (uint32_t)f2bf(o[1].x) | ((uint32_t)f2bf(o[1].y) << 16);
         *reinterpret_cast<uint2*>((bf16_t*)p.out + off) = u;
       } else {
-        *reinterpret_cast<float4*>((float*)p.out + off) = make_float4(o[0], o[1], o[2], o[3]);
+        *reinterpret_cast<float4*>((float*)p.out + off) = make_float4(o[0].x, o[0].y, o[1].x, o[1].y);
       }
     }
     if (lane == 0) {
@@ -123,7 +121,6 @@ NRSE_DEV void ld4(const void* p, int dt, long long i, float* o) {
 //  - the conv and dW FMAs run as packed fp32 (v_pk_fma_f32: two channels per instruction);
 //  - the next row's operands (10 samples, mean / rstd, up to two col2im taps of dy) are loaded
 //    while the current row computes, the two taps into separate registers (no load -> add chain).
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // One row's operands. BF (bf16 dy, the bf16 step): raw 8-byte words, unpacked at use, so no
 // unpack (and no wait for the load) sits between the prefetch and the use. Every load is issued
@@ -256,7 +253,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
         xh[h] = (y[h] - cur.mean) * cur.rstd;
         const f32x2 z = xh[h] * ga[h] + be[h];
         const f32x2 dy = h == 0 ? f32x2{dd.x, dd.y} : f32x2{dd.z, dd.w};
-        const f32x2 gg = dy * f32x2{gelu_grad_f(z.x), gelu_grad_f(z.y)};
+        const f32x2 gg = dy * f32x2{gelu_grad_f(z.x), gelu_grad_f(z.y)};  // (packed form measured slower here)
         dga[h] += gg * xh[h];
         dbe[h] += gg;
         g[h] = gg * ga[h];

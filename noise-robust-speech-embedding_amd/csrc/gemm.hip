@@ -20,6 +20,8 @@
 
 bool nrse_gemm_dma_ok(const nrse_gemm_params* p);        // gemm_dma.hip
 int nrse_gemm_dma(const nrse_gemm_params* p, hipStream_t st);
+bool nrse_posconv_ok(const nrse_gemm_params* p);         // posconv.hip
+int nrse_posconv(const nrse_gemm_params* p, hipStream_t st);
 bool nrse_gemm256_ok(const nrse_gemm_params* p);         // gemm256.hip
 long long nrse_gemm256_tiles(const nrse_gemm_params* p);
 int nrse_gemm256(const nrse_gemm_params* p, hipStream_t st);
@@ -391,6 +393,9 @@ extern "C" int nrse_gemm(const nrse_gemm_params* p, void* stream) {
   // (split-K atomic problems stay on 128x128: 4x the tiles of a 256x256 decomposition means 4x
   // fewer K splits for the same occupancy, i.e. 4x less atomic traffic per FLOP)
   const bool big = nrse_gemm256_tiles(p) >= 128 && !(p->flags & NRSE_EPI_ATOMIC);
+  // the grouped pos-conv pattern (sliding-window A operand, N = 64): its own kernel unless a
+  // generation is pinned (NRSE_GEMM_GEN=1|2|3 benchmarks the generic kernels on it)
+  if ((gen == 0 || gen == 4) && nrse_posconv_ok(p)) return nrse_posconv(p, st);
   if (gen != 1 && gen != 2 && nrse_gemm256_ok(p) && (gen == 3 || big))
     return nrse_gemm256(p, st);
   if (gen != 1 && nrse_gemm_dma_ok(p)) return nrse_gemm_dma(p, st);

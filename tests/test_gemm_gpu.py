@@ -107,3 +107,63 @@ def test_splitk_reduce(nrse_device):
         assert rel(dst, ref) < 1e-6
         _lib.call("nrse_splitk_reduce", K.ptr(dst), K.ptr(slabs), S, n, 0, K.stream_ptr())
         assert rel(dst, slabs.double().sum(0)) < 1e-6
+
+
+def _posconv_call(K, _lib, hpad, wf, out, T, H, G, pk, *, fwd, bias=None, pre=None, resid=None, p=0.0, seed=0):
+    cpg = H // G
+    cs = cpg.bit_length() - 1
+    B = hpad.shape[0]
+    A = K.Operand(hpad, True, H, chunk_shift=cs, ld_chunk=H, z1=(T + pk) * H, z2=cpg)
+    Bw = K.Operand(wf, True, pk * cpg, z2=cpg * pk * cpg)
+    if fwd:
+        K.gemm(A, Bw, out, T, cpg, pk * cpg, ldc=H, batch=B * G, zdiv=G, c_z1=T * H, c_z2=cpg, bias=bias,
+               bias_z2=cpg, flags=_lib.EPI_GELU | _lib.EPI_DROP_AFTER, aux=pre, ldaux=H, aux_z1=T * H, aux_z2=cpg,
+               resid=resid, ldr=H, r_z1=T * H, r_z2=cpg, dropout_p=p, seed=seed)
+    else:
+        K.gemm(A, Bw, out, T, cpg, pk * cpg, ldc=H, batch=B * G, zdiv=G, c_z1=T * H, c_z2=cpg,
+               flags=_lib.EPI_ACCUM)
+
+
+@pytest.mark.parametrize("T", [399, 100, 600])
+def test_posconv_sliding_window(nrse_device, T):
+    """The grouped pos-conv (H = 1024, 16 groups of 64, 128 taps) routed to the sliding-window
+    kernel (csrc/posconv.hip): forward with the fused bias + GELU (+ pre-activation) + residual +
+    dropout epilogue, and the dgrad form accumulating into C, against float64 torch conv1d and
+    against the generic LDS-DMA GEMM on the same call (same dropout mask)."""
+    from nrse_amd import kernels as K, _lib
+    dev = nrse_device
+    B, H, G, pk = 3, 1024, 16, 128
+    cpg = H // G
+    g = torch.Generator(device=dev).manual_seed(T)
+    x = torch.randn(B, T, H, device=dev, generator=g)
+    hpad = torch.zeros(B, T + pk, H, device=dev, dtype=torch.bfloat16)
+    hpad[:, pk // 2:pk // 2 + T] = x.to(torch.bfloat16)
+    wf = (torch.randn(G, cpg, pk * cpg, device=dev, generator=g) * 0.02).to(torch.bfloat16)
+    bias = torch.randn(H, device=dev, generator=g) * 0.1
+    resid = torch.randn(B * T, H, device=dev, generator=g)
+    # float64 reference: conv1d with W[g*cpg + o, i, tap] = wf[g, o, tap*cpg + i]
+    W = wf.double().view(G, cpg, pk, cpg).permute(0, 1, 3, 2).reshape(H, cpg, pk)
+    conv = torch.nn.functional.conv1d(hpad.double().transpose(1, 2), W, groups=G)[:, :, :T].transpose(1, 2)
+    ref_pre = conv.reshape(B * T, H) + bias.double()
+    ref = torch.nn.functional.gelu(ref_pre) + resid.double()
+    out = torch.empty(B * T, H, device=dev)
+    pre = torch.empty(B * T, H, device=dev, dtype=torch.bfloat16)
+    _posconv_call(K, _lib, hpad, wf, out, T, H, G, pk, fwd=True, bias=bias, pre=pre, resid=resid)
+    assert rel(out, ref) < 1e-5
+    assert rel(pre.float(), ref_pre) < 5e-3
+    # dropout after the residual: the same mask and values as the generic kernel
+    o1 = torch.empty(B * T, H, device=dev)
+    o2 = torch.empty(B * T, H, device=dev)
+    _posconv_call(K, _lib, hpad, wf, o1, T, H, G, pk, fwd=True, bias=bias, pre=pre, resid=resid, p=0.1, seed=7)
+    prev = K.gemm_select(2)
+    try:
+        _posconv_call(K, _lib, hpad, wf, o2, T, H, G, pk, fwd=True, bias=bias, pre=pre, resid=resid, p=0.1, seed=7)
+    finally:
+        K.gemm_select(prev)
+    assert torch.equal(o1 == 0, o2 == 0)
+    assert rel(o1, o2) < 1e-6
+    # dgrad form: C += conv (EPI_ACCUM)
+    c0 = torch.randn(B * T, H, device=dev, generator=g)
+    c = c0.clone()
+    _posconv_call(K, _lib, hpad, wf, c, T, H, G, pk, fwd=False)
+    assert rel(c, c0.double() + conv.reshape(B * T, H)) < 1e-5
