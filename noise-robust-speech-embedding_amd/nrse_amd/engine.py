@@ -281,7 +281,10 @@ class ByolEngine:
         cpg = H // G
         mask = None
         if train and mask_np is not None and mask_np.any():
-            mask = torch.from_numpy(mask_np.astype(np.uint8)).to(dev, non_blocking=True)
+            # pinned staging: a copy from pageable memory blocks the host until the stream
+            # reaches it, which stalled the enqueue of the rest of the step behind the GPU
+            # (the two views' forwards then ran one after the other instead of concurrently)
+            mask = torch.from_numpy(mask_np.astype(np.uint8)).pin_memory().to(dev, non_blocking=True)
         hpad = torch.empty(B, T + pk, H, device=dev, dtype=cdt)
         K.specaug_pad(h, mask, Pm.get("masked_spec_embed"), hpad, B, T, H, pk // 2, pk - pk // 2)
         # -------- positional conv + residual + dropout ([TF]modeling_wavlm.py:48-90, 476-483)
