@@ -376,8 +376,10 @@ int nrse_health(const void* x, int dtype, long long n, float* stats, void* strea
  * mode (`do_normalize` argument): 0 = raw mix y = s + k n (add_noise_to_speech), 1 = + peak
  * normalisation, 2 = + feature-extractor normalisation. noise_len[b] <= noise_stride.
  * status[b] follows oracle/snr_mix.py codes (0 = ok); outputs of failed pairs are zeroed.
- * scratch: unused (may be null).
+ * scratch: batch * NRSE_SNR_SCRATCH_PER_PAIR doubles -> the chunked form (16 workgroups per pair,
+ * four launches, per-chunk f64 partials folded in chunk order); null -> one workgroup per pair.
  * ------------------------------------------------------------------------------------------ */
+#define NRSE_SNR_SCRATCH_PER_PAIR 256
 int nrse_snr_mix(const float* clean, const float* noise, const int* noise_len, long long noise_stride,
                  const float* snr_db, float* clean_out, float* noisy_out, int* status, float* kscale, double* scratch,
                  int batch, int L, int do_normalize, void* stream);

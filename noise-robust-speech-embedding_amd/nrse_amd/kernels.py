@@ -530,14 +530,16 @@ def health(x, stats):
 
 
 SNR_RAW, SNR_PEAK, SNR_PEAK_ZMUV = 0, 1, 2
+SNR_SCRATCH_PER_PAIR = 256  # NRSE_SNR_SCRATCH_PER_PAIR (include/nrse_hip.h)
 
 
 def snr_mix(clean, noise, noise_len, snr_db, clean_out, noisy_out, status, kscale, mode=SNR_PEAK_ZMUV):
     """Fused on-GPU SNR mix (nrse_snr_mix); mode 0 raw / 1 peak / 2 peak + feature-extractor norm."""
     B, L = clean.shape
     assert noise.dim() == 2 and noise.shape[0] == B and clean.is_contiguous() and noise.stride(1) == 1
+    scratch = torch.empty(B * SNR_SCRATCH_PER_PAIR, device=clean.device, dtype=torch.float64)
     _call("nrse_snr_mix", ptr(clean), ptr(noise), ptr(noise_len), noise.stride(0), ptr(snr_db), ptr(clean_out),
-          ptr(noisy_out), ptr(status), ptr(kscale), None, B, L, int(mode), stream_ptr())
+          ptr(noisy_out), ptr(status), ptr(kscale), ptr(scratch), B, L, int(mode), stream_ptr())
 
 
 # ----------------------------------------------------------------------------- emotion head

@@ -262,6 +262,37 @@ def test_snr_mix_matches_reference_fixture(nrse_device):
             assert rel(n_out[0], torch.from_numpy(z[f"c{i}_noisy_raw"]).to(dev)) < 1e-6
 
 
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_snr_mix_chunked_matches_single_workgroup(nrse_device, mode):
+    """The chunked SNR mix (16 workgroups per pair, scratch partials) against the one-workgroup-
+    per-pair form on a batch with tiled short noise, longer noise, a NaN speech pair, a silent
+    noise pair and a silent speech pair: same status codes, same outputs (f64 sums reordered)."""
+    from nrse_amd import kernels as K, _lib
+    dev = nrse_device
+    B, L, NS = 6, 48000, 60000
+    g = torch.Generator(device=dev).manual_seed(4)
+    s = torch.randn(B, L, device=dev, generator=g) * 0.1
+    n = torch.randn(B, NS, device=dev, generator=g)
+    nlen = torch.tensor([NS, 7001, 48000, 20000, 100, 33333], device=dev, dtype=torch.int32)
+    s[2, 1234] = float("nan")
+    n[3] = 0.0
+    s[4] = 0.0
+    snr = torch.tensor([4.0, 8.0, 0.0, 12.0, 4.0, -2.0], device=dev)
+    outs = []
+    for scratch in (torch.empty(B * K.SNR_SCRATCH_PER_PAIR, device=dev, dtype=torch.float64), None):
+        c_out = torch.full_like(s, 7.0); n_out = torch.full_like(s, 7.0)
+        st = torch.full((B,), -1, device=dev, dtype=torch.int32); ks = torch.empty(B, device=dev)
+        _lib.call("nrse_snr_mix", K.ptr(s), K.ptr(n), K.ptr(nlen), n.stride(0), K.ptr(snr), K.ptr(c_out),
+                  K.ptr(n_out), K.ptr(st), K.ptr(ks), K.ptr(scratch), B, L, mode, K.stream_ptr())
+        outs.append((c_out, n_out, st, ks))
+    (c1, n1, s1, k1), (c2, n2, s2, k2) = outs
+    assert torch.equal(s1, s2), (s1, s2)
+    assert int(s1[2]) == 1 and int(s1[4]) == 3 and int(s1[3]) == 4
+    ok = s1 == 0
+    assert rel(c1[ok], c2[ok]) < 1e-6 and rel(n1[ok], n2[ok]) < 1e-6 and rel(k1[ok], k2[ok]) < 1e-6
+    assert float(c1[~ok].abs().max()) == 0.0 and float(n1[~ok].abs().max()) == 0.0
+
+
 def test_health_flags(nrse_device):
     from nrse_amd import kernels as K
     x = torch.randn(10000, device=nrse_device)
