@@ -45,6 +45,11 @@ NRSE_DEV void store4(void* p, int dt, long long i, const float* o) {
   else V4<float>::store((float*)p + i, o);
 }
 
+NRSE_DEV void unpack_bf4(uint2 v, float* o) {
+  o[0] = __uint_as_float(v.x << 16); o[1] = __uint_as_float(v.x & 0xffff0000u);
+  o[2] = __uint_as_float(v.y << 16); o[3] = __uint_as_float(v.y & 0xffff0000u);
+}
+
 // element c of a row held by this lane: c = (k*64 + lane)*4 + e, k < NK = C/256
 template <int NK>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const nrse_ln_fwd_params p) {
@@ -87,6 +92,67 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const nrse_ln_fwd_params p)
   if (lane == 0) {
     if (p.mean) p.mean[row] = mean;
     if (p.rstd) p.rstd[row] = rstd;
+  }
+}
+
+// bf16-in form of the forward for the long row sweeps of the conv stack (x bf16, C <= 512):
+// each wave takes RPW rows, all of their raw 8-byte words loaded first (clamped rows, no
+// branches), so RPW KiB are in flight per wave instead of one row's 1 KiB
+template <int NK, int RPW>
+__global__ __launch_bounds__(256) void ln_fwd_bf16_kernel(const nrse_ln_fwd_params p) {
+  const int lane = threadIdx.x & 63;
+  const long long row0 = ((long long)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * RPW;
+  if (row0 >= p.rows) return;
+  const int C = p.C;
+  const float invC = 1.f / C;
+  uint2 raw[RPW][NK];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const long long row = min(row0 + r, p.rows - 1);
+#pragma unroll
+    for (int k = 0; k < NK; ++k)
+      raw[r][k] = ldg(reinterpret_cast<const uint2*>((const bf16_t*)p.x + row * C + (k * 64 + lane) * CH));
+  }
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const long long row = row0 + r;
+    float v[NK][CH];
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      unpack_bf4(raw[r][k], v[k]);
+#pragma unroll
+      for (int e = 0; e < CH; ++e) s += v[k][e];
+    }
+    const float mean = wave_sum(s) / C;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < NK; ++k)
+#pragma unroll
+      for (int e = 0; e < CH; ++e) { const float d = v[k][e] - mean; q += d * d; }
+    const float rstd = rsqrtf(wave_sum(q) / C + p.eps);
+    (void)invC;
+    if (row >= p.rows) break;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      const int c0 = (k * 64 + lane) * CH;
+      float4 g = *reinterpret_cast<const float4*>(p.gamma + c0);
+      float4 b = *reinterpret_cast<const float4*>(p.beta + c0);
+      float o[CH] = {(v[k][0] - mean) * rstd * g.x + b.x, (v[k][1] - mean) * rstd * g.y + b.y,
+                     (v[k][2] - mean) * rstd * g.z + b.z, (v[k][3] - mean) * rstd * g.w + b.w};
+      if (p.flags & NRSE_LN_GELU) {
+#pragma unroll
+        for (int e = 0; e < CH; ++e) o[e] = gelu_f(o[e]);
+      } else if (p.flags & NRSE_LN_RELU) {
+#pragma unroll
+        for (int e = 0; e < CH; ++e) o[e] = fmaxf(o[e], 0.f);
+      }
+      store4(p.y, p.y_dtype, row * C + c0, o);
+    }
+    if (lane == 0) {
+      if (p.mean) p.mean[row] = mean;
+      if (p.rstd) p.rstd[row] = rstd;
+    }
   }
 }
 
@@ -140,10 +206,6 @@ struct LnRow {
   bool v0, v1;  // BF: col2im taps present (their loads are issued regardless, from a valid address)
 };
 
-NRSE_DEV void unpack_bf4(uint2 v, float* o) {
-  o[0] = __uint_as_float(v.x << 16); o[1] = __uint_as_float(v.x & 0xffff0000u);
-  o[2] = __uint_as_float(v.y << 16); o[3] = __uint_as_float(v.y & 0xffff0000u);
-}
 
 // element offsets of the (up to) two col rows feeding LN row `row` (-1: no such tap)
 NRSE_DEV void col_taps(const nrse_ln_bwd_params& p, long long row, long long& o0, long long& o1) {
@@ -420,6 +482,13 @@ bool c_ok(int C) { return C == 256 || C == 512 || C == 1024; }
 extern "C" int nrse_layernorm_fwd(const nrse_ln_fwd_params* p, void* stream) {
   NRSE_REQUIRE(p && p->x && p->y && p->gamma && p->beta && p->rows > 0, "nrse_layernorm_fwd: bad args");
   if (!c_ok(p->C)) { nrse_set_error("nrse_layernorm_fwd: C=%d not in {256,512,1024}", p->C); return NRSE_ERR_UNSUPPORTED; }
+  if (p->x_dtype == NRSE_BF16 && p->C <= 512 && ((uintptr_t)p->x & 7) == 0) {
+    constexpr int RPW = 4;
+    const dim3 g((unsigned)((p->rows + 4 * RPW - 1) / (4 * RPW)));
+    if (p->C == 512) hipLaunchKernelGGL((ln_fwd_bf16_kernel<2, RPW>), g, dim3(256), 0, (hipStream_t)stream, *p);
+    else hipLaunchKernelGGL((ln_fwd_bf16_kernel<1, RPW>), g, dim3(256), 0, (hipStream_t)stream, *p);
+    return nrse_check_launch("nrse_layernorm_fwd");
+  }
   dim3 grid((unsigned)((p->rows + 3) / 4));
   NRSE_DISPATCH_NK(ln_fwd_kernel, p->C, grid, (hipStream_t)stream, *p);
   return nrse_check_launch("nrse_layernorm_fwd");

@@ -69,3 +69,7 @@ col0 = torch.randn(32 * Tin, 3 * 512, device=dev).to(torch.bfloat16)
 dw0 = torch.zeros(512, 10, device=dev); dg0 = torch.zeros(512, device=dev); db0 = torch.zeros(512, device=dev)
 us = timeit(lambda: K.conv0_bwd(wav, w0, g0, b0, m0, r0, col0, dw0, dg0, db0, T0, 10, 5, (3, 2, Tin)), iters=10)
 print(f"conv0 bwd col2im 819168x512: {us:.1f} us  {32 * Tin * 3 * 512 * 2 / us / 1e3:.0f} GB/s (col read)", flush=True)
+# conv-stack LN + GELU forward, bf16 in / out (conv1: 409568 x 512)
+yc = torch.empty(B * Tin, Cin, device=dev, dtype=torch.bfloat16)
+us = timeit(lambda: K.ln_fwd(xc, gc, bc, yc, mc, rc, 1e-5, gelu=True), iters=10)
+print(f"conv1 LN+GELU fwd 409568x512 bf16: {us:.1f} us  {B * Tin * Cin * 4 / us / 1e3:.0f} GB/s", flush=True)
