@@ -70,7 +70,7 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(const nrse_conv0_params 
     f32x2 s2 = f32x2{0.f, 0.f};
 #pragma unroll
     for (int q = 0; q < NQ; ++q) s2 += y[q][0] + y[q][1];
-    const float mean = wave_sum(s2.x + s2.y) * invC;
+    const float mean = wave_sum_dpp(s2.x + s2.y) * invC;
     f32x2 v2 = f32x2{0.f, 0.f};
 #pragma unroll
     for (int q = 0; q < NQ; ++q)
@@ -79,7 +79,7 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(const nrse_conv0_params 
         const f32x2 d = y[q][h] - mean;
         v2 = pk_fma(d, d, v2);
       }
-    const float rstd = rsqrtf(wave_sum(v2.x + v2.y) * invC + p.eps);
+    const float rstd = rsqrtf(wave_sum_dpp(v2.x + v2.y) * invC + p.eps);
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       f32x2 o[2];
@@ -262,8 +262,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
         s2 += gx.x + gx.y;
       }
     }
-    s1 = wave_sum(s1);
-    s2 = wave_sum(s2);
+    s1 = wave_sum_dpp(s1);
+    s2 = wave_sum_dpp(s2);
     if constexpr (WPR > 1) {
       const int par = (int)(it & 1);
       if (lane == 0) xch[par][w] = f32x2{s1, s2};

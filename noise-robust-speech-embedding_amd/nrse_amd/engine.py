@@ -485,32 +485,35 @@ class ByolEngine:
         del dh
         dypad = torch.empty(B, T + pk, H, device=dev, dtype=cdt)
         K.gelu_bwd_pad(ds, tape.pos_pre, dypad, B, T, H, pk // 2 - 1, pk - pk // 2 + 1)
-        K.colsum(dypad, Gv["encoder.pos_conv_embed.conv.bias"])
+        # bias + weight gradients (wgrad over (b, t) -> dWf [G][cpg][pk*cpg], weight-norm
+        # backward) on the side stream, beside the dgrad chain down the front end
+        with self._wgrad_stream(main, dypad, tape.hpad):
+            K.colsum(dypad, Gv["encoder.pos_conv_embed.conv.bias"])
+            dWf = torch.zeros(G, cpg, pk * cpg, device=dev, dtype=F32)
+            S = _divisor_at_most(B, 8)
+            off = (pk // 2 - 1) * H
+            K.gemm(K.Operand(dypad, False, H, offset=off, seg_stride=(T + pk) * H, z1=cpg),
+                   K.Operand(tape.hpad, False, H, chunk_shift=cs, ld_chunk=H, seg_stride=(T + pk) * H, z1=cpg),
+                   dWf, cpg, pk * cpg, T, ldc=pk * cpg, nseg=B // S, splits=S, batch=G, c_z1=cpg * pk * cpg,
+                   flags=_lib.EPI_ATOMIC)
+            pre = "encoder.pos_conv_embed.conv.parametrizations.weight."
+            wn_scratch = torch.empty(pk, device=dev, dtype=F32)
+            K.weight_norm_bwd(dWf, Pm[pre + "original0"], Pm[pre + "original1"], W.wn_norms, Gv[pre + "original0"],
+                              Gv[pre + "original1"], wn_scratch, H, cpg, pk)
+            del dWf
         # dgrad: ds += conv_transpose(dpre) (flipped taps, dypad has pk/2-1 leading zero rows)
         K.gemm(K.Operand(dypad, True, H, chunk_shift=cs, ld_chunk=H, z1=(T + pk) * H, z2=cpg),
                K.Operand(W.wd, True, pk * cpg, z2=cpg * pk * cpg), ds, T, cpg, pk * cpg, ldc=H, batch=B * G, zdiv=G,
                c_z1=T * H, c_z2=cpg, flags=_lib.EPI_ACCUM)
-        # wgrad over (b, t) -> dWf [G][cpg][pk*cpg]
-        dWf = torch.zeros(G, cpg, pk * cpg, device=dev, dtype=F32)
-        S = _divisor_at_most(B, 8)
-        off = (pk // 2 - 1) * H
-        K.gemm(K.Operand(dypad, False, H, offset=off, seg_stride=(T + pk) * H, z1=cpg),
-               K.Operand(tape.hpad, False, H, chunk_shift=cs, ld_chunk=H, seg_stride=(T + pk) * H, z1=cpg),
-               dWf, cpg, pk * cpg, T, ldc=pk * cpg, nseg=B // S, splits=S, batch=G, c_z1=cpg * pk * cpg,
-               flags=_lib.EPI_ATOMIC)
         del dypad
-        pre = "encoder.pos_conv_embed.conv.parametrizations.weight."
-        wn_scratch = torch.empty(pk, device=dev, dtype=F32)
-        K.weight_norm_bwd(dWf, Pm[pre + "original0"], Pm[pre + "original1"], W.wn_norms, Gv[pre + "original0"],
-                          Gv[pre + "original1"], wn_scratch, H, cpg, pk)
-        del dWf
         # SpecAugment + feature-projection dropout backward
         dproj = torch.empty(BT, H, device=dev, dtype=cdt)
         K.specaug_bwd(ds, tape.mask, Gv.get("masked_spec_embed"), dproj, B, T, H, a.feat_proj_dropout,
                       R.site_seed(fseed, R.SITE_FEAT_PROJ))
         del ds
-        K.linear_wgrad(dproj, tape.xn, Gv["feature_projection.projection.weight"])
-        K.colsum(dproj, Gv["feature_projection.projection.bias"])
+        with self._wgrad_stream(main, dproj, tape.xn):
+            K.linear_wgrad(dproj, tape.xn, Gv["feature_projection.projection.weight"])
+            K.colsum(dproj, Gv["feature_projection.projection.bias"])
         C = a.conv_dim[-1]
         dxn = torch.empty(BT, C, device=dev, dtype=F32)
         K.linear_dgrad(dproj, Ps["feature_projection.projection.weight"], dxn)
@@ -538,21 +541,24 @@ class ByolEngine:
                          beta=Pm[p + "layer_norm.bias"], gelu=True, dgamma=Gv[p + "layer_norm.weight"],
                          dbeta=Gv[p + "layer_norm.bias"], mode=_lib.DY_COL2IM, col=col)
             del dy_src
-            # wgrad -> [co][k*ci] then into the [co][ci][k] grad layout
-            A_op = K.Operand(dpre, False, Cc, seg_stride=Tout * Cc)
-            B_op = K.Operand(c["x"], False, s * Cin, seg_stride=Tin * Cin)
-            if cdt == torch.bfloat16:
-                # split-K over utterances into f32 slabs on the 256x256 kernel + ordered reduce
-                dWr = torch.empty(Cc, k * Cin, device=dev, dtype=F32)
-                S = K.slab_splits_for(((Cc + 255) // 256) * ((k * Cin + 255) // 256), B)
-                K.gemm_slab(A_op, B_op, dWr, Cc, k * Cin, Tout, nseg=B // S, splits=S, accumulate=False)
-            else:
-                dWr = torch.zeros(Cc, k * Cin, device=dev, dtype=F32)
-                tiles = ((Cc + 127) // 128) * ((k * Cin + 127) // 128)
-                S = _divisor_at_most(B, max(1, 512 // tiles))
-                K.gemm(A_op, B_op, dWr, Cc, k * Cin, Tout, ldc=k * Cin, nseg=B // S, splits=S, flags=_lib.EPI_ATOMIC)
-            K.swap12(dWr, Gv[p + "conv.weight"], Cc, k, Cin, accumulate=True)
-            del dWr
+            # wgrad -> [co][k*ci] then into the [co][ci][k] grad layout, on the side stream beside
+            # the dgrad / LN backward chain down the conv stack
+            with self._wgrad_stream(main, dpre, c["x"]):
+                A_op = K.Operand(dpre, False, Cc, seg_stride=Tout * Cc)
+                B_op = K.Operand(c["x"], False, s * Cin, seg_stride=Tin * Cin)
+                if cdt == torch.bfloat16:
+                    # split-K over utterances into f32 slabs on the 256x256 kernel + ordered reduce
+                    dWr = torch.empty(Cc, k * Cin, device=dev, dtype=F32)
+                    S = K.slab_splits_for(((Cc + 255) // 256) * ((k * Cin + 255) // 256), B)
+                    K.gemm_slab(A_op, B_op, dWr, Cc, k * Cin, Tout, nseg=B // S, splits=S, accumulate=False)
+                else:
+                    dWr = torch.zeros(Cc, k * Cin, device=dev, dtype=F32)
+                    tiles = ((Cc + 127) // 128) * ((k * Cin + 127) // 128)
+                    S = _divisor_at_most(B, max(1, 512 // tiles))
+                    K.gemm(A_op, B_op, dWr, Cc, k * Cin, Tout, ldc=k * Cin, nseg=B // S, splits=S,
+                           flags=_lib.EPI_ATOMIC)
+                K.swap12(dWr, Gv[p + "conv.weight"], Cc, k, Cin, accumulate=True)
+                del dWr
             # dgrad -> G [B*Tout, k*Cin] (col2im folded into the next LN backward)
             Gd = torch.empty(B * Tout, k * Cin, device=dev, dtype=cdt)
             K.gemm(K.Operand(dpre, True, Cc), K.Operand(W.conv_r[i - 1], False, k * Cin), Gd, B * Tout, k * Cin, Cc,
@@ -566,6 +572,7 @@ class ByolEngine:
                     c0["mean"], c0["rstd"], dy_src, Gv[p + "conv.weight"], Gv[p + "layer_norm.weight"],
                     Gv[p + "layer_norm.bias"], c0["T"], a.conv_kernel[0], a.conv_stride[0], col[:3])
         tape.conv = []
+        main.wait_stream(self._bwd_side_stream())  # every gradient written before clip / AdamW
 
     def grad_flat_for(self, Gv):
         return self.grad
