@@ -181,13 +181,20 @@ def test_overlapped_optimizer_train_steps_match_oracle(nrse_device):
     for e in (eng, ser):
         e.cfg.ema_decay = 0.99
     eng.cfg.overlap_optimizer = True
+    # grad norm: vs the serial engine every step (the overlap must not change it); vs the oracle
+    # at step 0 only — after two Adam steps the near-zero-gradient entries that atomic-order noise
+    # flips (~lr each) move the heads' BatchNorm inputs, which the heads amplify ~800x, so the f32
+    # engine's step-2 norm sits ~1 % from the oracle's for the serial and overlapped paths alike
+    # (tools/diag_overlap.py)
     for i in range(3):
         loss = float(eng.train_step(clean.cuda(), noisy.cuda(), lr=1e-4, step_seed=i))
         ls = float(ser.train_step(clean.cuda(), noisy.cuda(), lr=1e-4, step_seed=i))
         r = O.train_step(st, clean, noisy, lr=1e-4, weight_decay=eng.cfg.weight_decay, ema_decay=0.99, step_seed=i)
         assert abs(loss - ls) < 2e-5, (i, loss, ls)
         assert abs(loss - r["loss"]) < 5e-4, (i, loss, r["loss"])
-        assert abs(eng.grad_norm() - r["grad_norm"]) / r["grad_norm"] < 1e-3
+        assert abs(eng.grad_norm() - ser.grad_norm()) / ser.grad_norm() < 1e-3, (i, eng.grad_norm(), ser.grad_norm())
+        if i == 0:
+            assert abs(eng.grad_norm() - r["grad_norm"]) / r["grad_norm"] < 1e-4
     # parameters: Adam's first steps move near-zero-gradient entries by ~lr * sign(g), which
     # atomic-order noise flips, so two runs differ by ~1e-5 rel (the bitwise equivalence of the
     # segmented update itself: test_overlapped_optimizer_is_bitwise_serial)
