@@ -387,6 +387,38 @@ __global__ __launch_bounds__(256) void wn_norm_part_kernel(const float* __restri
   }
 }
 
+// Backward per-tap dot products sdot[j] = <v[:, :, j], dW[:, :, j]> with both operands read
+// coalesced: v[go] is [cpg][K] (j contiguous) and dWf[go] is [K][cpg] (i contiguous), transposes
+// of each other, so each output-channel slab of dWf goes through LDS ([j][i], row pad 1 float:
+// the column reads by thread j are conflict-free). Thread (j, ih) accumulates i-half ih of tap j
+// over the block's go range in f64; the two halves meet in LDS; part[block][j] as in the norm
+// form (wn_norm_final_kernel adds the blocks in order). Needs K * cpg <= 8192, 2 * K <= 256.
+constexpr int WN_DOT_LDS = 128 * 65;
+__global__ __launch_bounds__(256) void wn_dot_part_kernel(const float* __restrict__ v, const float* __restrict__ dWf,
+                                                          double* __restrict__ part, int ngo, int cpg, int K, int gpb) {
+  __shared__ float tr[WN_DOT_LDS];
+  __shared__ double red[256];
+  const int tid = threadIdx.x;
+  const int j = tid % K, ih = tid / K;  // 2 * K threads active
+  const int ihalf = cpg / 2;
+  const int ld = cpg + 1;
+  double acc = 0.0;
+  const int go0 = blockIdx.x * gpb, go1 = min(ngo, go0 + gpb);
+  for (int go = go0; go < go1; ++go) {
+    const float* d = dWf + (long long)go * K * cpg;
+    __syncthreads();
+    for (int e = tid; e < K * cpg; e += 256) tr[(e / cpg) * ld + (e % cpg)] = d[e];  // [j][i]
+    __syncthreads();
+    if (tid < 2 * K) {
+      const float* vv = v + (long long)go * cpg * K;
+      for (int i = ih * ihalf; i < (ih + 1) * ihalf; ++i) acc += (double)vv[(long long)i * K + j] * tr[j * ld + i];
+    }
+  }
+  red[tid] = tid < 2 * K ? acc : 0.0;
+  __syncthreads();
+  if (tid < K) part[(long long)blockIdx.x * K + tid] = red[tid] + red[tid + K];
+}
+
 // one block per tap: thread b loads block b's partial, fixed-order tree (wave shuffles, then the
 // 4 wave sums in order): deterministic, one load latency instead of nb dependent ones
 __global__ __launch_bounds__(256) void wn_norm_final_kernel(const double* __restrict__ part, int nb, int K,
@@ -409,6 +441,13 @@ __global__ __launch_bounds__(256) void wn_norm_final_kernel(const double* __rest
 constexpr int WN_NB = 256;  // blocks of the two-stage reduction (part holds WN_NB * K doubles)
 void wn_norm(hipStream_t st, const float* v, float* norms, const float* dWf, float* sdot, int H, int cpg, int K,
              double* part) {
+  if (part && dWf && 2 * K <= 256 && K * cpg <= 8192 && cpg % 2 == 0 && K * (cpg + 1) <= WN_DOT_LDS) {
+    const int ngo = H;  // [go][cpg][K] slabs of v, [go][K][cpg] of dWf
+    const int gpb = (ngo + WN_NB - 1) / WN_NB;
+    hipLaunchKernelGGL(wn_dot_part_kernel, dim3(WN_NB), dim3(256), 0, st, v, dWf, part, ngo, cpg, K, gpb);
+    hipLaunchKernelGGL(wn_norm_final_kernel, dim3(K), dim3(256), 0, st, part, WN_NB, K, norms, sdot);
+    return;
+  }
   if (part && K <= 256 && 256 % K == 0) {
     const long long n = (long long)H * cpg;
     const long long epb = (n + WN_NB - 1) / WN_NB;
@@ -437,6 +476,30 @@ __global__ void wn_apply_kernel(const float* __restrict__ g, const float* __rest
     wf[e] = from_f<T>(wv);
     // wd[g][i][(K-1-j)*cpg + o]
     wd[((gi * cpg + i) * K + (K - 1 - j)) * cpg + o] = from_f<T>(wv);
+  }
+}
+
+// dv (+)= (g_j / n_j) (dW - (sdot_j / n_j^2) v) per output-channel slab, dWf's [j][i] slab read
+// coalesced into LDS (transposed to v's [i][j] order), v / dv streamed coalesced
+__global__ __launch_bounds__(256) void wn_bwd_slab_kernel(const float* __restrict__ dWf, const float* __restrict__ g,
+                                                          const float* __restrict__ v, const float* __restrict__ norms,
+                                                          const float* __restrict__ sdot, float* __restrict__ dv,
+                                                          int ngo, int cpg, int K, int gpb) {
+  __shared__ float tr[WN_DOT_LDS];
+  const int tid = threadIdx.x;
+  const int ld = cpg + 1;
+  const int go0 = blockIdx.x * gpb, go1 = min(ngo, go0 + gpb);
+  for (int go = go0; go < go1; ++go) {
+    const float* d = dWf + (long long)go * K * cpg;
+    __syncthreads();
+    for (int e = tid; e < K * cpg; e += 256) tr[(e / cpg) * ld + (e % cpg)] = d[e];  // [j][i]
+    __syncthreads();
+    const long long base = (long long)go * cpg * K;
+    for (int e = tid; e < cpg * K; e += 256) {
+      const int i = e / K, j = e - i * K;
+      const float nj = norms[j];
+      dv[base + e] += (g[j] / nj) * (tr[j * ld + i] - (sdot[j] / (nj * nj)) * v[base + e]);
+    }
   }
 }
 
@@ -528,9 +591,14 @@ extern "C" int nrse_weight_norm_bwd(const float* dWf, const float* g, const floa
   hipStream_t st = (hipStream_t)stream;
   wn_norm(st, v, nullptr, dWf, scratch, H, cpg, K, part);
   const long long total = (long long)H * cpg * K;
-  int blocks = (int)((total + 255) / 256);
-  if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(wn_bwd_kernel, dim3(blocks), dim3(256), 0, st, dWf, g, v, norms, scratch, dv, H, cpg, K);
+  if (K * (cpg + 1) <= WN_DOT_LDS) {
+    const int gpb = (H + WN_NB - 1) / WN_NB;
+    hipLaunchKernelGGL(wn_bwd_slab_kernel, dim3(WN_NB), dim3(256), 0, st, dWf, g, v, norms, scratch, dv, H, cpg, K, gpb);
+  } else {
+    int blocks = (int)((total + 255) / 256);
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(wn_bwd_kernel, dim3(blocks), dim3(256), 0, st, dWf, g, v, norms, scratch, dv, H, cpg, K);
+  }
   hipLaunchKernelGGL(wn_dg_kernel, dim3((K + 255) / 256), dim3(256), 0, st, scratch, norms, dg, K);
   return nrse_check_launch("nrse_weight_norm_bwd");
 }
