@@ -6,6 +6,7 @@ is a libnrse_hip.so kernel. Wrappers validate shapes on the host before launchin
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 
 import torch
@@ -213,25 +214,37 @@ def _slab_splits(M: int, N: int, K: int) -> int:
     """Split count of the slab wgrad: a divisor S of the token count M with ceil(N/256) *
     ceil(K/256) * S 256x256 tiles filling 70-100 % of one wave on the 256 CUs (0: none fits)."""
     tiles = ((N + 255) // 256) * ((K + 255) // 256)
+    cap = _SLAB_MAX_TILES
     best = 0
     for s in range(1, 65):
-        if M % s or M // s < 256 or tiles * s > 256:
+        if M % s or M // s < 256 or tiles * s > cap:
             continue
-        if tiles * s >= 0.7 * 256:
+        if tiles * s >= 0.7 * cap:
             best = s
     return best
+
+
+# The slab wgrads run on the backward side stream beside the dgrad chain's GEMMs, so they size
+# their split-K to half a wave of 256x256 workgroups (fewer, longer K ranges: less slab traffic and
+# prologue/epilogue per FLOP) rather than to the whole chip: 128 measured +0.6 % pairs/s vs 256,
+# 64 -5 % (NRSE_SLAB_MAX_TILES overrides, for tuning).
+_SLAB_MAX_TILES = int(os.environ.get("NRSE_SLAB_MAX_TILES", "128"))
 
 
 _SLAB_WGRAD = True
 
 
 def slab_splits_for(tiles256: int, n_units: int) -> int:
-    """Largest divisor S of n_units with tiles256 * S <= 256 (one wave of 256x256 workgroups)."""
+    """Largest divisor S of n_units with tiles256 * S <= the slab tile cap (see _SLAB_MAX_TILES)."""
     best = 1
     for s in range(1, n_units + 1):
-        if n_units % s == 0 and tiles256 * s <= 256:
+        if n_units % s == 0 and tiles256 * s <= _CONV_SLAB_MAX_TILES:
             best = s
     return best
+
+
+# the conv-stack wgrads keep a full wave (their long token ranges; 128 measured -0.6 %)
+_CONV_SLAB_MAX_TILES = int(os.environ.get("NRSE_CONV_SLAB_MAX_TILES", "256"))
 
 
 def gemm_slab(A: "Operand", B: "Operand", out: torch.Tensor, M: int, N: int, K: int, *, nseg: int, splits: int,
