@@ -221,14 +221,24 @@ def _slab_splits(M: int, N: int, K: int) -> int:
             continue
         if tiles * s >= 0.7 * cap:
             best = s
+    if _SLAB_FORCE256 and best and tiles * best < 128:
+        # below 128 tiles nrse_gemm hands the problem to the 128x128 kernel: take the smallest
+        # split that keeps it on the 256x256 one
+        for s in range(best + 1, 65):
+            if M % s == 0 and M // s >= 256 and tiles * s >= 128:
+                return s
     return best
 
 
 # The slab wgrads run on the backward side stream beside the dgrad chain's GEMMs, so they size
 # their split-K to half a wave of 256x256 workgroups (fewer, longer K ranges: less slab traffic and
 # prologue/epilogue per FLOP) rather than to the whole chip: 128 measured +0.6 % pairs/s vs 256,
-# 64 -5 % (NRSE_SLAB_MAX_TILES overrides, for tuning).
+# 64 -5 % (NRSE_SLAB_MAX_TILES overrides, for tuning). A split landing below 128 tiles (the QKV
+# wgrad's 48 x 2) is raised to the smallest one at or above it, so the problem stays on the 256x256
+# kernel instead of falling to the 128x128 one (same-box 522 -> 525 pairs/s; NRSE_SLAB_FORCE256=0
+# restores the fall-through).
 _SLAB_MAX_TILES = int(os.environ.get("NRSE_SLAB_MAX_TILES", "128"))
+_SLAB_FORCE256 = os.environ.get("NRSE_SLAB_FORCE256", "1") == "1"
 
 
 _SLAB_WGRAD = True

@@ -84,10 +84,14 @@ def test_reference_loop_runs_unchanged_and_tracks_engine(nrse_device, dtype):
     cur_lr = lr
     for i, (c, n, next_lr) in enumerate(batches):
         l_e = float(eng.train_step(c.squeeze(1), n.squeeze(1), lr=cur_lr, step_seed=i))
-        # bf16: two runs of the same kernels differ by ~5e-3 rel-L2 in the step-0 gradient (atomic
+        # step 0 (same weights, same batch) agrees to ~2e-7 in both modes. bf16 later steps: two
+        # runs of the same kernels differ by ~5e-3 rel-L2 in the step-0 gradient (atomic
         # accumulation order through the ill-conditioned heads), so Adam's lr*sign(g) moves a few
-        # weights differently and later losses drift by ~2e-3 (f32: 1e-7; tools/dbg/loop_vs_engine.py)
-        assert abs(l_e - losses[i]) < (1e-2 if dtype == torch.bfloat16 else 2e-4), (i, l_e, losses[i])
+        # weights differently; over the loader's unseeded synthetic batches the step-1/2 losses
+        # drift by up to 1.4e-2 (tools/diag_dropin.py, 5 runs: |d| 1.3e-4 .. 1.35e-2); f32: 1e-7
+        # (tools/dbg/loop_vs_engine.py)
+        tol = 1e-5 if i == 0 else (3e-2 if dtype == torch.bfloat16 else 2e-4)
+        assert abs(l_e - losses[i]) < tol, (i, l_e, losses[i])
         cur_lr = next_lr[0]
     d_loop = model.engine.online - flat0
     d_eng = eng.online - flat0

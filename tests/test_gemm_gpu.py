@@ -167,3 +167,46 @@ def test_posconv_sliding_window(nrse_device, T):
     c = c0.clone()
     _posconv_call(K, _lib, hpad, wf, c, T, H, G, pk, fwd=False)
     assert rel(c, c0.double() + conv.reshape(B * T, H)) < 1e-5
+
+
+@pytest.mark.parametrize("T,nseg,splits", [(399, 1, 3), (100, 3, 1), (600, 1, 3)])
+def test_posconv_wgrad_sliding_window(nrse_device, T, nseg, splits):
+    """The pos-conv weight gradient as the engine poses it (engine.py encoder_backward: A = dy
+    rows of the padded dypad, B = the chunked Xp, M = 64, N = 128 taps x 64, K = T per utterance
+    segment, f32 atomics into a zeroed dWf) routed to csrc/posconv.hip's posconv_wgrad_kernel:
+    against a float64 einsum over the unfolded windows and against the generic 128x128 kernel."""
+    from nrse_amd import kernels as K, _lib
+    dev = nrse_device
+    B, H, G, pk = nseg * splits, 1024, 16, 128
+    cpg = H // G
+    cs = cpg.bit_length() - 1
+    g = torch.Generator(device=dev).manual_seed(T + 1)
+    hpad = torch.zeros(B, T + pk, H, device=dev, dtype=torch.bfloat16)
+    hpad[:, pk // 2:pk // 2 + T] = torch.randn(B, T, H, device=dev, generator=g).to(torch.bfloat16)
+    lead = pk // 2 - 1
+    dypad = torch.zeros(B, T + pk, H, device=dev, dtype=torch.bfloat16)
+    dypad[:, lead:lead + T] = torch.randn(B, T, H, device=dev, generator=g).to(torch.bfloat16)
+
+    def run():
+        dWf = torch.zeros(G, cpg, pk * cpg, device=dev)
+        K.gemm(K.Operand(dypad, False, H, offset=lead * H, seg_stride=(T + pk) * H, z1=cpg),
+               K.Operand(hpad, False, H, chunk_shift=cs, ld_chunk=H, seg_stride=(T + pk) * H, z1=cpg),
+               dWf, cpg, pk * cpg, T, ldc=pk * cpg, nseg=nseg, splits=splits, batch=G, c_z1=cpg * pk * cpg,
+               flags=_lib.EPI_ATOMIC)
+        return dWf
+
+    got = run()
+    again = run()
+    assert torch.equal(got, again)  # two partial sums per element onto zeros: order-independent
+    prev = K.gemm_select(2)
+    try:
+        generic = run()
+    finally:
+        K.gemm_select(prev)
+    dy = dypad[:, lead:lead + T].double()
+    win = hpad.double().unfold(1, pk, 1)[:, :T]  # [B, T, H, pk]: rows t .. t + pk - 1
+    for gi in range(G):
+        sl = slice(gi * cpg, (gi + 1) * cpg)
+        ref = torch.einsum("bto,btip->opi", dy[..., sl], win[:, :, sl]).reshape(cpg, pk * cpg)
+        assert rel(got[gi], ref) < 1e-5, gi
+    assert rel(got, generic) < 1e-5

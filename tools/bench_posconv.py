@@ -46,3 +46,24 @@ for gen, name in ((0, "sliding-window posconv"), (2, "generic LDS-DMA GEMM")):
     us = timeit(call)
     K.gemm_select(prev)
     print(f"{name}: {us:.1f} us  {flops / us / 1e6:.0f} TFLOP/s", flush=True)
+
+# weight gradient as encoder_backward issues it (f32 atomics into a zeroed dWf; the zeroing is
+# part of the timed call for both kernels)
+lead = pk // 2 - 1
+dypad = (torch.randn(B, T + pk, H, device=dev) * 0.5).to(torch.bfloat16)
+dWf = torch.zeros(G, cpg, pk * cpg, device=dev)
+
+
+def wcall():
+    dWf.zero_()
+    K.gemm(K.Operand(dypad, False, H, offset=lead * H, seg_stride=(T + pk) * H, z1=cpg),
+           K.Operand(hpad, False, H, chunk_shift=6, ld_chunk=H, seg_stride=(T + pk) * H, z1=cpg),
+           dWf, cpg, pk * cpg, T, ldc=pk * cpg, nseg=4, splits=8, batch=G, c_z1=cpg * pk * cpg,
+           flags=_lib.EPI_ATOMIC)
+
+
+for gen, name in ((0, "wgrad sliding-window"), (2, "wgrad generic 128x128")):
+    prev = K.gemm_select(gen)
+    us = timeit(wcall)
+    K.gemm_select(prev)
+    print(f"{name}: {us:.1f} us  {flops / us / 1e6:.0f} TFLOP/s", flush=True)
