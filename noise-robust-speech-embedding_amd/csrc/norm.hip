@@ -95,6 +95,57 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const nrse_ln_fwd_params p)
   }
 }
 
+// f32-in form (the encoder LNs: x is the f32 residual stream): the row's four 16-B words and
+// the lane's gamma / beta issued together, unconditionally, before the reductions. The generic
+// kernel's runtime dtype branch per word made the compiler wait for each load before issuing
+// the next (four serial round trips per row).
+template <int NK>
+__global__ __launch_bounds__(256) void ln_fwd_f32_kernel(const nrse_ln_fwd_params p) {
+  const int lane = threadIdx.x & 63;
+  const long long row = (long long)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (row >= p.rows) return;
+  const int C = p.C;
+  const float* xr = (const float*)p.x + row * C;
+  float4 xv[NK], gv[NK], bv[NK];
+#pragma unroll
+  for (int k = 0; k < NK; ++k) xv[k] = *reinterpret_cast<const float4*>(xr + (k * 64 + lane) * CH);
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    gv[k] = *reinterpret_cast<const float4*>(p.gamma + (k * 64 + lane) * CH);
+    bv[k] = *reinterpret_cast<const float4*>(p.beta + (k * 64 + lane) * CH);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < NK; ++k) s += (xv[k].x + xv[k].y) + (xv[k].z + xv[k].w);
+  const float mean = wave_sum(s) / C;
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const float d0 = xv[k].x - mean, d1 = xv[k].y - mean, d2 = xv[k].z - mean, d3 = xv[k].w - mean;
+    q += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
+  }
+  const float rstd = rsqrtf(wave_sum(q) / C + p.eps);
+  const long long base = row * C;
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const int c0 = (k * 64 + lane) * CH;
+    float o[CH] = {(xv[k].x - mean) * rstd * gv[k].x + bv[k].x, (xv[k].y - mean) * rstd * gv[k].y + bv[k].y,
+                   (xv[k].z - mean) * rstd * gv[k].z + bv[k].z, (xv[k].w - mean) * rstd * gv[k].w + bv[k].w};
+    if (p.flags & NRSE_LN_GELU) {
+#pragma unroll
+      for (int e = 0; e < CH; ++e) o[e] = gelu_f(o[e]);
+    } else if (p.flags & NRSE_LN_RELU) {
+#pragma unroll
+      for (int e = 0; e < CH; ++e) o[e] = fmaxf(o[e], 0.f);
+    }
+    store4(p.y, p.y_dtype, base + c0, o);
+  }
+  if (lane == 0) {
+    if (p.mean) p.mean[row] = mean;
+    if (p.rstd) p.rstd[row] = rstd;
+  }
+}
+
 // bf16-in form of the forward for the long row sweeps of the conv stack (x bf16, C <= 512):
 // each wave takes RPW rows, all of their raw 8-byte words loaded first (clamped rows, no
 // branches), so RPW KiB are in flight per wave instead of one row's 1 KiB
@@ -490,7 +541,11 @@ extern "C" int nrse_layernorm_fwd(const nrse_ln_fwd_params* p, void* stream) {
     return nrse_check_launch("nrse_layernorm_fwd");
   }
   dim3 grid((unsigned)((p->rows + 3) / 4));
-  NRSE_DISPATCH_NK(ln_fwd_kernel, p->C, grid, (hipStream_t)stream, *p);
+  if (p->x_dtype == NRSE_F32 && ((uintptr_t)p->x & 15) == 0) {
+    NRSE_DISPATCH_NK(ln_fwd_f32_kernel, p->C, grid, (hipStream_t)stream, *p);
+  } else {
+    NRSE_DISPATCH_NK(ln_fwd_kernel, p->C, grid, (hipStream_t)stream, *p);
+  }
   return nrse_check_launch("nrse_layernorm_fwd");
 }
 

@@ -36,6 +36,10 @@ us = timeit(lambda: K.ln_bwd(dy, x, g, mean, rstd, dx, resid=r, dgamma=dg, dbeta
                              dv_seed=1))
 byt = rows * C * (4 * 3 + 4 + 2)
 print(f"encoder LN bwd 12768x1024 (+fused dv): {us:.1f} us  {byt / us / 1e3:.0f} GB/s", flush=True)
+yb = torch.empty(rows, C, device=dev, dtype=torch.bfloat16)
+us = timeit(lambda: K.ln_fwd(x, g, b, yb, mean, rstd, 1e-5))
+byt = rows * C * (4 + 2)
+print(f"encoder LN fwd 12768x1024 f32 -> bf16: {us:.1f} us  {byt / us / 1e3:.0f} GB/s", flush=True)
 B, Tin, Tout, Cin, k, s = 32, 12799, 6399, 512, 3, 2
 xc = torch.randn(B * Tin, Cin, device=dev).to(torch.bfloat16)
 G = torch.randn(B * Tout, k * Cin, device=dev).to(torch.bfloat16)
