@@ -275,10 +275,28 @@ NRSE_DEV void col_taps(const nrse_ln_bwd_params& p, long long row, long long& o0
   o1 = o[1];
 }
 
-template <int NK, bool RES, bool COL, bool BF>
+// FD (encoder form, RES): x, dy and the residual all f32, dy direct: three unconditional 16-B
+// loads per word, no dtype / mode branches (each of which had made the compiler wait for the load)
+template <int NK, bool RES, bool COL, bool BF, bool FD>
 NRSE_DEV void ln_bwd_load(const nrse_ln_bwd_params& p, long long row, int lane, LnRow<NK, RES, COL, BF>& b) {
   b.mean = p.mean[row];
   b.rstd = p.rstd[row];
+  if constexpr (FD) {
+    const float* xr = (const float*)p.x + row * p.C;
+    const float* dr = (const float*)p.dy + row * p.C;
+    const float* rr = p.resid + row * p.C;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      const int c0 = (k * 64 + lane) * CH;
+      const float4 xv = *reinterpret_cast<const float4*>(xr + c0);
+      const float4 dv = *reinterpret_cast<const float4*>(dr + c0);
+      const float4 rv = *reinterpret_cast<const float4*>(rr + c0);
+      b.x[k][0] = xv.x; b.x[k][1] = xv.y; b.x[k][2] = xv.z; b.x[k][3] = xv.w;
+      b.dy[k][0] = dv.x; b.dy[k][1] = dv.y; b.dy[k][2] = dv.z; b.dy[k][3] = dv.w;
+      b.r[RES ? k : 0][0] = rv.x; b.r[RES ? k : 0][1] = rv.y; b.r[RES ? k : 0][2] = rv.z; b.r[RES ? k : 0][3] = rv.w;
+    }
+    return;
+  }
   long long o0 = -1, o1 = -1;
   if constexpr (COL) col_taps(p, row, o0, o1);
   else if constexpr (BF) o0 = row * p.C;  // direct dy
@@ -317,14 +335,15 @@ NRSE_DEV void ln_bwd_load(const nrse_ln_bwd_params& p, long long row, int lane, 
 
 // RES: the encoder-layer form (residual input, fused dropout-cast consumer); !RES (conv / feature
 // projection LNs) drops their registers: 137 -> fewer VGPRs, more waves for the long row sweeps
-template <int NK, bool RES, bool COL, bool BF>
+template <int NK, bool RES, bool COL, bool BF, bool FD = false>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const nrse_ln_bwd_params p) {
+  constexpr bool GBL = RES && !FD;  // gamma / beta read from global memory per row
   __shared__ float red[4][NK * 64 * CH];
   // gamma / beta staged once: read per row from LDS (lgkmcnt), not global memory, whose per-row
   // loads were the youngest vmcnt entries and made every row wait for the prefetched next row
   // (the encoder form keeps global reads: hoisted LDS copies would cost it 32 VGPRs)
-  __shared__ __attribute__((aligned(16))) float gb[RES ? 1 : 2][RES ? 4 : NK * 64 * CH];
-  if constexpr (!RES) {
+  __shared__ __attribute__((aligned(16))) float gb[GBL ? 1 : 2][GBL ? 4 : NK * 64 * CH];
+  if constexpr (!GBL) {
     for (int c = threadIdx.x; c < p.C; c += 256) {
       gb[0][c] = p.gamma[c];
       gb[1][c] = (p.flags & (NRSE_LN_GELU | NRSE_LN_RELU)) ? p.beta[c] : 0.f;
@@ -355,7 +374,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const nrse_ln_bwd_params p)
     for (int k = 0; k < NK; ++k) {
       const int c0 = (k * 64 + lane) * CH;
       float gam[CH], be[CH] = {0.f, 0.f, 0.f, 0.f};
-      if constexpr (RES) {
+      if constexpr (GBL) {
         const float4 ga = *reinterpret_cast<const float4*>(p.gamma + c0);
         gam[0] = ga.x; gam[1] = ga.y; gam[2] = ga.z; gam[3] = ga.w;
         if (p.flags & (NRSE_LN_GELU | NRSE_LN_RELU)) {
@@ -365,7 +384,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const nrse_ln_bwd_params p)
       } else {
         const float4 ga = *reinterpret_cast<const float4*>(&gb[0][c0]);
         gam[0] = ga.x; gam[1] = ga.y; gam[2] = ga.z; gam[3] = ga.w;
-        const float4 bb = *reinterpret_cast<const float4*>(&gb[RES ? 0 : 1][c0]);
+        const float4 bb = *reinterpret_cast<const float4*>(&gb[GBL ? 0 : 1][c0]);
         be[0] = bb.x; be[1] = bb.y; be[2] = bb.z; be[3] = bb.w;
       }
       float xv[CH], dv0[CH], dv1[CH] = {0.f, 0.f, 0.f, 0.f};
@@ -427,24 +446,24 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const nrse_ln_bwd_params p)
   long long row = (long long)blockIdx.x * 4 + w;
   LnRow<NK, RES, COL, BF> ba, bb;
   const long long last = p.rows - 1;
-  if (row < p.rows) ln_bwd_load(p, row, lane, ba);
+  if (row < p.rows) ln_bwd_load<NK, RES, COL, BF, FD>(p, row, lane, ba);
   for (; row < p.rows; row += 2 * nw) {
     const long long rb = row + nw;
     // BF: unconditional (clamped) prefetch, fenced from the scheduler, which otherwise sinks the
     // loads below part of the current row's math to save registers (and then waits for them)
-    if (BF) {
-      ln_bwd_load(p, rb < last ? rb : last, lane, bb);
+    if (BF || FD) {
+      ln_bwd_load<NK, RES, COL, BF, FD>(p, rb < last ? rb : last, lane, bb);
       __builtin_amdgcn_sched_barrier(0);
     } else if (rb < p.rows) {
-      ln_bwd_load(p, rb, lane, bb);
+      ln_bwd_load<NK, RES, COL, BF, FD>(p, rb, lane, bb);
     }
     compute(ba, row);
     if (rb >= p.rows) break;
-    if (BF) {
-      ln_bwd_load(p, rb + nw < last ? rb + nw : last, lane, ba);
+    if (BF || FD) {
+      ln_bwd_load<NK, RES, COL, BF, FD>(p, rb + nw < last ? rb + nw : last, lane, ba);
       __builtin_amdgcn_sched_barrier(0);
     } else if (rb + nw < p.rows) {
-      ln_bwd_load(p, rb + nw, lane, ba);
+      ln_bwd_load<NK, RES, COL, BF, FD>(p, rb + nw, lane, ba);
     }
     compute(bb, rb);
   }
@@ -579,8 +598,13 @@ extern "C" int nrse_layernorm_bwd(const nrse_ln_bwd_params* p, void* stream) {
   // bf16 x and dy (conv / feature-projection LNs of the bf16 step), direct or two-tap col2im dy
   const bool bf = !res && p->x_dtype == NRSE_BF16 && p->dy_dtype == NRSE_BF16 &&
                   (col2 || p->dy_mode == NRSE_DY_DIRECT);
+  // encoder form with every operand f32 and dy direct: the branch-free loads
+  const bool fd = res && p->resid && p->x_dtype == NRSE_F32 && p->dy_dtype == NRSE_F32 &&
+                  p->dy_mode == NRSE_DY_DIRECT &&
+                  ((((uintptr_t)p->x) | ((uintptr_t)p->dy) | ((uintptr_t)p->resid)) & 15) == 0;
 #define NRSE_LN_BWD_NK(NK)                                                                          \
-  if (res) hipLaunchKernelGGL((ln_bwd_kernel<NK, true, false, false>), grid, dim3(256), 0, st, *p);    \
+  if (fd) hipLaunchKernelGGL((ln_bwd_kernel<NK, true, false, false, true>), grid, dim3(256), 0, st, *p); \
+  else if (res) hipLaunchKernelGGL((ln_bwd_kernel<NK, true, false, false>), grid, dim3(256), 0, st, *p);    \
   else if (bf && col2) hipLaunchKernelGGL((ln_bwd_kernel<NK, false, true, true>), grid, dim3(256), 0, st, *p); \
   else if (bf) hipLaunchKernelGGL((ln_bwd_kernel<NK, false, false, true>), grid, dim3(256), 0, st, *p); \
   else if (col2) hipLaunchKernelGGL((ln_bwd_kernel<NK, false, true, false>), grid, dim3(256), 0, st, *p); \
