@@ -3,6 +3,8 @@
 // (one query/key row per lane). The f32 kernels are the parity path (fp32 mode) and the
 // fallback for shapes the MFMA flash kernels (attention_mfma.hip) do not cover; they compute
 // in f32 for both storage dtypes.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -88,6 +90,9 @@ struct GateW {
   }
 };
 
+// GATE_U item groups per wave and iteration, their loads issued together (clamped, no branch):
+// one group's 1 KiB per wave in flight left the sweep latency-bound (1.9 TB/s)
+constexpr int GATE_U = 4;
 template <typename T>
 __global__ __launch_bounds__(256) void gate_fwd_kernel(const void* __restrict__ x1, const float* __restrict__ W,
                                                        const float* __restrict__ bv, const float* __restrict__ c,
@@ -97,17 +102,24 @@ __global__ __launch_bounds__(256) void gate_fwd_kernel(const void* __restrict__ 
   const long long total = (long long)batch * Tn * H;
   const long long wave = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const long long nwave = (long long)gridDim.x * (blockDim.x >> 6);
-  for (long long n0 = wave * 8; n0 < total; n0 += nwave * 8) {
-    const long long n = n0 + ig;
-    float x[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (n < total) ld8v<T>(x1, n * HD + 8 * sub, x);
-    float a, b;
-    gw.ab(x, a, b);
-    if (sub == 0 && n < total) {
-      const long long row = n / H;
-      const int h = (int)(n % H);
-      const long long bi = row / Tn, t = row % Tn;
-      gate[(bi * H + h) * Tn + t] = a * (b * c[h] - 1.f) + 2.f;
+  for (long long n0 = wave * 8 * GATE_U; n0 < total; n0 += nwave * 8 * GATE_U) {
+    float x[GATE_U][8];
+#pragma unroll
+    for (int j = 0; j < GATE_U; ++j) {
+      const long long n = n0 + 8 * j + ig;
+      ld8v<T>(x1, (n < total ? n : total - 1) * HD + 8 * sub, x[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < GATE_U; ++j) {
+      const long long n = n0 + 8 * j + ig;
+      float a, b;
+      gw.ab(x[j], a, b);
+      if (sub == 0 && n < total) {
+        const long long row = n / H;
+        const int h = (int)(n % H);
+        const long long bi = row / Tn, t = row % Tn;
+        gate[(bi * H + h) * Tn + t] = a * (b * c[h] - 1.f) + 2.f;
+      }
     }
   }
 }
@@ -119,6 +131,7 @@ __global__ __launch_bounds__(256) void gate_fwd_kernel(const void* __restrict__ 
 // The grid is a multiple of H workgroups, so the item stride (8 per wave per step) is a
 // multiple of H and every 8-lane group keeps one head for the whole loop.
 constexpr int GATE_BWD_BLOCKS_PER_HEAD = 16;
+constexpr int GATE_BU = 4;
 template <typename T>
 __global__ __launch_bounds__(256) void gate_bwd_kernel(const void* __restrict__ x1, const float* __restrict__ W,
                                                        const float* __restrict__ bv, const float* __restrict__ c,
@@ -136,33 +149,47 @@ __global__ __launch_bounds__(256) void gate_bwd_kernel(const void* __restrict__ 
   const float ch = c[h];
   float accA[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, accB[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   float sdpa = 0.f, sdpb = 0.f, sdc = 0.f;
-  for (long long n0 = wave * 8; n0 < total; n0 += nwave * 8) {
-    const long long n = n0 + ig;
-    const bool ok = n < total;
-    float x[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (ok) ld8v<T>(x1, n * HD + 8 * sub, x);
-    float a, b;
-    gw.ab(x, a, b);
-    float dg = 0.f;
-    if (ok) {
-      const long long row = n / H;
-      const long long bi = row / Tn, t = row % Tn;
-      dg = dgate[(bi * H + h) * Tn + t];
-    }
-    const float dpa = dg * (b * ch - 1.f) * a * (1.f - a);
-    const float dpb = dg * a * ch * b * (1.f - b);
-    if (ok) {
-      float4* d = reinterpret_cast<float4*>(dx1 + n * HD + 8 * sub);
-      float4 u = d[0], v = d[1];
-      u.x += dpa * gw.wa[0] + dpb * gw.wb[0]; u.y += dpa * gw.wa[1] + dpb * gw.wb[1];
-      u.z += dpa * gw.wa[2] + dpb * gw.wb[2]; u.w += dpa * gw.wa[3] + dpb * gw.wb[3];
-      v.x += dpa * gw.wa[4] + dpb * gw.wb[4]; v.y += dpa * gw.wa[5] + dpb * gw.wb[5];
-      v.z += dpa * gw.wa[6] + dpb * gw.wb[6]; v.w += dpa * gw.wa[7] + dpb * gw.wb[7];
-      d[0] = u; d[1] = v;
+  // GATE_BU items per lane and iteration, one grid stride apart (so the lane's head is the same
+  // for all of them), every load issued up front from a clamped index; 32-bit index math (the
+  // host checks total < 2^31)
+  const int tot = (int)total, stride = (int)(nwave * 8);
+  for (int n0 = (int)(wave * 8) + ig; n0 < tot; n0 += stride * GATE_BU) {
+    float x[GATE_BU][8], dgv[GATE_BU];
+    float4 du[GATE_BU], dw[GATE_BU];
+#pragma unroll
+    for (int j = 0; j < GATE_BU; ++j) {
+      const int n = n0 + j * stride;
+      const int nc = n < tot ? n : tot - 1;
+      ld8v<T>(x1, (long long)nc * HD + 8 * sub, x[j]);
+      const int row = nc / H;
+      const int bi = row / Tn, t = row - bi * Tn;
+      dgv[j] = dgate[((long long)bi * H + h) * Tn + t];
+      const float4* d = reinterpret_cast<const float4*>(dx1 + (long long)nc * HD + 8 * sub);
+      du[j] = d[0];
+      dw[j] = d[1];
     }
 #pragma unroll
-    for (int e = 0; e < 8; ++e) { accA[e] += dpa * x[e]; accB[e] += dpb * x[e]; }
-    sdpa += dpa; sdpb += dpb; sdc += dg * a * b;
+    for (int j = 0; j < GATE_BU; ++j) {
+      const int n = n0 + j * stride;
+      const bool ok = n < tot;
+      float a, b;
+      gw.ab(x[j], a, b);
+      const float dg = ok ? dgv[j] : 0.f;
+      const float dpa = dg * (b * ch - 1.f) * a * (1.f - a);
+      const float dpb = dg * a * ch * b * (1.f - b);
+      if (ok) {
+        float4 u = du[j], v = dw[j];
+        u.x += dpa * gw.wa[0] + dpb * gw.wb[0]; u.y += dpa * gw.wa[1] + dpb * gw.wb[1];
+        u.z += dpa * gw.wa[2] + dpb * gw.wb[2]; u.w += dpa * gw.wa[3] + dpb * gw.wb[3];
+        v.x += dpa * gw.wa[4] + dpb * gw.wb[4]; v.y += dpa * gw.wa[5] + dpb * gw.wb[5];
+        v.z += dpa * gw.wa[6] + dpb * gw.wb[6]; v.w += dpa * gw.wa[7] + dpb * gw.wb[7];
+        float4* d = reinterpret_cast<float4*>(dx1 + (long long)n * HD + 8 * sub);
+        d[0] = u; d[1] = v;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { accA[e] += dpa * x[j][e]; accB[e] += dpb * x[j][e]; }
+      sdpa += dpa; sdpb += dpb; sdc += dg * a * b;
+    }
   }
   // per-head term: one atomic per 8-lane group
   if (sub == 0 && sdc != 0.f) atomicAdd(dc + h, sdc);
@@ -458,8 +485,8 @@ extern "C" int nrse_gate_fwd(const void* x1, int x_dtype, const float* W, const 
   NRSE_REQUIRE(x1 && W && bvec && c && gate && batch > 0 && T > 0 && H > 0, "nrse_gate_fwd: bad args");
   NRSE_REQUIRE(((uintptr_t)x1 & 15) == 0, "nrse_gate_fwd: x1 not 16-byte aligned");
   const long long total = (long long)batch * T * H;
-  const long long blocks = (total + 31) / 32;  // 8 items per wave, 4 waves per block
-  dim3 grid((unsigned)(blocks < 4096 ? blocks : 4096));
+  const long long blocks = (total + 32 * GATE_U - 1) / (32 * GATE_U);  // 8 * GATE_U items per wave, 4 waves
+  dim3 grid((unsigned)(blocks < 2048 ? blocks : 2048));
   hipStream_t st = (hipStream_t)stream;
   if (x_dtype == NRSE_BF16) hipLaunchKernelGGL(gate_fwd_kernel<bf16_t>, grid, dim3(256), 0, st, x1, W, bvec, c, gate, batch, T, H);
   else hipLaunchKernelGGL(gate_fwd_kernel<float>, grid, dim3(256), 0, st, x1, W, bvec, c, gate, batch, T, H);
@@ -472,9 +499,11 @@ extern "C" int nrse_gate_bwd(const void* x1, int x_dtype, const float* W, const 
   NRSE_REQUIRE(x1 && W && bvec && c && dgate && dx1 && dW && db && dc && batch > 0 && T > 0 && H > 0,
                "nrse_gate_bwd: bad args");
   NRSE_REQUIRE(((uintptr_t)x1 & 15) == 0 && ((uintptr_t)dx1 & 15) == 0, "nrse_gate_bwd: x1/dx1 not 16-byte aligned");
+  NRSE_REQUIRE((long long)batch * T * H < (1LL << 31) - (1LL << 24), "nrse_gate_bwd: too many items");
   hipStream_t st = (hipStream_t)stream;
   // a multiple of H workgroups: each 8-lane item group then keeps one head (see the kernel)
-  dim3 grid((unsigned)(GATE_BWD_BLOCKS_PER_HEAD * H));
+  static const int bph = getenv("NRSE_GATE_BWD_BPH") ? atoi(getenv("NRSE_GATE_BWD_BPH")) : GATE_BWD_BLOCKS_PER_HEAD;
+  dim3 grid((unsigned)(bph * H));
   if (x_dtype == NRSE_BF16)
     hipLaunchKernelGGL(gate_bwd_kernel<bf16_t>, grid, dim3(256), 0, st, x1, W, bvec, c, dgate, dx1, dW, db, dc, batch,
                        T, H);
