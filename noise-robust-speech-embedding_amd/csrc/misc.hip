@@ -362,15 +362,29 @@ extern "C" int nrse_cast(const void* x, int xdt, void* y, int ydt, long long n, 
 }
 
 // dst (+)= sum over splits of the f32 partial slabs, 16 B per lane, grid-stride; the slabs are
-// streamed once (HBM-bound: (splits + 1 or 2) * n * 4 bytes)
+// streamed once (HBM-bound: (splits + 1 or 2) * n * 4 bytes). S > 0: the split count as a
+// template constant, so every slab's load (and dst's) is issued before the first add; with the
+// runtime count the loop waited for each load in turn. The sum order (dst, slab 0, 1, ...) is
+// the same in both forms.
+template <int S, bool ACC = false>
 static __global__ __launch_bounds__(256) void splitk_reduce_kernel(float* __restrict__ dst, const float* __restrict__ slabs,
-                                                            int splits, long long n4, long long n, int acc) {
+                                                                   int splits, long long n4, long long n, int acc) {
   const long long stride = (long long)gridDim.x * 256;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
-    float4 s = acc ? reinterpret_cast<const float4*>(dst)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int k = 0; k < splits; ++k) {
-      const float4 v = reinterpret_cast<const float4*>(slabs + (long long)k * n)[i];
-      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    float4 s;
+    if constexpr (S > 0) {
+      float4 v[S];
+      s = ACC ? reinterpret_cast<const float4*>(dst)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int k = 0; k < S; ++k) v[k] = reinterpret_cast<const float4*>(slabs + (long long)k * n)[i];
+#pragma unroll
+      for (int k = 0; k < S; ++k) { s.x += v[k].x; s.y += v[k].y; s.z += v[k].z; s.w += v[k].w; }
+    } else {
+      s = acc ? reinterpret_cast<const float4*>(dst)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int k = 0; k < splits; ++k) {
+        const float4 v = reinterpret_cast<const float4*>(slabs + (long long)k * n)[i];
+        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      }
     }
     reinterpret_cast<float4*>(dst)[i] = s;
   }
@@ -389,8 +403,31 @@ extern "C" int nrse_splitk_reduce(float* dst, const float* slabs, int splits, lo
                "nrse_splitk_reduce: dst / slabs must be 16-byte aligned and n a multiple of 4");
   const long long n4 = n / 4;
   const long long blocks = std::min<long long>((n4 + 255) / 256, 2048);
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)std::max<long long>(blocks, 1)), dim3(256), 0,
-                     (hipStream_t)stream, dst, slabs, splits, n4, n, accumulate);
+  const dim3 g((unsigned)std::max<long long>(blocks, 1));
+  hipStream_t st = (hipStream_t)stream;
+  switch (splits) {
+    case 1:
+      if (accumulate) hipLaunchKernelGGL((splitk_reduce_kernel<1, true>), g, dim3(256), 0, st, dst, slabs, splits, n4, n, accumulate);
+      else hipLaunchKernelGGL((splitk_reduce_kernel<1, false>), g, dim3(256), 0, st, dst, slabs, splits, n4, n, accumulate);
+      break;
+    case 2:
+      if (accumulate) hipLaunchKernelGGL((splitk_reduce_kernel<2, true>), g, dim3(256), 0, st, dst, slabs, splits, n4, n, accumulate);
+      else hipLaunchKernelGGL((splitk_reduce_kernel<2, false>), g, dim3(256), 0, st, dst, slabs, splits, n4, n, accumulate);
+      break;
+    case 3:
+      if (accumulate) hipLaunchKernelGGL((splitk_reduce_kernel<3, true>), g, dim3(256), 0, st, dst, slabs, splits, n4, n, accumulate);
+      else hipLaunchKernelGGL((splitk_reduce_kernel<3, false>), g, dim3(256), 0, st, dst, slabs, splits, n4, n, accumulate);
+      break;
+    case 4:
+      if (accumulate) hipLaunchKernelGGL((splitk_reduce_kernel<4, true>), g, dim3(256), 0, st, dst, slabs, splits, n4, n, accumulate);
+      else hipLaunchKernelGGL((splitk_reduce_kernel<4, false>), g, dim3(256), 0, st, dst, slabs, splits, n4, n, accumulate);
+      break;
+    case 8:
+      if (accumulate) hipLaunchKernelGGL((splitk_reduce_kernel<8, true>), g, dim3(256), 0, st, dst, slabs, splits, n4, n, accumulate);
+      else hipLaunchKernelGGL((splitk_reduce_kernel<8, false>), g, dim3(256), 0, st, dst, slabs, splits, n4, n, accumulate);
+      break;
+    default: hipLaunchKernelGGL((splitk_reduce_kernel<0>), g, dim3(256), 0, st, dst, slabs, splits, n4, n, accumulate); break;
+  }
   return nrse_check_launch("nrse_splitk_reduce");
 }
 

@@ -99,7 +99,7 @@ def test_linear_wgrad_slab_splitk(nrse_device, shape):
 def test_splitk_reduce(nrse_device):
     from nrse_amd import kernels as K, _lib
     dev = nrse_device
-    for n, S in ((4096, 3), (1000, 1), (12, 5)):
+    for n, S in ((4096, 3), (1000, 1), (12, 5), (8192, 8), (4100, 2)):
         slabs = torch.randn(S, n, device=dev)
         dst = torch.randn(n, device=dev)
         ref = dst.double() + slabs.double().sum(0)
