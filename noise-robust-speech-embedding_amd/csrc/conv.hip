@@ -18,6 +18,23 @@ NRSE_DEV long long uniform_ll(long long v) {
   return ((long long)hi << 32) | (unsigned)lo;
 }
 
+// n / d for n < 2^31 and a runtime d >= 1 as one multiply-high (round-up form of Granlund and
+// Montgomery): l = ceil(log2 d), m = ceil(2^(31+l) / d) < 2^32, and (n * m) >> (31 + l) = n / d
+// exactly for every n < 2^31 (m d - 2^(31+l) < d <= 2^l). The row -> (utterance, frame) split
+// ran as a software 64-bit divide on the scalar unit per row (~180 SALU instructions per row and
+// wave in the backward, PMC); set up once per kernel, it is a few scalar ops per use.
+struct UDiv31 {
+  unsigned m;
+  int sh;
+  NRSE_DEV void init(unsigned d) {
+    int l = 0;
+    while ((1u << l) < d) ++l;
+    sh = 31 + l;
+    m = (unsigned)(((1ull << sh) + d - 1) / d);
+  }
+  NRSE_DEV unsigned div(unsigned n) const { return (unsigned)(((unsigned long long)n * m) >> sh); }
+};
+
 // LDS weight image wT[j][c] (tap-major) so lane reads 4 consecutive channels per tap
 NRSE_DEV void load_wT(float* wT, const float* w, int C, int k) {
   for (int e = threadIdx.x; e < C * KMAX; e += blockDim.x) {
@@ -47,11 +64,13 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(const nrse_conv0_params 
   const float invC = 1.f / C;
   const long long rows = (long long)p.batch * p.T0;
   const long long nw = (long long)gridDim.x * 4;
+  UDiv31 dT0;
+  dT0.init((unsigned)p.T0);
   for (long long r0 = (long long)blockIdx.x * 4 + (threadIdx.x >> 6); r0 < rows; r0 += nw) {
     const long long row = uniform_ll(r0);
-    const long long b = row / p.T0;
-    const int t = (int)(row - b * p.T0);
-    const float* x = p.wav + b * p.L + (long long)t * p.s;
+    const unsigned b = dT0.div((unsigned)row);  // rows < 2^31 (host check)
+    const int t = (int)((unsigned)row - b * (unsigned)p.T0);
+    const float* x = p.wav + (long long)b * p.L + (long long)t * p.s;
     float xs[KMAX];
 #pragma unroll
     for (int j = 0; j < KMAX; ++j) xs[j] = j < p.k ? x[j] : 0.f;
@@ -136,9 +155,10 @@ struct C0Row {
 };
 
 template <bool BF>
-NRSE_DEV void c0_load(const nrse_conv0_params& p, long long row, int c0, bool col2, C0Row<BF>& r) {
-  const long long b = row / p.T0;
-  const int t = (int)(row - b * p.T0);
+NRSE_DEV void c0_load(const nrse_conv0_params& p, const UDiv31& dT0, const UDiv31& dS, long long row, int c0,
+                      bool col2, C0Row<BF>& r) {
+  const long long b = dT0.div((unsigned)row);  // rows < 2^31 (host check)
+  const int t = (int)((unsigned)row - (unsigned)b * (unsigned)p.T0);
   const float* x = p.wav + b * p.L + (long long)t * p.s;
 #pragma unroll
   for (int j = 0; j < KMAX; ++j) r.xs[j] = j < p.k ? ldg(x + j) : 0.f;
@@ -148,9 +168,10 @@ NRSE_DEV void c0_load(const nrse_conv0_params& p, long long row, int c0, bool co
   bool v0 = true, v1 = false;
   if (p.dy_mode == NRSE_DY_COL2IM) {
     // taps j0 = t mod s and j0 + s (k <= 2s): col row (t - j) / s of tap j
-    const int j0 = t % p.col_s;
+    const int q = (int)dS.div((unsigned)t);
+    const int j0 = t - q * p.col_s;
     const int j1 = j0 + p.col_s;
-    const int t0 = (t - j0) / p.col_s, t1 = (t - j1) / p.col_s;
+    const int t0 = q, t1 = q - 1;  // (t - j1) / s where t >= j1 (v1); unused otherwise
     v0 = j0 < p.col_k && t0 < p.col_tout;
     v1 = j1 < p.col_k && t >= j1 && t1 < p.col_tout;
     o0 = v0 ? ((b * p.col_tout + t0) * p.col_k + j0) * (long long)p.C : 0;
@@ -221,11 +242,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
   // uniform trip count over the block (the row exchange is a block barrier)
   const long long iters = first < rows ? (rows - first + stride - 1) / stride : 0;
   const bool generic = p.dy_mode == NRSE_DY_COL2IM && p.col_k > 2 * p.col_s;
+  UDiv31 dT0, dS;
+  dT0.init((unsigned)p.T0);
+  dS.init(p.col_s > 0 ? (unsigned)p.col_s : 1u);
   const float invC = 1.f / C;
 
   auto step = [&](const C0Row<BF>& cur, C0Row<BF>& nxt, long long it, long long row) {
     const long long rn = row + stride;
-    c0_load<BF>(p, rn < last ? rn : last, c0, !generic, nxt);
+    c0_load<BF>(p, dT0, dS, rn < last ? rn : last, c0, !generic, nxt);
     __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this row's math
     const bool live = row < rows;
     f32x2 xh[2], g[2];
@@ -291,7 +315,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
 
   C0Row<BF> ra, rb;
   long long row = first + rg;
-  if (iters > 0) c0_load<BF>(p, row < last ? row : last, c0, !generic, ra);
+  if (iters > 0) c0_load<BF>(p, dT0, dS, row < last ? row : last, c0, !generic, ra);
   for (long long it = 0; it < iters; it += 2) {  // two row buffers, alternated (no copies)
     step(ra, rb, it, row);
     row += stride;
@@ -531,6 +555,7 @@ __global__ void wn_dg_kernel(const float* __restrict__ sdot, const float* __rest
 extern "C" int nrse_conv0_fwd(const nrse_conv0_params* p, void* stream) {
   NRSE_REQUIRE(p && p->wav && p->w && p->gamma && p->beta && p->out && p->mean && p->rstd, "nrse_conv0_fwd: bad args");
   NRSE_REQUIRE(p->k > 0 && p->k <= KMAX && p->T0 == (p->L - p->k) / p->s + 1, "nrse_conv0_fwd: bad geometry");
+  NRSE_REQUIRE((long long)p->batch * p->T0 < (1LL << 31), "nrse_conv0_fwd: too many rows");
   const long long rows = (long long)p->batch * p->T0;
   long long blocks = (rows + 3) / 4;
   if (blocks > 4096) blocks = 4096;
@@ -547,6 +572,7 @@ extern "C" int nrse_conv0_bwd(const nrse_conv0_params* p, void* stream) {
   NRSE_REQUIRE(p && p->wav && p->w && p->gamma && p->beta && p->mean && p->rstd && p->dy && p->dw && p->dgamma &&
                p->dbeta, "nrse_conv0_bwd: bad args");
   NRSE_REQUIRE(p->k > 0 && p->k <= KMAX, "nrse_conv0_bwd: bad k");
+  NRSE_REQUIRE((long long)p->batch * p->T0 < (1LL << 31), "nrse_conv0_bwd: too many rows");
   if (p->dy_mode == NRSE_DY_COL2IM) NRSE_REQUIRE(p->col_k > 0 && p->col_s > 0 && p->col_tout > 0, "nrse_conv0_bwd: col2im");
   const long long rows = (long long)p->batch * p->T0;
   const int rpb = p->C == 512 ? 2 : 4;

@@ -46,5 +46,19 @@ if what in ("all", "attn"):
     for _ in range(reps):
         K.attn_fwd(qkv, gate, bias, ctx, lse, B, T, H, 0.1, 123, bias_vec=bvec)
         K.attn_bwd(qkv, gate, bias, ctx, dctx, lse, delta, dqkv, dgate, diag, B, T, H, 0.1, 123, bias_vec=bvec)
+if what == "conv0":
+    # conv0 (1 -> 512, k10 s5) + LN + GELU forward, and its backward with dy = the col2im fold
+    # of conv1's dgrad [32 x 12799, 3 x 512] (bf16), as in the step
+    L0, T0, T1 = 128000, 25599, 12799
+    wav = torch.randn(32, L0, device=dev) * 0.1
+    w0 = torch.randn(512, 10, device=dev) * 0.3
+    g0 = torch.ones(512, device=dev); b0 = torch.zeros(512, device=dev)
+    o0 = torch.empty(32 * T0, 512, device=dev, dtype=torch.bfloat16)
+    m0 = torch.empty(32 * T0, device=dev); r0 = torch.empty(32 * T0, device=dev)
+    col = rnd(32 * T1, 3 * 512)
+    dw0 = torch.zeros(512, 10, device=dev); dg0 = torch.zeros(512, device=dev); db0 = torch.zeros(512, device=dev)
+    for _ in range(reps):
+        K.conv0_fwd(wav, w0, g0, b0, o0, m0, r0, T0, 10, 5, 1e-5)
+        K.conv0_bwd(wav, w0, g0, b0, m0, r0, col, dw0, dg0, db0, T0, 10, 5, (3, 2, T1))
 torch.cuda.synchronize()
 print("done", what)
