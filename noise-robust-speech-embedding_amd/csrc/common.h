@@ -136,6 +136,23 @@ NRSE_DEV bool attn_keep(uint32_t key, uint32_t row, uint32_t tp2, int k, uint32_
   return attn_half_keep(attn_pair_hash(key, row, tp2, k), k & 1, thr16);
 }
 
+// n / d for n < 2^31 and a runtime d >= 1 as one multiply-high (round-up form of Granlund and
+// Montgomery): l = ceil(log2 d), m = ceil(2^(31+l) / d) < 2^32, and (n * m) >> (31 + l) = n / d
+// exactly for every n < 2^31 (m d - 2^(31+l) < d <= 2^l). A row -> (utterance, frame) split as a
+// software 64-bit divide on the scalar unit cost ~180 SALU instructions per row and wave in the
+// conv0 backward (PMC); set up once per kernel, this is a few scalar ops per use.
+struct UDiv31 {
+  unsigned m;
+  int sh;
+  NRSE_DEV void init(unsigned d) {
+    int l = 0;
+    while ((1u << l) < d) ++l;
+    sh = 31 + l;
+    m = (unsigned)(((1ull << sh) + d - 1) / d);
+  }
+  NRSE_DEV unsigned div(unsigned n) const { return (unsigned)(((unsigned long long)n * m) >> sh); }
+};
+
 // Wave-wide reductions (wave64).
 NRSE_DEV float wave_sum(float v) {
 #pragma unroll

@@ -18,23 +18,6 @@ NRSE_DEV long long uniform_ll(long long v) {
   return ((long long)hi << 32) | (unsigned)lo;
 }
 
-// n / d for n < 2^31 and a runtime d >= 1 as one multiply-high (round-up form of Granlund and
-// Montgomery): l = ceil(log2 d), m = ceil(2^(31+l) / d) < 2^32, and (n * m) >> (31 + l) = n / d
-// exactly for every n < 2^31 (m d - 2^(31+l) < d <= 2^l). The row -> (utterance, frame) split
-// ran as a software 64-bit divide on the scalar unit per row (~180 SALU instructions per row and
-// wave in the backward, PMC); set up once per kernel, it is a few scalar ops per use.
-struct UDiv31 {
-  unsigned m;
-  int sh;
-  NRSE_DEV void init(unsigned d) {
-    int l = 0;
-    while ((1u << l) < d) ++l;
-    sh = 31 + l;
-    m = (unsigned)(((1ull << sh) + d - 1) / d);
-  }
-  NRSE_DEV unsigned div(unsigned n) const { return (unsigned)(((unsigned long long)n * m) >> sh); }
-};
-
 // LDS weight image wT[j][c] (tap-major) so lane reads 4 consecutive channels per tap
 NRSE_DEV void load_wT(float* wT, const float* w, int C, int k) {
   for (int e = threadIdx.x; e < C * KMAX; e += blockDim.x) {

@@ -259,15 +259,18 @@ struct LnRow {
 
 
 // element offsets of the (up to) two col rows feeding LN row `row` (-1: no such tap)
-NRSE_DEV void col_taps(const nrse_ln_bwd_params& p, long long row, long long& o0, long long& o1) {
-  const long long b = row / p.col_tin;
-  const int tau = (int)(row - b * p.col_tin);
-  const int j0 = tau % p.col_s;
+// (rows < 2^31, host check; the divides by multiply-high, UDiv31: set up once per kernel in cd)
+struct ColDiv { UDiv31 tin, s; };
+NRSE_DEV void col_taps(const nrse_ln_bwd_params& p, const ColDiv& cd, long long row, long long& o0, long long& o1) {
+  const long long b = cd.tin.div((unsigned)row);
+  const int tau = (int)((unsigned)row - (unsigned)b * (unsigned)p.col_tin);
+  const int q = (int)cd.s.div((unsigned)tau);
+  const int j0 = tau - q * p.col_s;
   long long o[2];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int j = j0 + u * p.col_s;
-    const int t = (tau - j) / p.col_s;
+    const int t = q - u;  // (tau - j) / s where tau >= j (checked below)
     o[u] = (j < p.col_k && tau >= j && t < p.col_tout)
                ? ((b * p.col_tout + t) * p.col_k + j) * (long long)p.C : -1;
   }
@@ -278,7 +281,8 @@ NRSE_DEV void col_taps(const nrse_ln_bwd_params& p, long long row, long long& o0
 // FD (encoder form, RES): x, dy and the residual all f32, dy direct: three unconditional 16-B
 // loads per word, no dtype / mode branches (each of which had made the compiler wait for the load)
 template <int NK, bool RES, bool COL, bool BF, bool FD>
-NRSE_DEV void ln_bwd_load(const nrse_ln_bwd_params& p, long long row, int lane, LnRow<NK, RES, COL, BF>& b) {
+NRSE_DEV void ln_bwd_load(const nrse_ln_bwd_params& p, const ColDiv& cd, long long row, int lane,
+                          LnRow<NK, RES, COL, BF>& b) {
   b.mean = p.mean[row];
   b.rstd = p.rstd[row];
   if constexpr (FD) {
@@ -298,7 +302,7 @@ NRSE_DEV void ln_bwd_load(const nrse_ln_bwd_params& p, long long row, int lane, 
     return;
   }
   long long o0 = -1, o1 = -1;
-  if constexpr (COL) col_taps(p, row, o0, o1);
+  if constexpr (COL) col_taps(p, cd, row, o0, o1);
   else if constexpr (BF) o0 = row * p.C;  // direct dy
   if constexpr (BF) {
     // every load is issued on every row: a load skipped on some path leaves the wait-count pass
@@ -444,26 +448,31 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const nrse_ln_bwd_params p)
 
   const long long nw = (long long)gridDim.x * 4;
   long long row = (long long)blockIdx.x * 4 + w;
+  ColDiv cd;
+  if constexpr (COL) {
+    cd.tin.init((unsigned)p.col_tin);
+    cd.s.init((unsigned)p.col_s);
+  }
   LnRow<NK, RES, COL, BF> ba, bb;
   const long long last = p.rows - 1;
-  if (row < p.rows) ln_bwd_load<NK, RES, COL, BF, FD>(p, row, lane, ba);
+  if (row < p.rows) ln_bwd_load<NK, RES, COL, BF, FD>(p, cd, row, lane, ba);
   for (; row < p.rows; row += 2 * nw) {
     const long long rb = row + nw;
     // BF: unconditional (clamped) prefetch, fenced from the scheduler, which otherwise sinks the
     // loads below part of the current row's math to save registers (and then waits for them)
     if (BF || FD) {
-      ln_bwd_load<NK, RES, COL, BF, FD>(p, rb < last ? rb : last, lane, bb);
+      ln_bwd_load<NK, RES, COL, BF, FD>(p, cd, rb < last ? rb : last, lane, bb);
       __builtin_amdgcn_sched_barrier(0);
     } else if (rb < p.rows) {
-      ln_bwd_load<NK, RES, COL, BF, FD>(p, rb, lane, bb);
+      ln_bwd_load<NK, RES, COL, BF, FD>(p, cd, rb, lane, bb);
     }
     compute(ba, row);
     if (rb >= p.rows) break;
     if (BF || FD) {
-      ln_bwd_load<NK, RES, COL, BF, FD>(p, rb + nw < last ? rb + nw : last, lane, ba);
+      ln_bwd_load<NK, RES, COL, BF, FD>(p, cd, rb + nw < last ? rb + nw : last, lane, ba);
       __builtin_amdgcn_sched_barrier(0);
     } else if (rb + nw < p.rows) {
-      ln_bwd_load<NK, RES, COL, BF, FD>(p, rb + nw, lane, ba);
+      ln_bwd_load<NK, RES, COL, BF, FD>(p, cd, rb + nw, lane, ba);
     }
     compute(bb, rb);
   }
@@ -573,6 +582,7 @@ extern "C" int nrse_layernorm_bwd(const nrse_ln_bwd_params* p, void* stream) {
                "nrse_layernorm_bwd: bad args");
   NRSE_REQUIRE(!(p->flags & (NRSE_LN_GELU | NRSE_LN_RELU)) || p->beta, "nrse_layernorm_bwd: GELU/ReLU need beta");
   NRSE_REQUIRE((p->dgamma == nullptr) == (p->dbeta == nullptr), "nrse_layernorm_bwd: dgamma/dbeta together");
+  NRSE_REQUIRE(p->rows < (1LL << 31), "nrse_layernorm_bwd: too many rows");
   if (p->dy_mode == NRSE_DY_COL2IM)
     NRSE_REQUIRE(p->col_k > 0 && p->col_s > 0 && p->col_tin > 0 && p->col_tout > 0 && p->rows % p->col_tin == 0,
                  "nrse_layernorm_bwd: bad col2im geometry");
