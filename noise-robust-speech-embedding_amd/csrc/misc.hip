@@ -16,12 +16,15 @@ __global__ void specaug_pad_kernel(float* __restrict__ h, const unsigned char* _
                                    int T, int C, int pf, int pb) {
   const int Tp = T + pf + pb;
   const long long total = (long long)batch * Tp * C;
+  UDiv31 dC, dTp;
+  dC.init((unsigned)C);
+  dTp.init((unsigned)Tp);
   for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
        e += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(e % C);
-    const long long r = e / C;
-    const int tp = (int)(r % Tp);
-    const long long b = r / Tp;
+    const unsigned r = dC.div((unsigned)e);  // total < 2^31 (host check): multiply-high divides
+    const int c = (int)((unsigned)e - r * (unsigned)C);
+    const long long b = dTp.div(r);
+    const int tp = (int)(r - (unsigned)b * (unsigned)Tp);
     const int t = tp - pf;
     float v = 0.f;
     if (t >= 0 && t < T) {
@@ -41,12 +44,15 @@ __global__ void pad_rows_kernel(const void* __restrict__ src, int sdt, void* __r
                                 int T, int C, int pf, int pb) {
   const int Tp = T + pf + pb;
   const long long total = (long long)batch * Tp * C;
+  UDiv31 dC, dTp;
+  dC.init((unsigned)C);
+  dTp.init((unsigned)Tp);
   for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
        e += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(e % C);
-    const long long r = e / C;
-    const int tp = (int)(r % Tp);
-    const long long b = r / Tp;
+    const unsigned r = dC.div((unsigned)e);  // total < 2^31 (host check): multiply-high divides
+    const int c = (int)((unsigned)e - r * (unsigned)C);
+    const long long b = dTp.div(r);
+    const int tp = (int)(r - (unsigned)b * (unsigned)Tp);
     const int t = tp - pf;
     const float v = (t >= 0 && t < T) ? load_as_f(src, sdt, (b * T + t) * C + c) : 0.f;
     store_from_f(dst, ddt, e, v);
@@ -252,12 +258,15 @@ __global__ void gelu_bwd_pad_kernel(const float* __restrict__ dy, const void* __
                                     void* __restrict__ out, int odt, int batch, int T, int C, int pf, int pb) {
   const int Tp = T + pf + pb;
   const long long total = (long long)batch * Tp * C;
+  UDiv31 dC, dTp;
+  dC.init((unsigned)C);
+  dTp.init((unsigned)Tp);
   for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
        e += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(e % C);
-    const long long r = e / C;
-    const int tp = (int)(r % Tp);
-    const long long b = r / Tp;
+    const unsigned r = dC.div((unsigned)e);  // total < 2^31 (host check): multiply-high divides
+    const int c = (int)((unsigned)e - r * (unsigned)C);
+    const long long b = dTp.div(r);
+    const int tp = (int)(r - (unsigned)b * (unsigned)Tp);
     const int t = tp - pf;
     float v = 0.f;
     if (t >= 0 && t < T) {
@@ -282,6 +291,7 @@ extern "C" int nrse_specaug_pad(float* h, const unsigned char* mask, const float
   NRSE_REQUIRE(dst && batch > 0 && T > 0 && C > 0 && pf >= 0 && pb >= 0, "nrse_specaug_pad: bad args");
   NRSE_REQUIRE(!mask || embed, "nrse_specaug_pad: mask without embed");
   const long long total = (long long)batch * (T + pf + pb) * C;
+  NRSE_REQUIRE(total < (1LL << 31), "nrse_specaug_pad: too many elements");
   hipLaunchKernelGGL(specaug_pad_kernel, dim3(blocks_for(total)), dim3(256), 0, (hipStream_t)stream, h, mask, embed,
                      dst, dst_dtype, batch, T, C, pf, pb);
   return nrse_check_launch("nrse_specaug_pad");
@@ -291,6 +301,7 @@ extern "C" int nrse_pad_rows(const void* src, int sdt, void* dst, int ddt, int b
                              void* stream) {
   NRSE_REQUIRE(src && dst && batch > 0 && T > 0 && C > 0, "nrse_pad_rows: bad args");
   const long long total = (long long)batch * (T + pf + pb) * C;
+  NRSE_REQUIRE(total < (1LL << 31), "nrse_pad_rows: too many elements");
   hipLaunchKernelGGL(pad_rows_kernel, dim3(blocks_for(total)), dim3(256), 0, (hipStream_t)stream, src, sdt, dst, ddt,
                      batch, T, C, pf, pb);
   return nrse_check_launch("nrse_pad_rows");
@@ -444,6 +455,7 @@ extern "C" int nrse_gelu_bwd_pad(const float* dy, const void* pre, int pdt, void
                                  int pf, int pb, void* stream) {
   NRSE_REQUIRE(dy && pre && out && batch > 0 && T > 0 && C > 0, "nrse_gelu_bwd_pad: bad args");
   const long long total = (long long)batch * (T + pf + pb) * C;
+  NRSE_REQUIRE(total < (1LL << 31), "nrse_gelu_bwd_pad: too many elements");
   hipLaunchKernelGGL(gelu_bwd_pad_kernel, dim3(blocks_for(total)), dim3(256), 0, (hipStream_t)stream, dy, pre, pdt,
                      out, odt, batch, T, C, pf, pb);
   return nrse_check_launch("nrse_gelu_bwd_pad");
