@@ -102,6 +102,9 @@ __global__ __launch_bounds__(256) void gate_fwd_kernel(const void* __restrict__ 
   const long long total = (long long)batch * Tn * H;
   const long long wave = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const long long nwave = (long long)gridDim.x * (blockDim.x >> 6);
+  UDiv31 dH, dT;
+  dH.init((unsigned)H);
+  dT.init((unsigned)Tn);
   for (long long n0 = wave * 8 * GATE_U; n0 < total; n0 += nwave * 8 * GATE_U) {
     float x[GATE_U][8];
 #pragma unroll
@@ -115,10 +118,10 @@ __global__ __launch_bounds__(256) void gate_fwd_kernel(const void* __restrict__ 
       float a, b;
       gw.ab(x[j], a, b);
       if (sub == 0 && n < total) {
-        const long long row = n / H;
-        const int h = (int)(n % H);
-        const long long bi = row / Tn, t = row % Tn;
-        gate[(bi * H + h) * Tn + t] = a * (b * c[h] - 1.f) + 2.f;
+        const unsigned row = dH.div((unsigned)n);  // total < 2^31 (host check): multiply-high divides
+        const int h = (int)((unsigned)n - row * (unsigned)H);
+        const unsigned bi = dT.div(row), t = row - bi * (unsigned)Tn;
+        gate[((long long)bi * H + h) * Tn + t] = a * (b * c[h] - 1.f) + 2.f;
       }
     }
   }
@@ -485,6 +488,7 @@ extern "C" int nrse_gate_fwd(const void* x1, int x_dtype, const float* W, const 
   NRSE_REQUIRE(x1 && W && bvec && c && gate && batch > 0 && T > 0 && H > 0, "nrse_gate_fwd: bad args");
   NRSE_REQUIRE(((uintptr_t)x1 & 15) == 0, "nrse_gate_fwd: x1 not 16-byte aligned");
   const long long total = (long long)batch * T * H;
+  NRSE_REQUIRE(total < (1LL << 31), "nrse_gate_fwd: too many items");
   const long long blocks = (total + 32 * GATE_U - 1) / (32 * GATE_U);  // 8 * GATE_U items per wave, 4 waves
   dim3 grid((unsigned)(blocks < 2048 ? blocks : 2048));
   hipStream_t st = (hipStream_t)stream;
