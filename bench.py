@@ -158,6 +158,27 @@ def bench_emotion(args):
     print(json.dumps(result), flush=True)
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """`--gpus N > 1` without a torch.distributed environment: start the N rank processes here
+    (one per GPU, torch.distributed.run on 127.0.0.1) as children, before this process has made
+    any GPU call, and return their exit status. Each rank re-runs this script with the same
+    arguments and finds WORLD_SIZE set."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this host driver (RCCL)
+    env.setdefault("OMP_NUM_THREADS", "4")
+    import subprocess
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -175,16 +196,23 @@ def main():
                     help="fixed: configs[1] (8 s pairs, the metric); varlen: configs[4] (3-12 s length-bucketed "
                          "pairs, MUSAN-style noise of its own length, SNR {4, 8}); emotion: configs[3] (dimensional "
                          "emotion head over the frozen encoder, 36 x 5 s)")
+    ap.add_argument("--wire", default="f32", choices=["f32", "bf16"],
+                    help="gradient all-reduce wire dtype for N > 1 (f32: the exact sum; bf16: half the xGMI bytes)")
     args = ap.parse_args()
+
+    if args.workload == "emotion":
+        return bench_emotion(args)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no torchrun around us: become the launcher (nothing has touched the GPU yet)
+        sys.exit(launch_ranks(args.gpus))
 
     from nrse_amd import arch as A, ddp, kernels as K
     from nrse_amd.engine import ByolEngine, StepConfig
 
-    if args.workload == "emotion":
-        return bench_emotion(args)
     rank, world, local = ddp.init_from_env()
-    if world != args.gpus and not (world == 1 and args.gpus == 1):
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    if world != args.gpus:
+        print(f"error: --gpus {args.gpus} but the launched world has WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     arch = A.LARGE
@@ -193,7 +221,8 @@ def main():
     cdt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     eng = ByolEngine(arch, 1024, 2048, device=dev, compute_dtype=cdt, seed=1234,
                      step_cfg=StepConfig(ema_decay=0.997, overlap_optimizer=not args.serial_optimizer))
-    allreduce = ddp.GradAllReduce() if world > 1 else None
+    allreduce = (ddp.GradAllReduce(wire_dtype=torch.bfloat16 if args.wire == "bf16" else None)
+                 if world > 1 else None)
 
     # synthetic pairs resident in HBM: clean ~ N(0, 0.1^2), noise ~ N(0, 1), SNR from the YAML
     gen = torch.Generator(device=dev)
@@ -305,7 +334,8 @@ def main():
                                                          "mix), random-init WavLM-Large weights",
         "config": ({"workload": "configs[1]: WavLM-large BYOL train step, synthetic 8s@16kHz clean/noisy pairs, "
                                 "batch=32 per GPU", "global_batch": B * world, "seq_len": L, "frames": arch.frames(L),
-                    "parallelism": f"dp{world}", "layerdrop_executed_layers": avg_exec}
+                    "parallelism": f"dp{world}", "layerdrop_executed_layers": avg_exec,
+                    "grad_wire": args.wire if world > 1 else None}
                    if varlen_batches is None else
                    {"workload": "configs[4]: WavLM-large BYOL, synthetic 3-12 s pairs in 1 s length buckets (padded "
                                 "to 0.5 s), noise of independent length tiled on GPU, SNR {4,8} dB, batch=32 per GPU",

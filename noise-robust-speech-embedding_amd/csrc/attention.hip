@@ -506,7 +506,13 @@ extern "C" int nrse_gate_bwd(const void* x1, int x_dtype, const float* W, const 
   NRSE_REQUIRE((long long)batch * T * H < (1LL << 31) - (1LL << 24), "nrse_gate_bwd: too many items");
   hipStream_t st = (hipStream_t)stream;
   // a multiple of H workgroups: each 8-lane item group then keeps one head (see the kernel)
-  static const int bph = getenv("NRSE_GATE_BWD_BPH") ? atoi(getenv("NRSE_GATE_BWD_BPH")) : GATE_BWD_BLOCKS_PER_HEAD;
+  // NRSE_GATE_BWD_BPH (tuning override) is clamped: <= 0 would launch an empty grid, a large value
+  // would overflow the kernel's 32-bit item stride
+  static const int bph = [] {
+    const char* e = getenv("NRSE_GATE_BWD_BPH");
+    const int v = e ? atoi(e) : GATE_BWD_BLOCKS_PER_HEAD;
+    return v < 1 ? 1 : (v > GATE_BWD_BLOCKS_PER_HEAD * 8 ? GATE_BWD_BLOCKS_PER_HEAD * 8 : v);
+  }();
   dim3 grid((unsigned)(bph * H));
   if (x_dtype == NRSE_BF16)
     hipLaunchKernelGGL(gate_bwd_kernel<bf16_t>, grid, dim3(256), 0, st, x1, W, bvec, c, dgate, dx1, dW, db, dc, batch,

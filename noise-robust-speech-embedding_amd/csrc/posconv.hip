@@ -340,7 +340,10 @@ bool nrse_posconv_wgrad_ok(const nrse_gemm_params* p) {
   if (a.dtype != NRSE_BF16 || b.dtype != NRSE_BF16 || a.kcontig || b.kcontig) return false;
   if (a.chunk_shift != 0 || b.chunk_shift != 6 || b.ld_chunk != b.ld) return false;
   if (p->M != PCH || p->N % (WTB * PCH) != 0 || p->K < 1 || p->zdiv != 1) return false;
+  // the kernel adds two partial sums per element straight into C (the caller zeroes it): per-split
+  // slabs (c_split > 0) are not supported here and take the generic path
   if (p->flags != NRSE_EPI_ATOMIC || p->c_dtype != NRSE_F32 || p->ldc < p->N || p->alpha != 1.f) return false;
+  if (p->c_split != 0) return false;
   if (a.ld % 8 || b.ld % 8 || a.seg_stride % 8 || b.seg_stride % 8 || a.z1 % 8 || b.z1 % 8) return false;
   if (b.seg_stride % b.ld != 0 || b.seg_stride / b.ld < (long long)p->K + p->N / PCH - 1) return false;
   if ((((uintptr_t)a.ptr) | ((uintptr_t)b.ptr)) & 15) return false;

@@ -7,15 +7,15 @@ src/utils/audio_utils.py (load_and_process_audio :9-64, get_audio_files :67-73).
 MI355X design: CPU workers only decode and crop raw waveforms; the SNR mix, the validity checks,
 peak normalisation and feature-extractor normalisation run for the whole batch in one fused
 kernel (nrse_snr_mix) on the device, producing the dict batches the training loop consumes.
-Audio decoding uses the stdlib `wave` reader (PCM WAV); torchaudio is not in this image, so
-compressed formats and resampling are not supported (files must be at the configured rate).
+Audio decoding uses the stdlib `wave` reader (PCM WAV) and a restated torchaudio sinc resampler
+(nrse_amd/audio.py); torchaudio is not in this image, so `.flac` / `.mp3` files are discovered as
+in the reference but take its load-error path (logged, `None`, retry).
 """
 from __future__ import annotations
 
 import functools
 import os
 import random
-import wave
 
 import logging
 
@@ -67,30 +67,8 @@ class GpuMixer:
 
 
 # ----------------------------------------------------------------------------- audio files
-def get_audio_files(path: str, exts=(".wav",)) -> list:
-    out = []
-    for root, _, files in os.walk(path):
-        for f in sorted(files):
-            if f.lower().endswith(exts):
-                out.append(os.path.join(root, f))
-    return sorted(out)
-
-
-def read_wav(path: str) -> tuple:
-    with wave.open(path, "rb") as w:
-        sr, ch, width, n = w.getframerate(), w.getnchannels(), w.getsampwidth(), w.getnframes()
-        buf = w.readframes(n)
-    if width == 2:
-        x = np.frombuffer(buf, dtype="<i2").astype(np.float32) / 32768.0
-    elif width == 4:
-        x = np.frombuffer(buf, dtype="<i4").astype(np.float32) / 2147483648.0
-    elif width == 1:
-        x = (np.frombuffer(buf, dtype=np.uint8).astype(np.float32) - 128.0) / 128.0
-    else:
-        raise ValueError(f"{path}: unsupported sample width {width}")
-    if ch > 1:
-        x = x.reshape(-1, ch).mean(axis=1)  # mono mix-down (audio_utils.py:27-29)
-    return x, sr
+# decoding / resampling / discovery: nrse_amd/audio.py (audio_utils.py:9-73)
+from .audio import AudioDecodeError, audio_info, get_audio_files, load_audio, read_wav  # noqa: E402,F401
 
 
 def crop_or_pad(x: np.ndarray, n: int, rng=random, random_crop: bool = True) -> np.ndarray:
@@ -131,12 +109,10 @@ class WavPairs(torch.utils.data.Dataset):
 
     def _load(self, path):
         try:
-            x, sr = read_wav(path)
+            x = load_audio(path, self.sr)   # decode, mono, resample (audio_utils.py:26-36)
         except Exception as e:   # audio_utils.py:62-64: load errors -> None
             logger.error(f"Error loading audio file {path}: {e}")
             return None
-        if sr != self.sr:
-            raise ValueError(f"{path}: sample rate {sr} != {self.sr} (no resampler in this build)")
         x = crop_or_pad(x, self.n)
         return x if audio_valid(x) else None
 
@@ -315,6 +291,21 @@ def _rank_share(ds, rank: int, world: int):
     return torch.utils.data.Subset(ds, list(range(rank, n, world)))
 
 
+def rank_generator(seed: int, rank: int) -> torch.Generator:
+    """The DataLoader's generator, distinct per rank. torch derives each worker's `random` /
+    torch seeds (base_seed + worker_id) from it, so with a per-rank generator the noise file,
+    SNR and crop draws of item k differ across ranks (the same torch.manual_seed on every rank
+    would otherwise repeat them rank to rank). With num_workers = 0 the items draw from the main
+    process's `random`, seeded per rank by `seed_host_rng`."""
+    return torch.Generator().manual_seed(int(seed) * 1000003 + 7919 * int(rank) + 1)
+
+
+def seed_host_rng(seed: int, rank: int) -> None:
+    """Seed the main process's `random` per rank (item draws at num_workers = 0, MixedLoader's
+    redraws); src/utils/setup_utils.py:4-7 seeds torch and numpy but not `random`."""
+    random.seed(int(seed) * 1000003 + 7919 * int(rank))
+
+
 def create_raw_dataloaders(config: dict, *, synthetic_items: int | None = None, rank: int = 0, world: int = 1):
     """(train_loader, val_loader, base dataset) of RAW batches, split 85/15 with the seeded
     generator as in create_dataloaders (noisy_speech_dataset.py:163-175)."""
@@ -332,8 +323,10 @@ def create_raw_dataloaders(config: dict, *, synthetic_items: int | None = None, 
     train_ds, val_ds = _rank_share(train_ds, rank, world), _rank_share(val_ds, rank, world)
     kw = dict(batch_size=int(t["batch_size"]), num_workers=min(int(t.get("num_workers", 4)), 8), pin_memory=True,
               drop_last=True)
-    train = torch.utils.data.DataLoader(train_ds, shuffle=True, **kw)
-    val = torch.utils.data.DataLoader(val_ds, shuffle=False, **kw) if len(val_ds) >= int(t["batch_size"]) else None
+    seed = int(t.get("seed", 42))
+    train = torch.utils.data.DataLoader(train_ds, shuffle=True, generator=rank_generator(seed, rank), **kw)
+    val = (torch.utils.data.DataLoader(val_ds, shuffle=False, generator=rank_generator(seed + 1, rank), **kw)
+           if len(val_ds) >= int(t["batch_size"]) else None)
     return train, val, ds
 
 
@@ -467,34 +460,63 @@ class SyntheticVarLenPairs(torch.utils.data.Dataset):
                          idx, 0)
 
 
-def wav_num_samples(path: str) -> int:
-    with wave.open(path, "rb") as w:
-        return w.getnframes()
+def wav_num_samples(path: str, sample_rate: int | None = None) -> int:
+    """Samples of `path` after resampling to `sample_rate` (torchaudio's ceil(new * n / orig))."""
+    n, sr = audio_info(path)
+    if sample_rate is None or sr == sample_rate:
+        return n
+    g = np.gcd(sr, sample_rate)
+    return -(-(sample_rate // g) * n // (sr // g))
 
 
 class WavVarLenPairs(torch.utils.data.Dataset):
-    """PCM WAV clean files at their own length (cropped to max_s), noise from a pool (MUSAN)."""
+    """Clean files at their own length (cropped to max_s), noise from a pool (MUSAN). Files the
+    build cannot decode (or whose header is broken) are logged and left out of the clean list
+    (their length, which the bucketing needs, is unknown); undecodable noise files take the
+    reference's retry path."""
 
     def __init__(self, clean_files, noise_files, sample_rate, max_s, snr_range):
-        self.clean_files, self.noise_files = clean_files, noise_files
         self.sr, self.nmax = sample_rate, int(max_s * sample_rate)
         self.snr_range = list(snr_range)
-        self.lengths = [min(wav_num_samples(f), self.nmax) for f in clean_files]
+        self.clean_files, self.lengths = [], []
+        for f in clean_files:
+            try:
+                n = wav_num_samples(f, sample_rate)
+            except Exception as e:
+                logger.error(f"Error loading audio file {f}: {e}")
+                continue
+            self.clean_files.append(f)
+            self.lengths.append(min(n, self.nmax))
+        self.noise_files = noise_files
 
     def __len__(self):
         return len(self.clean_files)
 
     def _load(self, path, crop: bool):
-        x, sr = read_wav(path)
-        if sr != self.sr:
-            raise ValueError(f"{path}: sample rate {sr} != {self.sr} (no resampler in this build)")
-        return crop_or_pad(x, self.nmax) if (crop and x.shape[0] > self.nmax) else x
+        try:
+            x = load_audio(path, self.sr)
+        except Exception as e:   # audio_utils.py:62-64
+            logger.error(f"Error loading audio file {path}: {e}")
+            return None
+        x = crop_or_pad(x, self.nmax) if (crop and x.shape[0] > self.nmax) else x
+        return x if audio_valid(x) else None
 
     def __getitem__(self, idx):
-        # global `random`, as the reference: reseeded by torch per worker and per epoch
-        clean = self._load(self.clean_files[idx], True)
-        noise = self._load(self.noise_files[random.randint(0, len(self.noise_files) - 1)], True)
-        return _raw_item(clean, noise, random.choice(self.snr_range), idx, 1)
+        # the loader's per-rank, per-worker seeded `random` (create_varlen_loader)
+        for attempt in range(MAX_ATTEMPTS):
+            clean = self._load(self.clean_files[idx], True)
+            if clean is None:
+                logger.warning(f"Invalid clean speech file, trying next (attempt {attempt + 1})")
+                idx = (idx + 1) % len(self.clean_files)
+                continue
+            noise = self._load(self.noise_files[random.randint(0, len(self.noise_files) - 1)], True)
+            if noise is None:
+                logger.warning(f"Invalid noise file, trying another (attempt {attempt + 1})")
+                continue
+            # the bucket was chosen by lengths[idx]: keep the item at that length
+            clean = crop_or_pad(clean, self.lengths[idx], random_crop=False)
+            return _raw_item(clean, noise, random.choice(self.snr_range), idx, attempt + 1)
+        raise RuntimeError(f"no valid pair for item {idx} after {MAX_ATTEMPTS} attempts")
 
 
 def create_varlen_loader(dataset, batch_size: int, *, sample_rate: int = 16000, min_s: float = 3.0,
@@ -510,4 +532,4 @@ def create_varlen_loader(dataset, batch_size: int, *, sample_rate: int = 16000, 
     pad = int(pad_s * sample_rate)
     return torch.utils.data.DataLoader(dataset, batch_sampler=sampler, num_workers=num_workers,
                                        collate_fn=functools.partial(collate_varlen, pad_multiple=pad),
-                                       pin_memory=True)
+                                       pin_memory=True, generator=rank_generator(seed, rank))

@@ -49,8 +49,10 @@ class GradAllReduce:
         all-reduce (a device-side dependency, no host sync under NCCL/RCCL).
     """
 
-    def __init__(self, group=None, bucket_bytes: int = 64 << 20, wire_dtype=None):
+    def __init__(self, group=None, bucket_bytes: int = 64 << 20, wire_dtype=None, force: bool = False):
         self.group = group
+        # force=True: exchange even in a one-rank group (exercises the RCCL path on a one-GPU box)
+        self.force = force
         self.bucket_bytes = bucket_bytes
         # wire_dtype=torch.bfloat16: each bucket is cast to bf16, summed by RCCL in bf16 (half the
         # xGMI bytes: 652 MB instead of 1.30 GB per step at WavLM-Large) and cast back into the
@@ -60,7 +62,7 @@ class GradAllReduce:
         self.issued_elems = 0
 
     def active(self) -> bool:
-        return dist.is_initialized() and dist.get_world_size(self.group) > 1
+        return dist.is_initialized() and (self.force or dist.get_world_size(self.group) > 1)
 
     def start(self) -> None:
         self._works = []
@@ -88,6 +90,8 @@ class GradAllReduce:
             work.wait()
             if buf is not dst:
                 dst.copy_(buf)
+                if buf.is_cuda:  # the wire copy is freed after this; keep it until the cast-back ran
+                    buf.record_stream(torch.cuda.current_stream(buf.device))
         self._works = []
 
     def __call__(self, flat: torch.Tensor) -> None:

@@ -590,12 +590,18 @@ class ByolEngine:
         si = torch.empty(C, device=self.dev, dtype=F32)
         rm, rv, nbt = self.bn[bn_key]
         if train and self.sync_bn is not None:
-            # SyncBatchNorm: batch statistics over every rank's rows (one small all-reduce)
-            sums = torch.empty(2 * C, device=self.dev, dtype=torch.float64)
-            K.bn_stats(x, sums)
+            # SyncBatchNorm: batch statistics over every rank's rows (one small all-reduce); the
+            # rank's row count rides along, so ranks with uneven batches still normalise over the
+            # true global count (one host read of it per BN layer: SyncBN is the opt-in parity mode)
+            sums = torch.empty(2 * C + 1, device=self.dev, dtype=torch.float64)
+            K.bn_stats(x, sums[:2 * C])
+            sums[2 * C] = float(x.shape[0])
             self.sync_bn.all_reduce(sums)
-            n = x.shape[0] * self.sync_bn.world()
-            K.bn_fwd_global(x, P[name + ".weight"], P[name + ".bias"], y, rm, rv, sm, si, sums, n, relu)
+            n = int(round(float(sums[2 * C])))
+            K.bn_fwd_global(x, P[name + ".weight"], P[name + ".bias"], y, rm, rv, sm, si, sums[:2 * C], n, relu)
+            if train:
+                nbt.add_(1)
+            return y, (x, y, sm, si, n)
         else:
             K.bn_fwd(x, P[name + ".weight"], P[name + ".bias"], y, rm, rv, sm, si, train, relu)
         if train:
@@ -626,7 +632,7 @@ class ByolEngine:
         return dx
 
     def _bn_bwd(self, dy, cache, P, G, name, relu):
-        x, y, sm, si = cache
+        x, y, sm, si = cache[:4]
         dx = torch.empty_like(x)
         if self.sync_bn is not None:
             C = x.shape[1]
@@ -634,7 +640,7 @@ class ByolEngine:
             K.bn_bwd_sums(dy, x, y, sm, si, loc, relu)
             glob = loc.clone()
             self.sync_bn.all_reduce(glob)
-            K.bn_bwd_global(dy, x, y, P[name + ".weight"], sm, si, loc, glob, x.shape[0] * self.sync_bn.world(), dx,
+            K.bn_bwd_global(dy, x, y, P[name + ".weight"], sm, si, loc, glob, cache[4], dx,
                             G[name + ".weight"], G[name + ".bias"], relu)
         else:
             K.bn_bwd(dy, x, y, P[name + ".weight"], sm, si, dx, G[name + ".weight"], G[name + ".bias"], relu)
@@ -843,7 +849,7 @@ class ByolEngine:
         K.byol_loss(pred, tproj, self.loss_buf, dpred, self.loss_stats)
         self.sync_optimizer()  # the last update has read the gradient buffer
         self.grad.zero_()
-        self.backward(dpred, ctx, allreduce=allreduce if world_size > 1 else None)
+        self.backward(dpred, ctx, allreduce=allreduce)
         self.optimizer_step(lr, grad_scale=1.0 / world_size)
         return self.loss_buf
 

@@ -18,9 +18,9 @@ import time
 
 import torch
 
-from . import ddp
+from . import ddp, params as PR
 from .config import get_config
-from .data import create_dataloaders
+from .data import create_dataloaders, seed_host_rng
 from .health import HealthMonitor
 from .model import BYOLSpeechModel
 
@@ -60,6 +60,56 @@ class FusedAdamW(torch.optim.Optimizer):
     @property
     def lr(self):
         return self.param_groups[0]["lr"]
+
+    def _moments(self):
+        e = self.model.engine
+        e.sync_optimizer()
+        return PR.named_views(e.layout, e.m), PR.named_views(e.layout, e.v)
+
+    def state_dict(self):
+        """torch.optim.AdamW.state_dict() layout (what train_byol.py:209-215 checkpoints): per
+        online parameter tensor i, state[i] = {'step', 'exp_avg', 'exp_avg_sq'} (the engine's
+        fused moments, reshaped to the parameter), one param group with AdamW's hyper-parameters.
+        `param_groups[0]['param_names']` names each index with its state_dict key (the encoder's
+        tensors are in the flat layout's order, not transformers' module order)."""
+        e = self.model.engine
+        mv, vv = self._moments()
+        names = list(mv)
+        state = {}
+        if e.step_count > 0:
+            step = torch.tensor(float(e.step_count))
+            state = {i: {"step": step.clone(), "exp_avg": mv[k].detach().clone(),
+                         "exp_avg_sq": vv[k].detach().clone()} for i, k in enumerate(names)}
+        group = {k: v for k, v in self.param_groups[0].items() if k != "params"}
+        group.update(betas=tuple(e.cfg.betas), eps=e.cfg.eps, amsgrad=False, maximize=False, foreach=None,
+                     capturable=False, differentiable=False, fused=None,
+                     params=list(range(len(names))), param_names=names)
+        return {"state": state, "param_groups": [group]}
+
+    def load_state_dict(self, state_dict):
+        """Restore the moments, step count and lr / weight decay from `state_dict` (this class's
+        format, matched by `param_names`, or a plain AdamW state over the same tensor order)."""
+        e = self.model.engine
+        mv, vv = self._moments()
+        names = list(mv)
+        group = state_dict["param_groups"][0]
+        order = group.get("param_names") or names
+        if len(order) != len(names) or set(order) != set(names):
+            raise ValueError("optimizer state does not match this model's parameters")
+        st = state_dict["state"]
+        with torch.no_grad():
+            if not st:
+                e.m.zero_()
+                e.v.zero_()
+                e.step_count = 0
+            for i, k in enumerate(order):
+                if i in st:
+                    mv[k].copy_(st[i]["exp_avg"].reshape(mv[k].shape))
+                    vv[k].copy_(st[i]["exp_avg_sq"].reshape(vv[k].shape))
+                    e.step_count = int(float(st[i]["step"]))
+        for k in ("lr", "weight_decay", "initial_lr"):
+            if k in group:
+                self.param_groups[0][k] = group[k]
 
     def step(self, closure=None):  # used by the unfused path (autograd backward)
         eng = self.model.engine
@@ -139,6 +189,7 @@ def main(argv=None):
     torch.cuda.set_device(device)
     t = config["training"]
     torch.manual_seed(t.get("seed", 42))
+    seed_host_rng(t.get("seed", 42), rank)
     os.makedirs(t["checkpoint_dir"], exist_ok=True)
     os.makedirs(t["log_dir"], exist_ok=True)
     dtype = torch.float32 if config["runtime"]["dtype"] == "f32" else torch.bfloat16
@@ -167,6 +218,13 @@ def main(argv=None):
             print(f"Epoch {epoch + 1}/{t['num_epochs']} - Train Loss: {ep_loss:.4f}, Val Loss: {val_loss:.4f}, "
                   f"Val Avg Similarity: {vm['val_avg_similarity']:.4f} ({n} steps, "
                   f"{n * int(t['batch_size']) * world / (time.perf_counter() - t0):.1f} pairs/s)", flush=True)
+        # early stopping first: on the stopping epoch the reference breaks before any save
+        # (train_byol.py:192-196, then the checkpoints :207-240)
+        if stopper(val_loss if metric == "val_loss" else vm["val_avg_similarity"]):
+            if rank == 0:
+                print(f"Early stopping triggered after epoch {epoch + 1}")
+            break
+        if rank == 0:
             ck = {"epoch": epoch, "model_state_dict": model.state_dict(), "optimizer_state_dict": optimizer.state_dict(),
                   "loss": val_loss, "similarity": vm["val_avg_similarity"]}
             if val_loss < best_loss:
@@ -177,10 +235,6 @@ def main(argv=None):
                 torch.save(ck, os.path.join(t["checkpoint_dir"], "best_val_similarity.pt"))
             if epoch == int(t["num_epochs"]) - 1:
                 torch.save(ck, os.path.join(t["checkpoint_dir"], "last_model.pt"))
-        if stopper(val_loss if metric == "val_loss" else vm["val_avg_similarity"]):
-            if rank == 0:
-                print(f"Early stopping triggered after epoch {epoch + 1}")
-            break
         if max_steps is not None and step >= max_steps:
             break
     if world > 1:

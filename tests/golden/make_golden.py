@@ -10,7 +10,9 @@ What is generated (SURVEY.md §8c recipe):
   * buckets.npz   — WavLMAttention._relative_positions_bucket ([TF]modeling_wavlm.py:253-271)
   * byol_tiny.npz — reference BYOLSpeechModel + byol_loss on a tiny WavLM arch: eval forward and
                     one deterministic train step (train_byol.py:56-74 loop body)
-  * byol_large.npz— WavLM-Large arch, 2 x 8 s, eval forward and one det train step
+  * byol_large.npz— WavLM-Large arch, 4 x 8 s, eval forward and one det train step
+  * byol_large_3s.npz / byol_large_12s.npz — the same at the ends of configs[4]'s 3-12 s
+                    range (T = 149 and 599 frames), 4 utterances each (--varlen)
 Weights come from nrse_amd.params (portable seeded init), written to a local HF directory the
 reference loads through AutoModel.from_pretrained(config['model']['name']) (src/models/
 encoder.py:14). The reference's 3-D encoder output is pooled with a time-mean monkeypatch
@@ -269,7 +271,15 @@ def main():
     ap.add_argument("--skip-large", action="store_true")
     ap.add_argument("--configs-only", action="store_true")
     ap.add_argument("--manifest-only", action="store_true")
+    ap.add_argument("--varlen", action="store_true",
+                    help="only the WavLM-Large 3 s / 12 s fixtures (configs[4]'s length range)")
     args = ap.parse_args()
+    if args.varlen:
+        torch.set_num_threads(8)
+        for secs in (3, 12):
+            run_byol(A.LARGE.deterministic(), 4, 16000 * secs, 1024, 2048, 0.997, 1e-5, 1e-5, f"large_{secs}s",
+                     False, False)
+        return
     if args.manifest_only:
         make_state_manifest()
         return

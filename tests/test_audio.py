@@ -1,0 +1,115 @@
+"""Host-side audio feed (CPU): discovery of .wav/.flac/.mp3 (src/utils/audio_utils.py:67-73),
+resampling to the configured rate (:33-36), the load-error path for files this build cannot
+decode (:62-64), and per-rank item draws under DDP.
+
+Resampler parity is UNPINNED (torchaudio is not importable here and the reference holds no
+resampled fixture): the checks below are properties of torchaudio's published sinc_interp_hann
+filter that any faithful restatement has -- output length ceil(new*n/orig), unit DC gain, a tone
+below the cut-off kept at its frequency and amplitude, the identity at equal rates."""
+import math
+import os
+import wave
+
+import numpy as np
+import torch
+
+from nrse_amd import audio as AU, data as D
+
+
+def _write_wav(path, x, sr, ch=1):
+    x = np.clip(np.asarray(x, np.float64), -1, 1 - 1 / 32768)
+    pcm = (x * 32768).astype("<i2")
+    if ch > 1:
+        pcm = np.repeat(pcm[:, None], ch, axis=1).reshape(-1)
+    with wave.open(str(path), "wb") as w:
+        w.setnchannels(ch)
+        w.setsampwidth(2)
+        w.setframerate(sr)
+        w.writeframes(pcm.tobytes())
+
+
+def test_resample_length_dc_and_identity():
+    x = np.ones(48000, np.float32)
+    for orig, new in ((8000, 16000), (44100, 16000), (22050, 16000), (48000, 16000), (16000, 8000)):
+        y = AU.resample(x[: orig // 2], orig, new)
+        assert y.shape[0] == math.ceil(new * (orig // 2) / orig), (orig, new, y.shape)
+        mid = y[len(y) // 4: 3 * len(y) // 4]           # away from the zero-padded edges
+        assert np.allclose(mid, 1.0, atol=2e-3), (orig, new, mid.min(), mid.max())
+    z = np.random.default_rng(0).standard_normal(1000).astype(np.float32)
+    assert np.array_equal(AU.resample(z, 16000, 16000), z)
+
+
+def test_resample_keeps_a_tone():
+    for orig in (8000, 22050, 44100, 48000):
+        t = np.arange(orig) / orig
+        x = np.sin(2 * np.pi * 440.0 * t).astype(np.float32)
+        y = AU.resample(x, orig, 16000)
+        tt = np.arange(y.shape[0]) / 16000
+        ref = np.sin(2 * np.pi * 440.0 * tt)
+        sl = slice(2000, 14000)
+        err = np.abs(y[sl] - ref[sl]).max()
+        assert err < 5e-3, (orig, err)
+
+
+def test_discovery_resampling_and_undecodable_files(tmp_path):
+    clean = tmp_path / "clean"
+    noise = tmp_path / "noise"
+    for d in (clean, noise):
+        d.mkdir()
+    rng = np.random.default_rng(1)
+    _write_wav(clean / "a.wav", 0.1 * rng.standard_normal(8000), 8000)            # 1 s at 8 kHz
+    _write_wav(clean / "b.WAV", 0.1 * rng.standard_normal(16000), 16000, ch=2)     # stereo
+    (clean / "c.flac").write_bytes(b"fLaC\x00not-really")
+    (clean / "d.mp3").write_bytes(b"ID3\x03junk")
+    (clean / "e.txt").write_text("not audio")
+    _write_wav(noise / "n.wav", rng.standard_normal(44100), 44100)
+    files = AU.get_audio_files(str(clean))
+    assert [os.path.basename(f) for f in files] == ["a.wav", "b.WAV", "c.flac", "d.mp3"]
+    ds = D.WavPairs(files, AU.get_audio_files(str(noise)), 16000, 1.0, [5])
+    a = ds._load(files[0])
+    assert a.shape == (16000,) and np.abs(a).max() > 0.05     # 8 kHz -> 16 kHz, not zero padding
+    assert ds._load(files[2]) is None and ds._load(files[3]) is None   # load-error path -> None
+    n = ds._load(AU.get_audio_files(str(noise))[0])
+    assert n.shape == (16000,)
+    it = ds[2]                                   # c.flac fails -> the next file (d.mp3) fails -> a.wav
+    assert int(it["index"]) == 0 and int(it["attempts"]) == 3
+    vl = D.WavVarLenPairs(files, AU.get_audio_files(str(noise)), 16000, 12.0, [4, 8])
+    assert vl.lengths == [16000, 16000]           # undecodable clean files left out, 8 kHz counted at 16 kHz
+    assert vl[0]["clean"].shape[0] == 16000
+
+
+def _draws(tmp_path, rank, world, workers):
+    clean = tmp_path / "c"
+    noise = tmp_path / "n"
+    if not clean.exists():
+        clean.mkdir()
+        noise.mkdir()
+        rng = np.random.default_rng(2)
+        for i in range(48):
+            _write_wav(clean / f"{i:03d}.wav", 0.1 * rng.standard_normal(1600), 16000)
+        for i in range(16):
+            _write_wav(noise / f"{i:03d}.wav", rng.standard_normal(1600 + 37 * i), 16000)
+    cfg = {"data": {"clean_data_path": str(clean), "noise_data_path": str(noise), "sample_rate": 16000,
+                    "max_audio_length": 0.1, "snr_range": [0, 2, 5, 10, 15, 20, 25, 30], "validation_ratio": 0.0},
+           "training": {"batch_size": 4, "num_workers": workers, "seed": 42}}
+    torch.manual_seed(42)                        # what every rank's train.main does
+    D.seed_host_rng(42, rank)
+    train, _, _ = D.create_raw_dataloaders(cfg, rank=rank, world=world)
+    snr, nlen = [], []
+    for b in train:
+        snr += b["snr"].tolist()
+        nlen += b["noise"][:, 0].tolist()   # identifies the noise file (and its crop)
+    return snr, nlen
+
+
+def test_item_draws_differ_across_ranks_and_repeat_per_rank(tmp_path):
+    """with one torch seed on every rank, a rank-independent DataLoader generator
+    gave item k of every rank the same noise file and SNR. Per-rank generators (workers) and a
+    per-rank host `random` (num_workers = 0) make the draws differ across ranks and repeat per
+    rank."""
+    for workers in (0, 2):
+        r0 = _draws(tmp_path, 0, 2, workers)
+        r0b = _draws(tmp_path, 0, 2, workers)
+        r1 = _draws(tmp_path, 1, 2, workers)
+        assert r0 == r0b, workers                # reproducible
+        assert r0[0] != r1[0] and r0[1] != r1[1], workers

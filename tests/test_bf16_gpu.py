@@ -71,13 +71,14 @@ def _per_tensor(eng, g, gr, gf):
     return out
 
 
-@pytest.mark.parametrize("case", ["tiny", "large_3s"])
+@pytest.mark.parametrize("case", ["tiny", "large_3s", "large_8s", "large_12s"])
 def test_bf16_encoder_matches_bf16_oracle(nrse_device, case):
     torch.set_num_threads(min(16, torch.get_num_threads()))
     if case == "tiny":
         arch, proj, pred, B, L = A.TINY.deterministic(), 256, 512, 8, 16000
-    else:
-        arch, proj, pred, B, L = A.LARGE.deterministic(), 1024, 2048, 2, 48000
+    else:  # configs[4]'s 3 s and 12 s ends (T = 149, 599) and the benchmarked 8 s (T = 399)
+        secs = int(case.split("_")[1][:-1])
+        arch, proj, pred, B, L = A.LARGE.deterministic(), 1024, 2048, 2, 16000 * secs
     layout = PR.byol_layout(arch, proj, pred)
     flat = PR.init_byol_flat(layout, 1234)
     g = torch.Generator().manual_seed(5)

@@ -128,3 +128,55 @@ def test_sync_batchnorm_two_ranks_equal_one_rank_of_both(nrse_device):
     assert rel(out[0][3], eng.grad.cpu()) < 1e-3
     assert rel(out[0][5], eng.bn["online_projector.layers.1"][1].cpu()) < 1e-4
     assert torch.equal(out[0][4], out[1][4])
+
+
+def _rccl_worker(rank, world, port, out):
+    """One-rank RCCL ("nccl") group: the overlapped per-layer all-reduce path of the engine runs
+    through RCCL itself (GradAllReduce(force=True) exchanges even at world size 1)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0",
+                      HSA_ENABLE_IPC_MODE_LEGACY="0")
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "noise-robust-speech-embedding_amd"))
+    import torch.distributed as dist
+    from nrse_amd import arch as A, ddp, params as PR
+    from nrse_amd.engine import ByolEngine
+    torch.cuda.set_device(0)
+    dist.init_process_group(backend="nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    assert dist.get_backend() == "nccl"
+    arch = A.TINY.deterministic()
+    layout = PR.byol_layout(arch, 256, 512)
+    flat = PR.init_byol_flat(layout, 1234)
+    g = torch.Generator().manual_seed(70)
+    clean = (torch.randn(4, 16000, generator=g) * 0.1).cuda()
+    noisy = clean + 0.05 * torch.randn(4, 16000, generator=g).cuda()
+    res = {}
+    for tag, wire in (("local", None), ("f32", "f32"), ("bf16", "bf16")):
+        eng = ByolEngine(arch, 256, 512, device="cuda:0", compute_dtype=torch.float32, init_flat=flat)
+        ar = None if wire is None else ddp.GradAllReduce(bucket_bytes=1 << 20, force=True,
+                                                         wire_dtype=torch.bfloat16 if wire == "bf16" else None)
+        eng.train_step(clean, noisy, lr=1e-4, step_seed=3, allreduce=ar)
+        torch.cuda.synchronize()
+        res[tag] = (eng.grad.cpu(), 0 if ar is None else ar.issued_elems)
+        del eng
+    out[0] = (res, layout.numel)
+    dist.destroy_process_group()
+
+
+def test_rccl_overlapped_allreduce_one_rank(nrse_device):
+    """The engine's overlapped all-reduce through RCCL (backend "nccl"): at world size 1 the sum
+    is the identity, so the exchanged f32 gradient equals the local one and the bf16 wire equals
+    it rounded to bf16 (one bf16 ulp, 2^-8 relative, per element); every parameter range is sent."""
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_rccl_worker, args=(1, port, out), nprocs=1, join=True)
+    res, numel = out[0]
+    g_local = res["local"][0].double()
+
+    def rel(a):
+        return float((a.double() - g_local).norm() / g_local.norm())
+    assert rel(res["f32"][0]) < 1e-5, rel(res["f32"][0])
+    assert rel(res["bf16"][0]) < 4e-3, rel(res["bf16"][0])
+    assert rel(res["bf16"][0]) > 0  # the wire really was bf16
+    assert res["f32"][1] == numel and res["bf16"][1] == numel

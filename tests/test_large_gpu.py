@@ -1,6 +1,9 @@
 """WavLM-Large end to end on the HIP path against the REFERENCE's own outputs
 (tests/golden/byol_large.npz, written by tests/golden/make_golden.py from the reference
-BYOLSpeechModel / byol_loss / AdamW / _update_target_network on WavLM-Large, B = 4, 8 s).
+BYOLSpeechModel / byol_loss / AdamW / _update_target_network on WavLM-Large, B = 4, 8 s; and
+byol_large_3s.npz / byol_large_12s.npz at the two ends of configs[4]'s 3-12 s range, T = 149
+and 599 frames, reference src/utils/audio_utils.py:38-49 crop/pad lengths through
+src/models/encoder.py:17-29).
 
 This is the north-star tolerance check: embeddings within 1e-3 rel-L2 of the reference
 (BASELINE.json north_star; reference src/models/byol.py:75-128, src/models/encoder.py:17-32,
@@ -24,7 +27,7 @@ from nrse_amd import arch as A, params as PR
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-FIX = os.path.join(ROOT, "tests", "golden", "byol_large.npz")
+FIXTURES = {"8s": "byol_large.npz", "3s": "byol_large_3s.npz", "12s": "byol_large_12s.npz"}
 OUT = os.path.join(ROOT, "gpurun_out")
 
 
@@ -42,14 +45,14 @@ def make_inputs(B, L, seed):
     return clean.squeeze(1), noisy.squeeze(1)
 
 
-@pytest.fixture(scope="module")
-def large():
-    z = np.load(FIX)
+@pytest.fixture(scope="module", params=list(FIXTURES))
+def large(request):
+    z = np.load(os.path.join(ROOT, "tests", "golden", FIXTURES[request.param]))
     arch = A.LARGE.deterministic()
     layout = PR.byol_layout(arch, int(z["proj_dim"]), int(z["pred_dim"]))
     flat = PR.init_byol_flat(layout, int(z["seed"]))
     clean, noisy = make_inputs(int(z["B"]), int(z["L"]), int(z["seed"]) + 1)
-    return dict(z=z, arch=arch, layout=layout, flat=flat, clean=clean, noisy=noisy)
+    return dict(z=z, arch=arch, layout=layout, flat=flat, clean=clean, noisy=noisy, tag=request.param)
 
 
 def _engine(large, dtype):
@@ -125,7 +128,7 @@ def _record(tag, m):
 
 def test_large_f32_matches_reference(nrse_device, large):
     m = _run(large, torch.float32)
-    _record("f32", m)
+    _record(f"f32_{large['tag']}", m)
     tol = 1e-3   # north-star bound on embeddings
     assert m["eval_emb"] < tol, m
     assert m["eval_pred"] < tol and m["eval_tproj"] < tol, m
@@ -144,7 +147,7 @@ def test_large_bf16_deviation(nrse_device, large):
     """The benchmarked mode. Measured deviations are written to gpurun_out/large_parity_bf16.json
     and quoted in DESIGN.md §6; the bounds below are the stated bf16 tolerances."""
     m = _run(large, torch.bfloat16)
-    _record("bf16", m)
+    _record(f"bf16_{large['tag']}", m)
     assert m["eval_emb"] < 1e-2, m
     assert m["eval_pred"] < 3e-2 and m["eval_tproj"] < 3e-2, m
     assert m["hidden_norms"] < 1e-2, m

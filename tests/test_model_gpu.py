@@ -224,3 +224,78 @@ def test_validate_model_matches_oracle(nrse_device):
         assert abs(met["val_similarities"][k] - ref[k]) < 1e-5, (k, met["val_similarities"][k], ref[k])
     assert abs(met["val_avg_similarity"] - sum(ref.values()) / len(ref)) < 1e-5
     assert abs(val_loss - sum(losses) / len(losses)) < 1e-4 * max(1.0, abs(val_loss))
+
+
+def test_cli_early_stop_precedes_checkpoints(nrse_device, tmp_path):
+    """train_byol.py:192-196 before :207-240: on the epoch where early stopping fires the loop
+    breaks before saving anything. patience 1 and an unreachable min_delta stop at epoch 2, so
+    every checkpoint holds epoch 0 and no last_model.pt exists; the checkpoint's
+    optimizer_state_dict carries the AdamW moments (exp_avg / exp_avg_sq per parameter)."""
+    import yaml
+    c = {"model": {"name": "nrse/wavlm-tiny", "projection_dim": 256, "prediction_dim": 512, "ema_decay": 0.996},
+         "training": {"batch_size": 4, "num_workers": 0, "num_epochs": 3, "learning_rate": 1e-5,
+                      "weight_decay": 1e-5, "checkpoint_dir": str(tmp_path / "ck"), "log_dir": str(tmp_path / "lg"),
+                      "seed": 42, "early_stopping_metric": "val_loss", "early_stopping_patience": 1,
+                      "early_stopping_min_delta": 1e9},
+         "data": {"clean_data_path": "/nonexistent", "noise_data_path": "/nonexistent", "sample_rate": 16000,
+                  "max_audio_length": 0.5, "snr_range": [0, 5, 10, 15, 20], "validation_ratio": 0.15},
+         "logging": {"level": "WARNING"}}
+    p = tmp_path / "c.yaml"
+    p.write_text(yaml.safe_dump(c))
+    out = subprocess.run([sys.executable, os.path.join(PKG, "train_byol.py"), "--config", str(p), "--device",
+                          "cuda:0"], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert "Early stopping triggered after epoch 2" in out.stdout, out.stdout
+    assert not (tmp_path / "ck" / "last_model.pt").exists()
+    ck = torch.load(tmp_path / "ck" / "best_val_loss.pt", weights_only=True, map_location="cpu")
+    assert ck["epoch"] == 0
+    osd = ck["optimizer_state_dict"]
+    names = osd["param_groups"][0]["param_names"]
+    assert len(osd["state"]) == len(names) > 0
+    i = names.index("online_predictor.layers.6.weight")
+    assert osd["state"][i]["exp_avg"].shape == ck["model_state_dict"][names[i]].shape
+    assert float(osd["state"][i]["exp_avg_sq"].abs().sum()) > 0
+
+
+def test_optimizer_state_roundtrip_resumes(nrse_device, tmp_path):
+    """FusedAdamW.state_dict / load_state_dict (the optimizer half of train_byol.py:209-215):
+    a model + optimizer restored from a torch.save'd checkpoint take the same next step as the
+    run they were saved from."""
+    from nrse_amd import arch as A
+    from nrse_amd.model import BYOLSpeechModel
+    from nrse_amd.train import FusedAdamW
+    cfg = {"model": {"name": "nrse/wavlm-tiny", "projection_dim": 256, "prediction_dim": 512, "ema_decay": 0.996},
+           "training": {"learning_rate": 1e-4, "weight_decay": 1e-5, "seed": 42}}
+    det = A.TINY.deterministic()   # no dropout / SpecAugment / LayerDrop draws tied to the model's seed
+    g = torch.Generator().manual_seed(11)
+    clean = (torch.randn(4, 16000, generator=g) * 0.1).cuda()
+    noisy = clean + 0.05 * torch.randn(4, 16000, generator=g).cuda()
+    m1 = BYOLSpeechModel(cfg, compute_dtype=torch.float32, arch=det)
+    o1 = FusedAdamW(m1, lr=1e-4, weight_decay=1e-5)
+    for i in range(2):
+        m1.engine.train_step(clean, noisy, lr=o1.lr, step_seed=i)
+    torch.save({"model_state_dict": m1.state_dict(), "optimizer_state_dict": o1.state_dict()}, tmp_path / "ck.pt")
+    ck = torch.load(tmp_path / "ck.pt", weights_only=True, map_location="cpu")
+    assert int(ck["optimizer_state_dict"]["state"][0]["step"]) == 2
+    m2 = BYOLSpeechModel(cfg, compute_dtype=torch.float32, seed=7, arch=det)
+    o2 = FusedAdamW(m2, lr=1e-4, weight_decay=1e-5)
+    m2.load_state_dict(ck["model_state_dict"])
+    o2.load_state_dict(ck["optimizer_state_dict"])
+    assert torch.equal(m2.engine.m, m1.engine.m) and torch.equal(m2.engine.v, m1.engine.v)
+    assert m2.engine.step_count == 2
+    before = m1.engine.online.clone()
+    for m, o in ((m1, o1), (m2, o2)):
+        m.engine.train_step(clean, noisy, lr=o.lr, step_seed=5)
+    torch.cuda.synchronize()
+    # the two third steps differ only by the float-atomic summation order of the gradients (the
+    # k_proj biases, whose exact gradient is 0, carry pure rounding noise that Adam normalises
+    # to O(lr) steps): compare against the size of the step itself
+    step = (m1.engine.online - before).double()
+    d = float((m2.engine.online - m1.engine.online).double().norm() / step.norm())
+    assert d < 1e-2, d
+    # a fresh optimizer (no moments) takes a visibly different step: the restored state matters
+    m3 = BYOLSpeechModel(cfg, compute_dtype=torch.float32, arch=det)
+    m3.load_state_dict(ck["model_state_dict"])
+    m3.engine.train_step(clean, noisy, lr=1e-4, step_seed=5)
+    torch.cuda.synchronize()
+    assert float((m3.engine.online - m1.engine.online).double().norm() / step.norm()) > 0.1

@@ -58,7 +58,7 @@ def _state(tag, arch):
     return z, layout, O.OracleState(layout, flat)
 
 
-@pytest.mark.parametrize("tag", ["tiny", "large"])
+@pytest.mark.parametrize("tag", ["tiny", "large", "large_3s", "large_12s"])
 def test_oracle_eval_forward(tag):
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     arch = (A.TINY if tag == "tiny" else A.LARGE).deterministic()
@@ -77,7 +77,7 @@ def test_oracle_eval_forward(tag):
         assert rel(h, z["eval_hidden"]) < 1e-5
 
 
-@pytest.mark.parametrize("tag", ["tiny", "large"])
+@pytest.mark.parametrize("tag", ["tiny", "large", "large_3s", "large_12s"])
 def test_oracle_train_step(tag):
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     arch = (A.TINY if tag == "tiny" else A.LARGE).deterministic()
