@@ -207,6 +207,10 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // Padding is skipped, not computed: a wave whose 16 queries all lie past T (3 of the 4 waves
+  // of the last query block at T = 399) only stages and syncs, and in the last key tile the
+  // 16-key sub-tiles wholly past T get no MFMAs, exponentials or dropout hashes (nt16 < 4).
+  const bool wact = q0 + w * 16 < T;
   for (int it = 0; it < ntiles; ++it) {
     const int kb = it * 64;
     char* const Kt = kv0 + (it & 1) * 2 * TILE_B;
@@ -221,12 +225,16 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
       kv_dma_issue(kd, Kn, kb + 64, w);
       kv_dma_issue(vd, Kn + TILE_B, kb + 64, w);
     }
+    if (!wact) continue;
+    const int nt16 = min(4, (T - kb + 15) >> 4);  // 16-key sub-tiles holding a key < T (uniform)
     f32x4 s[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (t < nt16) {
 #pragma unroll
-      for (int ss = 0; ss < 2; ++ss) s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rd_row(Kt, 16 * t + i16, 4 * ss + g), qf[ss], s[t], 0, 0, 0);
+        for (int ss = 0; ss < 2; ++ss) s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rd_row(Kt, 16 * t + i16, 4 * ss + g), qf[ss], s[t], 0, 0, 0);
+      }
     }
     float v[4][4];
 #pragma unroll
@@ -245,7 +253,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
     }
     float mx = -INFINITY;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) mx = fmaxf(fmaxf(mx, fmaxf(v[t][0], v[t][1])), fmaxf(v[t][2], v[t][3]));
+    for (int t = 0; t < 4; ++t) mx = fmaxf(mx, fmaxf(fmaxf(v[t][0], v[t][1]), fmaxf(v[t][2], v[t][3])));
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float mn = fmaxf(m, mx);
@@ -254,20 +262,28 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
     float pd[4][4];
     float ps = 0.f;
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int t = 0; t < 4; ++t) {
+      if (t < nt16) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        pd[t][r] = exp2_(v[t][r] - mn);
-        ps += pd[t][r];
+        for (int r = 0; r < 4; ++r) {
+          pd[t][r] = exp2_(v[t][r] - mn);
+          ps += pd[t][r];
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pd[t][r] = 0.f;
       }
+    }
     if (drop) {
 #pragma unroll
       for (int t = 0; t < 4; ++t)
+        if (t < nt16) {
 #pragma unroll
-        for (int rp = 0; rp < 2; ++rp) {
-          const uint32_t hh = mix32((rowpair + (uint32_t)((kb >> 1) + 8 * t + rp)) ^ key);
-          pd[t][2 * rp] = attn_half_keep(hh, 0, thr) ? pd[t][2 * rp] : 0.f;
-          pd[t][2 * rp + 1] = attn_half_keep(hh, 1, thr) ? pd[t][2 * rp + 1] : 0.f;
+          for (int rp = 0; rp < 2; ++rp) {
+            const uint32_t hh = mix32((rowpair + (uint32_t)((kb >> 1) + 8 * t + rp)) ^ key);
+            pd[t][2 * rp] = attn_half_keep(hh, 0, thr) ? pd[t][2 * rp] : 0.f;
+            pd[t][2 * rp + 1] = attn_half_keep(hh, 1, thr) ? pd[t][2 * rp + 1] : 0.f;
+          }
         }
     }
     lpart = lpart * alpha + ps;
@@ -279,10 +295,12 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
     }
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-      const bf16x8 pa = pack8(pd[2 * c], pd[2 * c + 1]);
+      if (2 * c < nt16) {
+        const bf16x8 pa = pack8(pd[2 * c], pd[2 * c + 1]);
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt)
-        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, rd_tr(Vt, 32 * c, 32 * c + 16, 16 * dt, lane), o[dt], 0, 0, 0);
+        for (int dt = 0; dt < 4; ++dt)
+          o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, rd_tr(Vt, 32 * c, 32 * c + 16, 16 * dt, lane), o[dt], 0, 0, 0);
+      }
     }
   }
   float l = lpart + __shfl_xor(lpart, 16, 64);
@@ -366,6 +384,7 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
   f32x4 dq[4];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool wact = q0 + w * 16 < T;  // padding skipped as in the forward
   for (int it = 0; it < ntiles; ++it) {
     const int kb = it * 64;
     char* const Kt = kv0 + (it & 1) * 2 * TILE_B;
@@ -378,15 +397,19 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
       kv_dma_issue(kd, Kn, kb + 64, w);
       kv_dma_issue(vd, Kn + TILE_B, kb + 64, w);
     }
+    if (!wact) continue;
+    const int nt16 = min(4, (T - kb + 15) >> 4);
     f32x4 s[4], dp[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
       dp[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (t < nt16) {
 #pragma unroll
-      for (int ss = 0; ss < 2; ++ss) {
-        s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rd_row(Kt, 16 * t + i16, 4 * ss + g), qf[ss], s[t], 0, 0, 0);
-        dp[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rd_row(Vt, 16 * t + i16, 4 * ss + g), dof[ss], dp[t], 0, 0, 0);
+        for (int ss = 0; ss < 2; ++ss) {
+          s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rd_row(Kt, 16 * t + i16, 4 * ss + g), qf[ss], s[t], 0, 0, 0);
+          dp[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rd_row(Vt, 16 * t + i16, 4 * ss + g), dof[ss], dp[t], 0, 0, 0);
+        }
       }
     }
     // Straight-line per element; wave-uniform branches for dropout and for the last (partial)
@@ -401,17 +424,25 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
     if (drop) {
 #pragma unroll
       for (int t = 0; t < 4; ++t)
+        if (t < nt16) {
 #pragma unroll
-        for (int rp = 0; rp < 2; ++rp) {
-          const uint32_t hh = mix32((rowpair + (uint32_t)((kb >> 1) + 8 * t + rp)) ^ key);
-          dp[t][2 * rp] = attn_half_keep(hh, 0, thr) ? dp[t][2 * rp] * dsc : 0.f;
-          dp[t][2 * rp + 1] = attn_half_keep(hh, 1, thr) ? dp[t][2 * rp + 1] * dsc : 0.f;
+          for (int rp = 0; rp < 2; ++rp) {
+            const uint32_t hh = mix32((rowpair + (uint32_t)((kb >> 1) + 8 * t + rp)) ^ key);
+            dp[t][2 * rp] = attn_half_keep(hh, 0, thr) ? dp[t][2 * rp] * dsc : 0.f;
+            dp[t][2 * rp + 1] = attn_half_keep(hh, 1, thr) ? dp[t][2 * rp + 1] * dsc : 0.f;
+          }
         }
     }
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int t = 0; t < 4; ++t) {
+      if (t < nt16) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) ds[t][r] = exp2_(fmaf(s[t][r], c1, gl * bb[t][r]) - lse2) * (dp[t][r] - delta);
+        for (int r = 0; r < 4; ++r) ds[t][r] = exp2_(fmaf(s[t][r], c1, gl * bb[t][r]) - lse2) * (dp[t][r] - delta);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ds[t][r] = 0.f;
+      }
+    }
     if (kb + 64 > T) {
 #pragma unroll
       for (int t = 0; t < 4; ++t)
@@ -425,10 +456,12 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
     }
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-      const bf16x8 da = pack8(ds[2 * c], ds[2 * c + 1]);
+      if (2 * c < nt16) {
+        const bf16x8 da = pack8(ds[2 * c], ds[2 * c + 1]);
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt)
-        dq[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, rd_tr(Kt, 32 * c, 32 * c + 16, 16 * dt, lane), dq[dt], 0, 0, 0);
+        for (int dt = 0; dt < 4; ++dt)
+          dq[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, rd_tr(Kt, 32 * c, 32 * c + 16, 16 * dt, lane), dq[dt], 0, 0, 0);
+      }
     }
   }
   dgate += __shfl_xor(dgate, 16, 64);

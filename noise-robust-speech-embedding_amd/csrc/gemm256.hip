@@ -31,6 +31,8 @@
 //    deep so the 32 tiles an XCD runs at once share 8 A panels and 4 B panels in its L2.
 //  - the 256x256 f32 result leaves through LDS in four 64-row passes with the same fused
 //    epilogue as gemm_dma.hip (epi8).
+#include <cstdlib>
+
 #include "gemm_common.h"
 
 // Diagnostic builds only (tools/build_diag.sh): 1 = global loads dropped (zero-record
@@ -38,9 +40,10 @@
 // 4 = main-loop barriers removed, 5 = no LDS-DMA instructions, 6 = neither LDS-DMA nor MFMAs,
 // 7 = epilogue without its global stores (LDS passes kept), 8 = epilogue without LDS reads or
 // stores. Outputs of those builds are wrong; only their time matters.
-// NRSE_G3_STAMPS (diagnostic builds only): workgroup 0-thread writes s_memtime at kernel entry,
-// after the prologue wait, after the main loop and at the end to ((u64*)p.colsum)[4 * wg + i]
-// when the COLSUM flag is off (tools/diag_stamps.py).
+// NRSE_G3_STAMPS (diagnostic builds only): thread 0 of each workgroup writes s_memtime to
+// ((u64*)p.colsum)[8 * wg + i] when the COLSUM flag is off (tools/diag_stamps.py): 0 entry,
+// 1 after the prologue wait, 2 after the main loop, 3 after the epilogue's DMA drain, 4 after
+// pass 0's LDS staging, 5 after pass 0, 6 after pass 1, 7 at the end (stores retired).
 #ifndef NRSE_G3_STAMPS
 #define NRSE_G3_STAMPS 0
 #endif
@@ -48,7 +51,7 @@
 #define NRSE_STAMP(I)                                                                                 \
   do {                                                                                                \
     if (tid == 0 && p.colsum && !(p.flags & NRSE_EPI_COLSUM))                                         \
-      reinterpret_cast<unsigned long long*>(p.colsum)[4 * (long long)blockIdx.x + (I)] =              \
+      reinterpret_cast<unsigned long long*>(p.colsum)[8 * (long long)blockIdx.x + (I)] =              \
           __builtin_amdgcn_s_memtime();                                                               \
   } while (0)
 #else
@@ -69,13 +72,20 @@ constexpr int LEAD = 8;                 // half-tiles staged ahead of the phase 
 constexpr int CT_LD = 260;          // f32 row stride of a 64 x 256 epilogue pass
 static_assert(64 * CT_LD * 4 <= LDS_BYTES, "epilogue pass must fit the staging LDS");
 
-// Row r (0..127) of half-tile hh of a panel -> row of the 256-row tile.
-//  A: the 64-row blocks {hh*64, 128 + hh*64} (the M-half mh = hh of both M-waves)
+// Row r (0..127) of half-tile hh of a panel -> row of the tile, or -1 (slot unused: zero fill).
+//  A (BMT = 256 or 224 rows; M-wave wm owns rows wm*BMT/2 ..): the 64-row blocks
+//    {wm*BMT/2 + hh*64 + (r & 63)}: the M-half mh = hh of both M-waves. At BMT = 224 an M-wave
+//    has 112 rows, so its high half holds 48 (rows 48..63 of that block are unused).
 //  B: the 32-col blocks {wn*64 + hh*32 : wn < 4} (the N-half nh = hh of all four N-waves)
-template <bool IS_A>
+template <bool IS_A, int BMT>
 NRSE_DEV int tile_row(int hh, int r) {
-  if constexpr (IS_A) return (r >> 6) * 128 + hh * 64 + (r & 63);
-  else return (r >> 5) * 64 + hh * 32 + (r & 31);
+  if constexpr (IS_A) {
+    const int ri = r & 63;
+    if (BMT != 256 && hh == 1 && ri >= BMT / 2 - 64) return -1;
+    return (r >> 6) * (BMT / 2) + hh * 64 + ri;
+  } else {
+    return (r >> 5) * 64 + hh * 32 + (r & 31);
+  }
 }
 
 NRSE_DEV bf16x8 fake_frag(int x) {
@@ -97,7 +107,7 @@ struct Ld {
   int kpos[2][2];       // k of the lane inside the K-tile (K-tail masking)
 };
 
-template <bool KC, bool IS_A>
+template <bool KC, bool IS_A, int BMT>
 NRSE_DEV void ld_init(Ld& o, const nrse_gemm_operand& d, const char* base, int wave, int lane, int row0,
                       int rows_total) {
 #if NRSE_G3_ABLATE == 1
@@ -115,16 +125,18 @@ NRSE_DEV void ld_init(Ld& o, const nrse_gemm_operand& d, const char* base, int w
       if constexpr (KC) {
         // [row][k] image: 8 rows x 8 chunks per instruction, chunk position ^ ((row>>1)&7)
         const int r = 8 * i + (lane >> 3);
-        const int grow = row0 + tile_row<IS_A>(hh, r);
+        const int tr = tile_row<IS_A, BMT>(hh, r);
+        const int grow = row0 + tr;
         const int lc = (lane & 7) ^ ((r >> 1) & 7);
-        o.voff[hh][j] = grow < rows_total ? (unsigned)(((long long)grow * o.ld + lc * 8) * 2) : OOB;
+        o.voff[hh][j] = (tr >= 0 && grow < rows_total) ? (unsigned)(((long long)grow * o.ld + lc * 8) * 2) : OOB;
         o.kpos[hh][j] = lc * 8;
       } else {
         // [k][row] image: 4 k rows x 16 chunks per instruction, chunk position ^ fbank(k)
         const int k = 4 * i + (lane >> 4);
         const int lc = (lane & 15) ^ fbank(k);
-        const int gcol = row0 + tile_row<IS_A>(hh, lc * 8);
-        o.voff[hh][j] = gcol < rows_total ? (unsigned)(((long long)k * o.ld + gcol) * 2) : OOB;
+        const int tr = tile_row<IS_A, BMT>(hh, lc * 8);   // 8-row chunks: wholly used or unused
+        const int gcol = row0 + tr;
+        o.voff[hh][j] = (tr >= 0 && gcol < rows_total) ? (unsigned)(((long long)k * o.ld + gcol) * 2) : OOB;
         o.kpos[hh][j] = k;
       }
     }
@@ -151,6 +163,166 @@ NRSE_DEV void ld_issue(const Ld& o, char* dst, int wave, int hh, unsigned soff, 
   }
 }
 
+// ------------------------------------------------------------------ register epilogue
+// The common epilogues of the step run with their flags fixed at compile time: the lane's
+// accumulator values are finished in registers -- bias, GELU (+ bf16 pre-activation to aux),
+// GELU' from the bf16 aux, dropout, residual -- and only the final values go through LDS,
+// packed as the output dtype, for 16-B coalesced row stores; column sums (bias gradients) are
+// taken from the staged image. Lane (g, li) of accumulator [mh*4 + fi][fn] holds tile row
+// wm*BMT/2 + mh*64 + fi*16 + li, columns wn*64 + fn*16 + 4g .. +3 (transposed MFMA). Two passes,
+// one per M-half mh of both M-waves (128 image rows; an f32 image is 130 KB, a bf16 one leaves
+// room for the pre-activation image). The dropout mask index is the general epilogue's.
+// Other flag sets (atomic, accumulate, ReLU, tanh, f32 aux, ...) take the general epilogue.
+enum : int { FE_BIAS = 1, FE_GELU = 2, FE_GELUB = 4, FE_DROP = 8, FE_RESID = 16, FE_OBF = 32, FE_RBF = 64 };
+
+// compile-time mode of the flag set, or -1 (general epilogue)
+NRSE_DEV int fast_epi_mode(const nrse_gemm_params& p) {
+  const int f = p.flags & ~NRSE_EPI_COLSUM;
+  if (f & ~(NRSE_EPI_BIAS | NRSE_EPI_GELU | NRSE_EPI_GELU_BWD | NRSE_EPI_DROPOUT | NRSE_EPI_RESID)) return -1;
+  if (p.c_dtype != NRSE_BF16 && p.c_dtype != NRSE_F32) return -1;
+  int m = 0;
+  if (f & NRSE_EPI_BIAS) m |= FE_BIAS;
+  if (f & NRSE_EPI_GELU) {
+    if (!p.aux || p.aux_dtype != NRSE_BF16 || p.c_dtype != NRSE_BF16) return -1;
+    m |= FE_GELU;
+  }
+  if (f & NRSE_EPI_GELU_BWD) {
+    if (!p.aux || p.aux_dtype != NRSE_BF16) return -1;
+    m |= FE_GELUB;
+  }
+  if (f & NRSE_EPI_DROPOUT) m |= FE_DROP;
+  if (f & NRSE_EPI_RESID) {
+    if (p.resid_dtype != NRSE_F32) return -1;
+    m |= FE_RESID;
+  }
+  if (p.c_dtype == NRSE_BF16) m |= FE_OBF;
+  return m;
+}
+
+template <int FE, int BMT>
+NRSE_DEV void fast_epilogue(const nrse_gemm_params& p, const f32x4 (&acc)[8][4], char* smem, int m0, int n0, int wm,
+                            int wn, int lane, int tid, long long zq, long long zr, int split) {
+  constexpr bool BIAS = FE & FE_BIAS, GELU = FE & FE_GELU, GELUB = FE & FE_GELUB, DROP = FE & FE_DROP;
+  constexpr bool RESID = FE & FE_RESID, OBF = FE & FE_OBF;
+  constexpr int NFI_HI = (BMT / 2 - 64) / 16;
+  constexpr int ES = OBF ? 2 : 4;
+  constexpr int PITCH = 256 * ES + 16;               // image row pitch (bytes), bank-spread
+  constexpr int APITCH = 256 * 2 + 16;
+  const int g = lane >> 4, li = lane & 15;
+  const Epi epi(p, zq, zr, split);
+  const bool colsum = (p.flags & NRSE_EPI_COLSUM) != 0;
+  const bool bias_on = BIAS && epi.bias_on;
+  char* const oimg = smem;
+  char* const aimg = smem + 128 * APITCH;            // pre-activation image (bf16 output only)
+  float* const colacc = reinterpret_cast<float*>(smem + 150 * 1024);  // [2 M-waves][256 columns]
+  float bias4[4][4];
+#pragma unroll
+  for (int fn = 0; fn < 4; ++fn) {
+    const int n = n0 + wn * 64 + fn * 16 + 4 * g;
+    float4 bb = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (BIAS && bias_on && n < p.N) bb = *reinterpret_cast<const float4*>(p.bias + epi.bbase + n);
+    bias4[fn][0] = bb.x; bias4[fn][1] = bb.y; bias4[fn][2] = bb.z; bias4[fn][3] = bb.w;
+  }
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+    for (int fi = 0; fi < 4; ++fi) {
+      if (pass == 1 && fi >= NFI_HI) continue;
+      const int a = pass * 4 + fi;
+      const int trow = wm * (BMT / 2) + pass * 64 + fi * 16 + li;
+      const int prow = wm * 64 + fi * 16 + li;
+      const int m = m0 + trow;
+      const bool mok = m < p.M;
+#pragma unroll
+      for (int fn = 0; fn < 4; ++fn) {
+        const int tcol = wn * 64 + fn * 16 + 4 * g;
+        const int n = n0 + tcol;
+        const bool ok = mok && n < p.N;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaf(acc[a][fn][e], p.alpha, BIAS ? bias4[fn][e] : 0.f);
+        if constexpr (GELU) {
+          uint2 u;
+          u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+          u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+          *reinterpret_cast<uint2*>(aimg + prow * APITCH + tcol * 2) = u;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = gelu_fast(v[e]);
+        }
+        if constexpr (GELUB) {
+          uint2 u = make_uint2(0, 0);
+          if (ok) u = *reinterpret_cast<const uint2*>((const bf16_t*)p.aux + epi.abase + (long long)m * p.ldaux + n);
+          v[0] *= gelu_grad_fast(__uint_as_float(u.x << 16));
+          v[1] *= gelu_grad_fast(__uint_as_float(u.x & 0xffff0000u));
+          v[2] *= gelu_grad_fast(__uint_as_float(u.y << 16));
+          v[3] *= gelu_grad_fast(__uint_as_float(u.y & 0xffff0000u));
+        }
+        if constexpr (DROP) {
+          const long long ci = epi.cbase + (long long)m * p.ldc + n;
+          if (!(p.flags & NRSE_EPI_DROP_AFTER)) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = dropout_keep(epi.key, (uint32_t)(ci + e), epi.thresh) ? v[e] * epi.dscale : 0.f;
+          }
+        }
+        if constexpr (RESID) {
+          float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (ok) r = *reinterpret_cast<const float4*>((const float*)p.resid + epi.rbase + (long long)m * p.ldr + n);
+          v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
+        }
+        if constexpr (DROP) {
+          const long long ci = epi.cbase + (long long)m * p.ldc + n;
+          if (p.flags & NRSE_EPI_DROP_AFTER) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = dropout_keep(epi.key, (uint32_t)(ci + e), epi.thresh) ? v[e] * epi.dscale : 0.f;
+          }
+        }
+        if constexpr (OBF) {
+          uint2 u;
+          u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+          u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+          *reinterpret_cast<uint2*>(oimg + prow * PITCH + tcol * 2) = u;
+        } else {
+          *reinterpret_cast<float4*>(oimg + prow * PITCH + tcol * 4) = make_float4(v[0], v[1], v[2], v[3]);
+        }
+      }
+    }
+    __syncthreads();
+    if (colsum) {
+      // column sums of the staged values (as stored: bf16-rounded for bf16 output): thread
+      // (column c, M-wave h) sums the image rows of M-wave h; both passes into its own slot
+      const int c = tid & 255, h = tid >> 8;
+      const int vrows = pass == 1 ? NFI_HI * 16 : 64;
+      const int mlim = p.M - (m0 + h * (BMT / 2) + pass * 64);
+      const int nr = vrows < mlim ? vrows : (mlim > 0 ? mlim : 0);
+      float sum = 0.f;
+      const char* col = oimg + (h * 64) * PITCH + c * ES;
+      for (int r = 0; r < nr; ++r) {
+        if constexpr (OBF) sum += bf2f(*reinterpret_cast<const bf16_t*>(col + r * PITCH));
+        else sum += *reinterpret_cast<const float*>(col + r * PITCH);
+      }
+      colacc[tid] = pass == 0 ? sum : colacc[tid] + sum;
+    }
+    // coalesced 16-B row stores of the image (and of the pre-activation image)
+    constexpr int CPR = 256 * ES / 16;               // 16-B chunks per image row
+#pragma unroll 4
+    for (int idx = tid; idx < 128 * CPR; idx += 512) {
+      const int prow = idx / CPR, ch = idx - prow * CPR;
+      if (pass == 1 && (prow & 63) >= NFI_HI * 16) continue;
+      const int m = m0 + (prow >> 6) * (BMT / 2) + pass * 64 + (prow & 63);
+      const int n = n0 + ch * (16 / ES);
+      if (m >= p.M || n >= p.N) continue;
+      const uint4 u = *reinterpret_cast<const uint4*>(oimg + prow * PITCH + ch * 16);
+      *reinterpret_cast<uint4*>((char*)p.c + (epi.cbase + (long long)m * p.ldc + n) * ES) = u;
+      if constexpr (GELU) {
+        const uint4 w = *reinterpret_cast<const uint4*>(aimg + prow * APITCH + ch * 16);
+        *reinterpret_cast<uint4*>((bf16_t*)p.aux + epi.abase + (long long)m * p.ldaux + n) = w;
+      }
+    }
+    __syncthreads();
+  }
+  if (colsum && tid < 256 && n0 + tid < p.N) atomicAdd(p.colsum + n0 + tid, colacc[tid] + colacc[256 + tid]);
+}
+
 // raw workgroup barrier: orders LDS accesses for the compiler, emits no vmcnt wait
 #if NRSE_G3_ABLATE == 4
 #define NRSE_BAR() asm volatile("" ::: "memory")
@@ -163,8 +335,13 @@ NRSE_DEV void ld_issue(const Ld& o, char* dst, int wave, int hh, unsigned soff, 
   } while (0)
 #endif
 
-template <bool AKC, bool BKC>
+// BMT: tile rows, 256 or 224 (= 7 x 32: e.g. M = 12768 = 57 x 224 frames of 32 utterances fills
+// 228 of the 256 CUs per N-column of tiles instead of 200; nrse_gemm256 picks the one that
+// needs fewer tile waves, see bm_choice)
+template <bool AKC, bool BKC, int BMT>
 __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params p, int mt, int nt) {
+  static_assert(BMT == 256 || BMT == 224, "tile rows");
+  constexpr int NFI_HI = (BMT / 2 - 64) / 16;  // 16-row blocks in an M-wave's high half: 4 or 3
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
   const int tid = threadIdx.x;
   NRSE_STAMP(0);
@@ -184,7 +361,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
   const int first_m = group * GM;
   const int gm = min(GM, mt - first_m);
   const int in_g = tt - group * GM * nt;
-  const int m0 = (first_m + in_g % gm) * BM;
+  const int m0 = (first_m + in_g % gm) * BMT;
   const int n0 = (in_g / gm) * BN;
 
   const int zb = z / p.splits;
@@ -192,8 +369,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
   const long long zq = zb / p.zdiv, zr = zb % p.zdiv;
 
   Ld la, lb;
-  ld_init<AKC, true>(la, p.a, (const char*)p.a.ptr + (zq * p.a.z1 + zr * p.a.z2) * 2, wave, lane, m0, p.M);
-  ld_init<BKC, false>(lb, p.b, (const char*)p.b.ptr + (zq * p.b.z1 + zr * p.b.z2) * 2, wave, lane, n0, p.N);
+  ld_init<AKC, true, BMT>(la, p.a, (const char*)p.a.ptr + (zq * p.a.z1 + zr * p.a.z2) * 2, wave, lane, m0, p.M);
+  ld_init<BKC, false, BMT>(lb, p.b, (const char*)p.b.ptr + (zq * p.b.z1 + zr * p.b.z2) * 2, wave, lane, n0, p.N);
 
   const int tps = (p.K + BK - 1) / BK;
   const int seg0 = split * p.nseg;
@@ -254,18 +431,23 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
 // columns 4g..4g+3, so the epilogue stages each quad into LDS with one 16-byte write
 #define NRSE_MFMA(C, A, B) C = __builtin_amdgcn_mfma_f32_16x16x32_bf16(B, A, C, 0, 0, 0)
 #endif
-#define NRSE_READ_A(SLOT)                                                                \
-  _Pragma("unroll") for (int fi = 0; fi < 4; ++fi)                                     \
+#define NRSE_READ_A(SLOT, NFI)                                                           \
+  _Pragma("unroll") for (int fi = 0; fi < (NFI); ++fi)                                 \
   _Pragma("unroll") for (int s = 0; s < 2; ++s)                                        \
     fa[fi][s] = NRSE_FRAG(AKC, smem + (SLOT) * HALF, wm * 64 + fi * 16, s, lane);
 #define NRSE_READ_B(SLOT, FB)                                                            \
   _Pragma("unroll") for (int fj = 0; fj < 2; ++fj)                                     \
   _Pragma("unroll") for (int s = 0; s < 2; ++s)                                        \
     FB[fj][s] = NRSE_FRAG(BKC, smem + (SLOT) * HALF, wn * 32 + fj * 16, s, lane);
+#if NRSE_G3_ABLATE == 10
+#define NRSE_BAR2() ((void)0)
+#else
+#define NRSE_BAR2() NRSE_BAR()
+#endif
 #define NRSE_QUAD(MH, NH, FB)                                                            \
   __builtin_amdgcn_s_setprio(1);                                                         \
   _Pragma("unroll") for (int s = 0; s < 2; ++s)                                        \
-  _Pragma("unroll") for (int fi = 0; fi < 4; ++fi)                                     \
+  _Pragma("unroll") for (int fi = 0; fi < ((MH) ? NFI_HI : 4); ++fi)                   \
   _Pragma("unroll") for (int fj = 0; fj < 2; ++fj)                                     \
     NRSE_MFMA(acc[(MH) * 4 + fi][(NH) * 2 + fj], fa[fi][s], FB[fj][s]);                  \
   __builtin_amdgcn_s_setprio(0);
@@ -273,7 +455,11 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
 #ifndef NRSE_G3_WAITMODE
 #define NRSE_G3_WAITMODE 0
 #endif
-#if NRSE_G3_WAITMODE == 1
+#if NRSE_G3_ABLATE == 9
+// diagnostic: no counted DMA waits in the loop (wrong results; measures the DMA-latency stalls)
+#define NRSE_WAIT() ((void)0)
+#define NRSE_WAIT3() ((void)0)
+#elif NRSE_G3_WAITMODE == 1
 // one wait per K-tile (phase 3): retire K-tile t+1 (read in phases 0-2 of the next iteration),
 // leaving the 4 half-tiles of K-tile t+2 (8 DMAs) in flight
 #define NRSE_WAIT() ((void)0)
@@ -292,33 +478,33 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
     // phase p stages half-tile j = p of K-tile t+2 (sequence 4t+8+p) into slot (4t+8+p) % 10
     const TilePos q2 = tile_pos(t + 2);
     // phase 0: quadrant (M-half 0, N-half 0) from A-lo, B-lo
-    NRSE_READ_A(s0)
+    NRSE_READ_A(s0, 4)
     NRSE_READ_B(s1, fbl)
     stage(0, q2, wrap(base + 8));
     NRSE_WAIT();
     NRSE_BAR();
     NRSE_QUAD(0, 0, fbl)
-    NRSE_BAR();
+    NRSE_BAR2();
     // phase 1: (0, 1) from B-hi
     NRSE_READ_B(s2, fbh)
     stage(1, q2, wrap(base + 9));
     NRSE_WAIT();
     NRSE_BAR();
     NRSE_QUAD(0, 1, fbh)
-    NRSE_BAR();
+    NRSE_BAR2();
     // phase 2: (1, 1) from A-hi
-    NRSE_READ_A(s3)
+    NRSE_READ_A(s3, NFI_HI)
     stage(2, q2, base);  // (4t + 10) % 10
     NRSE_WAIT();
     NRSE_BAR();
     NRSE_QUAD(1, 1, fbh)
-    NRSE_BAR();
+    NRSE_BAR2();
     // phase 3: (1, 0) from registers
     stage(3, q2, s1);    // (4t + 11) % 10
     NRSE_WAIT3();
     NRSE_BAR();
     NRSE_QUAD(1, 0, fbl)
-    NRSE_BAR();
+    NRSE_BAR2();
     base = wrap(base + 4);
   }
   if (wm == 0) __builtin_amdgcn_s_barrier();
@@ -331,11 +517,44 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
 #undef NRSE_FRAG
 #undef NRSE_MFMA
 
-  // ---------------------------------------------------------------- epilogue: 4 x 64-row passes
+  // ---------------------------------------------------------------- epilogue
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing zero-fill DMAs
   __syncthreads();
-  float* ct = reinterpret_cast<float*>(smem);
+  NRSE_STAMP(3);
   const int flags = p.flags;
+  {
+    const int fe = fast_epi_mode(p);
+    // the register epilogue, specialised at compile time for the flag sets the step issues
+    // (forward kernels: A and B k-contiguous; dgrad: B row-contiguous)
+#define NRSE_FE(MODE)                                                                            \
+  case MODE:                                                                                     \
+    fast_epilogue<MODE, BMT>(p, acc, smem, m0, n0, wm, wn, lane, tid, zq, zr, split);            \
+    NRSE_STAMP(7);                                                                               \
+    return;
+    if constexpr (AKC && BKC) {
+      switch (fe) {
+        NRSE_FE(FE_OBF)
+        NRSE_FE(FE_OBF | FE_BIAS)
+        NRSE_FE(FE_BIAS)
+        NRSE_FE(FE_OBF | FE_BIAS | FE_GELU)
+        NRSE_FE(FE_BIAS | FE_RESID)
+        NRSE_FE(FE_BIAS | FE_RESID | FE_DROP)
+        default: break;
+      }
+    } else if constexpr (AKC && !BKC) {
+      switch (fe) {
+        NRSE_FE(FE_OBF)
+        NRSE_FE(0)
+        NRSE_FE(FE_OBF | FE_GELUB)
+        NRSE_FE(FE_OBF | FE_GELUB | FE_DROP)
+        default: break;
+      }
+    }
+#undef NRSE_FE
+  }
+
+  // ---------------------------------------------------------------- general epilogue: 4 x 64-row passes
+  float* ct = reinterpret_cast<float*>(smem);
   Epi epi(p, zq, zr, split);
   epi.load_bias(p, n0 + (tid & 31) * 8);  // the epilogue columns of this thread (see the loop)
   const bool colsum = (flags & NRSE_EPI_COLSUM) != 0;
@@ -344,19 +563,21 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
   const int g = lane >> 4, li = lane & 15;
 #pragma unroll
   for (int pass = 0; pass < 4; ++pass) {
+    const int prows = (pass & 1) ? NFI_HI * 16 : 64;  // rows of this pass: (M-wave, M-half)
     if (wm == (pass >> 1)) {
       const int mh = pass & 1;
 #pragma unroll
-      for (int fi = 0; fi < 4; ++fi)
+      for (int fi = 0; fi < (mh ? NFI_HI : 4); ++fi)
 #pragma unroll
         for (int fn = 0; fn < 4; ++fn)
           *reinterpret_cast<f32x4*>(ct + (fi * 16 + li) * CT_LD + wn * 64 + fn * 16 + 4 * g) = acc[mh * 4 + fi][fn];
     }
     __syncthreads();
-    const int mrow0 = m0 + pass * 64;
+    if (pass == 0) NRSE_STAMP(4);
+    const int mrow0 = m0 + (pass >> 1) * (BMT / 2) + (pass & 1) * 64;
     if (flags & NRSE_EPI_ATOMIC) {
       // one row per wave instruction: 64 lanes on 64 consecutive columns (256-B atomics)
-      for (int row = wave; row < 64; row += 8) {
+      for (int row = wave; row < prows; row += 8) {
         const int m = mrow0 + row;
         if (m >= p.M) break;
 #pragma unroll
@@ -374,7 +595,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
         const int cs = (sgi & 31) * 8;
         const int m = mrow0 + row, n = n0 + cs;
         float* cr = ct + row * CT_LD + cs;
-        if (m >= p.M || n >= p.N) {
+        if (row >= prows || m >= p.M || n >= p.N) {
           if (colsum) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) cr[e] = 0.f;
@@ -395,23 +616,50 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
       }
     }
     __syncthreads();
+    if (pass == 0) NRSE_STAMP(5);
+    if (pass == 1) NRSE_STAMP(6);
   }
   if (colsum && n0 + ccol < p.N) atomicAdd(p.colsum + n0 + ccol, csum);
 #if NRSE_G3_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
-  NRSE_STAMP(3);
+  NRSE_STAMP(7);
+}
+
+// Tile rows for this problem: 224 when it needs no more waves of 256 workgroups (one per CU)
+// than 256-row tiles do -- its tiles are 7/8 the work, so the same number of waves finishes
+// sooner (M = 12768: N = 1024 -> 228 instead of 200 tiles, both one wave). NRSE_GEMM_BM=256 or
+// 224 forces one (A/B measurements).
+int g_tile_rows = -1;  // -1: not read yet, 0: automatic, 256 / 224: pinned
+
+int bm_choice(const nrse_gemm_params* p) {
+  if (g_tile_rows < 0) g_tile_rows = getenv("NRSE_GEMM_BM") ? atoi(getenv("NRSE_GEMM_BM")) : 0;
+  if (g_tile_rows == 256 || g_tile_rows == 224) return g_tile_rows;
+  const long long per = (long long)nrse_cdiv(p->N, BN) * p->batch * p->splits;
+  const long long w256 = (nrse_cdiv(p->M, 256) * per + 255) / 256;
+  const long long w224 = (nrse_cdiv(p->M, 224) * per + 255) / 256;
+  return w224 <= w256 ? 224 : 256;
 }
 
 template <bool AKC, bool BKC>
 int launch(const nrse_gemm_params* p, hipStream_t st) {
-  const int mt = nrse_cdiv(p->M, BM), nt = nrse_cdiv(p->N, BN);
+  const int bm = bm_choice(p);
+  const int mt = nrse_cdiv(p->M, bm), nt = nrse_cdiv(p->N, BN);
   const long long total = (long long)mt * nt * p->batch * p->splits;
-  hipLaunchKernelGGL((gemm256_kernel<AKC, BKC>), dim3((unsigned)total), dim3(NTHR), 0, st, *p, mt, nt);
+  if (bm == 224)
+    hipLaunchKernelGGL((gemm256_kernel<AKC, BKC, 224>), dim3((unsigned)total), dim3(NTHR), 0, st, *p, mt, nt);
+  else
+    hipLaunchKernelGGL((gemm256_kernel<AKC, BKC, 256>), dim3((unsigned)total), dim3(NTHR), 0, st, *p, mt, nt);
   return nrse_check_launch("nrse_gemm(256)");
 }
 
 }  // namespace
+
+extern "C" int nrse_gemm_tile_rows(int rows) {
+  const int prev = g_tile_rows < 0 ? 0 : g_tile_rows;
+  g_tile_rows = (rows == 256 || rows == 224) ? rows : 0;
+  return prev;
+}
 
 long long nrse_gemm256_tiles(const nrse_gemm_params* p) {
   return (long long)nrse_cdiv(p->M, BM) * nrse_cdiv(p->N, BN) * p->batch * p->splits;

@@ -112,6 +112,7 @@ _SIGNATURES = {
     "nrse_abi_version": ([], c_int),
     "nrse_gemm": ([_P(GemmParams), c_vp], c_int),
     "nrse_gemm_select": ([c_int], c_int),
+    "nrse_gemm_tile_rows": ([c_int], c_int),
     "nrse_layernorm_fwd": ([_P(LnFwdParams), c_vp], c_int),
     "nrse_layernorm_bwd": ([_P(LnBwdParams), c_vp], c_int),
     "nrse_ln_mean_fwd": ([c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_f, c_vp], c_int),

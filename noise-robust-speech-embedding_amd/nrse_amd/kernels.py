@@ -131,6 +131,11 @@ def gemm_select(generation: int) -> int:
     return int(_lib.lib().nrse_gemm_select(int(generation)))
 
 
+def gemm_tile_rows(rows: int) -> int:
+    """Pin the 256-column kernel's tile rows (0 auto, 256, 224); returns the old setting."""
+    return int(_lib.lib().nrse_gemm_tile_rows(int(rows)))
+
+
 _GEMM_PROBE_BYTES = []
 
 

@@ -33,6 +33,9 @@ def test_asp_fwd_bwd(nrse_device, xdt):
     from nrse_amd import kernels as K
     dev = nrse_device
     B, T, C = 3, 41, 512
+    # seeded: with unseeded draws the saturated attention softmax (logits ~ N(0, 200)) sometimes
+    # leaves only 1e-20-scale gradients, whose f32 rounding then dominates the relative error
+    torch.manual_seed(3)
     x = (torch.randn(B, T, C, device=dev) * 0.5).to(xdt)
     h = torch.tanh(torch.randn(B, T, C, device=dev))
     att = torch.randn(C, 1, device=dev)

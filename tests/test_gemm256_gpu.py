@@ -14,14 +14,16 @@ def rel(a, b):
     return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
 
 
-@pytest.fixture(params=[3], ids=["gen3"])
+@pytest.fixture(params=[256, 224], ids=["gen3_bm256", "gen3_bm224"])
 def gen3(nrse_device, request):
-    """The 256x256 kernel generation (gemm256.hip)."""
+    """The 256-column kernel generation (gemm256.hip) at each tile height."""
     from nrse_amd import kernels as K
-    old = K.gemm_select(request.param)
-    K.current_gen = request.param
+    old = K.gemm_select(3)
+    old_rows = K.gemm_tile_rows(request.param)
+    K.current_gen = 3
     yield K
     K.gemm_select(old)
+    K.gemm_tile_rows(old_rows)
 
 
 def bf(*shape, dev, scale=1.0):
@@ -30,7 +32,8 @@ def bf(*shape, dev, scale=1.0):
 
 @pytest.mark.parametrize("akc", [True, False])
 @pytest.mark.parametrize("bkc", [True, False])
-@pytest.mark.parametrize("shape", [(304, 264, 200), (520, 1000, 1032), (256, 256, 64), (1304, 136, 520)])
+@pytest.mark.parametrize("shape", [(304, 264, 200), (520, 1000, 1032), (256, 256, 64), (1304, 136, 520),
+                                   (672, 264, 136), (232, 520, 96)])
 def test_layouts_and_tails(gen3, nrse_device, akc, bkc, shape):
     K = gen3
     M, N, Kd = shape
@@ -109,6 +112,37 @@ def test_epilogue_colsum(gen3, nrse_device):
     ref = x.double() @ w.double().t()
     assert rel(c, ref) < 1e-5
     assert rel(cs, ref.sum(0)) < 1e-5
+
+
+@pytest.mark.parametrize("bkc", [True, False])
+@pytest.mark.parametrize("out_dtype", [torch.bfloat16, torch.float32])
+def test_epilogue_gelu_bwd_dropout_colsum(gen3, nrse_device, out_dtype, bkc):
+    """The FFN output-dense dgrad epilogue of the step (GELU' from the bf16 pre-activation, the
+    activation-dropout mask, the intermediate bias gradient as column sums), against the 128x128
+    kernel on the same operands: same dropped elements, same values, same column sums (the
+    256-column register epilogue sums the values as stored, so bf16-rounded for bf16 output)."""
+    K = gen3
+    from nrse_amd import _lib
+    dev = nrse_device
+    M, N, Kd = 700, 520, 384
+    dy, w = bf(M, Kd, dev=dev), bf(N, Kd, dev=dev)
+    pre = bf(M, N, dev=dev)
+    outs, sums = [], []
+    for g in (K.current_gen, 2):
+        K.gemm_select(g)
+        c = torch.empty(M, N, device=dev, dtype=out_dtype)
+        cs = torch.zeros(N, device=dev)
+        B = K.Operand(w, True, Kd) if bkc else K.Operand(w.t().contiguous(), False, N)
+        K.gemm(K.Operand(dy, True, Kd), B, c, M, N, Kd, ldc=N, flags=_lib.EPI_GELU_BWD,
+               aux=pre, ldaux=N, dropout_p=0.1, seed=77, colsum=cs)
+        outs.append(c)
+        sums.append(cs)
+    K.gemm_select(K.current_gen)
+    assert torch.equal(outs[0] == 0, outs[1] == 0)
+    tol = 1e-5 if out_dtype == torch.float32 else 4e-3
+    assert rel(outs[0], outs[1]) < tol
+    assert rel(sums[0], sums[1]) < tol
+    assert rel(sums[0], outs[0].double().sum(0)) < tol
 
 
 @pytest.mark.parametrize("splits", [1, 3])

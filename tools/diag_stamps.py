@@ -16,12 +16,15 @@ K.gemm_select(3)
 CLK_MHZ = float(os.environ.get("CLK_MHZ", "100"))  # s_memtime counts shader clocks; reported in kcycles
 
 
-def run(M, N, Kd, reps=5):
+def run(M, N, Kd, rows=256, gelu=False, reps=5):
+    K.gemm_tile_rows(rows)
     a = (torch.rand(M, Kd, device="cuda") * 2 - 1).to(torch.bfloat16)
     w = (torch.rand(N, Kd, device="cuda") * 2 - 1).to(torch.bfloat16)
     c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-    nwg = -(-M // 256) * -(-N // 256)
-    st = torch.zeros(4 * nwg, dtype=torch.int64, device="cuda")
+    aux = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    bias = torch.randn(N, device="cuda")
+    nwg = -(-M // rows) * -(-N // 256)
+    st = torch.zeros(8 * nwg, dtype=torch.int64, device="cuda")
     p = _lib.GemmParams()
     p.a = K.Operand(a, True, Kd).c()
     p.b = K.Operand(w, True, Kd).c()
@@ -31,21 +34,31 @@ def run(M, N, Kd, reps=5):
     p.c_dtype = _lib.BF16
     p.ldc = N
     p.colsum = st.data_ptr()
+    if gelu:
+        p.flags = _lib.EPI_BIAS | _lib.EPI_GELU
+        p.bias = bias.data_ptr()
+        p.aux = aux.data_ptr()
+        p.aux_dtype = _lib.BF16
+        p.ldaux = N
     for _ in range(reps):
         _lib.check(_lib.lib().nrse_gemm(ctypes.byref(p), K.stream_ptr()), "nrse_gemm")
     torch.cuda.synchronize()
-    t = st.view(nwg, 4).cpu().double()
+    t = st.view(nwg, 8).cpu().double()
     t0 = t[:, 0].min()
-    pro = (t[:, 1] - t[:, 0]).median() / 1e3
-    loop = (t[:, 2] - t[:, 1]).median() / 1e3
-    epi = (t[:, 3] - t[:, 2]).median() / 1e3
-    start = (t[:, 0] - t0)
-    end = (t[:, 3] - t0)
-    print(f"M={M} N={N} K={Kd} wgs={nwg}: prologue {pro:.1f} loop {loop:.1f} ({loop / (Kd // 64):.2f}/K-tile) "
-          f"epilogue {epi:.1f} kcyc; entry spread p50 {start.median() / 1e3:.1f} max {start.max() / 1e3:.1f}; "
-          f"last end {end.max() / 1e3:.1f} kcyc", flush=True)
+    d = [(t[:, i + 1] - t[:, i]).median().item() / 1e3 for i in range(7)]
+    names = ["prologue", "loop", "drain", "stage0", "pass0", "pass1", "pass2+3"]
+    end = (t[:, 7] - t0)
+    print(f"M={M} N={N} K={Kd} rows={rows} gelu={int(gelu)} wgs={nwg}: " +
+          " ".join(f"{n} {v:.1f}" for n, v in zip(names, d)) +
+          f" kcyc (loop {d[1] / (Kd // 64):.2f}/K-tile); entry max {(t[:, 0] - t0).max().item() / 1e3:.1f}, "
+          f"last end {end.max().item() / 1e3:.1f} kcyc", flush=True)
 
 
-for shape in ((12768, 1024, 1024), (12768, 3072, 1024), (12768, 4096, 1024), (12768, 1024, 4096),
-              (16384, 1024, 1024), (16384, 4096, 1024), (16384, 1024, 256)):
-    run(*shape)
+if os.environ.get("SHAPES") == "short":
+    run(12768, 1024, 1024, rows=256)
+    run(12768, 1024, 4096, rows=256)
+else:
+    for shape in ((12768, 1024, 1024), (12768, 4096, 1024), (12768, 1024, 4096)):
+        for rows in (256, 224):
+            run(*shape, rows=rows)
+    run(12768, 4096, 1024, rows=224, gelu=True)
