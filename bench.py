@@ -77,11 +77,14 @@ def cpu_baseline(arch_large, seconds_hint=20.0):
                       f"os.cpu_count()={os.cpu_count()}"}
 
 
+TRAFFIC_FILE = "r03_gemm_traffic.json"
+
+
 def gemm_traffic():
-    """HBM bytes per nrse_gemm launch from the committed rocprofv3 PMC summary
-    (tools/pmc_gemm.sh -> profiles/r01_gemm_traffic.json: FETCH_SIZE x 2 (gfx950 correction) +
-    WRITE_SIZE, averaged over the GEMM launches of a bench step). None if absent."""
-    path = os.path.join(ROOT, "profiles", "r01_gemm_traffic.json")
+    """HBM bytes per nrse_gemm launch from the committed rocprofv3 PMC summary of the current
+    step (tools/pmc_gemm.sh -> profiles/r03_gemm_traffic.json: FETCH_SIZE x 2 (gfx950
+    correction) + WRITE_SIZE, averaged over the GEMM launches of a bench step). None if absent."""
+    path = os.path.join(ROOT, "profiles", TRAFFIC_FILE)
     try:
         with open(path) as fh:
             return float(json.load(fh)["family_hbm_bytes_per_launch"])
@@ -262,7 +265,7 @@ def main():
             raise SystemExit("varlen: not enough bucketed batches for the requested steps")
 
         def step(i):  # noqa: F811
-            r = varlen_batches[i]
+            r = varlen_batches[i % len(varlen_batches)]
             Lb = r["clean"].shape[1]
             c = torch.empty(B, Lb, device=dev)
             n = torch.empty(B, Lb, device=dev)
@@ -300,6 +303,27 @@ def main():
         dt = float(tt)
     loss = float(eng.loss_buf)
     st_ok = int((status == 0).sum())
+    # Roofline probe: the timed region runs GEMMs on up to three streams at once, so its event
+    # durations include time shared with the other streams' kernels. One extra step after the
+    # timed region runs with the streams serialised (target view, weight gradients and the
+    # optimizer on the main stream) and brackets every GEMM launch with HIP events on its launch
+    # stream: per-launch durations of the kernels alone, whose sum stays below the step time.
+    from nrse_amd import engine as E
+    serial_prev, overlap_prev = E._SERIAL_TARGET, eng.cfg.overlap_optimizer
+    E._SERIAL_TARGET, eng.cfg.overlap_optimizer = True, False
+    eng.sync_optimizer()
+    torch.cuda.synchronize()
+    sprobe = []
+    ts0 = time.perf_counter()
+    K.set_gemm_probe(sprobe)
+    step(args.warmup + args.steps)
+    K.set_gemm_probe(None)
+    torch.cuda.synchronize()
+    sdt_ms = (time.perf_counter() - ts0) * 1e3
+    sbytes = K.gemm_probe_bytes()
+    E._SERIAL_TARGET, eng.cfg.overlap_optimizer = serial_prev, overlap_prev
+    s_gflops = sum(f for f, _, _, _ in sprobe)
+    s_ms = sum(e0.elapsed_time(e1) for _, e0, e1, _ in sprobe)
     # live roofline of the dominant kernel family (nrse_gemm, MFMA-bound)
     gflops = sum(f for f, _, _, _ in probe)
     gbytes = sum(b for b in K.gemm_probe_bytes())
@@ -325,6 +349,8 @@ def main():
         audio_s = sum(float(varlen_batches[args.warmup + i]["lengths"].sum()) for i in range(args.steps)) / 16000.0
     pairs = B * world * args.steps
     value = pairs / dt
+    peak = BF16_DENSE_PEAK_TFS if cdt == torch.bfloat16 else F32_MFMA_PEAK_TFS
+    s_achieved = s_gflops / (s_ms * 1e-3) / 1e12 if s_ms > 0 else 0.0
     result = {
         "metric": ("BYOL utterance-pairs/sec, WavLM-large, 8s@16kHz, batch=32 per GPU" if varlen_batches is None else
                    "BYOL utterance-pairs/sec, WavLM-large, 3-12s@16kHz length-bucketed, batch=32 per GPU"),
@@ -341,17 +367,21 @@ def main():
                                 "to 0.5 s), noise of independent length tiled on GPU, SNR {4,8} dB, batch=32 per GPU",
                     "global_batch": B * world, "parallelism": f"dp{world}", "layerdrop_executed_layers": avg_exec,
                     "audio_seconds_per_s_per_rank": round(audio_s / dt, 1)}),
-        "roofline": {"bound": "mfma", "kernel": f"nrse_gemm (every launch of {probed_steps} of the {args.steps} "
-                                                 "timed steps)",
-                     "achieved": round(achieved_tfs, 1), "peak": BF16_DENSE_PEAK_TFS if cdt == torch.bfloat16 else
-                     F32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                     "frac": round(achieved_tfs / (BF16_DENSE_PEAK_TFS if cdt == torch.bfloat16 else F32_MFMA_PEAK_TFS),
-                                   4),
-                     "traffic": gemm_traffic(), "traffic_unit": "HBM bytes per launch (PMC, profiles/r01_gemm_traffic.json)",
+        "roofline": {"bound": "mfma", "kernel": "nrse_gemm (every GEMM launch of one step, streams serialised: "
+                                                "the probe after the timed region)",
+                     "achieved": round(s_achieved, 1), "peak": peak, "unit": "TFLOP/s",
+                     "frac": round(s_achieved / peak, 4),
+                     "traffic": gemm_traffic(), "traffic_unit": f"HBM bytes per GEMM launch (PMC, profiles/{TRAFFIC_FILE})",
+                     "algorithmic_bytes_per_launch": round(sum(sbytes) / max(len(sprobe), 1)),
+                     "avg_launch_ms": round(s_ms / max(len(sprobe), 1), 4), "launches": len(sprobe),
+                     "gemm_tflop_per_step": round(s_gflops / 1e12, 3), "gemm_ms_per_step": round(s_ms, 3),
+                     "probe_step_ms": round(sdt_ms, 2), "gemm_share_of_step": round(s_ms / sdt_ms, 3),
                      "mfma_busy_pmc": gemm_mfma_busy(),
-                     "algorithmic_bytes_per_launch": round(gbytes / max(n_launch, 1)),
-                     "avg_launch_ms": round(gms / max(n_launch, 1), 4), "launches": n_launch,
-                     "gemm_share_of_step": round(gms / (dt * 1e3 * probed_steps / args.steps), 3)},
+                     "in_step_events": {"achieved": round(achieved_tfs, 1), "frac": round(achieved_tfs / peak, 4),
+                                        "launches": n_launch, "avg_launch_ms": round(gms / max(n_launch, 1), 4),
+                                        "note": f"events around every GEMM of {probed_steps} of the {args.steps} timed "
+                                                "steps; durations include time shared with concurrent streams",
+                                        "gemm_share_of_step": round(gms / (dt * 1e3 * probed_steps / args.steps), 3)}},
         "step_tflops": round(fpp * value / world / 1e12, 1),
         "loss_last": round(loss, 5), "snr_mix_ok": st_ok,
     }

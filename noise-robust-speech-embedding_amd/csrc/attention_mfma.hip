@@ -15,14 +15,6 @@
 // image stay (nearly) conflict-free.
 #include "common.h"
 
-// Diagnostic builds only (NRSE_ATT_ABLATE, tools/build_diag.sh): in attn_bwd_kv,
-// 1 = no diagonal LDS atomics, 2 = no dropout hash, 3 = no Q/dO/bias re-staging after the first
-// query block, 4 = no final global atomics of the diagonal sums, 5 = plain LDS stores instead of
-// the per-tile diagonal staging, 6 = no DPP diagonal rotations. Outputs of those builds are wrong; only their time matters.
-#ifndef NRSE_ATT_ABLATE
-#define NRSE_ATT_ABLATE 0
-#endif
-
 namespace {
 
 constexpr int D = 64;
@@ -635,7 +627,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
       ds[t][2] = exp2_(fmaf(s[t][2], c1, g4.z * b4.z) - l4.z);
       ds[t][3] = exp2_(fmaf(s[t][3], c1, g4.w * b4.w) - l4.w);
     }
-#if NRSE_ATT_ABLATE != 2
     if (drop) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -653,7 +644,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
         }
       }
     } else
-#endif
     {
 #pragma unroll
       for (int t = 0; t < 4; ++t)
@@ -670,18 +660,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
       ds[t][2] *= dp[t][2] - d4.z; gv[t][2] = ds[t][2] * (g4.z * kvf);
       ds[t][3] *= dp[t][3] - d4.w; gv[t][3] = ds[t][3] * (g4.w * kvf);
     }
-#if NRSE_ATT_ABLATE != 1
     if (p.diag) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         dacc[t] += gv[t][0];
-#if NRSE_ATT_ABLATE == 6
-        dacc[t] += gv[t][1] + gv[t][2] + gv[t][3];
-#else
         diag_rot<1>(gv[t][1], wlo[0], whi[0], dacc[t], dacc[t + 1]);
         diag_rot<2>(gv[t][2], wlo[1], whi[1], dacc[t], dacc[t + 1]);
         diag_rot<3>(gv[t][3], wlo[2], whi[2], dacc[t], dacc[t + 1]);
-#endif
       }
       // diagonals i16 - 4g - 16j + 16w (j < 4) relative to kb0 - qb are complete: stage, fold
 #pragma unroll
@@ -690,7 +675,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
       dacc[1] = dacc[2] = dacc[3] = dacc[4] = 0.f;
       fold(kb0 - qb - dbase);
     }
-#endif
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       const bf16x8 pa = pack8(pd[2 * c], pd[2 * c + 1]);
@@ -723,7 +707,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     fold(kb0 - qend - dbase);
   }
   __syncthreads();
-#if NRSE_ATT_ABLATE != 4
   if (p.diag) {
     const int nd = 2 * T - 1;
     for (int e = tid; e < ndiag; e += 256) {
@@ -732,7 +715,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
       if (dd >= 0 && dd < nd && v != 0.f) atomicAdd(p.diag + (long long)h * nd + dd, v);
     }
   }
-#endif
 }
 
 }  // namespace

@@ -35,15 +35,10 @@
 
 #include "gemm_common.h"
 
-// Diagnostic builds only (tools/build_diag.sh): 1 = global loads dropped (zero-record
-// descriptors), 2 = LDS fragment reads replaced by register values, 3 = MFMAs removed,
-// 4 = main-loop barriers removed, 5 = no LDS-DMA instructions, 6 = neither LDS-DMA nor MFMAs,
-// 7 = epilogue without its global stores (LDS passes kept), 8 = epilogue without LDS reads or
-// stores. Outputs of those builds are wrong; only their time matters.
 // NRSE_G3_STAMPS (diagnostic builds only): thread 0 of each workgroup writes s_memtime to
 // ((u64*)p.colsum)[8 * wg + i] when the COLSUM flag is off (tools/diag_stamps.py): 0 entry,
-// 1 after the prologue wait, 2 after the main loop, 3 after the epilogue's DMA drain, 4 after
-// pass 0's LDS staging, 5 after pass 0, 6 after pass 1, 7 at the end (stores retired).
+// 1 after the prologue wait, 2 after the main loop, 3 after the epilogue's DMA drain, 4 / 5
+// after pass 0's LDS staging / stores (general epilogue), 6 after pass 1, 7 at the end.
 #ifndef NRSE_G3_STAMPS
 #define NRSE_G3_STAMPS 0
 #endif
@@ -57,8 +52,21 @@
 #else
 #define NRSE_STAMP(I) ((void)0)
 #endif
-#ifndef NRSE_G3_ABLATE
-#define NRSE_G3_ABLATE 0
+// NRSE_G3_PHASE_STAMPS (diagnostic builds only): threads 0 and 256 (one wave of each ping-pong
+// group) of workgroup 0 write s_memtime after every main-loop barrier to ((u64*)p.aux)[group *
+// 1024 + 8 * t + i] (tools/diag_phases.py; plain launches, where aux is unused).
+#ifndef NRSE_G3_PHASE_STAMPS
+#define NRSE_G3_PHASE_STAMPS 0
+#endif
+#if NRSE_G3_PHASE_STAMPS
+#define NRSE_PSTAMP(I)                                                                                \
+  do {                                                                                                \
+    if (blockIdx.x == 0 && (tid & 255) == 0 && t < 128)                                               \
+      ((unsigned long long*)(p.aux))[(tid >> 8) * 1024 + 8 * t + (I)] =                              \
+          __builtin_amdgcn_s_memtime();                                                               \
+  } while (0)
+#else
+#define NRSE_PSTAMP(I) ((void)0)
 #endif
 
 namespace {
@@ -88,12 +96,6 @@ NRSE_DEV int tile_row(int hh, int r) {
   }
 }
 
-NRSE_DEV bf16x8 fake_frag(int x) {
-  typedef short short8v __attribute__((ext_vector_type(8)));
-  short8v v = {(short)x, (short)(x + 1), (short)(x + 2), (short)(x + 3), (short)(x + 4), (short)(x + 5),
-               (short)(x + 6), (short)(x + 7)};
-  return __builtin_bit_cast(bf16x8, v);
-}
 
 // Operand loader. Every DMA source offset splits into a per-lane part fixed for the whole kernel
 // (row/column inside the tile, 16-B chunk, k row inside the K-tile) and a wave-uniform part fixed
@@ -110,11 +112,7 @@ struct Ld {
 template <bool KC, bool IS_A, int BMT>
 NRSE_DEV void ld_init(Ld& o, const nrse_gemm_operand& d, const char* base, int wave, int lane, int row0,
                       int rows_total) {
-#if NRSE_G3_ABLATE == 1
-  o.rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0, 0x00020000);
-#else
   o.rs = make_rsrc(base);
-#endif
   o.dead = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0, 0x00020000);
   o.ld = d.ld; o.seg = d.seg_stride;
 #pragma unroll
@@ -155,11 +153,7 @@ NRSE_DEV void ld_issue(const Ld& o, char* dst, int wave, int hh, unsigned soff, 
   for (int j = 0; j < 2; ++j) {
     unsigned voff = o.voff[hh][j];
     if (krem < BK) voff = o.kpos[hh][j] < krem ? voff : OOB;
-#if NRSE_G3_ABLATE == 5 || NRSE_G3_ABLATE == 6
-    asm volatile("" ::"v"(voff), "s"(soff));
-#else
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(dst + (wave * 2 + j) * 1024), 16, voff, soff, 0, 0);
-#endif
   }
 }
 
@@ -324,16 +318,12 @@ NRSE_DEV void fast_epilogue(const nrse_gemm_params& p, const f32x4 (&acc)[8][4],
 }
 
 // raw workgroup barrier: orders LDS accesses for the compiler, emits no vmcnt wait
-#if NRSE_G3_ABLATE == 4
-#define NRSE_BAR() asm volatile("" ::: "memory")
-#else
 #define NRSE_BAR()                            \
   do {                                        \
     asm volatile("" ::: "memory");            \
     __builtin_amdgcn_s_barrier();             \
     asm volatile("" ::: "memory");            \
   } while (0)
-#endif
 
 // BMT: tile rows, 256 or 224 (= 7 x 32: e.g. M = 12768 = 57 x 224 frames of 32 utterances fills
 // 228 of the 256 CUs per N-column of tiles instead of 200; nrse_gemm256 picks the one that
@@ -378,17 +368,17 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
 
   // K-tile t -> uniform source offsets of A and B and the K remainder; t >= ntiles -> dead
   struct TilePos { unsigned sa, sb; int krem; bool live; };
-  auto tile_pos = [&](int t) {
+  auto tile_pos_at = [&](bool live, int sgi, int ki) {
     TilePos q;
-    q.live = t < ntiles;
-    const int tc = q.live ? t : 0;
-    const int sg = seg0 + tc / tps;
-    const int k0 = (tc % tps) * BK;
+    q.live = live;
+    const int sg = seg0 + (live ? sgi : 0);
+    const int k0 = (live ? ki : 0) * BK;
     q.sa = ld_soff<AKC>(la, sg, k0);
     q.sb = ld_soff<BKC>(lb, sg, k0);
     q.krem = p.K - k0;
     return q;
   };
+  auto tile_pos = [&](int t) { return tile_pos_at(t < ntiles, t / tps, t % tps); };
   // half-tile index j of a K-tile in staging (= first-read) order: 0 A-lo, 1 B-lo, 2 B-hi, 3 A-hi
   auto stage = [&](int j, const TilePos& q, int slot) {
     char* dst = smem + slot * HALF;
@@ -419,18 +409,11 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
   NRSE_STAMP(1);
 
   bf16x8 fa[4][2], fbl[2][2], fbh[2][2];
-#if NRSE_G3_ABLATE == 2
-#define NRSE_FRAG(KC, L, B, S, LN) fake_frag((B) + (S) + (LN) + t)
-#else
+
 #define NRSE_FRAG(KC, L, B, S, LN) frag<KC>(L, B, S, LN)
-#endif
-#if NRSE_G3_ABLATE == 3 || NRSE_G3_ABLATE == 6
-#define NRSE_MFMA(C, A, B) asm volatile("" ::"v"(A), "v"(B))
-#else
 // transposed product (B fragment in the A slot): lane (g, i) of an accumulator holds output row i,
 // columns 4g..4g+3, so the epilogue stages each quad into LDS with one 16-byte write
 #define NRSE_MFMA(C, A, B) C = __builtin_amdgcn_mfma_f32_16x16x32_bf16(B, A, C, 0, 0, 0)
-#endif
 #define NRSE_READ_A(SLOT, NFI)                                                           \
   _Pragma("unroll") for (int fi = 0; fi < (NFI); ++fi)                                 \
   _Pragma("unroll") for (int s = 0; s < 2; ++s)                                        \
@@ -439,11 +422,6 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
   _Pragma("unroll") for (int fj = 0; fj < 2; ++fj)                                     \
   _Pragma("unroll") for (int s = 0; s < 2; ++s)                                        \
     FB[fj][s] = NRSE_FRAG(BKC, smem + (SLOT) * HALF, wn * 32 + fj * 16, s, lane);
-#if NRSE_G3_ABLATE == 10
-#define NRSE_BAR2() ((void)0)
-#else
-#define NRSE_BAR2() NRSE_BAR()
-#endif
 #define NRSE_QUAD(MH, NH, FB)                                                            \
   __builtin_amdgcn_s_setprio(1);                                                         \
   _Pragma("unroll") for (int s = 0; s < 2; ++s)                                        \
@@ -452,59 +430,57 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
     NRSE_MFMA(acc[(MH) * 4 + fi][(NH) * 2 + fj], fa[fi][s], FB[fj][s]);                  \
   __builtin_amdgcn_s_setprio(0);
 // the wait before each phase's first barrier retires every half-tile the NEXT phase reads
-#ifndef NRSE_G3_WAITMODE
-#define NRSE_G3_WAITMODE 0
-#endif
-#if NRSE_G3_ABLATE == 9
-// diagnostic: no counted DMA waits in the loop (wrong results; measures the DMA-latency stalls)
-#define NRSE_WAIT() ((void)0)
-#define NRSE_WAIT3() ((void)0)
-#elif NRSE_G3_WAITMODE == 1
-// one wait per K-tile (phase 3): retire K-tile t+1 (read in phases 0-2 of the next iteration),
-// leaving the 4 half-tiles of K-tile t+2 (8 DMAs) in flight
-#define NRSE_WAIT() ((void)0)
-#define NRSE_WAIT3() asm volatile("s_waitcnt vmcnt(8)" ::: "memory")
-#else
 #define NRSE_WAIT() asm volatile("s_waitcnt vmcnt(12)" ::: "memory")
-#define NRSE_WAIT3() NRSE_WAIT()
-#endif
 
   // ping-pong start: group 1 falls one barrier behind (schedule and hand-off rules: header)
   if (wm == 1) __builtin_amdgcn_s_barrier();
   int base = 0;  // slot of half-tile sequence number 4t
+  // K-tile t+2 as (segment, K-tile within the segment), advanced by one per iteration: the
+  // division by the segment's K-tile count stays out of the loop (done per iteration by all 8
+  // waves on the CU's one scalar unit, it lengthened each K-tile's first phase by ~200 cycles)
+  int u_sg = 2 / tps, u_k = 2 % tps;
 #pragma unroll 1
   for (int t = 0; t < ntiles; ++t) {
     const int s0 = base, s1 = wrap(base + 1), s2 = wrap(base + 2), s3 = wrap(base + 3);
     // phase p stages half-tile j = p of K-tile t+2 (sequence 4t+8+p) into slot (4t+8+p) % 10
-    const TilePos q2 = tile_pos(t + 2);
+    const TilePos q2 = tile_pos_at(t + 2 < ntiles, u_sg, u_k);
+    if (++u_k == tps) { u_k = 0; ++u_sg; }
     // phase 0: quadrant (M-half 0, N-half 0) from A-lo, B-lo
     NRSE_READ_A(s0, 4)
     NRSE_READ_B(s1, fbl)
     stage(0, q2, wrap(base + 8));
     NRSE_WAIT();
     NRSE_BAR();
+    NRSE_PSTAMP(0);
     NRSE_QUAD(0, 0, fbl)
-    NRSE_BAR2();
+    NRSE_BAR();
+    NRSE_PSTAMP(1);
     // phase 1: (0, 1) from B-hi
     NRSE_READ_B(s2, fbh)
     stage(1, q2, wrap(base + 9));
     NRSE_WAIT();
     NRSE_BAR();
+    NRSE_PSTAMP(2);
     NRSE_QUAD(0, 1, fbh)
-    NRSE_BAR2();
+    NRSE_BAR();
+    NRSE_PSTAMP(3);
     // phase 2: (1, 1) from A-hi
     NRSE_READ_A(s3, NFI_HI)
     stage(2, q2, base);  // (4t + 10) % 10
     NRSE_WAIT();
     NRSE_BAR();
+    NRSE_PSTAMP(4);
     NRSE_QUAD(1, 1, fbh)
-    NRSE_BAR2();
+    NRSE_BAR();
+    NRSE_PSTAMP(5);
     // phase 3: (1, 0) from registers
     stage(3, q2, s1);    // (4t + 11) % 10
-    NRSE_WAIT3();
+    NRSE_WAIT();
     NRSE_BAR();
+    NRSE_PSTAMP(6);
     NRSE_QUAD(1, 0, fbl)
-    NRSE_BAR2();
+    NRSE_BAR();
+    NRSE_PSTAMP(7);
     base = wrap(base + 4);
   }
   if (wm == 0) __builtin_amdgcn_s_barrier();
@@ -513,7 +489,6 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
 #undef NRSE_READ_B
 #undef NRSE_QUAD
 #undef NRSE_WAIT
-#undef NRSE_WAIT3
 #undef NRSE_FRAG
 #undef NRSE_MFMA
 
@@ -602,13 +577,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
           }
           continue;
         }
-#if NRSE_G3_ABLATE == 7
-        if (cr[0] == 12345.f) epi8(p, epi, m, n, cr, colsum);  // never: keeps the LDS reads
-#elif NRSE_G3_ABLATE == 8
-        (void)cr;
-#else
         epi8(p, epi, m, n, cr, colsum);
-#endif
       }
       if (colsum) {
         __syncthreads();
