@@ -199,10 +199,9 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // Padding is skipped, not computed: a wave whose 16 queries all lie past T (3 of the 4 waves
-  // of the last query block at T = 399) only stages and syncs, and in the last key tile the
-  // 16-key sub-tiles wholly past T get no MFMAs, exponentials or dropout hashes (nt16 < 4).
-  const bool wact = q0 + w * 16 < T;
+  // In the last key tile the 16-key sub-tiles wholly past T get no dropout hashes (nt16 < 4); their
+  // probabilities are already 0. (Skipping the query waves past T with a wave-uniform branch made
+  // the compiler duplicate the loop and stage the MFMA accumulators through AGPRs: slower.)
   for (int it = 0; it < ntiles; ++it) {
     const int kb = it * 64;
     char* const Kt = kv0 + (it & 1) * 2 * TILE_B;
@@ -217,16 +216,15 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
       kv_dma_issue(kd, Kn, kb + 64, w);
       kv_dma_issue(vd, Kn + TILE_B, kb + 64, w);
     }
-    if (!wact) continue;
     const int nt16 = min(4, (T - kb + 15) >> 4);  // 16-key sub-tiles holding a key < T (uniform)
+    // the MFMAs run on every sub-tile (a conditional MFMA makes the compiler stage its result
+    // through AGPRs); only the element work below is skipped past T
     f32x4 s[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (t < nt16) {
 #pragma unroll
-        for (int ss = 0; ss < 2; ++ss) s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rd_row(Kt, 16 * t + i16, 4 * ss + g), qf[ss], s[t], 0, 0, 0);
-      }
+      for (int ss = 0; ss < 2; ++ss) s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rd_row(Kt, 16 * t + i16, 4 * ss + g), qf[ss], s[t], 0, 0, 0);
     }
     float v[4][4];
 #pragma unroll
@@ -254,18 +252,12 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
     float pd[4][4];
     float ps = 0.f;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      if (t < nt16) {
+    for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          pd[t][r] = exp2_(v[t][r] - mn);
-          ps += pd[t][r];
-        }
-      } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) pd[t][r] = 0.f;
+      for (int r = 0; r < 4; ++r) {
+        pd[t][r] = exp2_(v[t][r] - mn);
+        ps += pd[t][r];
       }
-    }
     if (drop) {
 #pragma unroll
       for (int t = 0; t < 4; ++t)
@@ -287,12 +279,10 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
     }
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-      if (2 * c < nt16) {
-        const bf16x8 pa = pack8(pd[2 * c], pd[2 * c + 1]);
+      const bf16x8 pa = pack8(pd[2 * c], pd[2 * c + 1]);
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt)
-          o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, rd_tr(Vt, 32 * c, 32 * c + 16, 16 * dt, lane), o[dt], 0, 0, 0);
-      }
+      for (int dt = 0; dt < 4; ++dt)
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, rd_tr(Vt, 32 * c, 32 * c + 16, 16 * dt, lane), o[dt], 0, 0, 0);
     }
   }
   float l = lpart + __shfl_xor(lpart, 16, 64);
@@ -376,7 +366,6 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
   f32x4 dq[4];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const bool wact = q0 + w * 16 < T;  // padding skipped as in the forward
   for (int it = 0; it < ntiles; ++it) {
     const int kb = it * 64;
     char* const Kt = kv0 + (it & 1) * 2 * TILE_B;
@@ -389,19 +378,16 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
       kv_dma_issue(kd, Kn, kb + 64, w);
       kv_dma_issue(vd, Kn + TILE_B, kb + 64, w);
     }
-    if (!wact) continue;
     const int nt16 = min(4, (T - kb + 15) >> 4);
     f32x4 s[4], dp[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
       dp[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (t < nt16) {
 #pragma unroll
-        for (int ss = 0; ss < 2; ++ss) {
-          s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rd_row(Kt, 16 * t + i16, 4 * ss + g), qf[ss], s[t], 0, 0, 0);
-          dp[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rd_row(Vt, 16 * t + i16, 4 * ss + g), dof[ss], dp[t], 0, 0, 0);
-        }
+      for (int ss = 0; ss < 2; ++ss) {
+        s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rd_row(Kt, 16 * t + i16, 4 * ss + g), qf[ss], s[t], 0, 0, 0);
+        dp[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rd_row(Vt, 16 * t + i16, 4 * ss + g), dof[ss], dp[t], 0, 0, 0);
       }
     }
     // Straight-line per element; wave-uniform branches for dropout and for the last (partial)
@@ -448,12 +434,10 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
     }
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-      if (2 * c < nt16) {
-        const bf16x8 da = pack8(ds[2 * c], ds[2 * c + 1]);
+      const bf16x8 da = pack8(ds[2 * c], ds[2 * c + 1]);
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt)
-          dq[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, rd_tr(Kt, 32 * c, 32 * c + 16, 16 * dt, lane), dq[dt], 0, 0, 0);
-      }
+      for (int dt = 0; dt < 4; ++dt)
+        dq[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, rd_tr(Kt, 32 * c, 32 * c + 16, 16 * dt, lane), dq[dt], 0, 0, 0);
     }
   }
   dgate += __shfl_xor(dgate, 16, 64);
