@@ -100,21 +100,52 @@ NRSE_DEV f32x2 gelu2(f32x2 x) { return splat2(0.5f) * x * (splat2(1.0f) + erf_fa
 NRSE_DEV float gelu_f(float x) { return gelu_fast(x); }
 NRSE_DEV float gelu_grad_f(float x) { return gelu_grad_fast(x); }
 
-// Counter-based dropout hash (bijective 32-bit mixer, "lowbias32"). The mask of element i at
-// a dropout site seeded with `seed` is keep = hash(i ^ mix(seed)) >= p * 2^32. Deterministic
-// and stateless, so backward regenerates the forward mask from (seed, i).
+// Counter-based dropout hash (bijective 32-bit mixer, "lowbias32"), one hash per PAIR of
+// elements, 16 bits each: the mask of flat element i at a dropout site seeded with `seed` is
+//   h = mix32((i >> 1) ^ site_key(seed)), keep = (i odd ? h >> 16 : h & 0xffff) >= thr16,
+//   thr16 = round(p * 65536) (P(drop) within 8e-6 of p).
+// mix32's two 32-bit multiplies are quarter-rate VALU (16 cycles per wave64 instruction): per
+// element they cost more than the rest of a GEMM epilogue's dropout, so pairs halve that.
+// Deterministic and stateless, so backward regenerates the forward mask from (seed, i).
 NRSE_DEV uint32_t mix32(uint32_t x) {
   x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
   return x;
 }
 NRSE_DEV uint32_t site_key(uint32_t seed) { return mix32(seed * 0x9e3779b9U + 0x632be5abU); }
-NRSE_DEV bool dropout_keep(uint32_t key, uint32_t idx, uint32_t thresh) {
-  return mix32(idx ^ key) >= thresh;
-}
 __host__ __device__ inline uint32_t dropout_threshold(float p) {
-  double t = (double)p * 4294967296.0;
-  if (t >= 4294967295.0) return 0xffffffffU;
-  return (uint32_t)t;
+  const double t = (double)p * 65536.0 + 0.5;
+  return t >= 65536.0 ? 65536u : (uint32_t)t;
+}
+NRSE_DEV bool dropout_keep(uint32_t key, uint32_t idx, uint32_t thr16) {
+  const uint32_t h = mix32((idx >> 1) ^ key);
+  return ((idx & 1u) ? (h >> 16) : (h & 0xffffu)) >= thr16;
+}
+// keep[0..N-1] of elements idx0 .. idx0+N-1, idx0 EVEN (N even): N/2 hashes
+template <int N>
+NRSE_DEV void dropout_keep_run(uint32_t key, uint32_t idx0, uint32_t thr16, bool (&keep)[N]) {
+  static_assert(N % 2 == 0, "pairs");
+#pragma unroll
+  for (int j = 0; j < N / 2; ++j) {
+    const uint32_t h = mix32(((idx0 >> 1) + (uint32_t)j) ^ key);
+    keep[2 * j] = (h & 0xffffu) >= thr16;
+    keep[2 * j + 1] = (h >> 16) >= thr16;
+  }
+}
+// o[e] = keep(idx0 + e) ? o[e] * sc : 0 -- pairs when idx0 is even (every vector site of the
+// step: row strides and column groups are even), per element otherwise
+template <int N>
+NRSE_DEV void dropout_apply(uint32_t key, uint32_t idx0, uint32_t thr16, float sc, float (&o)[N]) {
+  if constexpr (N % 2 == 0) {
+    if (!(idx0 & 1u)) {
+      bool k[N];
+      dropout_keep_run<N>(key, idx0, thr16, k);
+#pragma unroll
+      for (int e = 0; e < N; ++e) o[e] = k[e] ? o[e] * sc : 0.f;
+      return;
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < N; ++e) o[e] = dropout_keep(key, idx0 + (uint32_t)e, thr16) ? o[e] * sc : 0.f;
 }
 
 // Attention-probability dropout (the [B, H, T, T] site, the largest): one mixer hash per PAIR of

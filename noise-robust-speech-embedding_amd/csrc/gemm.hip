@@ -27,8 +27,6 @@ int nrse_posconv_wgrad(const nrse_gemm_params* p, hipStream_t st);
 bool nrse_gemm256_ok(const nrse_gemm_params* p);         // gemm256.hip
 long long nrse_gemm256_tiles(const nrse_gemm_params* p);
 int nrse_gemm256(const nrse_gemm_params* p, hipStream_t st);
-bool nrse_gemm2wg_ok(const nrse_gemm_params* p);         // gemm2wg.hip
-int nrse_gemm2wg(const nrse_gemm_params* p, hipStream_t st);
 
 namespace {
 
@@ -399,10 +397,8 @@ extern "C" int nrse_gemm(const nrse_gemm_params* p, void* stream) {
   const bool big = nrse_gemm256_tiles(p) >= 128 && !(p->flags & NRSE_EPI_ATOMIC);
   // the grouped pos-conv pattern (sliding-window A operand, N = 64): its own kernel unless a
   // generation is pinned (NRSE_GEMM_GEN=1|2|3 benchmarks the generic kernels on it)
-  if ((gen == 0 || gen >= 4) && nrse_posconv_ok(p)) return nrse_posconv(p, st);
-  if ((gen == 0 || gen >= 4) && nrse_posconv_wgrad_ok(p)) return nrse_posconv_wgrad(p, st);
-  // NRSE_GEMM_GEN=5: the two-workgroups-per-CU kernel for the k-contiguous problems it takes
-  if (gen == 5 && nrse_gemm2wg_ok(p)) return nrse_gemm2wg(p, st);
+  if ((gen == 0 || gen == 4) && nrse_posconv_ok(p)) return nrse_posconv(p, st);
+  if ((gen == 0 || gen == 4) && nrse_posconv_wgrad_ok(p)) return nrse_posconv_wgrad(p, st);
   if (gen != 1 && gen != 2 && nrse_gemm256_ok(p) && (gen == 3 || big))
     return nrse_gemm256(p, st);
   if (gen != 1 && nrse_gemm_dma_ok(p)) return nrse_gemm_dma(p, st);

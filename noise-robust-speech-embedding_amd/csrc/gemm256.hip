@@ -38,7 +38,8 @@
 // NRSE_G3_STAMPS (diagnostic builds only): thread 0 of each workgroup writes s_memtime to
 // ((u64*)p.colsum)[8 * wg + i] when the COLSUM flag is off (tools/diag_stamps.py): 0 entry,
 // 1 after the prologue wait, 2 after the main loop, 3 after the epilogue's DMA drain, 4 / 5
-// after pass 0's LDS staging / stores (general epilogue), 6 after pass 1, 7 at the end.
+// after pass 0's LDS staging / stores, 6 after pass 1's staging (general epilogue: after pass 1),
+// 7 at the end.
 #ifndef NRSE_G3_STAMPS
 #define NRSE_G3_STAMPS 0
 #endif
@@ -195,7 +196,8 @@ NRSE_DEV int fast_epi_mode(const nrse_gemm_params& p) {
 
 template <int FE, int BMT>
 NRSE_DEV void fast_epilogue(const nrse_gemm_params& p, const f32x4 (&acc)[8][4], char* smem, int m0, int n0, int wm,
-                            int wn, int lane, int tid, long long zq, long long zr, int split) {
+                            int wn, int lane, int tid, long long zq, long long zr, int split,
+                            const float4 (&bpre)[4]) {
   constexpr bool BIAS = FE & FE_BIAS, GELU = FE & FE_GELU, GELUB = FE & FE_GELUB, DROP = FE & FE_DROP;
   constexpr bool RESID = FE & FE_RESID, OBF = FE & FE_OBF;
   constexpr int NFI_HI = (BMT / 2 - 64) / 16;
@@ -205,17 +207,18 @@ NRSE_DEV void fast_epilogue(const nrse_gemm_params& p, const f32x4 (&acc)[8][4],
   const int g = lane >> 4, li = lane & 15;
   const Epi epi(p, zq, zr, split);
   const bool colsum = (p.flags & NRSE_EPI_COLSUM) != 0;
+  // f32 output without column sums: stored straight from the registers (4 lanes write a row's
+  // 64 contiguous bytes; measured 8 % faster on the out-proj shape than the LDS-staged rows,
+  // while 32-byte bf16 row pieces measured slower, so those keep the staging)
+  const bool DIRECT = !OBF && !colsum;
   const bool bias_on = BIAS && epi.bias_on;
   char* const oimg = smem;
   char* const aimg = smem + 128 * APITCH;            // pre-activation image (bf16 output only)
   float* const colacc = reinterpret_cast<float*>(smem + 150 * 1024);  // [2 M-waves][256 columns]
-  float bias4[4][4];
+  float bias4[4][4];  // loaded before the main loop (bpre): no global-load latency here
 #pragma unroll
   for (int fn = 0; fn < 4; ++fn) {
-    const int n = n0 + wn * 64 + fn * 16 + 4 * g;
-    float4 bb = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (BIAS && bias_on && n < p.N) bb = *reinterpret_cast<const float4*>(p.bias + epi.bbase + n);
-    bias4[fn][0] = bb.x; bias4[fn][1] = bb.y; bias4[fn][2] = bb.z; bias4[fn][3] = bb.w;
+    bias4[fn][0] = bpre[fn].x; bias4[fn][1] = bpre[fn].y; bias4[fn][2] = bpre[fn].z; bias4[fn][3] = bpre[fn].w;
   }
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
@@ -254,8 +257,7 @@ NRSE_DEV void fast_epilogue(const nrse_gemm_params& p, const f32x4 (&acc)[8][4],
         if constexpr (DROP) {
           const long long ci = epi.cbase + (long long)m * p.ldc + n;
           if (!(p.flags & NRSE_EPI_DROP_AFTER)) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = dropout_keep(epi.key, (uint32_t)(ci + e), epi.thresh) ? v[e] * epi.dscale : 0.f;
+            dropout_apply<4>(epi.key, (uint32_t)ci, epi.thresh, epi.dscale, v);
           }
         }
         if constexpr (RESID) {
@@ -266,8 +268,7 @@ NRSE_DEV void fast_epilogue(const nrse_gemm_params& p, const f32x4 (&acc)[8][4],
         if constexpr (DROP) {
           const long long ci = epi.cbase + (long long)m * p.ldc + n;
           if (p.flags & NRSE_EPI_DROP_AFTER) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = dropout_keep(epi.key, (uint32_t)(ci + e), epi.thresh) ? v[e] * epi.dscale : 0.f;
+            dropout_apply<4>(epi.key, (uint32_t)ci, epi.thresh, epi.dscale, v);
           }
         }
         if constexpr (OBF) {
@@ -276,11 +277,17 @@ NRSE_DEV void fast_epilogue(const nrse_gemm_params& p, const f32x4 (&acc)[8][4],
           u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
           *reinterpret_cast<uint2*>(oimg + prow * PITCH + tcol * 2) = u;
         } else {
-          *reinterpret_cast<float4*>(oimg + prow * PITCH + tcol * 4) = make_float4(v[0], v[1], v[2], v[3]);
+          if (DIRECT) {
+            if (ok) *reinterpret_cast<float4*>((float*)p.c + epi.cbase + (long long)m * p.ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
+          } else {
+            *reinterpret_cast<float4*>(oimg + prow * PITCH + tcol * 4) = make_float4(v[0], v[1], v[2], v[3]);
+          }
         }
       }
     }
+    if (DIRECT) continue;
     __syncthreads();
+    NRSE_STAMP(4 + 2 * pass);
     if (colsum) {
       // column sums of the staged values (as stored: bf16-rounded for bf16 output): thread
       // (column c, M-wave h) sums the image rows of M-wave h; both passes into its own slot
@@ -313,6 +320,7 @@ NRSE_DEV void fast_epilogue(const nrse_gemm_params& p, const f32x4 (&acc)[8][4],
       }
     }
     __syncthreads();
+    if (pass == 0) NRSE_STAMP(5);
   }
   if (colsum && tid < 256 && n0 + tid < p.N) atomicAdd(p.colsum + n0 + tid, colacc[tid] + colacc[256 + tid]);
 }
@@ -388,6 +396,24 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
     else ld_issue(la, dst, wave, 1, q.sa, q.krem, q.live);
   };
   auto wrap = [](int x) { return x >= SLOTS ? x - SLOTS : x; };
+
+  // this lane's epilogue bias columns (wn * 64 + fn * 16 + 4g .. +3), fetched now so that their
+  // latency is hidden behind the main loop
+  // (buffer loads: columns past N, no bias or split > 0 read zeros without a branch, so the
+  // loads stay in flight under the prologue)
+  float4 bpre[4];
+  {
+    const bool bon = (p.flags & NRSE_EPI_BIAS) && split == 0;
+    const float* bb = bon ? p.bias + zq * p.bias_z1 + zr * p.bias_z2 : nullptr;
+    const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc((void*)bb, 0, bon ? 0x7fffffff : 0, 0x00020000);
+#pragma unroll
+    for (int fn = 0; fn < 4; ++fn) {
+      const int n = n0 + wn * 64 + fn * 16 + 4 * (lane >> 4);
+      const unsigned off = n < p.N ? (unsigned)n * 4u : OOB;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(brs, off, 0, 0);
+      bpre[fn] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+    }
+  }
 
   f32x4 acc[8][4];
 #pragma unroll
@@ -503,7 +529,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
     // (forward kernels: A and B k-contiguous; dgrad: B row-contiguous)
 #define NRSE_FE(MODE)                                                                            \
   case MODE:                                                                                     \
-    fast_epilogue<MODE, BMT>(p, acc, smem, m0, n0, wm, wn, lane, tid, zq, zr, split);            \
+    fast_epilogue<MODE, BMT>(p, acc, smem, m0, n0, wm, wn, lane, tid, zq, zr, split, bpre);          \
     NRSE_STAMP(7);                                                                               \
     return;
     if constexpr (AKC && BKC) {

@@ -154,8 +154,7 @@ NRSE_DEV void epi8(const nrse_gemm_params& p, const Epi& e, int m, int n, float*
   }
   const long long ci = e.cbase + (long long)m * p.ldc + n;
   if ((flags & NRSE_EPI_DROPOUT) && !(flags & NRSE_EPI_DROP_AFTER)) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = dropout_keep(e.key, (uint32_t)(ci + i), e.thresh) ? v[i] * e.dscale : 0.f;
+    dropout_apply<8>(e.key, (uint32_t)ci, e.thresh, e.dscale, v);
   }
   if (flags & NRSE_EPI_RESID) {
     float r[8];
@@ -164,8 +163,7 @@ NRSE_DEV void epi8(const nrse_gemm_params& p, const Epi& e, int m, int n, float*
     for (int i = 0; i < 8; ++i) v[i] += r[i];
   }
   if ((flags & NRSE_EPI_DROPOUT) && (flags & NRSE_EPI_DROP_AFTER)) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = dropout_keep(e.key, (uint32_t)(ci + i), e.thresh) ? v[i] * e.dscale : 0.f;
+    dropout_apply<8>(e.key, (uint32_t)ci, e.thresh, e.dscale, v);
   }
   if (keep) {
 #pragma unroll

@@ -96,8 +96,7 @@ __global__ void dropout_cast_kernel(const float* __restrict__ in, void* __restri
     float4 v = reinterpret_cast<const float4*>(in)[q];
     float o[4] = {v.x, v.y, v.z, v.w};
     if (p > 0.f) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = dropout_keep(key, (uint32_t)(q * 4 + e), thr) ? o[e] * sc : 0.f;
+      dropout_apply<4>(key, (uint32_t)(q * 4), thr, sc, o);
     }
     if (odt == NRSE_BF16) {
       uint2 u;
@@ -186,8 +185,7 @@ __global__ __launch_bounds__(256) void dropout_cast_colsum_kernel(const float* _
       const float4 v = *reinterpret_cast<const float4*>(in + i + 4);
       float o[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
       if (p > 0.f) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = dropout_keep(key, (uint32_t)(i + e), thr) ? o[e] * sc : 0.f;
+        dropout_apply<8>(key, (uint32_t)i, thr, sc, o);
       }
 #pragma unroll
       for (int e = 0; e < 8; ++e) a[e] += o[e];

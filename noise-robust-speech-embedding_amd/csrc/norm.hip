@@ -436,8 +436,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const nrse_ln_bwd_params p)
       if (fuse) {
         const long long i = row * C + c0;
         if (p.dv_p > 0.f) {
-#pragma unroll
-          for (int e = 0; e < CH; ++e) o[e] = dropout_keep(key, (uint32_t)(i + e), thr) ? o[e] * dsc : 0.f;
+          dropout_apply<CH>(key, (uint32_t)i, thr, dsc, o);
         }
 #pragma unroll
         for (int e = 0; e < CH; ++e) dc[RES ? k : 0][e] += o[e];

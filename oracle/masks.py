@@ -30,15 +30,18 @@ def site_key(seed: int) -> np.uint64:
 
 
 def threshold(p: float) -> int:
-    t = p * 4294967296.0
-    return 0xFFFFFFFF if t >= 4294967295.0 else int(t)
+    """16-bit keep threshold round(p * 65536) (csrc/common.h dropout_threshold)."""
+    t = p * 65536.0 + 0.5
+    return 65536 if t >= 65536.0 else int(t)
 
 
 def keep_mask(seed: int, p: float, n: int, start: int = 0) -> np.ndarray:
-    """keep[i] for flat element indices start..start+n-1 of one dropout site."""
+    """keep[i] for flat element indices start..start+n-1 of one dropout site: one mix32 hash per
+    pair of elements (i >> 1), 16 bits per element (odd i: high half)."""
     idx = np.arange(start, start + n, dtype=np.uint64)
-    h = mix32(idx ^ site_key(seed))
-    return h >= np.uint64(threshold(p))
+    h = mix32((idx >> np.uint64(1)) ^ site_key(seed))
+    half = np.where((idx & np.uint64(1)) == 1, h >> np.uint64(16), h & np.uint64(0xFFFF))
+    return half >= np.uint64(threshold(p))
 
 
 def dropout_mask(seed: int, p: float, shape) -> np.ndarray:

@@ -1,7 +1,7 @@
-"""Isolated forward GEMM rates at the WavLM-Large step shapes (M = 12768): the default dispatch
-(256x256 kernel) against NRSE_GEMM_GEN=5 (two workgroups per CU, gemm2wg.hip), with the step's
-epilogues (bias; bias + GELU + bf16 pre-activation; bias + dropout + f32 residual), and torch
-(hipBLASLt) for scale; interleaved rounds in one process (median of 5)."""
+"""Isolated forward GEMM rates at the WavLM-Large step shapes (M = 12768) with the step's
+epilogues (bias; bias + GELU + bf16 pre-activation; bias + dropout + f32 residual), for the kernel
+generations in GENS (default: the normal dispatch, i.e. the 256x256 kernel), against torch
+(hipBLASLt, plain product) for scale; interleaved rounds in one process (median of 5)."""
 import os, sys, statistics
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "noise-robust-speech-embedding_amd"))
 import torch
@@ -24,7 +24,7 @@ def timeit(fn, iters=20):
 
 
 M = int(os.environ.get("M", 12768))
-gens = [int(g) for g in os.environ.get("GENS", "0,5").split(",")]
+gens = [int(g) for g in os.environ.get("GENS", "0").split(",")]
 for name, N, Kd, epi in (("qkv", 3072, 1024, "bias"), ("out", 1024, 1024, "resid"), ("ffn1", 4096, 1024, "gelu"),
                          ("ffn2", 1024, 4096, "resid")):
     x = torch.randn(M, Kd, device=dev).to(torch.bfloat16)
