@@ -116,9 +116,13 @@ typedef struct {
   float dropout_p;
   uint32_t seed;         /* dropout mask = hash(seed, element offset of C[m,n] from c) */
   float* colsum;
+  /* optional f32 workspace of nrse_gemm_colsum_workspace(p) floats (COLSUM): the
+   * per-tile column sums are then added in a fixed order (deterministic) instead of by atomics */
+  float* colsum_part;
 } nrse_gemm_params;
 
 int nrse_gemm(const nrse_gemm_params* p, void* stream);
+long long nrse_gemm_colsum_workspace(const nrse_gemm_params* p);  /* floats for p->colsum_part */
 /* Kernel generation used by nrse_gemm for bf16 operands: 0 = automatic (default), 1 = register
  * staged 128x128, 2 = LDS-DMA 128x128, 3 = LDS-DMA 256x256 (falls back when a problem does not
  * fit it). Process-wide; for tests and benchmarks. Returns the previous setting. */
@@ -165,15 +169,21 @@ typedef struct {
    * nrse_dropout_cast_colsum pass over dx): dv = dropout(dx; dv_p, dv_seed) in dv_dtype,
    * dv_colsum[c] += sum_r dv[r, c] (if dv_colsum) */
   void* dv; int dv_dtype; float* dv_colsum; float dv_p; uint32_t dv_seed;
+  /* optional f32 workspace of nrse_layernorm_bwd_workspace(p) floats: the column sums (dgamma,
+   * dbeta, dv_colsum) are then added in a fixed order (deterministic) instead of by f32 atomics */
+  float* part;
 } nrse_ln_bwd_params;
 
 int nrse_layernorm_fwd(const nrse_ln_fwd_params* p, void* stream);
 int nrse_layernorm_bwd(const nrse_ln_bwd_params* p, void* stream);
+long long nrse_layernorm_bwd_workspace(const nrse_ln_bwd_params* p);  /* floats for p->part */
 
 /* Final encoder LN fused with the time-mean pooling shim:
- * emb[b, c] = mean_t LN(h[b, t])[c]; emb must be zeroed by the caller. */
+ * emb[b, c] = mean_t LN(h[b, t])[c]; emb must be zeroed by the caller. part: optional f32
+ * workspace of batch * ceil(T / 32) * C floats (the 32-frame chunk sums then add in a fixed
+ * order, deterministic; NULL: f32 atomics). */
 int nrse_ln_mean_fwd(const float* h, const float* gamma, const float* beta, float* emb, float* mean, float* rstd,
-                     int batch, int T, int C, float eps, void* stream);
+                     int batch, int T, int C, float eps, float* part, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Gated relative-position attention, WavLMAttention ([TF]modeling_wavlm.py:147-271) with
@@ -191,18 +201,24 @@ int nrse_bias_ld(int T);
 int nrse_rel_bias_fwd(const float* E, const int* bucket, float* bias, int H, int T, int nb, void* stream);
 /* bias_vec[h, e] = E[bucket[e], h], e in [0, 2T-1) */
 int nrse_rel_bias_vec(const float* E, const int* bucket, float* bias_vec, int H, int T, int nb, void* stream);
-/* dE[bucket[d], h] += diag[h, d] (compute_bias backward). */
-int nrse_rel_bias_bwd(const float* diag, const int* bucket, float* dE, int H, int T, void* stream);
+/* dE[bucket[d], h] += diag[h, d] (compute_bias backward), as a gather in a fixed order: order
+ * [2T-1] lists the offsets d sorted by bucket (increasing d within a bucket), offsets [nb+1] the
+ * start of each bucket's run (nrse_amd.hostside.bucket_runs). */
+int nrse_rel_bias_bwd(const float* diag, const int* order, const int* offsets, float* dE, int H, int T, int nb,
+                      void* stream);
 
 /* gate[b,h,t] = a*(b_*c_h - 1) + 2 with (a, b_) = sigmoid(pair sums of gru_rel_pos_linear(x_h))
  * ([TF]modeling_wavlm.py:164-176). x1 [B*T, Hd] (the LN1 output), W [8, 64], bias [8], c [H]. */
 int nrse_gate_fwd(const void* x1, int x_dtype, const float* W, const float* bvec, const float* c, float* gate,
                   int batch, int T, int H, void* stream);
 /* Gate backward, fused: dx1 (f32 [B*T, Hd]) += the gate-path gradient, and the parameter
- * gradients accumulated (f32 atomics): dW [8, 64] (gru_rel_pos_linear.weight), db [8] (its
+ * gradients accumulated: dW [8, 64] (gru_rel_pos_linear.weight), db [8] (its
  * bias), dc [H] (gru_rel_pos_const). x1, dx1 16-byte aligned. */
 int nrse_gate_bwd(const void* x1, int x_dtype, const float* W, const float* bvec, const float* c, const float* dgate,
-                  float* dx1, float* dW, float* db, float* dc, int batch, int T, int H, void* stream);
+                  float* dx1, float* dW, float* db, float* dc, int batch, int T, int H, float* part, void* stream);
+/* part (optional): f32 workspace of nrse_gate_bwd_workspace(H) floats; the per-workgroup
+ * parameter gradients are then added in a fixed order (deterministic) instead of by atomics */
+long long nrse_gate_bwd_workspace(int H);
 
 typedef struct {
   const void* qkv; int dtype;     /* q/k/v (bf16 or f32) */
@@ -227,6 +243,10 @@ typedef struct {
   int batch, T, H, head_dim;
   float scale; float dropout_p; uint32_t seed;
   const float* bias_vec;               /* [H, 2T-1] (bf16 MFMA path) */
+  float* diag_part;                    /* optional (bf16 MFMA path): f32 workspace of
+                                          H * B * ceil(T/64) * (2T-1) floats; the per-block diag rows
+                                          are then added in a fixed order (deterministic) instead of
+                                          by f32 atomics */
 } nrse_attn_bwd_params;
 
 int nrse_attn_fwd(const nrse_attn_fwd_params* p, void* stream);
@@ -250,9 +270,13 @@ typedef struct {
   const void* dy; int dy_dtype; int dy_mode; int col_k, col_s, col_tout;   /* bwd only */
   float* dw; float* dgamma; float* dbeta;     /* bwd only; dw is [k][C] (tap-major) */
   int batch, T0, C, k, s; float eps;
+  float* part;                    /* bwd, optional: f32 workspace of nrse_conv0_bwd_workspace(p)
+                                     floats; dw / dgamma / dbeta are then added in a fixed order
+                                     (deterministic) instead of by f32 atomics */
 } nrse_conv0_params;
 int nrse_conv0_fwd(const nrse_conv0_params* p, void* stream);
 int nrse_conv0_bwd(const nrse_conv0_params* p, void* stream);
+long long nrse_conv0_bwd_workspace(const nrse_conv0_params* p);
 
 /* weight_norm(dim=2) of the grouped pos-conv ([TF]modeling_wavlm.py:61-77):
  * w[o, i, j] = g[j] * v[o, i, j] / ||v[:, :, j]||.  Writes the two GEMM weight layouts
@@ -280,7 +304,9 @@ int nrse_pad_rows(const void* src, int src_dtype, void* dst, int dst_dtype, int 
 /* SpecAugment + dropout backward on the feature-projection output:
  * dembed[c] += sum over masked rows of dh; out = (masked ? 0 : dh) * dropout_mask(seed, p). */
 int nrse_specaug_bwd(const float* dh, const unsigned char* mask, float* dembed, void* out, int out_dtype, int batch,
-                     int T, int C, float dropout_p, uint32_t seed, void* stream);
+                     int T, int C, float dropout_p, uint32_t seed, float* part, void* stream);
+/* part (optional): f32 workspace of min(B*T, 2048) * C floats: dembed's per-workgroup sums are
+ * then added in a fixed order (deterministic) instead of by f32 atomics */
 /* out[i] = in[i] * dropout_mask(seed, p)[i] (cast); in f32, out f32/bf16 */
 int nrse_dropout_cast(const float* in, void* out, int out_dtype, long long n, float dropout_p, uint32_t seed,
                       void* stream);
@@ -288,15 +314,24 @@ int nrse_dropout_cast(const float* in, void* out, int out_dtype, long long n, fl
  * in one pass (the nn.Dropout backward feeding a Linear: its input gradient and bias gradient,
  * [TF]modeling_wavlm.py:294, 482). C % 8 == 0, 16-byte aligned. */
 int nrse_dropout_cast_colsum(const float* in, void* out, int out_dtype, long long rows, int C, float dropout_p,
-                             uint32_t seed, float* colsum, void* stream);
-/* colsum[c] += sum_r x[r, c] (f32 atomics) */
-int nrse_colsum(const void* x, int dtype, float* colsum, long long rows, int C, void* stream);
+                             uint32_t seed, float* colsum, float* part, void* stream);
+/* colsum[c] += sum_r x[r, c]. part: optional f32 workspace of nrse_colsum_workspace(rows, C) floats
+ * (also for nrse_dropout_cast_colsum): the row-chunk sums are then added in a fixed order
+ * (deterministic) instead of by f32 atomics. */
+int nrse_colsum(const void* x, int dtype, float* colsum, long long rows, int C, float* part, void* stream);
+long long nrse_colsum_workspace(long long rows, int C);
 /* y = x cast (f32 <-> bf16), n elements */
 int nrse_cast(const void* x, int x_dtype, void* y, int y_dtype, long long n, void* stream);
 /* Split-K reduction of a weight gradient (the Linear wgrads of the backward, train_byol.py:65):
  * dst[i] (+)= sum_s slabs[s * n + i], s = 0 .. splits-1, in split order (deterministic); f32;
  * accumulate = 0 overwrites dst. The partial slabs are written by nrse_gemm with c_split = n. */
 int nrse_splitk_reduce(float* dst, const float* slabs, int splits, long long n, int accumulate, void* stream);
+/* Ordered reduction of per-workgroup partial rows (the deterministic form of the gradient
+ * column sums and accumulators): a slab row is [d0: n0 | d1: n1 | d2: n2] (d1, d2 optional, in
+ * order); d_j[b * n_j + c] (+)= sum_{s < S} slab[(b * S + s) * n + off_j + c] in s order, for
+ * b < batch (16-byte vectors when every n_j % 4 == 0 and the pointers are aligned). */
+int nrse_rows_reduce(float* d0, long long n0, float* d1, long long n1, float* d2, long long n2, const float* slab, int S,
+                     int batch, int accumulate, void* stream);
 /* dst[a][c][b] (+)= src[a][b][c]  (conv weight [co][ci][k] <-> implicit-GEMM layout [co][k][ci]) */
 int nrse_swap12(const void* src, int src_dtype, void* dst, int dst_dtype, int d0, int d1, int d2, int accumulate,
                 void* stream);
@@ -331,7 +366,9 @@ int nrse_bn_bwd_global(const float* dy, const float* x, const float* y, const fl
 /* loss[0] = 2 - 2 mean_b clamp(<p_b/|p_b|, z_b/|z_b|>, -1, 1) (+1e-10 offsets, eps 1e-10);
  * dp = dloss/dp (scaled by grad_scale); stats[0..1] = NaN flags before/after normalisation. */
 int nrse_byol_loss(const float* p, const float* z, float* loss, float* dp, float* stats, int rows, int D,
-                   float grad_scale, void* stream);
+                   float grad_scale, float* part, void* stream);
+/* part (optional): f32 workspace of rows * (stats ? 3 : 1) floats; the per-row loss terms (and
+ * NaN flags) are then added in row order (deterministic) instead of by f32 atomics */
 
 /* ------------------------------------------------------------------------------------------
  * Downstream emotion head (BASELINE configs[3]; src/models/emotion.py over the frozen encoder).
@@ -357,7 +394,9 @@ int nrse_ccc_loss(const float* pred, int ld, const float* target, float* loss, f
  * Optimiser tail over the flat f32 parameter / gradient buffers (train_byol.py:67-71,
  * src/models/byol.py:62-73): sum of squares (f64 accumulation), clip + AdamW, target EMA.
  * ------------------------------------------------------------------------------------------ */
-int nrse_sumsq(const float* x, long long n, double* out, void* stream);
+int nrse_sumsq(const float* x, long long n, double* out, double* part, void* stream);
+/* part (optional): f64 workspace of 4096 doubles; the per-workgroup sums are then added in a
+ * fixed order (deterministic) instead of by f64 atomics */
 typedef struct {
   float* p; const float* g; float* m; float* v; void* p_shadow; int shadow_dtype;
   long long n;

@@ -36,12 +36,18 @@ __global__ void rel_bias_vec_kernel(const float* __restrict__ E, const int* __re
     vec[(long long)h * nd + e] = E[bucket[e] * H + h];
 }
 
-__global__ void rel_bias_bwd_kernel(const float* __restrict__ diag, const int* __restrict__ bucket,
-                                    float* __restrict__ dE, int H, int T) {
+// dE[k, h] += sum of diag[h, d] over the offsets d of bucket k, in increasing d: a gather over
+// the bucket's index list (order[offsets[k] .. offsets[k+1]), the d sorted by bucket) instead of a
+// scatter with f32 atomics, so the sum order is fixed
+__global__ void rel_bias_bwd_kernel(const float* __restrict__ diag, const int* __restrict__ order,
+                                    const int* __restrict__ offsets, float* __restrict__ dE, int H, int T, int nb) {
   const int nd = 2 * T - 1;
-  const int d = blockIdx.x * blockDim.x + threadIdx.x;
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
   const int h = blockIdx.y;
-  if (d < nd) atomicAdd(dE + bucket[d] * H + h, diag[(long long)h * nd + d]);
+  if (k >= nb) return;
+  float s = 0.f;
+  for (int i = offsets[k]; i < offsets[k + 1]; ++i) s += diag[(long long)h * nd + order[i]];
+  dE[k * H + h] += s;
 }
 
 // Gate projections. gru_rel_pos_linear is Linear(64 -> 8) shared by all heads, and only the
@@ -140,9 +146,11 @@ __global__ __launch_bounds__(256) void gate_bwd_kernel(const void* __restrict__ 
                                                        const float* __restrict__ bv, const float* __restrict__ c,
                                                        const float* __restrict__ dgate, float* __restrict__ dx1,
                                                        float* __restrict__ dW, float* __restrict__ db,
-                                                       float* __restrict__ dc, int batch, int Tn, int H) {
+                                                       float* __restrict__ dc, int batch, int Tn, int H,
+                                                       float* __restrict__ part) {
   __shared__ float red[4][2][HD];
   __shared__ float reds[4][2];
+  __shared__ float redc[4][8];
   const int lane = threadIdx.x & 63, sub = lane & 7, ig = lane >> 3, w = threadIdx.x >> 6;
   const GateW gw(W, bv, sub);
   const long long total = (long long)batch * Tn * H;
@@ -194,8 +202,13 @@ __global__ __launch_bounds__(256) void gate_bwd_kernel(const void* __restrict__ 
       sdpa += dpa; sdpb += dpb; sdc += dg * a * b;
     }
   }
-  // per-head term: one atomic per 8-lane group
-  if (sub == 0 && sdc != 0.f) atomicAdd(dc + h, sdc);
+  // per-head term: one atomic per 8-lane group (or, with the partial-row workspace, the groups'
+  // sums per head added in group order below)
+  if (part) {
+    if (sub == 0) redc[w][ig] = sdc;
+  } else if (sub == 0 && sdc != 0.f) {
+    atomicAdd(dc + h, sdc);
+  }
   // sum over the 8 groups of the wave (lanes with equal sub hold the same dims)
 #pragma unroll
   for (int o = 8; o < 64; o <<= 1) {
@@ -210,15 +223,32 @@ __global__ __launch_bounds__(256) void gate_bwd_kernel(const void* __restrict__ 
     if (sub == 0) { reds[w][0] = sdpa; reds[w][1] = sdpb; }
   }
   __syncthreads();
+  // partial row [dW 8 x HD | db 8 | dc H] of this workgroup (nrse_rows_reduce adds the rows in
+  // workgroup order), or f32 atomics
+  float* prow = part ? part + (long long)blockIdx.x * (8 * HD + 8 + H) : nullptr;
   if (threadIdx.x < 2 * HD) {
     const int j = threadIdx.x / HD, i = threadIdx.x % HD;
     const float v = red[0][j][i] + red[1][j][i] + red[2][j][i] + red[3][j][i];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) atomicAdd(dW + (4 * j + r) * HD + i, v);
+    for (int r = 0; r < 4; ++r) {
+      if (prow) prow[(4 * j + r) * HD + i] = v;
+      else atomicAdd(dW + (4 * j + r) * HD + i, v);
+    }
   } else if (threadIdx.x < 2 * HD + 8) {
     const int r = threadIdx.x - 2 * HD;
     const int j = r >> 2;
-    atomicAdd(db + r, reds[0][j] + reds[1][j] + reds[2][j] + reds[3][j]);
+    const float v = reds[0][j] + reds[1][j] + reds[2][j] + reds[3][j];
+    if (prow) prow[8 * HD + r] = v;
+    else atomicAdd(db + r, v);
+  } else if (prow && threadIdx.x < 2 * HD + 8 + H) {
+    // head hh: the 8-lane groups of this workgroup with (global wave * 8 + group) % H == hh
+    const int hh = threadIdx.x - 2 * HD - 8;
+    const long long wave0 = (long long)blockIdx.x * (blockDim.x >> 6);
+    float v = 0.f;
+    for (int ww = 0; ww < 4; ++ww)
+      for (int gg = 0; gg < 8; ++gg)
+        if ((int)(((wave0 + ww) * 8 + gg) % H) == hh) v += redc[ww][gg];
+    prow[8 * HD + 8 + hh] = v;
   }
 }
 
@@ -475,11 +505,11 @@ extern "C" int nrse_rel_bias_vec(const float* E, const int* bucket, float* vec, 
   return nrse_check_launch("nrse_rel_bias_vec");
 }
 
-extern "C" int nrse_rel_bias_bwd(const float* diag, const int* bucket, float* dE, int H, int T, void* stream) {
-  NRSE_REQUIRE(diag && bucket && dE && H > 0 && T > 0, "nrse_rel_bias_bwd: bad args");
-  const int nd = 2 * T - 1;
-  hipLaunchKernelGGL(rel_bias_bwd_kernel, dim3((nd + 255) / 256, H), dim3(256), 0, (hipStream_t)stream, diag, bucket,
-                     dE, H, T);
+extern "C" int nrse_rel_bias_bwd(const float* diag, const int* order, const int* offsets, float* dE, int H, int T,
+                                 int nb, void* stream) {
+  NRSE_REQUIRE(diag && order && offsets && dE && H > 0 && T > 0 && nb > 0, "nrse_rel_bias_bwd: bad args");
+  hipLaunchKernelGGL(rel_bias_bwd_kernel, dim3((nb + 63) / 64, H), dim3(64), 0, (hipStream_t)stream, diag, order,
+                     offsets, dE, H, T, nb);
   return nrse_check_launch("nrse_rel_bias_bwd");
 }
 
@@ -497,9 +527,21 @@ extern "C" int nrse_gate_fwd(const void* x1, int x_dtype, const float* W, const 
   return nrse_check_launch("nrse_gate_fwd");
 }
 
+static int gate_bwd_bph() {
+  static const int bph = [] {
+    const char* e = getenv("NRSE_GATE_BWD_BPH");
+    const int v = e ? atoi(e) : GATE_BWD_BLOCKS_PER_HEAD;
+    return v < 1 ? 1 : (v > GATE_BWD_BLOCKS_PER_HEAD * 8 ? GATE_BWD_BLOCKS_PER_HEAD * 8 : v);
+  }();
+  return bph;
+}
+
+// floats of nrse_gate_bwd's partial-row workspace
+extern "C" long long nrse_gate_bwd_workspace(int H) { return (long long)gate_bwd_bph() * H * (8 * HD + 8 + H); }
+
 extern "C" int nrse_gate_bwd(const void* x1, int x_dtype, const float* W, const float* bvec, const float* c,
                              const float* dgate, float* dx1, float* dW, float* db, float* dc, int batch, int T, int H,
-                             void* stream) {
+                             float* part, void* stream) {
   NRSE_REQUIRE(x1 && W && bvec && c && dgate && dx1 && dW && db && dc && batch > 0 && T > 0 && H > 0,
                "nrse_gate_bwd: bad args");
   NRSE_REQUIRE(((uintptr_t)x1 & 15) == 0 && ((uintptr_t)dx1 & 15) == 0, "nrse_gate_bwd: x1/dx1 not 16-byte aligned");
@@ -508,19 +550,17 @@ extern "C" int nrse_gate_bwd(const void* x1, int x_dtype, const float* W, const 
   // a multiple of H workgroups: each 8-lane item group then keeps one head (see the kernel)
   // NRSE_GATE_BWD_BPH (tuning override) is clamped: <= 0 would launch an empty grid, a large value
   // would overflow the kernel's 32-bit item stride
-  static const int bph = [] {
-    const char* e = getenv("NRSE_GATE_BWD_BPH");
-    const int v = e ? atoi(e) : GATE_BWD_BLOCKS_PER_HEAD;
-    return v < 1 ? 1 : (v > GATE_BWD_BLOCKS_PER_HEAD * 8 ? GATE_BWD_BLOCKS_PER_HEAD * 8 : v);
-  }();
-  dim3 grid((unsigned)(bph * H));
+  NRSE_REQUIRE(!part || H <= 256 - 2 * HD - 8, "nrse_gate_bwd: H too large for the partial-row form");
+  dim3 grid((unsigned)(gate_bwd_bph() * H));
   if (x_dtype == NRSE_BF16)
     hipLaunchKernelGGL(gate_bwd_kernel<bf16_t>, grid, dim3(256), 0, st, x1, W, bvec, c, dgate, dx1, dW, db, dc, batch,
-                       T, H);
+                       T, H, part);
   else
     hipLaunchKernelGGL(gate_bwd_kernel<float>, grid, dim3(256), 0, st, x1, W, bvec, c, dgate, dx1, dW, db, dc, batch,
-                       T, H);
-  return nrse_check_launch("nrse_gate_bwd");
+                       T, H, part);
+  const int rc = nrse_check_launch("nrse_gate_bwd");
+  if (rc || !part) return rc;
+  return nrse_rows_reduce(dW, 8 * HD, db, 8, dc, H, part, (int)grid.x, 1, 1, st);
 }
 
 int nrse_attn_fwd_mfma(const nrse_attn_fwd_params* p, hipStream_t st);  // attention_mfma.hip

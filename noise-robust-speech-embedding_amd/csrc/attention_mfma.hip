@@ -693,10 +693,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   __syncthreads();
   if (p.diag) {
     const int nd = 2 * T - 1;
-    for (int e = tid; e < ndiag; e += 256) {
-      const int dd = dbase + e + T - 1;  // index of d = kj - qi in [0, 2T-1)
-      const float v = diag[e];
-      if (dd >= 0 && dd < nd && v != 0.f) atomicAdd(p.diag + (long long)h * nd + dd, v);
+    if (p.diag_part) {
+      // this block's whole row of the [H][B * key tiles][2T-1] partial slab (zeros off its band),
+      // added in (b, key tile) order by nrse_rows_reduce: deterministic
+      float* prow = p.diag_part + (((long long)h * p.batch + b) * ntiles + bp.blk) * nd;
+      for (int dd = tid; dd < nd; dd += 256) {
+        const int e = dd - (dbase + T - 1);
+        prow[dd] = (e >= 0 && e < ndiag) ? diag[e] : 0.f;
+      }
+    } else {
+      for (int e = tid; e < ndiag; e += 256) {
+        const int dd = dbase + e + T - 1;  // index of d = kj - qi in [0, 2T-1)
+        const float v = diag[e];
+        if (dd >= 0 && dd < nd && v != 0.f) atomicAdd(p.diag + (long long)h * nd + dd, v);
+      }
     }
   }
 }
@@ -737,6 +747,10 @@ int nrse_attn_bwd_mfma(const nrse_attn_bwd_params* p, hipStream_t st) {
   // the dQ kernel also produces delta = rowsum(dO * O), which the dK/dV kernel reads
   hipLaunchKernelGGL(attn_bwd_q_kernel, grid, dim3(256), lds_q, st, *p);
   hipLaunchKernelGGL(attn_bwd_kv_kernel, grid, dim3(256), lds_kv, st, *p);
-  return nrse_check_launch("nrse_attn_bwd(mfma)");
+  const int rc = nrse_check_launch("nrse_attn_bwd(mfma)");
+  if (rc || !p->diag || !p->diag_part) return rc;
+  const int ntiles = (p->T + 63) / 64;
+  return nrse_rows_reduce(p->diag, 2LL * p->T - 1, nullptr, 0, nullptr, 0, p->diag_part, p->batch * ntiles, p->H, 1,
+                          st);
 }
 

@@ -100,6 +100,14 @@ NRSE_DEV f32x2 gelu2(f32x2 x) { return splat2(0.5f) * x * (splat2(1.0f) + erf_fa
 NRSE_DEV float gelu_f(float x) { return gelu_fast(x); }
 NRSE_DEV float gelu_grad_f(float x) { return gelu_grad_fast(x); }
 
+// Column sums of the COLSUM epilogue: with p.colsum_part, each workgroup writes its two half-tile
+// partial sums to rows (z * mt + m_tile) * 2 + {0, 1} of the [rows][N] slab (added in order by
+// nrse_rows_reduce in nrse_gemm: deterministic); without it, f32 atomics into p.colsum.
+NRSE_DEV void colsum_out(const nrse_gemm_params& p, int z, int mt, int mtile, int sub, int n, float v) {
+  if (p.colsum_part) p.colsum_part[(((long long)z * mt + mtile) * 2 + sub) * p.N + n] = v;
+  else atomicAdd(p.colsum + n, v);
+}
+
 // Counter-based dropout hash (bijective 32-bit mixer, "lowbias32"), one hash per PAIR of
 // elements, 16 bits each: the mask of flat element i at a dropout site seeded with `seed` is
 //   h = mix32((i >> 1) ^ site_key(seed)), keep = (i odd ? h >> 16 : h & 0xffff) >= thr16,

@@ -323,7 +323,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
       float v = 0.f;
 #pragma unroll
       for (int q = 0; q < RPB; ++q) v += red[q][c];
-      if (j < p.k) atomicAdd(p.dw + (long long)j * C + c, v);  // [k][C]: 256-B atomic wave-instructions
+      if (p.part) p.part[((long long)blockIdx.x * (p.k + 2) + j) * C + c] = v;  // row [dw | dgamma | dbeta]
+      else if (j < p.k) atomicAdd(p.dw + (long long)j * C + c, v);  // [k][C]: 256-B atomic wave-instructions
       else if (j == p.k) atomicAdd(p.dgamma + c, v);
       else atomicAdd(p.dbeta + c, v);
     }
@@ -551,6 +552,14 @@ extern "C" int nrse_conv0_fwd(const nrse_conv0_params* p, void* stream) {
   return nrse_check_launch("nrse_conv0_fwd");
 }
 
+// each block adds (k + 2) * C partial sums at the end (atomics or its partial row)
+static long long conv0_bwd_blocks(const nrse_conv0_params* p) {
+  const long long rows = (long long)p->batch * p->T0;
+  const int rpb = p->C == 512 ? 2 : 4;
+  const long long blocks = (rows + rpb - 1) / rpb;
+  return blocks > 1024 ? 1024 : blocks;
+}
+
 extern "C" int nrse_conv0_bwd(const nrse_conv0_params* p, void* stream) {
   NRSE_REQUIRE(p && p->wav && p->w && p->gamma && p->beta && p->mean && p->rstd && p->dy && p->dw && p->dgamma &&
                p->dbeta, "nrse_conv0_bwd: bad args");
@@ -560,8 +569,7 @@ extern "C" int nrse_conv0_bwd(const nrse_conv0_params* p, void* stream) {
   const long long rows = (long long)p->batch * p->T0;
   const int rpb = p->C == 512 ? 2 : 4;
   const bool bf = p->dy_dtype == NRSE_BF16;
-  long long blocks = (rows + rpb - 1) / rpb;
-  if (blocks > 1024) blocks = 1024;  // each block adds (k + 2) * C partial sums at the end
+  const long long blocks = conv0_bwd_blocks(p);
   hipStream_t st = (hipStream_t)stream;
   switch (p->C) {
     case 256:
@@ -574,7 +582,15 @@ extern "C" int nrse_conv0_bwd(const nrse_conv0_params* p, void* stream) {
       break;
     default: nrse_set_error("nrse_conv0_bwd: C=%d unsupported", p->C); return NRSE_ERR_UNSUPPORTED;
   }
-  return nrse_check_launch("nrse_conv0_bwd");
+  const int rc = nrse_check_launch("nrse_conv0_bwd");
+  if (rc || !p->part) return rc;
+  return nrse_rows_reduce(p->dw, (long long)p->k * p->C, p->dgamma, p->C, p->dbeta, p->C, p->part, (int)blocks, 1, 1,
+                          st);
+}
+
+extern "C" long long nrse_conv0_bwd_workspace(const nrse_conv0_params* p) {
+  if (!p || p->batch <= 0 || p->T0 <= 0) return 0;
+  return conv0_bwd_blocks(p) * (p->k + 2) * (long long)p->C;
 }
 
 extern "C" int nrse_weight_norm_fwd(const float* g, const float* v, void* wf, void* wd, int w_dtype, float* norms,

@@ -27,6 +27,7 @@ int nrse_posconv_wgrad(const nrse_gemm_params* p, hipStream_t st);
 bool nrse_gemm256_ok(const nrse_gemm_params* p);         // gemm256.hip
 long long nrse_gemm256_tiles(const nrse_gemm_params* p);
 int nrse_gemm256(const nrse_gemm_params* p, hipStream_t st);
+int nrse_gemm256_rows(const nrse_gemm_params* p);           // its tile rows for p (256 or 224)
 
 namespace {
 
@@ -329,7 +330,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const nrse_gemm_params p)
     if (flags & NRSE_EPI_COLSUM) {
       csum += __shfl_xor(csum, 16, 64);
       csum += __shfl_xor(csum, 32, 64);
-      if (g == 0 && nok) atomicAdd(p.colsum + n, csum);
+      if (g == 0 && nok) colsum_out(p, z, gridDim.y, blockIdx.y, wm, n, csum);
     }
   }
 }
@@ -399,10 +400,28 @@ extern "C" int nrse_gemm(const nrse_gemm_params* p, void* stream) {
   // generation is pinned (NRSE_GEMM_GEN=1|2|3 benchmarks the generic kernels on it)
   if ((gen == 0 || gen == 4) && nrse_posconv_ok(p)) return nrse_posconv(p, st);
   if ((gen == 0 || gen == 4) && nrse_posconv_wgrad_ok(p)) return nrse_posconv_wgrad(p, st);
-  if (gen != 1 && gen != 2 && nrse_gemm256_ok(p) && (gen == 3 || big))
-    return nrse_gemm256(p, st);
-  if (gen != 1 && nrse_gemm_dma_ok(p)) return nrse_gemm_dma(p, st);
-  return p->a.dtype == NRSE_BF16 ? launch_dt<bf16_t>(p, st) : launch_dt<float>(p, st);
+  const bool part = (p->flags & NRSE_EPI_COLSUM) && p->colsum_part;
+  int rc, mt;
+  if (gen != 1 && gen != 2 && nrse_gemm256_ok(p) && (gen == 3 || big)) {
+    rc = nrse_gemm256(p, st);
+    mt = nrse_cdiv(p->M, nrse_gemm256_rows(p));
+  } else if (gen != 1 && nrse_gemm_dma_ok(p)) {
+    rc = nrse_gemm_dma(p, st);
+    mt = nrse_cdiv(p->M, 128);
+  } else {
+    rc = p->a.dtype == NRSE_BF16 ? launch_dt<bf16_t>(p, st) : launch_dt<float>(p, st);
+    mt = nrse_cdiv(p->M, BM);
+  }
+  if (rc || !part) return rc;
+  // the kernels wrote 2 partial rows per (z, M-tile): add them in order
+  const long long rows = 2LL * mt * p->batch * p->splits;
+  return nrse_rows_reduce(p->colsum, p->N, nullptr, 0, nullptr, 0, p->colsum_part, (int)rows, 1, 1, stream);
+}
+
+// floats of colsum_part any kernel generation may write: 2 rows of N per (z, 128-row M-tile)
+extern "C" long long nrse_gemm_colsum_workspace(const nrse_gemm_params* p) {
+  if (!p || p->M <= 0 || p->N <= 0) return 0;
+  return 2LL * nrse_cdiv(p->M, 128) * p->batch * p->splits * p->N;
 }
 
 extern "C" int nrse_gemm_select(int generation) {

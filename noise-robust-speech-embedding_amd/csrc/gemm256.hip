@@ -10,8 +10,9 @@
 //  - one K-tile (BK = 64) is 4 half-tiles of 16 KiB: A-lo = A rows {0-63,128-191}, A-hi = A rows
 //    {64-127,192-255}, B-lo = B cols {wn*64 + 0..31}, B-hi = B cols {wn*64 + 32..63}. Each wave
 //    computes its 128x64 output as 4 quadrants (64x32, 16 MFMAs) in 4 phases: p0 (A-lo,B-lo),
-//    p1 (A-lo,B-hi), p2 (A-hi,B-hi), p3 (A-hi,B-lo), reading A-lo and B-lo in p0, B-hi in p1,
-//    A-hi in p2 and keeping fragments in registers for their second use.
+//    p1 (A-lo,B-hi), p2 (A-hi,B-hi), p3 (A-hi,B-lo), reading A-lo in p0, B-hi in p1, A-hi in p2
+//    and the NEXT K-tile's B-lo in p3 (8 / 4 / 8 / 4 fragment reads per phase), keeping fragments
+//    in registers for their second use.
 //  - LDS is a ring of 10 half-tile slots (160 KiB). Half-tiles are numbered in first-read order
 //    (seq = 4t + {A-lo, B-lo, B-hi, A-hi}), seq n lives in slot n % 10, and phase P stages
 //    seq P + 8 (K-tile t+2): every DMA has >= 6 phases (~1.3 us at full MFMA rate, more than the
@@ -22,7 +23,8 @@
 //    MFMAs run in (#2P, #2P+1); group 1 is shifted by one. Hand-off rules that follow:
 //      RAW: data read in phase Q is waited for (vmcnt) by every issuing wave before the FIRST
 //           barrier of phase Q-1: vmcnt(12) there leaves the 6 youngest half-tiles (seq
-//           P+3..P+8) in flight and retires seq <= P+2, which covers phase P+1's reads.
+//           P+3..P+8) in flight and retires seq <= P+2, which covers phase P+1's reads; phase 2
+//           waits with vmcnt(10) (retires seq <= 4t+5, the B-lo that phase 3 reads).
 //      WAR: a slot is restaged >= 2 phases after its last read: seq n is staged in phase n-8
 //           into the slot of seq n-10, last read in phase <= n-10.
 //    No wait is vmcnt(0) and the barriers are raw s_barrier (no fence), so DMAs stay in flight
@@ -197,7 +199,7 @@ NRSE_DEV int fast_epi_mode(const nrse_gemm_params& p) {
 template <int FE, int BMT>
 NRSE_DEV void fast_epilogue(const nrse_gemm_params& p, const f32x4 (&acc)[8][4], char* smem, int m0, int n0, int wm,
                             int wn, int lane, int tid, long long zq, long long zr, int split,
-                            const float4 (&bpre)[4]) {
+                            const float4 (&bpre)[4], int z, int mt) {
   constexpr bool BIAS = FE & FE_BIAS, GELU = FE & FE_GELU, GELUB = FE & FE_GELUB, DROP = FE & FE_DROP;
   constexpr bool RESID = FE & FE_RESID, OBF = FE & FE_OBF;
   constexpr int NFI_HI = (BMT / 2 - 64) / 16;
@@ -322,14 +324,17 @@ NRSE_DEV void fast_epilogue(const nrse_gemm_params& p, const f32x4 (&acc)[8][4],
     __syncthreads();
     if (pass == 0) NRSE_STAMP(5);
   }
-  if (colsum && tid < 256 && n0 + tid < p.N) atomicAdd(p.colsum + n0 + tid, colacc[tid] + colacc[256 + tid]);
+  if (colsum && tid < 512 && n0 + (tid & 255) < p.N)
+    colsum_out(p, z, mt, m0 / BMT, tid >> 8, n0 + (tid & 255), colacc[tid]);
 }
 
 // raw workgroup barrier: orders LDS accesses for the compiler, emits no vmcnt wait
 #define NRSE_BAR()                            \
   do {                                        \
     asm volatile("" ::: "memory");            \
+    __builtin_amdgcn_sched_barrier(0);        \
     __builtin_amdgcn_s_barrier();             \
+    __builtin_amdgcn_sched_barrier(0);        \
     asm volatile("" ::: "memory");            \
   } while (0)
 
@@ -465,50 +470,66 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
   // division by the segment's K-tile count stays out of the loop (done per iteration by all 8
   // waves on the CU's one scalar unit, it lengthened each K-tile's first phase by ~200 cycles)
   int u_sg = 2 / tps, u_k = 2 % tps;
-#pragma unroll 1
-  for (int t = 0; t < ntiles; ++t) {
-    const int s0 = base, s1 = wrap(base + 1), s2 = wrap(base + 2), s3 = wrap(base + 3);
-    // phase p stages half-tile j = p of K-tile t+2 (sequence 4t+8+p) into slot (4t+8+p) % 10
-    const TilePos q2 = tile_pos_at(t + 2 < ntiles, u_sg, u_k);
-    if (++u_k == tps) { u_k = 0; ++u_sg; }
-    // phase 0: quadrant (M-half 0, N-half 0) from A-lo, B-lo
-    NRSE_READ_A(s0, 4)
-    NRSE_READ_B(s1, fbl)
-    stage(0, q2, wrap(base + 8));
-    NRSE_WAIT();
-    NRSE_BAR();
-    NRSE_PSTAMP(0);
-    NRSE_QUAD(0, 0, fbl)
-    NRSE_BAR();
-    NRSE_PSTAMP(1);
-    // phase 1: (0, 1) from B-hi
-    NRSE_READ_B(s2, fbh)
-    stage(1, q2, wrap(base + 9));
-    NRSE_WAIT();
-    NRSE_BAR();
-    NRSE_PSTAMP(2);
-    NRSE_QUAD(0, 1, fbh)
-    NRSE_BAR();
-    NRSE_PSTAMP(3);
-    // phase 2: (1, 1) from A-hi
-    NRSE_READ_A(s3, NFI_HI)
-    stage(2, q2, base);  // (4t + 10) % 10
-    NRSE_WAIT();
-    NRSE_BAR();
-    NRSE_PSTAMP(4);
-    NRSE_QUAD(1, 1, fbh)
-    NRSE_BAR();
-    NRSE_PSTAMP(5);
-    // phase 3: (1, 0) from registers
-    stage(3, q2, s1);    // (4t + 11) % 10
-    NRSE_WAIT();
-    NRSE_BAR();
-    NRSE_PSTAMP(6);
-    NRSE_QUAD(1, 0, fbl)
-    NRSE_BAR();
-    NRSE_PSTAMP(7);
-    base = wrap(base + 4);
+  // B-lo of K-tile t is read in phase 3 of K-tile t-1 (into the register set B-hi is done with),
+  // so the reads are 8 / 4 / 8 / 4 fragments over the 4 phases instead of 12 / 4 / 8 / 0: phase 0
+  // was LDS-bound (its reads plus the half-tile DMA into LDS outlasted the other group's
+  // 16-MFMA segment). The two B register sets swap roles every K-tile (loop unrolled by 2).
+  // Phase 2's wait therefore retires one more half-tile (vmcnt(10): B-lo of t+1, seq 4t+5).
+  NRSE_READ_B(1, fbl)
+#define NRSE_KTILE(T, X, Y)                                                                     \
+  {                                                                                             \
+    const int t = (T);                                                                          \
+    const int s0 = base, s1 = wrap(base + 1), s2 = wrap(base + 2), s3 = wrap(base + 3);         \
+    /* phase p stages half-tile j = p of K-tile t+2 (sequence 4t+8+p) into slot (4t+8+p) % 10 */ \
+    const TilePos q2 = tile_pos_at(t + 2 < ntiles, u_sg, u_k);                                  \
+    if (++u_k == tps) { u_k = 0; ++u_sg; }                                                      \
+    /* phase 0: quadrant (M-half 0, N-half 0) from A-lo and B-lo (in X since phase 3 of t-1) */ \
+    NRSE_READ_A(s0, 4)                                                                          \
+    stage(0, q2, wrap(base + 8));                                                               \
+    NRSE_WAIT();                                                                                \
+    NRSE_BAR();                                                                                 \
+    NRSE_PSTAMP(0);                                                                             \
+    NRSE_QUAD(0, 0, X)                                                                          \
+    NRSE_BAR();                                                                                 \
+    NRSE_PSTAMP(1);                                                                             \
+    /* phase 1: (0, 1) from B-hi */                                                             \
+    NRSE_READ_B(s2, Y)                                                                          \
+    stage(1, q2, wrap(base + 9));                                                               \
+    NRSE_WAIT();                                                                                \
+    NRSE_BAR();                                                                                 \
+    NRSE_PSTAMP(2);                                                                             \
+    NRSE_QUAD(0, 1, Y)                                                                          \
+    NRSE_BAR();                                                                                 \
+    NRSE_PSTAMP(3);                                                                             \
+    /* phase 2: (1, 1) from A-hi */                                                             \
+    NRSE_READ_A(s3, NFI_HI)                                                                     \
+    stage(2, q2, base); /* (4t + 10) % 10 */                                                    \
+    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");                                           \
+    NRSE_BAR();                                                                                 \
+    NRSE_PSTAMP(4);                                                                             \
+    NRSE_QUAD(1, 1, Y)                                                                          \
+    NRSE_BAR();                                                                                 \
+    NRSE_PSTAMP(5);                                                                             \
+    /* phase 3: (1, 0) from registers; B-lo of K-tile t+1 (seq 4t+5) into Y */                  \
+    NRSE_READ_B(wrap(base + 5), Y)                                                              \
+    stage(3, q2, s1); /* (4t + 11) % 10 */                                                      \
+    NRSE_WAIT();                                                                                \
+    NRSE_BAR();                                                                                 \
+    NRSE_PSTAMP(6);                                                                             \
+    NRSE_QUAD(1, 0, X)                                                                          \
+    NRSE_BAR();                                                                                 \
+    NRSE_PSTAMP(7);                                                                             \
+    base = wrap(base + 4);                                                                      \
   }
+#pragma unroll 1
+  for (int kt = 0; kt < ntiles; ++kt) {
+    NRSE_KTILE(kt, fbl, fbh)
+#pragma unroll
+    for (int fj = 0; fj < 2; ++fj)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) fbl[fj][s] = fbh[fj][s];
+  }
+#undef NRSE_KTILE
   if (wm == 0) __builtin_amdgcn_s_barrier();
   NRSE_STAMP(2);
 #undef NRSE_READ_A
@@ -529,7 +550,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
     // (forward kernels: A and B k-contiguous; dgrad: B row-contiguous)
 #define NRSE_FE(MODE)                                                                            \
   case MODE:                                                                                     \
-    fast_epilogue<MODE, BMT>(p, acc, smem, m0, n0, wm, wn, lane, tid, zq, zr, split, bpre);          \
+    fast_epilogue<MODE, BMT>(p, acc, smem, m0, n0, wm, wn, lane, tid, zq, zr, split, bpre, z, mt);   \
     NRSE_STAMP(7);                                                                               \
     return;
     if constexpr (AKC && BKC) {
@@ -614,7 +635,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
     if (pass == 0) NRSE_STAMP(5);
     if (pass == 1) NRSE_STAMP(6);
   }
-  if (colsum && n0 + ccol < p.N) atomicAdd(p.colsum + n0 + ccol, csum);
+  if (colsum && n0 + ccol < p.N) colsum_out(p, z, mt, m0 / BMT, chalf, n0 + ccol, csum);
 #if NRSE_G3_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
@@ -665,6 +686,8 @@ bool nrse_gemm256_ok(const nrse_gemm_params* p) {
          p->a.seg_stride >= 0 && p->b.seg_stride >= 0 && dma_layout_ok(p, 256) &&
          nrse_gemm256_tiles(p) < (1LL << 31);
 }
+
+int nrse_gemm256_rows(const nrse_gemm_params* p) { return bm_choice(p); }
 
 int nrse_gemm256(const nrse_gemm_params* p, hipStream_t st) {
   if (p->a.kcontig && p->b.kcontig) return launch<true, true>(p, st);

@@ -208,7 +208,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_dma_kernel(const nrse_gemm_param
     if (n0 + col < p.N) {
       float s = 0.f;
       for (int r = half * 64; r < half * 64 + 64; ++r) s += ct[r * CT_LD + col];
-      atomicAdd(p.colsum + n0 + col, s);
+      colsum_out(p, z, mt, m0 / BM, half, n0 + col, s);
     }
   }
 }

@@ -144,7 +144,8 @@ __global__ void bn_bwd_global_kernel(const float* __restrict__ dy, const float* 
 // one wave per row
 __global__ __launch_bounds__(256) void byol_loss_kernel(const float* __restrict__ p, const float* __restrict__ z,
                                                         float* __restrict__ loss, float* __restrict__ dp,
-                                                        float* __restrict__ stats, int rows, int D, float gscale) {
+                                                        float* __restrict__ stats, int rows, int D, float gscale,
+                                                        float* __restrict__ part) {
   const int lane = threadIdx.x & 63;
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= rows) return;
@@ -166,10 +167,18 @@ __global__ __launch_bounds__(256) void byol_loss_kernel(const float* __restrict_
   nan0 = __any(nan0);
   const int nan1 = isnan(s);
   if (lane == 0) {
-    atomicAdd(loss, -2.f * sc / rows + (r == 0 ? 2.f : 0.f));
-    if (stats) {
-      if (nan0) atomicAdd(stats + 0, 1.f);
-      if (nan1) atomicAdd(stats + 1, 1.f);
+    const float lr = -2.f * sc / rows + (r == 0 ? 2.f : 0.f);
+    if (part) {
+      // row r of the [rows][1 (+2)] partial slab: loss term (and NaN flags), added in row order
+      float* pr_ = part + (long long)r * (stats ? 3 : 1);
+      pr_[0] = lr;
+      if (stats) { pr_[1] = nan0 ? 1.f : 0.f; pr_[2] = nan1 ? 1.f : 0.f; }
+    } else {
+      atomicAdd(loss, lr);
+      if (stats) {
+        if (nan0) atomicAdd(stats + 0, 1.f);
+        if (nan1) atomicAdd(stats + 1, 1.f);
+      }
     }
   }
   if (!dp) return;
@@ -240,9 +249,11 @@ extern "C" int nrse_bn_bwd_global(const float* dy, const float* x, const float* 
 }
 
 extern "C" int nrse_byol_loss(const float* p, const float* z, float* loss, float* dp, float* stats, int rows, int D,
-                              float gscale, void* stream) {
+                              float gscale, float* part, void* stream) {
   NRSE_REQUIRE(p && z && loss && rows > 0 && D > 0, "nrse_byol_loss: bad args");
   hipLaunchKernelGGL(byol_loss_kernel, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream, p, z, loss, dp, stats,
-                     rows, D, gscale);
-  return nrse_check_launch("nrse_byol_loss");
+                     rows, D, gscale, part);
+  const int rc = nrse_check_launch("nrse_byol_loss");
+  if (rc || !part) return rc;
+  return nrse_rows_reduce(loss, 1, stats, stats ? 2 : 0, nullptr, 0, part, rows, 1, 1, stream);
 }

@@ -62,7 +62,7 @@ __global__ void pad_rows_kernel(const void* __restrict__ src, int sdt, void* __r
 // one block per row chunk; thread per column
 __global__ void specaug_bwd_kernel(const float* __restrict__ dh, const unsigned char* __restrict__ mask,
                                    float* __restrict__ dembed, void* __restrict__ out, int odt, int batch, int T, int C,
-                                   float p, uint32_t seed) {
+                                   float p, uint32_t seed, float* __restrict__ part) {
   const long long rows = (long long)batch * T;
   const uint32_t key = site_key(seed);
   const uint32_t thr = dropout_threshold(p);
@@ -82,7 +82,10 @@ __global__ void specaug_bwd_kernel(const float* __restrict__ dh, const unsigned 
       }
       store_from_f(out, odt, i, o);
     }
-    if (mask && dembed && acc != 0.f) atomicAdd(dembed + c, acc);
+    if (mask && dembed) {
+      if (part) part[(long long)blockIdx.x * C + c] = acc;  // added in block order (nrse_rows_reduce)
+      else if (acc != 0.f) atomicAdd(dembed + c, acc);
+    }
   }
 }
 
@@ -121,7 +124,7 @@ __global__ void dropout_cast_kernel(const float* __restrict__ in, void* __restri
 // column i: the full memory-side atomic rate, MI355X_MICROARCH.md "Global float atomics").
 template <typename T>
 __global__ __launch_bounds__(256) void colsum8_kernel(const void* __restrict__ x, float* __restrict__ out,
-                                                      long long rows, int C, int chunk) {
+                                                      long long rows, int C, int chunk, float* __restrict__ pr) {
   __shared__ float part[4][512];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int cb0 = blockIdx.x * 512;
@@ -155,7 +158,8 @@ __global__ __launch_bounds__(256) void colsum8_kernel(const void* __restrict__ x
     const int col = threadIdx.x + 256 * h;
     if (cb0 + col < C) {
       const float s = part[0][col] + part[1][col] + part[2][col] + part[3][col];
-      atomicAdd(out + cb0 + col, s);
+      if (pr) pr[(long long)blockIdx.y * C + cb0 + col] = s;  // partial row of this row chunk
+      else atomicAdd(out + cb0 + col, s);
     }
   }
 }
@@ -166,7 +170,8 @@ __global__ __launch_bounds__(256) void colsum8_kernel(const void* __restrict__ x
 template <typename TO>
 __global__ __launch_bounds__(256) void dropout_cast_colsum_kernel(const float* __restrict__ in, TO* __restrict__ out,
                                                                   float* __restrict__ colsum, long long rows, int C,
-                                                                  int chunk, float p, uint32_t seed) {
+                                                                  int chunk, float p, uint32_t seed,
+                                                                  float* __restrict__ pr) {
   __shared__ float part[4][512];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int cb0 = blockIdx.x * 512;
@@ -208,7 +213,11 @@ __global__ __launch_bounds__(256) void dropout_cast_colsum_kernel(const float* _
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int col = threadIdx.x + 256 * h;
-    if (cb0 + col < C) atomicAdd(colsum + cb0 + col, part[0][col] + part[1][col] + part[2][col] + part[3][col]);
+    if (cb0 + col < C) {
+      const float s = part[0][col] + part[1][col] + part[2][col] + part[3][col];
+      if (pr) pr[(long long)blockIdx.y * C + cb0 + col] = s;
+      else atomicAdd(colsum + cb0 + col, s);
+    }
   }
 }
 
@@ -221,14 +230,15 @@ long long sweep_chunk(long long rows, int C) {
 
 // colsum, scalar form: grid (ceil(C/256), row chunks)
 __global__ void colsum_kernel(const void* __restrict__ x, int dt, float* __restrict__ out, long long rows, int C,
-                              int chunk) {
+                              int chunk, float* __restrict__ pr) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   const long long r0 = (long long)blockIdx.y * chunk;
   const long long r1 = min(rows, r0 + chunk);
   float a = 0.f;
   for (long long r = r0; r < r1; ++r) a += load_as_f(x, dt, r * C + c);
-  atomicAdd(out + c, a);
+  if (pr) pr[(long long)blockIdx.y * C + c] = a;
+  else atomicAdd(out + c, a);
 }
 
 __global__ void cast_kernel(const void* __restrict__ x, int xdt, void* __restrict__ y, int ydt, long long n) {
@@ -306,13 +316,16 @@ extern "C" int nrse_pad_rows(const void* src, int sdt, void* dst, int ddt, int b
 }
 
 extern "C" int nrse_specaug_bwd(const float* dh, const unsigned char* mask, float* dembed, void* out, int odt,
-                                int batch, int T, int C, float p, uint32_t seed, void* stream) {
+                                int batch, int T, int C, float p, uint32_t seed, float* part, void* stream) {
   NRSE_REQUIRE(dh && out && batch > 0 && T > 0 && C > 0, "nrse_specaug_bwd: bad args");
   const long long rows = (long long)batch * T;
-  int blocks = (int)(rows < 2048 ? rows : 2048);
+  const int blocks = (int)(rows < 2048 ? rows : 2048);
+  if (!mask || !dembed) part = nullptr;
   hipLaunchKernelGGL(specaug_bwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, dh, mask, dembed, out, odt,
-                     batch, T, C, p, seed);
-  return nrse_check_launch("nrse_specaug_bwd");
+                     batch, T, C, p, seed, part);
+  const int rc = nrse_check_launch("nrse_specaug_bwd");
+  if (rc || !part) return rc;
+  return nrse_rows_reduce(dembed, C, nullptr, 0, nullptr, 0, part, blocks, 1, 1, stream);
 }
 
 extern "C" int nrse_dropout_cast(const float* in, void* out, int odt, long long n, float p, uint32_t seed,
@@ -324,43 +337,67 @@ extern "C" int nrse_dropout_cast(const float* in, void* out, int odt, long long 
   return nrse_check_launch("nrse_dropout_cast");
 }
 
+// row chunks of the column-sum sweeps (vector form: C % 8 == 0 and x 16-byte aligned)
+static long long colsum_chunks(long long rows, int C, bool vec, long long* chunk_out) {
+  long long chunk;
+  if (vec) {
+    chunk = sweep_chunk(rows, C);
+  } else {
+    chunk = 64;
+    while ((rows + chunk - 1) / chunk > 4096) chunk *= 2;
+  }
+  *chunk_out = chunk;
+  return (rows + chunk - 1) / chunk;
+}
+
+// floats of the partial-row workspace of nrse_colsum / nrse_dropout_cast_colsum
+extern "C" long long nrse_colsum_workspace(long long rows, int C) {
+  if (rows <= 0 || C <= 0) return 0;
+  long long c0, c1;
+  const long long a = colsum_chunks(rows, C, true, &c0), b = colsum_chunks(rows, C, false, &c1);
+  return (a > b ? a : b) * C;
+}
+
 extern "C" int nrse_dropout_cast_colsum(const float* in, void* out, int out_dtype, long long rows, int C, float p,
-                                        uint32_t seed, float* colsum, void* stream) {
+                                        uint32_t seed, float* colsum, float* part, void* stream) {
   NRSE_REQUIRE(in && out && colsum && rows > 0 && C > 0 && C % 8 == 0, "nrse_dropout_cast_colsum: bad args");
   NRSE_REQUIRE(((uintptr_t)in & 15) == 0 && ((uintptr_t)out & 15) == 0, "nrse_dropout_cast_colsum: unaligned");
   const int cb = (C + 511) / 512;
-  const long long chunk = sweep_chunk(rows, C);
-  const dim3 grid(cb, (unsigned)((rows + chunk - 1) / chunk));
+  long long chunk;
+  const long long nchunks = colsum_chunks(rows, C, true, &chunk);
+  const dim3 grid(cb, (unsigned)nchunks);
   if (out_dtype == NRSE_BF16)
     hipLaunchKernelGGL(dropout_cast_colsum_kernel<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, in, (bf16_t*)out,
-                       colsum, rows, C, (int)chunk, p, seed);
+                       colsum, rows, C, (int)chunk, p, seed, part);
   else
     hipLaunchKernelGGL(dropout_cast_colsum_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, in, (float*)out,
-                       colsum, rows, C, (int)chunk, p, seed);
-  return nrse_check_launch("nrse_dropout_cast_colsum");
+                       colsum, rows, C, (int)chunk, p, seed, part);
+  const int rc = nrse_check_launch("nrse_dropout_cast_colsum");
+  if (rc || !part) return rc;
+  return nrse_rows_reduce(colsum, C, nullptr, 0, nullptr, 0, part, (int)nchunks, 1, 1, stream);
 }
 
-extern "C" int nrse_colsum(const void* x, int dt, float* colsum, long long rows, int C, void* stream) {
+extern "C" int nrse_colsum(const void* x, int dt, float* colsum, long long rows, int C, float* part, void* stream) {
   NRSE_REQUIRE(x && colsum && rows > 0 && C > 0, "nrse_colsum: bad args");
-  if (C % 8 == 0 && ((uintptr_t)x & 15) == 0) {
+  const bool vec = C % 8 == 0 && ((uintptr_t)x & 15) == 0;
+  long long chunk;
+  const long long nchunks = colsum_chunks(rows, C, vec, &chunk);
+  if (vec) {
     // ~1024 blocks; each row lane reads >= 4 rows
     const int cb = (C + 511) / 512;
-    const long long chunk = sweep_chunk(rows, C);
-    const long long nchunks = (rows + chunk - 1) / chunk;
     if (dt == NRSE_BF16)
       hipLaunchKernelGGL(colsum8_kernel<bf16_t>, dim3(cb, (unsigned)nchunks), dim3(256), 0, (hipStream_t)stream, x,
-                         colsum, rows, C, (int)chunk);
+                         colsum, rows, C, (int)chunk, part);
     else
       hipLaunchKernelGGL(colsum8_kernel<float>, dim3(cb, (unsigned)nchunks), dim3(256), 0, (hipStream_t)stream, x,
-                         colsum, rows, C, (int)chunk);
-    return nrse_check_launch("nrse_colsum");
+                         colsum, rows, C, (int)chunk, part);
+  } else {
+    hipLaunchKernelGGL(colsum_kernel, dim3((C + 255) / 256, (unsigned)nchunks), dim3(256), 0, (hipStream_t)stream, x,
+                       dt, colsum, rows, C, (int)chunk, part);
   }
-  int chunk = 64;
-  long long nchunks = (rows + chunk - 1) / chunk;
-  while (nchunks > 4096) { chunk *= 2; nchunks = (rows + chunk - 1) / chunk; }
-  hipLaunchKernelGGL(colsum_kernel, dim3((C + 255) / 256, (unsigned)nchunks), dim3(256), 0, (hipStream_t)stream, x, dt,
-                     colsum, rows, C, chunk);
-  return nrse_check_launch("nrse_colsum");
+  const int rc = nrse_check_launch("nrse_colsum");
+  if (rc || !part) return rc;
+  return nrse_rows_reduce(colsum, C, nullptr, 0, nullptr, 0, part, (int)nchunks, 1, 1, stream);
 }
 
 extern "C" int nrse_cast(const void* x, int xdt, void* y, int ydt, long long n, void* stream) {
@@ -457,4 +494,108 @@ extern "C" int nrse_gelu_bwd_pad(const float* dy, const void* pre, int pdt, void
   hipLaunchKernelGGL(gelu_bwd_pad_kernel, dim3(blocks_for(total)), dim3(256), 0, (hipStream_t)stream, dy, pre, pdt,
                      out, odt, batch, T, C, pf, pb);
   return nrse_check_launch("nrse_gelu_bwd_pad");
+}
+
+// ------------------------------------------------------------------ ordered partial-row reduction
+// The deterministic replacement of the per-workgroup f32 atomics of the gradient reductions
+// (LayerNorm dgamma / dbeta, bias column sums, conv / gate / rel-pos parameter gradients, loss
+// and norm accumulators): each producing workgroup writes its partial row to slab[s][0..n) and
+// this kernel adds the rows in a fixed order into up to three destination vectors,
+//   row = [d0: n0 | d1: n1 | d2: n2],   d_j[c] (+)= sum_s slab[s][off_j + c],
+// so the result is the same on every run whatever the workgroups' completion order. 1024 threads
+// per 256 columns: thread (r, q) sums rows r, r + 16, ... of columns 4q..4q+3 (16 B loads, 4
+// independent loads in flight), then the 16 row-group sums are added in order r = 0..15.
+// Row groups of `batch` (slab [batch][S][n], dst_j + b * n_j): per-utterance sums.
+struct RowsDst { float* d[3]; long long n[3]; };
+
+__global__ __launch_bounds__(1024) void rows_reduce_kernel(RowsDst dst, const float* __restrict__ slab, int S,
+                                                           long long n, int acc) {
+  __shared__ float4 red[16][64];
+  const int q = threadIdx.x & 63, r = threadIdx.x >> 6;
+  const long long col = (long long)blockIdx.x * 256 + 4 * q;
+  const float* sl = slab + (long long)blockIdx.y * S * n;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (col < n) {
+    int k = r;
+    for (; k + 48 < S; k += 64) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(sl + (long long)(k + 16 * u) * n + col);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w; }
+    }
+    for (; k < S; k += 16) {
+      const float4 v = *reinterpret_cast<const float4*>(sl + (long long)k * n + col);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+  }
+  red[r][q] = s;
+  __syncthreads();
+  if (r == 0 && col < n) {
+    float4 t = red[0][q];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) { t.x += red[i][q].x; t.y += red[i][q].y; t.z += red[i][q].z; t.w += red[i][q].w; }
+    int j = 0;
+    long long c = col;
+    while (j < 2 && c >= dst.n[j]) { c -= dst.n[j]; ++j; }
+    float* d = dst.d[j] + (long long)blockIdx.y * dst.n[j] + c;
+    if (acc) {
+      const float4 o = *reinterpret_cast<const float4*>(d);
+      t.x += o.x; t.y += o.y; t.z += o.z; t.w += o.w;
+    }
+    *reinterpret_cast<float4*>(d) = t;
+  }
+}
+
+// the same with one column per thread (lengths that are not multiples of 4, unaligned vectors)
+__global__ __launch_bounds__(1024) void rows_reduce1_kernel(RowsDst dst, const float* __restrict__ slab, int S,
+                                                            long long n, int acc) {
+  __shared__ float red[16][64];
+  const int q = threadIdx.x & 63, r = threadIdx.x >> 6;
+  const long long col = (long long)blockIdx.x * 64 + q;
+  const float* sl = slab + (long long)blockIdx.y * S * n;
+  float s = 0.f;
+  if (col < n) {
+    int k = r;
+    for (; k + 48 < S; k += 64) {
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = sl[(long long)(k + 16 * u) * n + col];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s += v[u];
+    }
+    for (; k < S; k += 16) s += sl[(long long)k * n + col];
+  }
+  red[r][q] = s;
+  __syncthreads();
+  if (r == 0 && col < n) {
+    float t = red[0][q];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) t += red[i][q];
+    int j = 0;
+    long long c = col;
+    while (j < 2 && c >= dst.n[j]) { c -= dst.n[j]; ++j; }
+    float* d = dst.d[j] + (long long)blockIdx.y * dst.n[j] + c;
+    *d = acc ? *d + t : t;
+  }
+}
+
+extern "C" int nrse_rows_reduce(float* d0, long long n0, float* d1, long long n1, float* d2, long long n2,
+                                const float* slab, int S, int batch, int accumulate, void* stream) {
+  NRSE_REQUIRE(d0 && n0 > 0 && slab && S >= 1 && batch >= 1, "nrse_rows_reduce: bad args");
+  NRSE_REQUIRE((!d1 || n1 > 0) && (!d2 || (d1 && n2 > 0)), "nrse_rows_reduce: destinations d0[, d1[, d2]] in order");
+  auto al16 = [](const void* x) { return ((uintptr_t)x & 15) == 0; };
+  RowsDst dst;
+  dst.d[0] = d0; dst.d[1] = d1; dst.d[2] = d2;
+  dst.n[0] = n0; dst.n[1] = d1 ? n1 : 0; dst.n[2] = d2 ? n2 : 0;
+  const long long n = dst.n[0] + dst.n[1] + dst.n[2];
+  const bool vec = n0 % 4 == 0 && dst.n[1] % 4 == 0 && dst.n[2] % 4 == 0 && al16(d0) && (!d1 || al16(d1)) &&
+                   (!d2 || al16(d2)) && al16(slab);
+  if (vec)
+    hipLaunchKernelGGL(rows_reduce_kernel, dim3((unsigned)((n + 255) / 256), (unsigned)batch), dim3(1024), 0,
+                       (hipStream_t)stream, dst, slab, S, n, accumulate);
+  else
+    hipLaunchKernelGGL(rows_reduce1_kernel, dim3((unsigned)((n + 63) / 64), (unsigned)batch), dim3(1024), 0,
+                       (hipStream_t)stream, dst, slab, S, n, accumulate);
+  return nrse_check_launch("nrse_rows_reduce");
 }

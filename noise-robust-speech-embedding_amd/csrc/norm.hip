@@ -476,21 +476,29 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const nrse_ln_bwd_params p)
     compute(bb, rb);
   }
 
-  auto reduce = [&](auto& acc, float* dst) {
+  // the workgroup's column sums: into its row of the partial slab (p.part, added in workgroup
+  // order by nrse_rows_reduce: deterministic), or f32 atomics into dst (no workspace)
+  const int nd = (p.dgamma ? 2 : 0) + ((RES && fuse && p.dv_colsum) ? 1 : 0);
+  auto reduce = [&](auto& acc, float* dst, int j) {
 #pragma unroll
     for (int k = 0; k < NK; ++k)
 #pragma unroll
       for (int e = 0; e < CH; ++e) red[w][(k * 64 + lane) * CH + e] = acc[k][e];
     __syncthreads();
-    for (int c = threadIdx.x; c < C; c += 256) atomicAdd(dst + c, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
+    float* prow = p.part ? p.part + ((long long)blockIdx.x * nd + j) * C : nullptr;
+    for (int c = threadIdx.x; c < C; c += 256) {
+      const float v = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+      if (prow) prow[c] = v;
+      else atomicAdd(dst + c, v);
+    }
     __syncthreads();
   };
   if (p.dgamma) {
-    reduce(dg, p.dgamma);
-    reduce(db, p.dbeta);
+    reduce(dg, p.dgamma, 0);
+    reduce(db, p.dbeta, 1);
   }
   if constexpr (RES) {
-    if (fuse && p.dv_colsum) reduce(dc, p.dv_colsum);
+    if (fuse && p.dv_colsum) reduce(dc, p.dv_colsum, p.dgamma ? 2 : 0);
   }
 }
 
@@ -499,7 +507,7 @@ template <int NK>
 __global__ __launch_bounds__(256) void ln_mean_kernel(const float* __restrict__ h, const float* __restrict__ gamma,
                                                       const float* __restrict__ beta, float* __restrict__ emb,
                                                       float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                      int T, int C, float eps, int rpb) {
+                                                      int T, int C, float eps, int rpb, float* __restrict__ part) {
   __shared__ float red[4][NK * 64 * CH];
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
@@ -542,8 +550,14 @@ __global__ __launch_bounds__(256) void ln_mean_kernel(const float* __restrict__ 
     for (int e = 0; e < CH; ++e) red[w][(k * 64 + lane) * CH + e] = acc[k][e];
   __syncthreads();
   const float inv = 1.0f / T;
-  for (int c = threadIdx.x; c < C; c += 256)
-    atomicAdd(emb + (long long)b * C + c, (red[0][c] + red[1][c] + red[2][c] + red[3][c]) * inv);
+  // partial row of this time chunk ([batch][chunk][C], added in chunk order by nrse_rows_reduce)
+  // or f32 atomics (no workspace)
+  float* prow = part ? part + ((long long)b * gridDim.x + blockIdx.x) * C : nullptr;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const float v = (red[0][c] + red[1][c] + red[2][c] + red[3][c]) * inv;
+    if (prow) prow[c] = v;
+    else atomicAdd(emb + (long long)b * C + c, v);
+  }
 }
 
 #define NRSE_DISPATCH_NK(KERNEL, C, GRID, ST, ARG)                                  \
@@ -576,6 +590,23 @@ extern "C" int nrse_layernorm_fwd(const nrse_ln_fwd_params* p, void* stream) {
   return nrse_check_launch("nrse_layernorm_fwd");
 }
 
+// grid-stride: 2 blocks per CU (8 waves, each with two rows of loads in flight) when the
+// column sums are accumulated, so the per-block partial rows stay ~3 * C * 512
+static long long ln_bwd_blocks(const nrse_ln_bwd_params* p) {
+  long long blocks = (p->rows + 3) / 4;
+  long long cap = 8192;
+  if (p->dgamma || p->dv_colsum) {
+    // >= 2 blocks per CU; long row sweeps (the conv layers' 4e5 rows) get up to 8 per CU
+    cap = p->rows / 192;
+    cap = cap < 512 ? 512 : (cap > 2048 ? 2048 : cap);
+  }
+  static const long long cap_env = getenv("NRSE_LN_BWD_CAP") ? atoll(getenv("NRSE_LN_BWD_CAP")) : 0;
+  if (cap_env > 0) cap = cap_env;  // tuning experiments (tools/bench_ln.py)
+  return blocks > cap ? cap : blocks;
+}
+// column-sum vectors per workgroup: dgamma, dbeta, the fused dropout consumer's colsum
+static int ln_bwd_nd(const nrse_ln_bwd_params* p) { return (p->dgamma ? 2 : 0) + ((p->dv && p->dv_colsum) ? 1 : 0); }
+
 extern "C" int nrse_layernorm_bwd(const nrse_ln_bwd_params* p, void* stream) {
   NRSE_REQUIRE(p && p->dy && p->x && p->gamma && p->mean && p->rstd && p->dx && p->rows > 0,
                "nrse_layernorm_bwd: bad args");
@@ -588,18 +619,9 @@ extern "C" int nrse_layernorm_bwd(const nrse_ln_bwd_params* p, void* stream) {
   if (p->dy_mode == NRSE_DY_BCAST) NRSE_REQUIRE(p->bcast_t > 0, "nrse_layernorm_bwd: bad bcast_t");
   if (!c_ok(p->C)) { nrse_set_error("nrse_layernorm_bwd: C=%d not in {256,512,1024}", p->C); return NRSE_ERR_UNSUPPORTED; }
   NRSE_REQUIRE(!p->dv || (p->dv_dtype == NRSE_BF16 || p->dv_dtype == NRSE_F32), "nrse_layernorm_bwd: bad dv dtype");
-  // grid-stride: 2 blocks per CU (8 waves, each with two rows of loads in flight) when the
-  // column sums are accumulated, so the per-block atomics stay ~3 * C * 512
-  long long blocks = (p->rows + 3) / 4;
-  long long cap = 8192;
-  if (p->dgamma || p->dv_colsum) {
-    // >= 2 blocks per CU; long row sweeps (the conv layers' 4e5 rows) get up to 8 per CU
-    cap = p->rows / 192;
-    cap = cap < 512 ? 512 : (cap > 2048 ? 2048 : cap);
-  }
-  static const long long cap_env = getenv("NRSE_LN_BWD_CAP") ? atoll(getenv("NRSE_LN_BWD_CAP")) : 0;
-  if (cap_env > 0) cap = cap_env;  // tuning experiments (tools/bench_ln.py)
-  if (blocks > cap) blocks = cap;
+  const long long blocks = ln_bwd_blocks(p);
+  const int nd = ln_bwd_nd(p);
+  NRSE_REQUIRE(!p->part || nd > 0, "nrse_layernorm_bwd: workspace given without column sums");
   const dim3 grid((unsigned)blocks);
   hipStream_t st = (hipStream_t)stream;
   const bool res = p->resid || p->dv;
@@ -624,20 +646,34 @@ extern "C" int nrse_layernorm_bwd(const nrse_ln_bwd_params* p, void* stream) {
     default: NRSE_LN_BWD_NK(4) break;
   }
 #undef NRSE_LN_BWD_NK
-  return nrse_check_launch("nrse_layernorm_bwd");
+  const int rc = nrse_check_launch("nrse_layernorm_bwd");
+  if (rc || !p->part) return rc;
+  float* d[3] = {nullptr, nullptr, nullptr};
+  int j = 0;
+  if (p->dgamma) { d[j++] = p->dgamma; d[j++] = p->dbeta; }
+  if (j < nd) d[j++] = p->dv_colsum;
+  const long long C = p->C;
+  return nrse_rows_reduce(d[0], C, d[1], d[1] ? C : 0, d[2], d[2] ? C : 0, p->part, (int)blocks, 1, 1, stream);
+}
+
+extern "C" long long nrse_layernorm_bwd_workspace(const nrse_ln_bwd_params* p) {
+  if (!p || p->rows <= 0) return 0;
+  return ln_bwd_blocks(p) * ln_bwd_nd(p) * (long long)p->C;
 }
 
 extern "C" int nrse_ln_mean_fwd(const float* h, const float* gamma, const float* beta, float* emb, float* mean,
-                                float* rstd, int batch, int T, int C, float eps, void* stream) {
+                                float* rstd, int batch, int T, int C, float eps, float* part, void* stream) {
   NRSE_REQUIRE(h && gamma && beta && emb && mean && rstd && batch > 0 && T > 0, "nrse_ln_mean_fwd: bad args");
   if (!c_ok(C)) { nrse_set_error("nrse_ln_mean_fwd: C=%d unsupported", C); return NRSE_ERR_UNSUPPORTED; }
   const int rpb = 32;
   dim3 grid((T + rpb - 1) / rpb, batch);
   hipStream_t st = (hipStream_t)stream;
   switch (C / 256) {
-    case 1: hipLaunchKernelGGL(ln_mean_kernel<1>, grid, dim3(256), 0, st, h, gamma, beta, emb, mean, rstd, T, C, eps, rpb); break;
-    case 2: hipLaunchKernelGGL(ln_mean_kernel<2>, grid, dim3(256), 0, st, h, gamma, beta, emb, mean, rstd, T, C, eps, rpb); break;
-    default: hipLaunchKernelGGL(ln_mean_kernel<4>, grid, dim3(256), 0, st, h, gamma, beta, emb, mean, rstd, T, C, eps, rpb); break;
+    case 1: hipLaunchKernelGGL(ln_mean_kernel<1>, grid, dim3(256), 0, st, h, gamma, beta, emb, mean, rstd, T, C, eps, rpb, part); break;
+    case 2: hipLaunchKernelGGL(ln_mean_kernel<2>, grid, dim3(256), 0, st, h, gamma, beta, emb, mean, rstd, T, C, eps, rpb, part); break;
+    default: hipLaunchKernelGGL(ln_mean_kernel<4>, grid, dim3(256), 0, st, h, gamma, beta, emb, mean, rstd, T, C, eps, rpb, part); break;
   }
-  return nrse_check_launch("nrse_ln_mean_fwd");
+  const int rc = nrse_check_launch("nrse_ln_mean_fwd");
+  if (rc || !part) return rc;
+  return nrse_rows_reduce(emb, C, nullptr, 0, nullptr, 0, part, (int)grid.x, batch, 1, stream);
 }

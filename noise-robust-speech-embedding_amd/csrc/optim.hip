@@ -9,7 +9,8 @@
 
 namespace {
 
-__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x, long long n, double* __restrict__ out) {
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x, long long n, double* __restrict__ out,
+                                                    double* __restrict__ part) {
   __shared__ double red[4];
   double a = 0.0;
   const long long n4 = n / 4;
@@ -22,7 +23,23 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x,
   a = wave_sum_d(a);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = a;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(out, red[0] + red[1] + red[2] + red[3]);
+  if (threadIdx.x == 0) {
+    const double s = red[0] + red[1] + red[2] + red[3];
+    if (part) part[blockIdx.x] = s;  // added in block order by sum_parts_kernel
+    else atomicAdd(out, s);
+  }
+}
+
+// out += sum_b part[b], b < nb, in a fixed order (per-lane strided sums, then fixed trees)
+__global__ __launch_bounds__(256) void sum_parts_kernel(const double* __restrict__ part, int nb,
+                                                        double* __restrict__ out) {
+  __shared__ double red[4];
+  double a = 0.0;
+  for (int b = threadIdx.x; b < nb; b += 256) a += part[b];
+  a = wave_sum_d(a);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = a;
+  __syncthreads();
+  if (threadIdx.x == 0) *out += red[0] + red[1] + red[2] + red[3];
 }
 
 __global__ __launch_bounds__(256) void adamw_kernel(const nrse_adamw_params p) {
@@ -144,11 +161,13 @@ int grid_for(long long n) {
 
 }  // namespace
 
-extern "C" int nrse_sumsq(const float* x, long long n, double* out, void* stream) {
+extern "C" int nrse_sumsq(const float* x, long long n, double* out, double* part, void* stream) {
   NRSE_REQUIRE(x && out && n >= 0, "nrse_sumsq: bad args");
   NRSE_REQUIRE(((uintptr_t)x & 15) == 0, "nrse_sumsq: x must be 16-byte aligned");
   if (n == 0) return NRSE_OK;
-  hipLaunchKernelGGL(sumsq_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, n, out);
+  const int nb = (int)grid_for(n);
+  hipLaunchKernelGGL(sumsq_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, x, n, out, part);
+  if (part) hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, part, nb, out);
   return nrse_check_launch("nrse_sumsq");
 }
 

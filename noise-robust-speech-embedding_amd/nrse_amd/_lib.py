@@ -58,7 +58,8 @@ class GemmParams(ctypes.Structure):
                 ("bias", c_vp), ("bias_z1", c_ll), ("bias_z2", c_ll),
                 ("aux", c_vp), ("aux_dtype", c_int), ("ldaux", c_ll), ("aux_z1", c_ll),
                 ("aux_z2", c_ll), ("resid", c_vp), ("resid_dtype", c_int), ("ldr", c_ll), ("r_z1", c_ll),
-                ("r_z2", c_ll), ("dropout_p", c_f), ("seed", c_u32), ("colsum", c_vp)]
+                ("r_z2", c_ll), ("dropout_p", c_f), ("seed", c_u32), ("colsum", c_vp),
+                ("colsum_part", c_vp)]
 
 
 class LnFwdParams(ctypes.Structure):
@@ -73,7 +74,8 @@ class LnBwdParams(ctypes.Structure):
                 ("x", c_vp), ("x_dtype", c_int), ("gamma", c_vp), ("beta", c_vp), ("mean", c_vp), ("rstd", c_vp),
                 ("dx", c_vp), ("dx_dtype", c_int), ("resid", c_vp), ("dgamma", c_vp), ("dbeta", c_vp),
                 ("rows", c_ll), ("C", c_int), ("flags", c_int),
-                ("dv", c_vp), ("dv_dtype", c_int), ("dv_colsum", c_vp), ("dv_p", c_f), ("dv_seed", c_u32)]
+                ("dv", c_vp), ("dv_dtype", c_int), ("dv_colsum", c_vp), ("dv_p", c_f), ("dv_seed", c_u32),
+                ("part", c_vp)]
 
 
 class AttnFwdParams(ctypes.Structure):
@@ -86,7 +88,7 @@ class AttnBwdParams(ctypes.Structure):
     _fields_ = [("qkv", c_vp), ("dtype", c_int), ("gate", c_vp), ("bias", c_vp), ("ctx", c_vp), ("dctx", c_vp),
                 ("lse", c_vp), ("delta", c_vp), ("dqkv", c_vp), ("dgate", c_vp), ("diag", c_vp),
                 ("batch", c_int), ("T", c_int), ("H", c_int), ("head_dim", c_int), ("scale", c_f),
-                ("dropout_p", c_f), ("seed", c_u32), ("bias_vec", c_vp)]
+                ("dropout_p", c_f), ("seed", c_u32), ("bias_vec", c_vp), ("diag_part", c_vp)]
 
 
 class Conv0Params(ctypes.Structure):
@@ -94,7 +96,8 @@ class Conv0Params(ctypes.Structure):
                 ("out_dtype", c_int), ("mean", c_vp), ("rstd", c_vp),
                 ("dy", c_vp), ("dy_dtype", c_int), ("dy_mode", c_int), ("col_k", c_int), ("col_s", c_int),
                 ("col_tout", c_int), ("dw", c_vp), ("dgamma", c_vp), ("dbeta", c_vp),
-                ("batch", c_int), ("T0", c_int), ("C", c_int), ("k", c_int), ("s", c_int), ("eps", c_f)]
+                ("batch", c_int), ("T0", c_int), ("C", c_int), ("k", c_int), ("s", c_int), ("eps", c_f),
+                ("part", c_vp)]
 
 
 class AdamWParams(ctypes.Structure):
@@ -111,32 +114,38 @@ _SIGNATURES = {
     "nrse_last_error": ([], ctypes.c_char_p),
     "nrse_abi_version": ([], c_int),
     "nrse_gemm": ([_P(GemmParams), c_vp], c_int),
+    "nrse_gemm_colsum_workspace": ([_P(GemmParams)], c_ll),
     "nrse_gemm_select": ([c_int], c_int),
     "nrse_gemm_tile_rows": ([c_int], c_int),
     "nrse_layernorm_fwd": ([_P(LnFwdParams), c_vp], c_int),
     "nrse_layernorm_bwd": ([_P(LnBwdParams), c_vp], c_int),
-    "nrse_ln_mean_fwd": ([c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_f, c_vp], c_int),
+    "nrse_layernorm_bwd_workspace": ([_P(LnBwdParams)], c_ll),
+    "nrse_ln_mean_fwd": ([c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_f, c_vp, c_vp], c_int),
     "nrse_bias_ld": ([c_int], c_int),
     "nrse_rel_bias_fwd": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp], c_int),
     "nrse_rel_bias_vec": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp], c_int),
-    "nrse_rel_bias_bwd": ([c_vp, c_vp, c_vp, c_int, c_int, c_vp], c_int),
+    "nrse_rel_bias_bwd": ([c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp], c_int),
     "nrse_gate_fwd": ([c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp], c_int),
-    "nrse_gate_bwd": ([c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp],
+    "nrse_gate_bwd_workspace": ([c_int], c_ll),
+    "nrse_gate_bwd": ([c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp],
                       c_int),
     "nrse_attn_fwd": ([_P(AttnFwdParams), c_vp], c_int),
     "nrse_attn_bwd": ([_P(AttnBwdParams), c_vp], c_int),
     "nrse_conv0_fwd": ([_P(Conv0Params), c_vp], c_int),
     "nrse_conv0_bwd": ([_P(Conv0Params), c_vp], c_int),
+    "nrse_conv0_bwd_workspace": ([_P(Conv0Params)], c_ll),
     "nrse_weight_norm_fwd": ([c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_vp, c_vp], c_int),
     "nrse_weight_norm_bwd": ([c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp], c_int),
     "nrse_specaug_pad": ([c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
     "nrse_pad_rows": ([c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
-    "nrse_specaug_bwd": ([c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_f, c_u32, c_vp], c_int),
+    "nrse_specaug_bwd": ([c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_f, c_u32, c_vp, c_vp], c_int),
     "nrse_dropout_cast": ([c_vp, c_vp, c_int, c_ll, c_f, c_u32, c_vp], c_int),
-    "nrse_dropout_cast_colsum": ([c_vp, c_vp, c_int, c_ll, c_int, c_f, c_u32, c_vp, c_vp], c_int),
-    "nrse_colsum": ([c_vp, c_int, c_vp, c_ll, c_int, c_vp], c_int),
+    "nrse_dropout_cast_colsum": ([c_vp, c_vp, c_int, c_ll, c_int, c_f, c_u32, c_vp, c_vp, c_vp], c_int),
+    "nrse_colsum": ([c_vp, c_int, c_vp, c_ll, c_int, c_vp, c_vp], c_int),
+    "nrse_colsum_workspace": ([c_ll, c_int], c_ll),
     "nrse_cast": ([c_vp, c_int, c_vp, c_int, c_ll, c_vp], c_int),
     "nrse_splitk_reduce": ([c_vp, c_vp, c_int, c_ll, c_int, c_vp], c_int),
+    "nrse_rows_reduce": ([c_vp, c_ll, c_vp, c_ll, c_vp, c_ll, c_vp, c_int, c_int, c_int, c_vp], c_int),
     "nrse_swap12": ([c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
     "nrse_gelu_bwd_pad": ([c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
     "nrse_bn_fwd": ([c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_f, c_f, c_int, c_int, c_vp], c_int),
@@ -147,8 +156,8 @@ _SIGNATURES = {
     "nrse_bn_bwd_sums": ([c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp], c_int),
     "nrse_bn_bwd_global": ([c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_vp, c_vp, c_vp, c_int, c_int,
                             c_int, c_vp], c_int),
-    "nrse_byol_loss": ([c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_f, c_vp], c_int),
-    "nrse_sumsq": ([c_vp, c_ll, c_vp, c_vp], c_int),
+    "nrse_byol_loss": ([c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_f, c_vp, c_vp], c_int),
+    "nrse_sumsq": ([c_vp, c_ll, c_vp, c_vp, c_vp], c_int),
     "nrse_adamw": ([_P(AdamWParams), c_vp], c_int),
     "nrse_ema": ([c_vp, c_vp, c_vp, c_int, c_ll, c_f, c_vp], c_int),
     "nrse_health": ([c_vp, c_int, c_ll, c_vp, c_vp], c_int),

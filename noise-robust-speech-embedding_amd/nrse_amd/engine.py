@@ -28,7 +28,7 @@ from . import kernels as K
 from . import params as PR
 from . import rng as R
 from .arch import WavLMArch
-from .hostside import bucket_vector, compute_mask_indices, layerdrop_decisions
+from .hostside import bucket_runs, bucket_vector, compute_mask_indices, layerdrop_decisions
 
 F32 = torch.float32
 # NRSE_SERIAL_TARGET=1 runs the target view and the backward weight gradients on the main
@@ -222,6 +222,15 @@ class ByolEngine:
             a = self.arch
             self._buckets[T] = torch.from_numpy(bucket_vector(T, a.num_buckets, a.max_distance)).to(self.dev)
         return self._buckets[T]
+
+    def bucket_runs(self, T: int) -> tuple[torch.Tensor, torch.Tensor]:
+        """(order, offsets) of buckets(T) for the gather-form rel-pos bias backward."""
+        key = ("runs", T)
+        if key not in self._buckets:
+            order, offsets = bucket_runs(bucket_vector(T, self.arch.num_buckets, self.arch.max_distance),
+                                         self.arch.num_buckets)
+            self._buckets[key] = (torch.from_numpy(order).to(self.dev), torch.from_numpy(offsets).to(self.dev))
+        return self._buckets[key]
 
     # ------------------------------------------------------------------ encoder forward
     def encoder_forward(self, W: EncoderWeights, wav: torch.Tensor, *, train: bool, fseed: int = 0, skip=None,
@@ -475,7 +484,7 @@ class ByolEngine:
                 on_layer(li)
         tape.layers = []
         main.wait_stream(self._bwd_side_stream())
-        K.rel_bias_bwd(diag, self.buckets(T), Gv["encoder.layers.0.attention.rel_attn_embed.weight"], nh, T)
+        K.rel_bias_bwd(diag, *self.bucket_runs(T), Gv["encoder.layers.0.attention.rel_attn_embed.weight"], nh, T)
         # positional conv block: h0 = drop(h + gelu(conv(hpad) + b))
         pk, G = a.pos_kernel, a.pos_groups
         cpg = H // G
@@ -552,11 +561,11 @@ class ByolEngine:
                     S = K.slab_splits_for(((Cc + 255) // 256) * ((k * Cin + 255) // 256), B)
                     K.gemm_slab(A_op, B_op, dWr, Cc, k * Cin, Tout, nseg=B // S, splits=S, accumulate=False)
                 else:
-                    dWr = torch.zeros(Cc, k * Cin, device=dev, dtype=F32)
+                    # f32 parity mode: the same ordered slab reduction on the generic kernels
+                    dWr = torch.empty(Cc, k * Cin, device=dev, dtype=F32)
                     tiles = ((Cc + 127) // 128) * ((k * Cin + 127) // 128)
                     S = _divisor_at_most(B, max(1, 512 // tiles))
-                    K.gemm(A_op, B_op, dWr, Cc, k * Cin, Tout, ldc=k * Cin, nseg=B // S, splits=S,
-                           flags=_lib.EPI_ATOMIC)
+                    K.gemm_slab(A_op, B_op, dWr, Cc, k * Cin, Tout, nseg=B // S, splits=S, accumulate=False)
                 K.swap12(dWr, Gv[p + "conv.weight"], Cc, k, Cin, accumulate=True)
                 del dWr
             # dgrad -> G [B*Tout, k*Cin] (col2im folded into the next LN backward)

@@ -32,6 +32,16 @@ def bucket_vector(T: int, num_buckets: int = 320, max_distance: int = 800) -> np
     return (out + np.where(small, rp, large)).astype(np.int32)
 
 
+def bucket_runs(bucket: np.ndarray, nb: int) -> tuple[np.ndarray, np.ndarray]:
+    """(order, offsets) of the relative-position buckets: the offsets d sorted by bucket (stable,
+    so increasing d within a bucket) and each bucket's start in that list ([nb + 1]); the gather
+    form nrse_rel_bias_bwd sums a bucket's diagonals in this fixed order."""
+    b = np.asarray(bucket, dtype=np.int64)
+    order = np.argsort(b, kind="stable").astype(np.int32)
+    offsets = np.searchsorted(b[order], np.arange(nb + 1)).astype(np.int32)
+    return order, offsets
+
+
 def compute_mask_indices(rng: np.random.Generator, batch: int, T: int, mask_prob: float, mask_length: int,
                          min_masks: int = 0) -> np.ndarray:
     """SpecAugment time masks with the reference's span algorithm (no attention mask: every

@@ -41,6 +41,28 @@ def _call(name, *args):
     _lib.check(getattr(_lib.lib(), name)(*args), name)
 
 
+# Deterministic reductions (default): the per-workgroup column sums of the gradient reductions
+# are written to a workspace of partial rows and added in a fixed order (nrse_rows_reduce)
+# instead of f32 atomics, so a step's gradients are bit-identical run to run.
+# NRSE_ATOMIC_REDUCTIONS=1 restores the atomics (timing comparisons only).
+DETERMINISTIC = os.environ.get("NRSE_ATOMIC_REDUCTIONS", "0") != "1"
+
+
+def workspace(nfloats: int) -> torch.Tensor:
+    """f32 scratch on the current device and stream (the caching allocator keeps it stream-ordered)."""
+    return torch.empty(max(int(nfloats), 4), device="cuda", dtype=torch.float32)
+
+
+def rows_reduce(slab: torch.Tensor, S: int, *dsts, batch: int = 1, accumulate: bool = True) -> None:
+    """Ordered sum of S partial rows [d0 | d1 | d2] into the destinations (nrse_rows_reduce);
+    with batch > 1 the slab is [batch, S, n] and each destination [batch, n_j]."""
+    assert 1 <= len(dsts) <= 3
+    d = list(dsts) + [None] * (3 - len(dsts))
+    n = [0 if t is None else t.numel() // batch for t in d]
+    _call("nrse_rows_reduce", ptr(d[0]), n[0], ptr(d[1]), n[1], ptr(d[2]), n[2], ptr(slab), S, batch,
+          1 if accumulate else 0, stream_ptr())
+
+
 @dataclass
 class Operand:
     """GEMM operand descriptor (see nrse_gemm_operand in include/nrse_hip.h)."""
@@ -99,6 +121,10 @@ def gemm(A: Operand, B: Operand, C: torch.Tensor, M: int, N: int, K: int, *, ldc
     p.dropout_p = dropout_p
     p.seed = seed & 0xFFFFFFFF
     p.colsum = ptr(colsum)
+    ws = None
+    if colsum is not None and DETERMINISTIC:
+        ws = workspace(_lib.lib().nrse_gemm_colsum_workspace(ctypes.byref(p)))
+        p.colsum_part = ptr(ws)
     probe = _GEMM_PROBE
     if probe is not None:
         # algorithmic HBM bytes: A and B read once, C written once (read too when accumulated),
@@ -187,32 +213,42 @@ def _small_m_splits(M: int, N: int, K: int) -> int:
     return s
 
 
+def _slab_ok(out: torch.Tensor, M: int, N: int) -> bool:
+    """out can take the slab split-K (contiguous f32 [M, N], nrse_splitk_reduce's layout)."""
+    return (out.dtype == torch.float32 and out.is_contiguous() and out.numel() == M * N and (M * N) % 4 == 0
+            and out.data_ptr() % 16 == 0)
+
+
 def linear_fwd_small(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, *, bias=None) -> None:
-    """out[M,N] = x @ w^T (+ bias) for small M: split-K with f32 atomics (out is overwritten)."""
+    """out[M,N] = x @ w^T (+ bias) for small M: split-K into f32 slabs (the bias joins split 0),
+    added in split order by nrse_splitk_reduce (deterministic; out is overwritten)."""
     M, K = x.shape
     N = w.shape[0]
     S = _small_m_splits(M, N, K)
-    if S == 1 or out.dtype != torch.float32:
+    if S == 1 or not _slab_ok(out, M, N):
         linear_fwd(x, w, out, bias=bias)
         return
-    out.zero_()
     ks = K // S
-    gemm(Operand(x, True, x.stride(0), seg_stride=ks), Operand(w, True, w.stride(0), seg_stride=ks), out, M, N, ks,
-         ldc=out.stride(0), splits=S, bias=bias, flags=_lib.EPI_ATOMIC)
+    slab = torch.empty(S, M, N, device=out.device, dtype=torch.float32)
+    gemm(Operand(x, True, x.stride(0), seg_stride=ks), Operand(w, True, w.stride(0), seg_stride=ks), slab, M, N, ks,
+         ldc=N, splits=S, c_split=M * N, bias=bias)
+    _call("nrse_splitk_reduce", ptr(out), ptr(slab), S, M * N, 0, stream_ptr())
 
 
 def linear_dgrad_small(dy: torch.Tensor, w: torch.Tensor, dx: torch.Tensor) -> None:
-    """dx[M,K] = dy[M,N] @ w[N,K] for small M: split over N with f32 atomics (dx is overwritten)."""
+    """dx[M,K] = dy[M,N] @ w[N,K] for small M: split over N into f32 slabs, added in split order
+    (deterministic; dx is overwritten)."""
     M, N = dy.shape
     K = w.shape[1]
     S = _small_m_splits(M, K, N)
-    if S == 1 or dx.dtype != torch.float32:
+    if S == 1 or not _slab_ok(dx, M, K):
         linear_dgrad(dy, w, dx)
         return
-    dx.zero_()
     ns = N // S
+    slab = torch.empty(S, M, K, device=dx.device, dtype=torch.float32)
     gemm(Operand(dy, True, dy.stride(0), seg_stride=ns), Operand(w, False, w.stride(0), seg_stride=ns * w.stride(0)),
-         dx, M, K, ns, ldc=dx.stride(0), splits=S, flags=_lib.EPI_ATOMIC)
+         slab, M, K, ns, ldc=K, splits=S, c_split=M * K)
+    _call("nrse_splitk_reduce", ptr(dx), ptr(slab), S, M * K, 0, stream_ptr())
 
 
 def _slab_splits(M: int, N: int, K: int) -> int:
@@ -306,7 +342,12 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, *, splits:
             break
     seg = (M + splits - 1) // splits
     bulk = (M // seg) * seg
-    if bulk:
+    if bulk and bulk // seg > 1 and _slab_ok(dw, N, K):
+        # the splits' partials as slabs added in split order (deterministic)
+        gemm_slab(Operand(dy, False, dy.stride(0), seg_stride=seg * dy.stride(0)),
+                  Operand(x, False, x.stride(0), seg_stride=seg * x.stride(0)),
+                  dw, N, K, seg, nseg=1, splits=bulk // seg, accumulate=True)
+    elif bulk:
         gemm(Operand(dy, False, dy.stride(0), seg_stride=seg * dy.stride(0)),
              Operand(x, False, x.stride(0), seg_stride=seg * x.stride(0)),
              dw, N, K, seg, ldc=dw.stride(0), nseg=1, splits=bulk // seg, flags=_lib.EPI_ATOMIC)
@@ -345,12 +386,17 @@ def ln_bwd(dy, x, gamma, mean, rstd, dx, *, beta=None, gelu=False, relu=False, r
         assert dv.numel() == rows * C and (dv_colsum is None or dv_colsum.dtype == torch.float32)
         p.dv, p.dv_dtype, p.dv_colsum = ptr(dv), dtype_code(dv), ptr(dv_colsum)
         p.dv_p, p.dv_seed = dv_p, dv_seed & 0xFFFFFFFF
+    ws = None
+    if DETERMINISTIC and (dgamma is not None or (dv is not None and dv_colsum is not None)):
+        ws = workspace(_lib.lib().nrse_layernorm_bwd_workspace(ctypes.byref(p)))
+        p.part = ptr(ws)
     _call("nrse_layernorm_bwd", ctypes.byref(p), stream_ptr())
 
 
 def ln_mean_fwd(h, gamma, beta, emb, mean, rstd, batch, T, C, eps):
+    ws = workspace(batch * ((T + 31) // 32) * C) if DETERMINISTIC else None
     _call("nrse_ln_mean_fwd", ptr(h), ptr(gamma), ptr(beta), ptr(emb), ptr(mean), ptr(rstd), batch, T, C, eps,
-          stream_ptr())
+          ptr(ws), stream_ptr())
 
 
 # ----------------------------------------------------------------------------- attention
@@ -370,8 +416,9 @@ def rel_bias_vec(E, bucket, vec, H, T):
     _call("nrse_rel_bias_vec", ptr(E), ptr(bucket), ptr(vec), H, T, E.shape[0], stream_ptr())
 
 
-def rel_bias_bwd(diag, bucket, dE, H, T):
-    _call("nrse_rel_bias_bwd", ptr(diag), ptr(bucket), ptr(dE), H, T, stream_ptr())
+def rel_bias_bwd(diag, order, offsets, dE, H, T):
+    """dE[bucket(d), h] += diag[h, d], gathered per bucket in a fixed order (hostside.bucket_runs)."""
+    _call("nrse_rel_bias_bwd", ptr(diag), ptr(order), ptr(offsets), ptr(dE), H, T, offsets.numel() - 1, stream_ptr())
 
 
 def gate_fwd(x1, W, b, c, gate, batch, T, H):
@@ -381,8 +428,9 @@ def gate_fwd(x1, W, b, c, gate, batch, T, H):
 def gate_bwd(x1, W, b, c, dgate, dx1, dW, db, dc, batch, T, H):
     """dx1 += gate-path gradient; dW/db/dc accumulated (one fused kernel)."""
     assert dx1.dtype == torch.float32 and dW.dtype == db.dtype == dc.dtype == torch.float32
+    ws = workspace(_lib.lib().nrse_gate_bwd_workspace(H)) if DETERMINISTIC else None
     _call("nrse_gate_bwd", ptr(x1), dtype_code(x1), ptr(W), ptr(b), ptr(c), ptr(dgate), ptr(dx1), ptr(dW), ptr(db),
-          ptr(dc), batch, T, H, stream_ptr())
+          ptr(dc), batch, T, H, ptr(ws), stream_ptr())
 
 
 def attn_fwd(qkv, gate, bias, ctx, lse, batch, T, H, dropout_p=0.0, seed=0, bias_vec=None):
@@ -397,6 +445,10 @@ def attn_bwd(qkv, gate, bias, ctx, dctx, lse, delta, dqkv, dgate, diag, batch, T
     p = AttnBwdParams(ptr(qkv), dtype_code(qkv), ptr(gate), ptr(bias), ptr(ctx), ptr(dctx), ptr(lse), ptr(delta),
                       ptr(dqkv), ptr(dgate), ptr(diag), batch, T, H, 64, 0.125, dropout_p, seed & 0xFFFFFFFF,
                       ptr(bias_vec))
+    ws = None
+    if DETERMINISTIC and diag is not None and bias_vec is not None:
+        ws = workspace(H * batch * ((T + 63) // 64) * (2 * T - 1))
+        p.diag_part = ptr(ws)
     _call("nrse_attn_bwd", ctypes.byref(p), stream_ptr())
 
 
@@ -428,6 +480,10 @@ def conv0_bwd(wav, w, gamma, beta, mean, rstd, dy, dw, dgamma, dbeta, T0, k, s, 
         p.col_k, p.col_s, p.col_tout = col
     p.dw, p.dgamma, p.dbeta = ptr(dwT), ptr(dgamma), ptr(dbeta)
     p.batch, p.T0, p.C, p.k, p.s = B, T0, C, k, s
+    ws = None
+    if DETERMINISTIC:
+        ws = workspace(_lib.lib().nrse_conv0_bwd_workspace(ctypes.byref(p)))
+        p.part = ptr(ws)
     _call("nrse_conv0_bwd", ctypes.byref(p), stream_ptr())
     swap12(dwT, dw, 1, k, C, accumulate=True)
 
@@ -460,8 +516,11 @@ def pad_rows(src, dst, batch, T, C, pf, pb):
 
 
 def specaug_bwd(dh, mask, dembed, out, batch, T, C, p, seed):
+    ws = None
+    if DETERMINISTIC and mask is not None and dembed is not None:
+        ws = workspace(min(batch * T, 2048) * C)
     _call("nrse_specaug_bwd", ptr(dh), ptr(mask), ptr(dembed), ptr(out), dtype_code(out), batch, T, C, p,
-          seed & 0xFFFFFFFF, stream_ptr())
+          seed & 0xFFFFFFFF, ptr(ws), stream_ptr())
 
 
 def dropout_cast(x, out, p=0.0, seed=0):
@@ -469,17 +528,23 @@ def dropout_cast(x, out, p=0.0, seed=0):
     _call("nrse_dropout_cast", ptr(x), ptr(out), dtype_code(out), x.numel(), p, seed & 0xFFFFFFFF, stream_ptr())
 
 
+def _colsum_ws(rows: int, C: int):
+    return workspace(_lib.lib().nrse_colsum_workspace(rows, C)) if DETERMINISTIC else None
+
+
 def dropout_cast_colsum(x, out, colsum, p=0.0, seed=0):
     """out = dropout(x) (cast), colsum += column sums of out: one pass."""
     assert x.dtype == torch.float32 and x.numel() == out.numel() and colsum.dtype == torch.float32
     C = x.shape[-1]
+    ws = _colsum_ws(x.numel() // C, C)
     _call("nrse_dropout_cast_colsum", ptr(x), ptr(out), dtype_code(out), x.numel() // C, C, p, seed & 0xFFFFFFFF,
-          ptr(colsum), stream_ptr())
+          ptr(colsum), ptr(ws), stream_ptr())
 
 
 def colsum(x, out):
     C = x.shape[-1]
-    _call("nrse_colsum", ptr(x), dtype_code(x), ptr(out), x.numel() // C, C, stream_ptr())
+    ws = _colsum_ws(x.numel() // C, C)
+    _call("nrse_colsum", ptr(x), dtype_code(x), ptr(out), x.numel() // C, C, ptr(ws), stream_ptr())
 
 
 def cast(x, y):
@@ -534,11 +599,14 @@ def bn_bwd_global(dy, x, y, w, sm, si, lsums, gsums, nglobal, dx, dw, db, relu):
 
 def byol_loss(p, z, loss, dp=None, stats=None, grad_scale=1.0):
     rows, D = p.shape
-    _call("nrse_byol_loss", ptr(p), ptr(z), ptr(loss), ptr(dp), ptr(stats), rows, D, grad_scale, stream_ptr())
+    ws = workspace(rows * (3 if stats is not None else 1)) if DETERMINISTIC else None
+    _call("nrse_byol_loss", ptr(p), ptr(z), ptr(loss), ptr(dp), ptr(stats), rows, D, grad_scale, ptr(ws),
+          stream_ptr())
 
 
 def sumsq(x, out):
-    _call("nrse_sumsq", ptr(x), x.numel(), ptr(out), stream_ptr())
+    ws = torch.empty(4096, device=x.device, dtype=torch.float64) if DETERMINISTIC else None
+    _call("nrse_sumsq", ptr(x), x.numel(), ptr(out), ptr(ws), stream_ptr())
 
 
 def adamw(p, g, m, v, shadow, *, lr, beta1, beta2, eps, weight_decay, step, max_norm, sumsq_buf, grad_scale=1.0):

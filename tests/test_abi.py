@@ -14,7 +14,7 @@ PKG = os.path.join(ROOT, "noise-robust-speech-embedding_amd")
 def declared():
     text = open(HEADER).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\*?(nrse_\w+)\s*\(", text, flags=re.M)))
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?(?:\w+\s+)*\w+\*?\s+\*?(nrse_\w+)\s*\(", text, flags=re.M)))
 
 
 @pytest.fixture(scope="module")
@@ -35,7 +35,7 @@ def test_library_exports_every_declared_symbol(lib):
     L = lib.lib()
     for name in declared():
         assert hasattr(L, name), name
-    assert L.nrse_abi_version() == 2
+    assert L.nrse_abi_version() == 3
 
 
 def test_nm_dynamic_symbols(lib):

@@ -121,3 +121,17 @@ def test_attention_pair_hash_mask_statistics():
     assert MK.threshold16(0.0) == 0 and MK.threshold16(1.0) == 65536
     m = MK.attn_dropout_mask(7, p, (2, 3, T, T))
     assert set(np.unique(m)).issubset({0.0, np.float32(1 / (1 - p))})
+
+
+def test_bucket_runs_invert_the_bucket_vector():
+    """The gather form of the rel-pos bias backward (nrse_rel_bias_bwd) sums bucket k's diagonals
+    over order[offsets[k]:offsets[k+1]]: every offset d exactly once, increasing within a bucket."""
+    from nrse_amd.hostside import bucket_runs, bucket_vector
+    for T in (1, 7, 149, 399):
+        b = bucket_vector(T, 320, 800)
+        order, offsets = bucket_runs(b, 320)
+        assert offsets[0] == 0 and offsets[-1] == 2 * T - 1 and len(offsets) == 321
+        assert sorted(order.tolist()) == list(range(2 * T - 1))
+        for k in range(320):
+            run = order[offsets[k]:offsets[k + 1]]
+            assert (b[run] == k).all() and (np.diff(run) > 0).all()
