@@ -405,7 +405,17 @@ __global__ __launch_bounds__(64) void attn_bwd_kv_f32_kernel(const nrse_attn_bwd
       }
     }
     __syncthreads();
-    if (p.diag) {
+    if (p.diag && p.diag_part) {
+      // row (h, b, key tile, query tile) of the partial slab: this tile pair's 127 diagonals, zeros
+      // elsewhere (added in order by nrse_rows_reduce: deterministic)
+      const int nq = (Tn + 63) / 64;
+      float* prow = p.diag_part + ((((long long)h * p.batch + b) * gridDim.x + blockIdx.x) * nq + i0 / 64) * nd;
+      const int e0 = (blockIdx.x * 64 - i0) - 63 + Tn - 1;
+      for (int dd = threadIdx.x; dd < nd; dd += 64) {
+        const int e = dd - e0;
+        prow[dd] = (e >= 0 && e < 127) ? dg[e] : 0.f;
+      }
+    } else if (p.diag) {
       for (int e = threadIdx.x; e < 127; e += 64) {
         const int dd = (blockIdx.x * 64 - i0) + e - 63 + Tn - 1;
         if (dd >= 0 && dd < nd && dg[e] != 0.f) atomicAdd(p.diag + (long long)h * nd + dd, dg[e]);
@@ -580,6 +590,15 @@ extern "C" int nrse_attn_fwd(const nrse_attn_fwd_params* p, void* stream) {
   return nrse_check_launch("nrse_attn_fwd");
 }
 
+// diag partial rows: per (h, b, key tile) on the bf16 MFMA path, per (h, b, key tile, query tile)
+// on the f32 path
+extern "C" long long nrse_attn_bwd_workspace(const nrse_attn_bwd_params* p) {
+  if (!p || p->T <= 0 || p->batch <= 0 || p->H <= 0) return 0;
+  const long long nt = (p->T + 63) / 64;
+  const long long rows = nrse_attn_use_mfma(p->dtype, p->head_dim) ? nt : nt * nt;
+  return (long long)p->H * p->batch * rows * (2LL * p->T - 1);
+}
+
 extern "C" int nrse_attn_bwd(const nrse_attn_bwd_params* p, void* stream) {
   NRSE_REQUIRE(p && p->qkv && p->gate && (p->bias || p->bias_vec) && p->ctx && p->dctx && p->lse && p->delta && p->dqkv && p->dgate &&
                p->batch > 0 && p->T > 0 && p->H > 0, "nrse_attn_bwd: bad args");
@@ -599,5 +618,9 @@ extern "C" int nrse_attn_bwd(const nrse_attn_bwd_params* p, void* stream) {
     hipLaunchKernelGGL(attn_bwd_kv_f32_kernel<float>, grid, dim3(64), 0, st, *p);
     hipLaunchKernelGGL(attn_bwd_q_f32_kernel<float>, grid, dim3(64), 0, st, *p);
   }
-  return nrse_check_launch("nrse_attn_bwd");
+  const int rc = nrse_check_launch("nrse_attn_bwd");
+  if (rc || !p->diag || !p->diag_part) return rc;
+  const int nt = (p->T + 63) / 64;
+  return nrse_rows_reduce(p->diag, 2LL * p->T - 1, nullptr, 0, nullptr, 0, p->diag_part, p->batch * nt * nt, p->H, 1,
+                          st);
 }

@@ -10,9 +10,8 @@
 //  - one K-tile (BK = 64) is 4 half-tiles of 16 KiB: A-lo = A rows {0-63,128-191}, A-hi = A rows
 //    {64-127,192-255}, B-lo = B cols {wn*64 + 0..31}, B-hi = B cols {wn*64 + 32..63}. Each wave
 //    computes its 128x64 output as 4 quadrants (64x32, 16 MFMAs) in 4 phases: p0 (A-lo,B-lo),
-//    p1 (A-lo,B-hi), p2 (A-hi,B-hi), p3 (A-hi,B-lo), reading A-lo in p0, B-hi in p1, A-hi in p2
-//    and the NEXT K-tile's B-lo in p3 (8 / 4 / 8 / 4 fragment reads per phase), keeping fragments
-//    in registers for their second use.
+//    p1 (A-lo,B-hi), p2 (A-hi,B-hi), p3 (A-hi,B-lo), reading A-lo and B-lo in p0, B-hi in p1,
+//    A-hi in p2 and keeping fragments in registers for their second use.
 //  - LDS is a ring of 10 half-tile slots (160 KiB). Half-tiles are numbered in first-read order
 //    (seq = 4t + {A-lo, B-lo, B-hi, A-hi}), seq n lives in slot n % 10, and phase P stages
 //    seq P + 8 (K-tile t+2): every DMA has >= 6 phases (~1.3 us at full MFMA rate, more than the
@@ -23,8 +22,7 @@
 //    MFMAs run in (#2P, #2P+1); group 1 is shifted by one. Hand-off rules that follow:
 //      RAW: data read in phase Q is waited for (vmcnt) by every issuing wave before the FIRST
 //           barrier of phase Q-1: vmcnt(12) there leaves the 6 youngest half-tiles (seq
-//           P+3..P+8) in flight and retires seq <= P+2, which covers phase P+1's reads; phase 2
-//           waits with vmcnt(10) (retires seq <= 4t+5, the B-lo that phase 3 reads).
+//           P+3..P+8) in flight and retires seq <= P+2, which covers phase P+1's reads.
 //      WAR: a slot is restaged >= 2 phases after its last read: seq n is staged in phase n-8
 //           into the slot of seq n-10, last read in phase <= n-10.
 //    No wait is vmcnt(0) and the barriers are raw s_barrier (no fence), so DMAs stay in flight
@@ -332,9 +330,7 @@ NRSE_DEV void fast_epilogue(const nrse_gemm_params& p, const f32x4 (&acc)[8][4],
 #define NRSE_BAR()                            \
   do {                                        \
     asm volatile("" ::: "memory");            \
-    __builtin_amdgcn_sched_barrier(0);        \
     __builtin_amdgcn_s_barrier();             \
-    __builtin_amdgcn_sched_barrier(0);        \
     asm volatile("" ::: "memory");            \
   } while (0)
 
@@ -470,66 +466,50 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
   // division by the segment's K-tile count stays out of the loop (done per iteration by all 8
   // waves on the CU's one scalar unit, it lengthened each K-tile's first phase by ~200 cycles)
   int u_sg = 2 / tps, u_k = 2 % tps;
-  // B-lo of K-tile t is read in phase 3 of K-tile t-1 (into the register set B-hi is done with),
-  // so the reads are 8 / 4 / 8 / 4 fragments over the 4 phases instead of 12 / 4 / 8 / 0: phase 0
-  // was LDS-bound (its reads plus the half-tile DMA into LDS outlasted the other group's
-  // 16-MFMA segment). The two B register sets swap roles every K-tile (loop unrolled by 2).
-  // Phase 2's wait therefore retires one more half-tile (vmcnt(10): B-lo of t+1, seq 4t+5).
-  NRSE_READ_B(1, fbl)
-#define NRSE_KTILE(T, X, Y)                                                                     \
-  {                                                                                             \
-    const int t = (T);                                                                          \
-    const int s0 = base, s1 = wrap(base + 1), s2 = wrap(base + 2), s3 = wrap(base + 3);         \
-    /* phase p stages half-tile j = p of K-tile t+2 (sequence 4t+8+p) into slot (4t+8+p) % 10 */ \
-    const TilePos q2 = tile_pos_at(t + 2 < ntiles, u_sg, u_k);                                  \
-    if (++u_k == tps) { u_k = 0; ++u_sg; }                                                      \
-    /* phase 0: quadrant (M-half 0, N-half 0) from A-lo and B-lo (in X since phase 3 of t-1) */ \
-    NRSE_READ_A(s0, 4)                                                                          \
-    stage(0, q2, wrap(base + 8));                                                               \
-    NRSE_WAIT();                                                                                \
-    NRSE_BAR();                                                                                 \
-    NRSE_PSTAMP(0);                                                                             \
-    NRSE_QUAD(0, 0, X)                                                                          \
-    NRSE_BAR();                                                                                 \
-    NRSE_PSTAMP(1);                                                                             \
-    /* phase 1: (0, 1) from B-hi */                                                             \
-    NRSE_READ_B(s2, Y)                                                                          \
-    stage(1, q2, wrap(base + 9));                                                               \
-    NRSE_WAIT();                                                                                \
-    NRSE_BAR();                                                                                 \
-    NRSE_PSTAMP(2);                                                                             \
-    NRSE_QUAD(0, 1, Y)                                                                          \
-    NRSE_BAR();                                                                                 \
-    NRSE_PSTAMP(3);                                                                             \
-    /* phase 2: (1, 1) from A-hi */                                                             \
-    NRSE_READ_A(s3, NFI_HI)                                                                     \
-    stage(2, q2, base); /* (4t + 10) % 10 */                                                    \
-    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");                                           \
-    NRSE_BAR();                                                                                 \
-    NRSE_PSTAMP(4);                                                                             \
-    NRSE_QUAD(1, 1, Y)                                                                          \
-    NRSE_BAR();                                                                                 \
-    NRSE_PSTAMP(5);                                                                             \
-    /* phase 3: (1, 0) from registers; B-lo of K-tile t+1 (seq 4t+5) into Y */                  \
-    NRSE_READ_B(wrap(base + 5), Y)                                                              \
-    stage(3, q2, s1); /* (4t + 11) % 10 */                                                      \
-    NRSE_WAIT();                                                                                \
-    NRSE_BAR();                                                                                 \
-    NRSE_PSTAMP(6);                                                                             \
-    NRSE_QUAD(1, 0, X)                                                                          \
-    NRSE_BAR();                                                                                 \
-    NRSE_PSTAMP(7);                                                                             \
-    base = wrap(base + 4);                                                                      \
-  }
 #pragma unroll 1
-  for (int kt = 0; kt < ntiles; ++kt) {
-    NRSE_KTILE(kt, fbl, fbh)
-#pragma unroll
-    for (int fj = 0; fj < 2; ++fj)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) fbl[fj][s] = fbh[fj][s];
+  for (int t = 0; t < ntiles; ++t) {
+    const int s0 = base, s1 = wrap(base + 1), s2 = wrap(base + 2), s3 = wrap(base + 3);
+    // phase p stages half-tile j = p of K-tile t+2 (sequence 4t+8+p) into slot (4t+8+p) % 10
+    const TilePos q2 = tile_pos_at(t + 2 < ntiles, u_sg, u_k);
+    if (++u_k == tps) { u_k = 0; ++u_sg; }
+    // phase 0: quadrant (M-half 0, N-half 0) from A-lo, B-lo
+    NRSE_READ_A(s0, 4)
+    NRSE_READ_B(s1, fbl)
+    stage(0, q2, wrap(base + 8));
+    NRSE_WAIT();
+    NRSE_BAR();
+    NRSE_PSTAMP(0);
+    NRSE_QUAD(0, 0, fbl)
+    NRSE_BAR();
+    NRSE_PSTAMP(1);
+    // phase 1: (0, 1) from B-hi
+    NRSE_READ_B(s2, fbh)
+    stage(1, q2, wrap(base + 9));
+    NRSE_WAIT();
+    NRSE_BAR();
+    NRSE_PSTAMP(2);
+    NRSE_QUAD(0, 1, fbh)
+    NRSE_BAR();
+    NRSE_PSTAMP(3);
+    // phase 2: (1, 1) from A-hi
+    NRSE_READ_A(s3, NFI_HI)
+    stage(2, q2, base);  // (4t + 10) % 10
+    NRSE_WAIT();
+    NRSE_BAR();
+    NRSE_PSTAMP(4);
+    NRSE_QUAD(1, 1, fbh)
+    NRSE_BAR();
+    NRSE_PSTAMP(5);
+    // phase 3: (1, 0) from registers
+    stage(3, q2, s1);    // (4t + 11) % 10
+    NRSE_WAIT();
+    NRSE_BAR();
+    NRSE_PSTAMP(6);
+    NRSE_QUAD(1, 0, fbl)
+    NRSE_BAR();
+    NRSE_PSTAMP(7);
+    base = wrap(base + 4);
   }
-#undef NRSE_KTILE
   if (wm == 0) __builtin_amdgcn_s_barrier();
   NRSE_STAMP(2);
 #undef NRSE_READ_A

@@ -503,7 +503,7 @@ extern "C" int nrse_gelu_bwd_pad(const float* dy, const void* pre, int pdt, void
 // this kernel adds the rows in a fixed order into up to three destination vectors,
 //   row = [d0: n0 | d1: n1 | d2: n2],   d_j[c] (+)= sum_s slab[s][off_j + c],
 // so the result is the same on every run whatever the workgroups' completion order. 1024 threads
-// per 256 columns: thread (r, q) sums rows r, r + 16, ... of columns 4q..4q+3 (16 B loads, 4
+// per 256 columns: thread (r, q) sums rows r, r + 16, ... of columns 4q..4q+3 (16 B loads, 8
 // independent loads in flight), then the 16 row-group sums are added in order r = 0..15.
 // Row groups of `batch` (slab [batch][S][n], dst_j + b * n_j): per-utterance sums.
 struct RowsDst { float* d[3]; long long n[3]; };
@@ -517,12 +517,12 @@ __global__ __launch_bounds__(1024) void rows_reduce_kernel(RowsDst dst, const fl
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   if (col < n) {
     int k = r;
-    for (; k + 48 < S; k += 64) {
-      float4 v[4];
+    for (; k + 112 < S; k += 128) {
+      float4 v[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(sl + (long long)(k + 16 * u) * n + col);
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(sl + (long long)(k + 16 * u) * n + col);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) { s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w; }
+      for (int u = 0; u < 8; ++u) { s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w; }
     }
     for (; k < S; k += 16) {
       const float4 v = *reinterpret_cast<const float4*>(sl + (long long)k * n + col);
@@ -557,12 +557,12 @@ __global__ __launch_bounds__(1024) void rows_reduce1_kernel(RowsDst dst, const f
   float s = 0.f;
   if (col < n) {
     int k = r;
-    for (; k + 48 < S; k += 64) {
-      float v[4];
+    for (; k + 112 < S; k += 128) {
+      float v[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = sl[(long long)(k + 16 * u) * n + col];
+      for (int u = 0; u < 8; ++u) v[u] = sl[(long long)(k + 16 * u) * n + col];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) s += v[u];
+      for (int u = 0; u < 8; ++u) s += v[u];
     }
     for (; k < S; k += 16) s += sl[(long long)k * n + col];
   }

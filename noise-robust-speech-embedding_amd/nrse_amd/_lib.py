@@ -131,6 +131,7 @@ _SIGNATURES = {
                       c_int),
     "nrse_attn_fwd": ([_P(AttnFwdParams), c_vp], c_int),
     "nrse_attn_bwd": ([_P(AttnBwdParams), c_vp], c_int),
+    "nrse_attn_bwd_workspace": ([_P(AttnBwdParams)], c_ll),
     "nrse_conv0_fwd": ([_P(Conv0Params), c_vp], c_int),
     "nrse_conv0_bwd": ([_P(Conv0Params), c_vp], c_int),
     "nrse_conv0_bwd_workspace": ([_P(Conv0Params)], c_ll),

@@ -501,10 +501,21 @@ class ByolEngine:
             dWf = torch.zeros(G, cpg, pk * cpg, device=dev, dtype=F32)
             S = _divisor_at_most(B, 8)
             off = (pk // 2 - 1) * H
-            K.gemm(K.Operand(dypad, False, H, offset=off, seg_stride=(T + pk) * H, z1=cpg),
-                   K.Operand(tape.hpad, False, H, chunk_shift=cs, ld_chunk=H, seg_stride=(T + pk) * H, z1=cpg),
-                   dWf, cpg, pk * cpg, T, ldc=pk * cpg, nseg=B // S, splits=S, batch=G, c_z1=cpg * pk * cpg,
-                   flags=_lib.EPI_ATOMIC)
+            A_op = K.Operand(dypad, False, H, offset=off, seg_stride=(T + pk) * H, z1=cpg)
+            B_op = K.Operand(tape.hpad, False, H, chunk_shift=cs, ld_chunk=H, seg_stride=(T + pk) * H, z1=cpg)
+            if S <= 2 or (cdt == torch.bfloat16 and cpg == 64):
+                # at most two partial sums per element onto the zeroed dWf (the bf16 pos-conv wgrad
+                # kernel of posconv.hip, 64-channel groups, adds two shares): an order-independent,
+                # deterministic f32 sum
+                K.gemm(A_op, B_op, dWf, cpg, pk * cpg, T, ldc=pk * cpg, nseg=B // S, splits=S, batch=G,
+                       c_z1=cpg * pk * cpg, flags=_lib.EPI_ATOMIC)
+            else:
+                # other shapes (generic kernels): split slabs added in split order
+                slab = torch.empty(S, G, cpg, pk * cpg, device=dev, dtype=F32)
+                K.gemm(A_op, B_op, slab, cpg, pk * cpg, T, ldc=pk * cpg, nseg=B // S, splits=S, batch=G,
+                       c_z1=cpg * pk * cpg, c_split=dWf.numel())
+                K.splitk_reduce(dWf, slab, S, accumulate=False)
+                del slab
             pre = "encoder.pos_conv_embed.conv.parametrizations.weight."
             wn_scratch = torch.empty(pk, device=dev, dtype=F32)
             K.weight_norm_bwd(dWf, Pm[pre + "original0"], Pm[pre + "original1"], W.wn_norms, Gv[pre + "original0"],

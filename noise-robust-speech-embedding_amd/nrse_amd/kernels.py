@@ -53,6 +53,12 @@ def workspace(nfloats: int) -> torch.Tensor:
     return torch.empty(max(int(nfloats), 4), device="cuda", dtype=torch.float32)
 
 
+def splitk_reduce(out: torch.Tensor, slab: torch.Tensor, S: int, accumulate: bool) -> None:
+    """out (+)= sum_s slab[s] in split order (nrse_splitk_reduce; out contiguous f32)."""
+    assert out.is_contiguous() and slab.numel() == S * out.numel()
+    _call("nrse_splitk_reduce", ptr(out), ptr(slab), S, out.numel(), 1 if accumulate else 0, stream_ptr())
+
+
 def rows_reduce(slab: torch.Tensor, S: int, *dsts, batch: int = 1, accumulate: bool = True) -> None:
     """Ordered sum of S partial rows [d0 | d1 | d2] into the destinations (nrse_rows_reduce);
     with batch > 1 the slab is [batch, S, n] and each destination [batch, n_j]."""
@@ -446,8 +452,8 @@ def attn_bwd(qkv, gate, bias, ctx, dctx, lse, delta, dqkv, dgate, diag, batch, T
                       ptr(dqkv), ptr(dgate), ptr(diag), batch, T, H, 64, 0.125, dropout_p, seed & 0xFFFFFFFF,
                       ptr(bias_vec))
     ws = None
-    if DETERMINISTIC and diag is not None and bias_vec is not None:
-        ws = workspace(H * batch * ((T + 63) // 64) * (2 * T - 1))
+    if DETERMINISTIC and diag is not None:
+        ws = workspace(_lib.lib().nrse_attn_bwd_workspace(ctypes.byref(p)))
         p.diag_part = ptr(ws)
     _call("nrse_attn_bwd", ctypes.byref(p), stream_ptr())
 
