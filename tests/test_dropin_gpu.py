@@ -73,9 +73,7 @@ def test_reference_loop_runs_unchanged_and_tracks_engine(nrse_device, dtype):
     batch0 = next(iter(train_loader))
     assert set(batch0) == {"clean_input_values", "noisy_input_values", "snr"}
     assert batch0["clean_input_values"].shape == (4, 1, 16000) and batch0["snr"].dtype == torch.int64
-    # lr = the config default 1e-5: the first Adam steps move every weight by ~lr*sign(g), and in
-    # bf16 the sign of near-zero gradient entries differs between two runs of the same kernels
-    # (atomic accumulation order, amplified by the heads' BatchNorm: test_bf16_gpu.py docstring)
+    # lr = the config default 1e-5: the first Adam steps move every weight by ~lr*sign(g)
     steps, lr = 3, 1e-5
     losses, batches = reference_loop(model, train_loader, config, device, steps, lr)
     # the fused engine on the same batches: AdamW + clip + EMA in kernels, LR as the loop had it
@@ -84,13 +82,13 @@ def test_reference_loop_runs_unchanged_and_tracks_engine(nrse_device, dtype):
     cur_lr = lr
     for i, (c, n, next_lr) in enumerate(batches):
         l_e = float(eng.train_step(c.squeeze(1), n.squeeze(1), lr=cur_lr, step_seed=i))
-        # step 0 (same weights, same batch) agrees to ~2e-7 in both modes. bf16 later steps: two
-        # runs of the same kernels differ by ~5e-3 rel-L2 in the step-0 gradient (atomic
-        # accumulation order through the ill-conditioned heads), so Adam's lr*sign(g) moves a few
-        # weights differently; over the loader's unseeded synthetic batches the step-1/2 losses
-        # drift by up to 1.4e-2 (tools/diag_dropin.py, 5 runs: |d| 1.3e-4 .. 1.35e-2); f32: 1e-7
-        # (tools/dbg/loop_vs_engine.py)
-        tol = 1e-5 if i == 0 else (3e-2 if dtype == torch.bfloat16 else 2e-4)
+        # step 0 (same weights, same batch) agrees to ~2e-7 in both modes; the gradient
+        # reductions are ordered (deterministic), so later steps differ only by the reference
+        # loop's torch clip / AdamW arithmetic against the fused kernels: f32 1e-7
+        # (tools/dbg/loop_vs_engine.py); in bf16 those last-bit parameter differences flip a few
+        # bf16 shadow roundings, which the heads' BatchNorm amplifies ~800x: the step-2 loss sits
+        # 4.8e-3 apart, the same on every run (it was 1.3e-4 .. 1.35e-2 with atomic reductions)
+        tol = 1e-5 if i == 0 else (1e-2 if dtype == torch.bfloat16 else 1e-3)
         assert abs(l_e - losses[i]) < tol, (i, l_e, losses[i])
         cur_lr = next_lr[0]
     d_loop = model.engine.online - flat0
