@@ -271,32 +271,33 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
         }
     }
     lpart = lpart * alpha + ps;
+    // O^T = V^T P^T (V in the A slot): lane (g, i16) holds O[its query][16 dt + 4g + r], so the
+    // rescale by its own row's alpha needs no cross-lane broadcast
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float ar = __shfl(alpha, 4 * g + r, 64);
+    for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) o[dt][r] *= ar;
-    }
+      for (int r = 0; r < 4; ++r) o[dt][r] *= alpha;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       const bf16x8 pa = pack8(pd[2 * c], pd[2 * c + 1]);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt)
-        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, rd_tr(Vt, 32 * c, 32 * c + 16, 16 * dt, lane), o[dt], 0, 0, 0);
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rd_tr(Vt, 32 * c, 32 * c + 16, 16 * dt, lane), pa, o[dt], 0, 0, 0);
     }
   }
   float l = lpart + __shfl_xor(lpart, 16, 64);
   l += __shfl_xor(l, 32, 64);
   bf16_t* ctx = (bf16_t*)p.ctx;
-  const int qrow0 = q0 + w * 16;
+  if (qv) {
+    // this lane's query row: 4 consecutive dims per dt (one 8-byte store each)
+    const float inv = dsc / l;
+    bf16_t* crow = ctx + ((long long)b * T + qi) * Hd + h * D + 4 * g;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const float lr = __shfl(l, 4 * g + r, 64);
-    const float inv = dsc / lr;
-    const int q = qrow0 + 4 * g + r;
-    if (q < T) {
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) ctx[((long long)b * T + q) * Hd + h * D + 16 * dt + i16] = f2bf(o[dt][r] * inv);
+    for (int dt = 0; dt < 4; ++dt) {
+      uint2 u;
+      u.x = (uint32_t)f2bf(o[dt][0] * inv) | ((uint32_t)f2bf(o[dt][1] * inv) << 16);
+      u.y = (uint32_t)f2bf(o[dt][2] * inv) | ((uint32_t)f2bf(o[dt][3] * inv) << 16);
+      *reinterpret_cast<uint2*>(crow + 16 * dt) = u;
     }
   }
   if (g == 0 && qv) p.lse[bh * T + qi] = (m + __builtin_amdgcn_logf(l)) * LN2;
