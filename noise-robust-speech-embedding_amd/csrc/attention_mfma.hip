@@ -151,6 +151,9 @@ NRSE_DEV void bv_stage(float* bv, const float* vec, int T, int q0, int tid) {
 // One workgroup = 64 queries (4 waves x 16) of one (b, h); K/V tiles double-buffered in LDS by
 // LDS-DMA, the next tile in flight while the current one is computed (one barrier per tile);
 // the gated bias gate[b,h,i] * vec[h, j-i+T-1] from the LDS Toeplitz copies.
+// DROP: dropout on (a compile-time branch: the runtime one made the compiler copy every
+// probability register across it, 16 v_mov per key tile)
+template <bool DROP>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_params p) {
   extern __shared__ __attribute__((aligned(16))) char dyn[];
   char* const kv0 = dyn;                       // [2 buffers][K tile, V tile]
@@ -190,7 +193,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
   const float* bvl_base = bv + bsel * bvl + (u00 - bsel);
   const uint32_t key = site_key(p.seed);
   const uint32_t thr = dropout_threshold16(p.dropout_p);
-  const bool drop = p.dropout_p > 0.f;
+  constexpr bool drop = DROP;
   const float dsc = drop ? 1.f / (1.f - p.dropout_p) : 1.f;
   // this lane's query row: key pair (kb + 16t + 4g)/2 + rp holds elements r = 2rp, 2rp + 1
   const uint32_t rowpair = (uint32_t)(bh * T + qi) * (uint32_t)((T + 1) >> 1) + (uint32_t)(2 * g);
@@ -244,8 +247,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
     float mx = -INFINITY;
 #pragma unroll
     for (int t = 0; t < 4; ++t) mx = fmaxf(mx, fmaxf(fmaxf(v[t][0], v[t][1]), fmaxf(v[t][2], v[t][3])));
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    mx = xor32_max(xor16_max(mx));
     const float mn = fmaxf(m, mx);
     const float alpha = exp2_(m - mn);
     m = mn;
@@ -258,7 +260,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
         pd[t][r] = exp2_(v[t][r] - mn);
         ps += pd[t][r];
       }
-    if (drop) {
+    if constexpr (DROP) {
 #pragma unroll
       for (int t = 0; t < 4; ++t)
         if (t < nt16) {
@@ -285,8 +287,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
         o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rd_tr(Vt, 32 * c, 32 * c + 16, 16 * dt, lane), pa, o[dt], 0, 0, 0);
     }
   }
-  float l = lpart + __shfl_xor(lpart, 16, 64);
-  l += __shfl_xor(l, 32, 64);
+  const float l = xor32_sum(xor16_sum(lpart));
   bf16_t* ctx = (bf16_t*)p.ctx;
   if (qv) {
     // this lane's query row: 4 consecutive dims per dt (one 8-byte store each)
@@ -345,8 +346,7 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
       dsum += __uint_as_float(dw[e] << 16) * __uint_as_float(ow[e] << 16) +
               __uint_as_float(dw[e] & 0xffff0000u) * __uint_as_float(ow[e] & 0xffff0000u);
   }
-  dsum += __shfl_xor(dsum, 16, 64);
-  dsum += __shfl_xor(dsum, 32, 64);
+  dsum = xor32_sum(xor16_sum(dsum));
   const long long bh = (long long)b * H + h;
   const float gi = qv ? p.gate[bh * T + qi] : 0.f;
   const float c1 = p.scale * LOG2E, gl = gi * LOG2E;
@@ -441,8 +441,7 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
         dq[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, rd_tr(Kt, 32 * c, 32 * c + 16, 16 * dt, lane), dq[dt], 0, 0, 0);
     }
   }
-  dgate += __shfl_xor(dgate, 16, 64);
-  dgate += __shfl_xor(dgate, 32, 64);
+  dgate = xor32_sum(xor16_sum(dgate));
   if (g == 0 && qv) p.dgate[bh * T + qi] = dgate;
   bf16_t* dqkv = (bf16_t*)p.dqkv + (long long)b * T * ld3;
   const int qrow0 = q0 + w * 16;
@@ -664,24 +663,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     for (int c = 0; c < 2; ++c) {
       const bf16x8 pa = pack8(pd[2 * c], pd[2 * c + 1]);
       const bf16x8 da = pack8(ds[2 * c], ds[2 * c + 1]);
+      // dV^T = dO^T P, dK^T = Q^T dS (the tiles in the A slot): lane (g, i16) accumulates its own
+      // key's dims 16 dt + 4g + r, stored as 8-byte runs below
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        dv[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, rd_tr(Ot, 32 * c, 32 * c + 16, 16 * dt, lane), dv[dt], 0, 0, 0);
-        dk[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, rd_tr(Qt, 32 * c, 32 * c + 16, 16 * dt, lane), dk[dt], 0, 0, 0);
+        dv[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rd_tr(Ot, 32 * c, 32 * c + 16, 16 * dt, lane), pa, dv[dt], 0, 0, 0);
+        dk[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rd_tr(Qt, 32 * c, 32 * c + 16, 16 * dt, lane), da, dk[dt], 0, 0, 0);
       }
     }
   }
   bf16_t* dqkv = (bf16_t*)p.dqkv + (long long)b * T * ld3;
-  const int krow0 = kb0 + w * 16;
+  if (kv) {
+    bf16_t* krow = dqkv + (long long)kj * ld3 + h * D + 4 * g;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int k = krow0 + 4 * g + r;
-    if (k < T) {
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        dqkv[(long long)k * ld3 + Hd + h * D + 16 * dt + i16] = f2bf(dk[dt][r] * p.scale);
-        dqkv[(long long)k * ld3 + 2 * Hd + h * D + 16 * dt + i16] = f2bf(dv[dt][r] * dsc);
-      }
+    for (int dt = 0; dt < 4; ++dt) {
+      uint2 uk, uv;
+      uk.x = (uint32_t)f2bf(dk[dt][0] * p.scale) | ((uint32_t)f2bf(dk[dt][1] * p.scale) << 16);
+      uk.y = (uint32_t)f2bf(dk[dt][2] * p.scale) | ((uint32_t)f2bf(dk[dt][3] * p.scale) << 16);
+      uv.x = (uint32_t)f2bf(dv[dt][0] * dsc) | ((uint32_t)f2bf(dv[dt][1] * dsc) << 16);
+      uv.y = (uint32_t)f2bf(dv[dt][2] * dsc) | ((uint32_t)f2bf(dv[dt][3] * dsc) << 16);
+      *reinterpret_cast<uint2*>(krow + Hd + 16 * dt) = uk;
+      *reinterpret_cast<uint2*>(krow + 2 * Hd + 16 * dt) = uv;
     }
   }
   if (p.diag) {  // the carried accumulator: diagonals i16 - 4g + 16w relative to kb0 - (last qb + 64)
@@ -727,7 +729,8 @@ int nrse_attn_fwd_mfma(const nrse_attn_fwd_params* p, hipStream_t st) {
     nrse_set_error("nrse_attn_fwd: T=%d too long for the LDS bias copies", p->T);
     return NRSE_ERR_UNSUPPORTED;
   }
-  hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), lds, st, *p);
+  if (p->dropout_p > 0.f) hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(256), lds, st, *p);
+  else hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(256), lds, st, *p);
   return nrse_check_launch("nrse_attn_fwd(mfma)");
 }
 

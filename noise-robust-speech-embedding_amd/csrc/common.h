@@ -193,6 +193,28 @@ struct UDiv31 {
 };
 
 // Wave-wide reductions (wave64).
+// Butterfly steps across the 16-lane rows of a wave64 with the gfx950 row-swap VALU ops instead
+// of ds_bpermute (no LDS round trip, no lane-address arithmetic): v_permlane16_swap exchanges rows
+// 1, 3 of its first operand with rows 0, 2 of its second, so with both operands = v every lane
+// gets {own, lane ^ 16} in some order; permlane32_swap likewise for lane ^ 32. max / + of the two
+// are order-independent (bitwise equal to the __shfl_xor form).
+NRSE_DEV float xor16_max(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+NRSE_DEV float xor32_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+NRSE_DEV float xor16_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+NRSE_DEV float xor32_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 NRSE_DEV float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -16,7 +16,9 @@ K.gemm_select(3)
 CLK_MHZ = float(os.environ.get("CLK_MHZ", "100"))  # s_memtime counts shader clocks; reported in kcycles
 
 
-def run(M, N, Kd, rows=256, gelu=False, reps=5):
+def run(M, N, Kd, rows=256, gelu=False, reps=5, layout="TT"):
+    """layout: TT = A and B k-contiguous (forward), FF = both m-contiguous (weight gradient:
+    A = dy^T, B = x^T over the token axis K), TF = B m-contiguous (dgrad)."""
     K.gemm_tile_rows(rows)
     a = (torch.rand(M, Kd, device="cuda") * 2 - 1).to(torch.bfloat16)
     w = (torch.rand(N, Kd, device="cuda") * 2 - 1).to(torch.bfloat16)
@@ -26,8 +28,14 @@ def run(M, N, Kd, rows=256, gelu=False, reps=5):
     nwg = -(-M // rows) * -(-N // 256)
     st = torch.zeros(8 * nwg, dtype=torch.int64, device="cuda")
     p = _lib.GemmParams()
-    p.a = K.Operand(a, True, Kd).c()
-    p.b = K.Operand(w, True, Kd).c()
+    if layout == "TT":
+        p.a = K.Operand(a, True, Kd).c()
+        p.b = K.Operand(w, True, Kd).c()
+    else:
+        at, wt = a.t().contiguous(), w.t().contiguous()
+        keep = (at, wt)
+        p.a = K.Operand(a, True, Kd).c() if layout == "TF" else K.Operand(at, False, M).c()
+        p.b = K.Operand(wt, False, N).c()
     p.M, p.N, p.K, p.nseg, p.splits, p.batch, p.zdiv = M, N, Kd, 1, 1, 1, 1
     p.alpha = 1.0
     p.c = c.data_ptr()
@@ -48,13 +56,18 @@ def run(M, N, Kd, rows=256, gelu=False, reps=5):
     d = [(t[:, i + 1] - t[:, i]).median().item() / 1e3 for i in range(7)]
     names = ["prologue", "loop", "drain", "stage0", "pass0", "pass1", "pass2+3"]
     end = (t[:, 7] - t0)
-    print(f"M={M} N={N} K={Kd} rows={rows} gelu={int(gelu)} wgs={nwg}: " +
+    print(f"{layout} M={M} N={N} K={Kd} rows={rows} gelu={int(gelu)} wgs={nwg}: " +
           " ".join(f"{n} {v:.1f}" for n, v in zip(names, d)) +
           f" kcyc (loop {d[1] / (Kd // 64):.2f}/K-tile); entry max {(t[:, 0] - t0).max().item() / 1e3:.1f}, "
           f"last end {end.max().item() / 1e3:.1f} kcyc", flush=True)
 
 
-if os.environ.get("SHAPES") == "short":
+if os.environ.get("SHAPES") == "layouts":
+    # the weight-gradient shapes of one slab split (token range 12768 / 4) and a dgrad
+    for lay in ("TT", "TF", "FF"):
+        run(1024, 4096, 3192, rows=256, layout=lay)
+        run(4096, 1024, 3192, rows=256, layout=lay)
+elif os.environ.get("SHAPES") == "short":
     run(12768, 1024, 1024, rows=256)
     run(12768, 1024, 4096, rows=256)
 else:
