@@ -305,6 +305,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
 }
 
 // ------------------------------------------------------------------------------ bwd: dQ, dgate
+template <bool DROP>
 __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_params p) {
   extern __shared__ __attribute__((aligned(16))) char dyn[];
   char* const kv0 = dyn;  // [2 buffers][K tile, V tile], LDS-DMA double buffer as in the forward
@@ -360,7 +361,7 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
   const float* bvl_base = bv + bsel * bvl + (u00 - bsel);
   const uint32_t key = site_key(p.seed);
   const uint32_t thr = dropout_threshold16(p.dropout_p);
-  const bool drop = p.dropout_p > 0.f;
+  constexpr bool drop = DROP;
   const float dsc = drop ? 1.f / (1.f - p.dropout_p) : 1.f;
   const uint32_t rowpair = (uint32_t)(bh * T + qi) * (uint32_t)((T + 1) >> 1) + (uint32_t)(2 * g);  // as fwd
   float dgate = 0.f;
@@ -400,7 +401,7 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
       const float4 v4 = *reinterpret_cast<const float4*>(bvl_base + kb + 16 * t);
       bb[t][0] = v4.x; bb[t][1] = v4.y; bb[t][2] = v4.z; bb[t][3] = v4.w;
     }
-    if (drop) {
+    if constexpr (DROP) {
 #pragma unroll
       for (int t = 0; t < 4; ++t)
         if (t < nt16) {
@@ -749,7 +750,8 @@ int nrse_attn_bwd_mfma(const nrse_attn_bwd_params* p, hipStream_t st) {
     return NRSE_ERR_UNSUPPORTED;
   }
   // the dQ kernel also produces delta = rowsum(dO * O), which the dK/dV kernel reads
-  hipLaunchKernelGGL(attn_bwd_q_kernel, grid, dim3(256), lds_q, st, *p);
+  if (p->dropout_p > 0.f) hipLaunchKernelGGL(attn_bwd_q_kernel<true>, grid, dim3(256), lds_q, st, *p);
+  else hipLaunchKernelGGL(attn_bwd_q_kernel<false>, grid, dim3(256), lds_q, st, *p);
   hipLaunchKernelGGL(attn_bwd_kv_kernel, grid, dim3(256), lds_kv, st, *p);
   const int rc = nrse_check_launch("nrse_attn_bwd(mfma)");
   if (rc || !p->diag || !p->diag_part) return rc;
