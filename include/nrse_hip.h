@@ -243,14 +243,14 @@ typedef struct {
   int batch, T, H, head_dim;
   float scale; float dropout_p; uint32_t seed;
   const float* bias_vec;               /* [H, 2T-1] (bf16 MFMA path) */
-  float* diag_part;                    /* optional (bf16 MFMA path): f32 workspace of
-                                          H * B * ceil(T/64) * (2T-1) floats; the per-block diag rows
-                                          are then added in a fixed order (deterministic) instead of
-                                          by f32 atomics */
+  float* diag_part;                    /* optional: f32 workspace of nrse_attn_bwd_workspace(p)
+                                          floats; the per-block diag rows are then added in a fixed
+                                          order (deterministic) instead of by f32 atomics */
 } nrse_attn_bwd_params;
 
 int nrse_attn_fwd(const nrse_attn_fwd_params* p, void* stream);
 int nrse_attn_bwd(const nrse_attn_bwd_params* p, void* stream);
+long long nrse_attn_bwd_workspace(const nrse_attn_bwd_params* p);  /* floats for p->diag_part */
 
 /* ------------------------------------------------------------------------------------------
  * Conv feature encoder front end and the positional-conv weight norm.
