@@ -197,14 +197,23 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
   const float dsc = drop ? 1.f / (1.f - p.dropout_p) : 1.f;
   // this lane's query row: key pair (kb + 16t + 4g)/2 + rp holds elements r = 2rp, 2rp + 1
   const uint32_t rowpair = (uint32_t)(bh * T + qi) * (uint32_t)((T + 1) >> 1) + (uint32_t)(2 * g);
-  float m = -INFINITY, lpart = 0.f;
+  // Lazy rescaling in the base-2 domain: mref is the row's reference maximum, and a tile's scores
+  // are formed relative to it in two packed fmas, v = s * c1 + (gl * bias - mref) (no separate
+  // subtract before the exponential). Only when some lane of the wave sees a score more than
+  // RESCALE_TAU above its reference (or on the first tile, where mref is not yet set) does the
+  // wave shift: mref += shift, v -= shift, o and the row sum by 2^-shift. Probabilities stay
+  // <= 2^RESCALE_TAU before normalisation, which f32 holds exactly as well as values <= 1; the
+  // output divides by the same row sum, so only bf16 rounding of P differs from rescaling per tile.
+  constexpr float RESCALE_TAU = 8.f;
+  float mref = 0.f;
+  f32x2 lpart2 = {0.f, 0.f};
   f32x4 o[4];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // In the last key tile the 16-key sub-tiles wholly past T get no dropout hashes (nt16 < 4); their
-  // probabilities are already 0. (Skipping the query waves past T with a wave-uniform branch made
-  // the compiler duplicate the loop and stage the MFMA accumulators through AGPRs: slower.)
+  // In the last key tile the keys past T get -inf scores, so probability 0 whatever the dropout
+  // hash says; every sub-tile is hashed (a per-sub-tile branch made the compiler copy the
+  // probability registers across it on every tile).
   for (int it = 0; it < ntiles; ++it) {
     const int kb = it * 64;
     char* const Kt = kv0 + (it & 1) * 2 * TILE_B;
@@ -219,9 +228,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
       kv_dma_issue(kd, Kn, kb + 64, w);
       kv_dma_issue(vd, Kn + TILE_B, kb + 64, w);
     }
-    const int nt16 = min(4, (T - kb + 15) >> 4);  // 16-key sub-tiles holding a key < T (uniform)
     // the MFMAs run on every sub-tile (a conditional MFMA makes the compiler stage its result
-    // through AGPRs); only the element work below is skipped past T
+    // through AGPRs)
     f32x4 s[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -230,13 +238,13 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
       for (int ss = 0; ss < 2; ++ss) s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rd_row(Kt, 16 * t + i16, 4 * ss + g), qf[ss], s[t], 0, 0, 0);
     }
     float v[4][4];
+    const f32x2 c12 = {c1, c1}, gl2 = {gl, gl}, nm2 = {-mref, -mref};
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const float4 bb = *reinterpret_cast<const float4*>(bvl_base + kb + 16 * t);
-      v[t][0] = fmaf(s[t][0], c1, gl * bb.x);
-      v[t][1] = fmaf(s[t][1], c1, gl * bb.y);
-      v[t][2] = fmaf(s[t][2], c1, gl * bb.z);
-      v[t][3] = fmaf(s[t][3], c1, gl * bb.w);
+      const f32x2 r0 = pk_fma(f32x2{s[t][0], s[t][1]}, c12, pk_fma(gl2, f32x2{bb.x, bb.y}, nm2));
+      const f32x2 r1 = pk_fma(f32x2{s[t][2], s[t][3]}, c12, pk_fma(gl2, f32x2{bb.z, bb.w}, nm2));
+      v[t][0] = r0.x; v[t][1] = r0.y; v[t][2] = r1.x; v[t][3] = r1.y;
     }
     if (kb + 64 > T) {
 #pragma unroll
@@ -248,37 +256,47 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
 #pragma unroll
     for (int t = 0; t < 4; ++t) mx = fmaxf(mx, fmaxf(fmaxf(v[t][0], v[t][1]), fmaxf(v[t][2], v[t][3])));
     mx = xor32_max(xor16_max(mx));
-    const float mn = fmaxf(m, mx);
-    const float alpha = exp2_(m - mn);
-    m = mn;
+    if (it == 0 || __builtin_amdgcn_ballot_w64(mx > RESCALE_TAU)) {
+      // shift to the tile's maximum: on the first tile unconditionally (mref = 0 was a
+      // placeholder; o and the row sum are still zero), later only upwards
+      const float sh = it == 0 ? mx : fmaxf(mx, 0.f);
+      const float alpha = it == 0 ? 1.f : exp2_(-sh);
+      mref += sh;
+      const f32x2 sh2 = {sh, sh}, al2 = {alpha, alpha};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const f32x2 a0 = f32x2{v[t][0], v[t][1]} - sh2, a1 = f32x2{v[t][2], v[t][3]} - sh2;
+        v[t][0] = a0.x; v[t][1] = a0.y; v[t][2] = a1.x; v[t][3] = a1.y;
+      }
+      lpart2 *= al2;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const f32x2 o0 = f32x2{o[dt][0], o[dt][1]} * al2, o1 = f32x2{o[dt][2], o[dt][3]} * al2;
+        o[dt] = f32x4{o0.x, o0.y, o1.x, o1.y};
+      }
+    }
     float pd[4][4];
-    float ps = 0.f;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        pd[t][r] = exp2_(v[t][r] - mn);
-        ps += pd[t][r];
-      }
+      for (int r = 0; r < 4; ++r) pd[t][r] = exp2_(v[t][r]);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) lpart2 += f32x2{pd[t][0], pd[t][1]} + f32x2{pd[t][2], pd[t][3]};
     if constexpr (DROP) {
 #pragma unroll
       for (int t = 0; t < 4; ++t)
-        if (t < nt16) {
 #pragma unroll
-          for (int rp = 0; rp < 2; ++rp) {
-            const uint32_t hh = mix32((rowpair + (uint32_t)((kb >> 1) + 8 * t + rp)) ^ key);
-            pd[t][2 * rp] = attn_half_keep(hh, 0, thr) ? pd[t][2 * rp] : 0.f;
-            pd[t][2 * rp + 1] = attn_half_keep(hh, 1, thr) ? pd[t][2 * rp + 1] : 0.f;
-          }
+        for (int rp = 0; rp < 2; ++rp) {
+          const uint32_t hh = mix32((rowpair + (uint32_t)((kb >> 1) + 8 * t + rp)) ^ key);
+          pd[t][2 * rp] = attn_half_keep(hh, 0, thr) ? pd[t][2 * rp] : 0.f;
+          pd[t][2 * rp + 1] = attn_half_keep(hh, 1, thr) ? pd[t][2 * rp + 1] : 0.f;
+          // opaque to the optimiser: otherwise it pushes the bf16 conversion into each select
+          // (16 conversions + 8 v_perm per tile instead of 8 packed conversions)
+          asm("" : "+v"(pd[t][2 * rp]), "+v"(pd[t][2 * rp + 1]));
         }
     }
-    lpart = lpart * alpha + ps;
     // O^T = V^T P^T (V in the A slot): lane (g, i16) holds O[its query][16 dt + 4g + r], so the
     // rescale by its own row's alpha needs no cross-lane broadcast
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) o[dt][r] *= alpha;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       const bf16x8 pa = pack8(pd[2 * c], pd[2 * c + 1]);
@@ -287,6 +305,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
         o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rd_tr(Vt, 32 * c, 32 * c + 16, 16 * dt, lane), pa, o[dt], 0, 0, 0);
     }
   }
+  const float lpart = lpart2.x + lpart2.y;
+  const float m = mref;
   const float l = xor32_sum(xor16_sum(lpart));
   bf16_t* ctx = (bf16_t*)p.ctx;
   if (qv) {
