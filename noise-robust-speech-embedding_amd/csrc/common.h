@@ -64,10 +64,21 @@ NRSE_DEV float erf_fast(float x) {
   return x * p * __builtin_amdgcn_rcpf(q);
 }
 NRSE_DEV float gelu_fast(float x) { return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f)); }
+// GELU'(x) = Phi(x) + x phi(x) with ONE exponential shared by both terms: Phi from the
+// Abramowitz-Stegun 7.1.26 form erfc(a) = poly(t) e^{-a^2}, t = 1 / (1 + p a), a = |x| / sqrt2,
+// so e = exp(-x^2 / 2) is also sqrt(2 pi) phi(x). |error| < 3.0e-7 over all x evaluated in f32
+// (the rational-erf form it replaces: 2.6e-7), 16 instructions instead of 22 (both with one rcp
+// and one exp): the GELU' of the conv0 / conv-stack LN backward and of the GELU_BWD epilogues.
 NRSE_DEV float gelu_grad_fast(float x) {
-  const float cdf = 0.5f * (1.0f + erf_fast(x * 0.70710678118654752f));
-  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
-  return cdf + x * pdf;
+  const float t = __builtin_amdgcn_rcpf(fmaf(__builtin_fabsf(x), 0.3275911f * 0.70710678118654752f, 1.0f));
+  float q = fmaf(t, 1.061405429f, -1.453152027f);
+  q = fmaf(t, q, 1.421413741f);
+  q = fmaf(t, q, -0.284496736f);
+  q = fmaf(t, q, 0.254829592f);
+  const float e = __builtin_amdgcn_exp2f((x * (-0.5f * 1.4426950408889634f)) * x);
+  const float h = 0.5f * (t * q) * e;  // 0.5 erfc(|x| / sqrt2)
+  const float cdf = x >= 0.f ? 1.0f - h : h;
+  return fmaf(x * 0.39894228040143268f, e, cdf);
 }
 // Two-lane (packed FP32) forms of the same evaluation, op for op: the polynomial FMAs and
 // products issue as v_pk_fma_f32 / v_pk_mul_f32 (two elements per VALU instruction); the clamp
