@@ -82,9 +82,10 @@ NRSE_DEV float gelu_grad_fast(float x) {
 }
 // Two-lane (packed FP32) forms of the same evaluation, op for op: the polynomial FMAs and
 // products issue as v_pk_fma_f32 / v_pk_mul_f32 (two elements per VALU instruction); the clamp
-// (v_med3), rcp and exp stay per element. Used where measured faster (conv0 forward, 5%); in the
-// GEMM epilogue the compiler's own packing of the scalar form measured 1% faster per step, and
-// in the LN kernels and conv0 backward the packed form was neutral or slower.
+// (v_med3), rcp and exp stay per element. Used where measured faster (conv0 forward, 5%; the
+// 256x256 GEMM's register epilogue, FFN-up +1.4 % isolated in r03 -- an r02 GEMM epilogue had
+// measured 1 % slower with it); in the LN kernels and conv0 backward the packed form was neutral
+// or slower.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 NRSE_DEV f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
 NRSE_DEV f32x2 splat2(float v) { return f32x2{v, v}; }

@@ -243,8 +243,10 @@ NRSE_DEV void fast_epilogue(const nrse_gemm_params& p, const f32x4 (&acc)[8][4],
           u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
           u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
           *reinterpret_cast<uint2*>(aimg + prow * APITCH + tcol * 2) = u;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = gelu_fast(v[e]);
+          {  // packed FP32 pairs (FFN-up 773-775 -> 781-789 TF isolated; step neutral)
+            const f32x2 g0 = gelu2(f32x2{v[0], v[1]}), g1 = gelu2(f32x2{v[2], v[3]});
+            v[0] = g0.x; v[1] = g0.y; v[2] = g1.x; v[3] = g1.y;
+          }
         }
         if constexpr (GELUB) {
           uint2 u = make_uint2(0, 0);
