@@ -123,8 +123,9 @@ def bench_emotion(args):
     torch.cuda.set_device(0)
     B = 36 if args.batch == 32 else args.batch
     L = int(5.0 * 16000)
-    cdt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
-    eng = ByolEngine(A.LARGE, 1024, 2048, device=dev, compute_dtype=cdt, seed=1234)
+    from nrse_amd.engine import compute_mode
+    cdt, wsplit = compute_mode(args.dtype)
+    eng = ByolEngine(A.LARGE, 1024, 2048, device=dev, compute_dtype=cdt, seed=1234, weight_split=wsplit)
     head = EmotionHead(1024, 1024, 8, dropout=0.3, device=dev, compute_dtype=cdt, seed=42)
     tr = EmotionDimTrainer(eng, head, lr=1e-5, weight_decay=1e-4)
     gen = torch.Generator(device=dev)
@@ -189,7 +190,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--seconds", type=float, default=8.0)
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "bf16sw", "f32"],
+                    help="bf16 (the metric's mode), bf16sw (bf16 activations x split hi+lo bf16 weights in the "
+                         "forward: embeddings within the north-star 1e-3), f32 (exact parity mode)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--detail", default=None, help="write per-shape GEMM timings here (json)")
     ap.add_argument("--serial-optimizer", action="store_true",
@@ -210,7 +213,7 @@ def main():
         sys.exit(launch_ranks(args.gpus))
 
     from nrse_amd import arch as A, ddp, kernels as K
-    from nrse_amd.engine import ByolEngine, StepConfig
+    from nrse_amd.engine import ByolEngine, StepConfig, compute_mode
 
     rank, world, local = ddp.init_from_env()
     if world != args.gpus:
@@ -221,8 +224,8 @@ def main():
     arch = A.LARGE
     B = args.batch
     L = int(args.seconds * 16000)
-    cdt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
-    eng = ByolEngine(arch, 1024, 2048, device=dev, compute_dtype=cdt, seed=1234,
+    cdt, wsplit = compute_mode(args.dtype)
+    eng = ByolEngine(arch, 1024, 2048, device=dev, compute_dtype=cdt, seed=1234, weight_split=wsplit,
                      step_cfg=StepConfig(ema_decay=0.997, overlap_optimizer=not args.serial_optimizer))
     allreduce = (ddp.GradAllReduce(wire_dtype=torch.bfloat16 if args.wire == "bf16" else None)
                  if world > 1 else None)

@@ -322,6 +322,9 @@ int nrse_colsum(const void* x, int dtype, float* colsum, long long rows, int C, 
 long long nrse_colsum_workspace(long long rows, int C);
 /* y = x cast (f32 <-> bf16), n elements */
 int nrse_cast(const void* x, int x_dtype, void* y, int y_dtype, long long n, void* stream);
+/* split-bf16 pair of an f32 tensor: hi = bf16(x), lo = bf16(x - hi) (the split-weight mode's GEMM
+ * operand planes: x @ (hi + lo) carries the f32 weight to ~2^-17 relative) */
+int nrse_split_bf16(const float* x, void* hi, void* lo, long long n, void* stream);
 /* Split-K reduction of a weight gradient (the Linear wgrads of the backward, train_byol.py:65):
  * dst[i] (+)= sum_s slabs[s * n + i], s = 0 .. splits-1, in split order (deterministic); f32;
  * accumulate = 0 overwrites dst. The partial slabs are written by nrse_gemm with c_split = n. */
@@ -403,10 +406,13 @@ typedef struct {
   float lr, beta1, beta2, eps, weight_decay; int step;
   float max_norm; const double* sumsq;    /* clip coefficient min(1, max_norm/(sqrt(sumsq)+1e-6)) */
   float grad_scale;                       /* extra multiplier on g (e.g. 1/world_size) */
+  void* p_shadow_lo;                      /* optional (bf16 shadow only): lo = bf16(p - shadow), the
+                                             split-weight mode's second weight plane */
 } nrse_adamw_params;
 int nrse_adamw(const nrse_adamw_params* p, void* stream);
+/* t_shadow_lo: optional, as nrse_adamw_params.p_shadow_lo */
 int nrse_ema(float* target, const float* online, void* t_shadow, int shadow_dtype, long long n, float decay,
-             void* stream);
+             void* t_shadow_lo, void* stream);
 /* health check (train_byol.py:52-59 / debugging_utils.py:4-30): accumulates into the caller-zeroed
  * stats[0..3] = NaN count, Inf count, sum|x| over finite x, max|x| over finite x (decisions on the
  * host, nrse_amd/health.py, in check_audio_tensor's order) */

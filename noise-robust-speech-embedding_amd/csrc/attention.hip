@@ -342,7 +342,9 @@ __global__ __launch_bounds__(64) void attn_bwd_kv_f32_kernel(const nrse_attn_bwd
   __shared__ float Qs[64][HD + 1];
   __shared__ float Os[64][HD + 1];   // dO tile
   __shared__ float rowc[4][64];      // lse, delta, gate per query
-  __shared__ float dg[128];
+  // rel-pos diagonal sums of this key tile over ALL query tiles (dynamic LDS, f32_diag_len(T)
+  // floats): diagonal j - i at dg[(j - i) - (j0 - Tq + 1)], Tq = T rounded up to the query tile
+  extern __shared__ float dg[];
   const int Tn = p.T, H = p.H, Hd = H * HD;
   const int b = blockIdx.z, h = blockIdx.y;
   const int j = blockIdx.x * 64 + threadIdx.x;
@@ -360,6 +362,10 @@ __global__ __launch_bounds__(64) void attn_bwd_kv_f32_kernel(const nrse_attn_bwd
   const uint32_t thr = dropout_threshold16(p.dropout_p);
   const float dsc = p.dropout_p > 0.f ? 1.f / (1.f - p.dropout_p) : 1.f;
   const int nd = 2 * Tn - 1;
+  const int nq = (Tn + 63) / 64;
+  const int ndg = nq * 64 + 63;       // diagonals j - i of this key tile: (j0 - Tq + 1) .. (j0 + 63)
+  const int dg0 = blockIdx.x * 64 - nq * 64 + 1;
+  for (int e = threadIdx.x; e < ndg; e += 64) dg[e] = 0.f;
   for (int i0 = 0; i0 < Tn; i0 += 64) {
     __syncthreads();
     for (int e = threadIdx.x; e < 64 * HD; e += 64) {
@@ -377,8 +383,6 @@ __global__ __launch_bounds__(64) void attn_bwd_kv_f32_kernel(const nrse_attn_bwd
       rowc[1][threadIdx.x] = ok ? p.delta[ri] : 0.f;
       rowc[2][threadIdx.x] = ok ? p.gate[ri] : 0.f;
     }
-    dg[threadIdx.x] = 0.f;
-    dg[64 + threadIdx.x] = 0.f;
     __syncthreads();
     const int ni = min(64, Tn - i0);
     if (valid) {
@@ -400,26 +404,25 @@ __global__ __launch_bounds__(64) void attn_bwd_kv_f32_kernel(const nrse_attn_bwd
         const float ds = pr * (dp - rowc[1][ii]);
 #pragma unroll
         for (int d = 0; d < HD; ++d) { dv[d] += pd * Os[ii][d]; dk[d] += ds * Qs[ii][d]; }
-        // diag index relative to this tile pair: (j - i) - (j0 - i0) + 63 in [0, 127)
-        atomicAdd(&dg[(j - blockIdx.x * 64) - ii + 63], ds * gi);
+        // one wave: for a given ii the 64 lanes add to 64 distinct diagonals, and the ii / i0
+        // order is program order, so the sums are deterministic
+        atomicAdd(&dg[(j - i) - dg0], ds * gi);
       }
     }
-    __syncthreads();
-    if (p.diag && p.diag_part) {
-      // row (h, b, key tile, query tile) of the partial slab: this tile pair's 127 diagonals, zeros
-      // elsewhere (added in order by nrse_rows_reduce: deterministic)
-      const int nq = (Tn + 63) / 64;
-      float* prow = p.diag_part + ((((long long)h * p.batch + b) * gridDim.x + blockIdx.x) * nq + i0 / 64) * nd;
-      const int e0 = (blockIdx.x * 64 - i0) - 63 + Tn - 1;
-      for (int dd = threadIdx.x; dd < nd; dd += 64) {
-        const int e = dd - e0;
-        prow[dd] = (e >= 0 && e < 127) ? dg[e] : 0.f;
-      }
-    } else if (p.diag) {
-      for (int e = threadIdx.x; e < 127; e += 64) {
-        const int dd = (blockIdx.x * 64 - i0) + e - 63 + Tn - 1;
-        if (dd >= 0 && dd < nd && dg[e] != 0.f) atomicAdd(p.diag + (long long)h * nd + dd, dg[e]);
-      }
+  }
+  __syncthreads();
+  if (p.diag && p.diag_part) {
+    // row (h, b, key tile) of the partial slab: this key tile's diagonals, zeros elsewhere
+    // (added in (b, key tile) order by nrse_rows_reduce: deterministic)
+    float* prow = p.diag_part + (((long long)h * p.batch + b) * gridDim.x + blockIdx.x) * nd;
+    for (int dd = threadIdx.x; dd < nd; dd += 64) {
+      const int e = dd - (Tn - 1) - dg0;
+      prow[dd] = (e >= 0 && e < ndg) ? dg[e] : 0.f;
+    }
+  } else if (p.diag) {
+    for (int e = threadIdx.x; e < ndg; e += 64) {
+      const int dd = dg0 + e + Tn - 1;
+      if (dd >= 0 && dd < nd && dg[e] != 0.f) atomicAdd(p.diag + (long long)h * nd + dd, dg[e]);
     }
   }
   if (!valid) return;
@@ -590,13 +593,11 @@ extern "C" int nrse_attn_fwd(const nrse_attn_fwd_params* p, void* stream) {
   return nrse_check_launch("nrse_attn_fwd");
 }
 
-// diag partial rows: per (h, b, key tile) on the bf16 MFMA path, per (h, b, key tile, query tile)
-// on the f32 path
+// diag partial rows: one per (h, b, key tile) on both paths
 extern "C" long long nrse_attn_bwd_workspace(const nrse_attn_bwd_params* p) {
   if (!p || p->T <= 0 || p->batch <= 0 || p->H <= 0) return 0;
   const long long nt = (p->T + 63) / 64;
-  const long long rows = nrse_attn_use_mfma(p->dtype, p->head_dim) ? nt : nt * nt;
-  return (long long)p->H * p->batch * rows * (2LL * p->T - 1);
+  return (long long)p->H * p->batch * nt * (2LL * p->T - 1);
 }
 
 extern "C" int nrse_attn_bwd(const nrse_attn_bwd_params* p, void* stream) {
@@ -611,16 +612,17 @@ extern "C" int nrse_attn_bwd(const nrse_attn_bwd_params* p, void* stream) {
   if (p->dtype == NRSE_BF16) hipLaunchKernelGGL(attn_delta_kernel<bf16_t>, g1, dim3(256), 0, st, *p);
   else hipLaunchKernelGGL(attn_delta_kernel<float>, g1, dim3(256), 0, st, *p);
   dim3 grid((p->T + 63) / 64, p->H, p->batch);
+  const size_t dg_lds = (size_t)(((p->T + 63) / 64) * 64 + 63) * sizeof(float);
+  NRSE_REQUIRE(dg_lds <= 96 * 1024, "nrse_attn_bwd: T=%d too long for the f32 path's diagonal accumulator", p->T);
   if (p->dtype == NRSE_BF16) {
-    hipLaunchKernelGGL(attn_bwd_kv_f32_kernel<bf16_t>, grid, dim3(64), 0, st, *p);
+    hipLaunchKernelGGL(attn_bwd_kv_f32_kernel<bf16_t>, grid, dim3(64), dg_lds, st, *p);
     hipLaunchKernelGGL(attn_bwd_q_f32_kernel<bf16_t>, grid, dim3(64), 0, st, *p);
   } else {
-    hipLaunchKernelGGL(attn_bwd_kv_f32_kernel<float>, grid, dim3(64), 0, st, *p);
+    hipLaunchKernelGGL(attn_bwd_kv_f32_kernel<float>, grid, dim3(64), dg_lds, st, *p);
     hipLaunchKernelGGL(attn_bwd_q_f32_kernel<float>, grid, dim3(64), 0, st, *p);
   }
   const int rc = nrse_check_launch("nrse_attn_bwd");
   if (rc || !p->diag || !p->diag_part) return rc;
   const int nt = (p->T + 63) / 64;
-  return nrse_rows_reduce(p->diag, 2LL * p->T - 1, nullptr, 0, nullptr, 0, p->diag_part, p->batch * nt * nt, p->H, 1,
-                          st);
+  return nrse_rows_reduce(p->diag, 2LL * p->T - 1, nullptr, 0, nullptr, 0, p->diag_part, p->batch * nt, p->H, 1, st);
 }

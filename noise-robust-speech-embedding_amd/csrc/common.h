@@ -28,6 +28,11 @@ NRSE_DEV bf16_t f2bf(float x) {
   __bf16 b = (__bf16)x;  // v_cvt_pk_bf16_f32: round-to-nearest-even, NaN stays NaN
   return *reinterpret_cast<bf16_t*>(&b);
 }
+// low half of the split-bf16 pair of x: bf16(x - float(bf16(x)))
+NRSE_DEV bf16_t bf16_lo(float x) {
+  const bf16_t h = f2bf(x);
+  return f2bf(x - __uint_as_float((uint32_t)h << 16));
+}
 
 template <typename T> NRSE_DEV float to_f(T x);
 template <> NRSE_DEV float to_f<float>(float x) { return x; }

@@ -246,6 +246,15 @@ __global__ void cast_kernel(const void* __restrict__ x, int xdt, void* __restric
     store_from_f(y, ydt, i, load_as_f(x, xdt, i));
 }
 
+__global__ void split_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ hi, bf16_t* __restrict__ lo,
+                                  long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float v = x[i];
+    hi[i] = f2bf(v);
+    lo[i] = bf16_lo(v);
+  }
+}
+
 __global__ void swap12_kernel(const void* __restrict__ src, int sdt, void* __restrict__ dst, int ddt, int d0, int d1,
                               int d2, int acc) {
   const long long total = (long long)d0 * d1 * d2;
@@ -398,6 +407,14 @@ extern "C" int nrse_colsum(const void* x, int dt, float* colsum, long long rows,
   const int rc = nrse_check_launch("nrse_colsum");
   if (rc || !part) return rc;
   return nrse_rows_reduce(colsum, C, nullptr, 0, nullptr, 0, part, (int)nchunks, 1, 1, stream);
+}
+
+extern "C" int nrse_split_bf16(const float* x, void* hi, void* lo, long long n, void* stream) {
+  NRSE_REQUIRE(x && hi && lo && n >= 0, "nrse_split_bf16: bad args");
+  if (n == 0) return NRSE_OK;
+  hipLaunchKernelGGL(split_bf16_kernel, dim3(blocks_for(n)), dim3(256), 0, (hipStream_t)stream, x, (bf16_t*)hi,
+                     (bf16_t*)lo, n);
+  return nrse_check_launch("nrse_split_bf16");
 }
 
 extern "C" int nrse_cast(const void* x, int xdt, void* y, int ydt, long long n, void* stream) {

@@ -9,6 +9,21 @@
 
 namespace {
 
+// bf16 shadow of 4 consecutive f32 values at float4 index q; with lo (the split-weight mode), also
+// the residual plane lo = bf16(x - hi), so hi + lo carries the f32 weight to ~2^-17 relative
+NRSE_DEV void store_bf16x4(void* hi, void* lo, long long q, const float* x) {
+  uint2 u;
+  u.x = (uint32_t)f2bf(x[0]) | ((uint32_t)f2bf(x[1]) << 16);
+  u.y = (uint32_t)f2bf(x[2]) | ((uint32_t)f2bf(x[3]) << 16);
+  reinterpret_cast<uint2*>(hi)[q] = u;
+  if (lo) {
+    uint2 w;
+    w.x = (uint32_t)f2bf(x[0] - __uint_as_float(u.x << 16)) | ((uint32_t)f2bf(x[1] - __uint_as_float(u.x & 0xffff0000u)) << 16);
+    w.y = (uint32_t)f2bf(x[2] - __uint_as_float(u.y << 16)) | ((uint32_t)f2bf(x[3] - __uint_as_float(u.y & 0xffff0000u)) << 16);
+    reinterpret_cast<uint2*>(lo)[q] = w;
+  }
+}
+
 __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x, long long n, double* __restrict__ out,
                                                     double* __restrict__ part) {
   __shared__ double red[4];
@@ -78,10 +93,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(const nrse_adamw_params p) {
     reinterpret_cast<float4*>(p.v)[q] = vv;
     if (p.p_shadow) {
       if (p.shadow_dtype == NRSE_BF16) {
-        uint2 u;
-        u.x = (uint32_t)f2bf(pa[0]) | ((uint32_t)f2bf(pa[1]) << 16);
-        u.y = (uint32_t)f2bf(pa[2]) | ((uint32_t)f2bf(pa[3]) << 16);
-        reinterpret_cast<uint2*>(p.p_shadow)[q] = u;
+        store_bf16x4(p.p_shadow, p.p_shadow_lo, q, pa);
       } else {
         reinterpret_cast<float4*>(p.p_shadow)[q] = pv;
       }
@@ -95,11 +107,13 @@ __global__ __launch_bounds__(256) void adamw_kernel(const nrse_adamw_params p) {
     const float denom = sqrtf(p.v[i]) / bc2s + p.eps;
     p.p[i] = w - step_size * p.m[i] / denom;
     if (p.p_shadow) store_from_f(p.p_shadow, p.shadow_dtype, i, p.p[i]);
+    if (p.p_shadow_lo) ((bf16_t*)p.p_shadow_lo)[i] = bf16_lo(p.p[i]);
   }
 }
 
 __global__ __launch_bounds__(256) void ema_kernel(float* __restrict__ t, const float* __restrict__ o,
-                                                  void* __restrict__ ts, int sdt, long long n, float decay) {
+                                                  void* __restrict__ ts, int sdt, long long n, float decay,
+                                                  void* __restrict__ tlo) {
   const float om = 1.f - decay;
   const long long n4 = n / 4;
   for (long long q = (long long)blockIdx.x * 256 + threadIdx.x; q < n4; q += (long long)gridDim.x * 256) {
@@ -110,10 +124,7 @@ __global__ __launch_bounds__(256) void ema_kernel(float* __restrict__ t, const f
     reinterpret_cast<float4*>(t)[q] = tv;
     if (ts) {
       if (sdt == NRSE_BF16) {
-        uint2 u;
-        u.x = (uint32_t)f2bf(tv.x) | ((uint32_t)f2bf(tv.y) << 16);
-        u.y = (uint32_t)f2bf(tv.z) | ((uint32_t)f2bf(tv.w) << 16);
-        reinterpret_cast<uint2*>(ts)[q] = u;
+        store_bf16x4(ts, tlo, q, &tv.x);
       } else {
         reinterpret_cast<float4*>(ts)[q] = tv;
       }
@@ -122,6 +133,7 @@ __global__ __launch_bounds__(256) void ema_kernel(float* __restrict__ t, const f
   for (long long i = n4 * 4 + (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
     t[i] = decay * t[i] + om * o[i];
     if (ts) store_from_f(ts, sdt, i, t[i]);
+    if (tlo) ((bf16_t*)tlo)[i] = bf16_lo(t[i]);
   }
 }
 
@@ -175,16 +187,21 @@ extern "C" int nrse_adamw(const nrse_adamw_params* p, void* stream) {
   NRSE_REQUIRE(p && p->p && p->g && p->m && p->v && p->n >= 0 && p->step >= 1, "nrse_adamw: bad args");
   NRSE_REQUIRE((((uintptr_t)p->p | (uintptr_t)p->g | (uintptr_t)p->m | (uintptr_t)p->v) & 15) == 0,
                "nrse_adamw: buffers must be 16-byte aligned");
+  NRSE_REQUIRE(!p->p_shadow_lo || (p->p_shadow && p->shadow_dtype == NRSE_BF16 && ((uintptr_t)p->p_shadow_lo & 7) == 0),
+               "nrse_adamw: p_shadow_lo needs a bf16 p_shadow and 8-byte alignment");
   if (p->n == 0) return NRSE_OK;
   hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(p->n)), dim3(256), 0, (hipStream_t)stream, *p);
   return nrse_check_launch("nrse_adamw");
 }
 
-extern "C" int nrse_ema(float* t, const float* o, void* ts, int sdt, long long n, float decay, void* stream) {
+extern "C" int nrse_ema(float* t, const float* o, void* ts, int sdt, long long n, float decay, void* ts_lo,
+                        void* stream) {
   NRSE_REQUIRE(t && o && n >= 0, "nrse_ema: bad args");
   NRSE_REQUIRE((((uintptr_t)t | (uintptr_t)o) & 15) == 0, "nrse_ema: buffers must be 16-byte aligned");
+  NRSE_REQUIRE(!ts_lo || (ts && sdt == NRSE_BF16 && ((uintptr_t)ts_lo & 7) == 0),
+               "nrse_ema: t_shadow_lo needs a bf16 t_shadow and 8-byte alignment");
   if (n == 0) return NRSE_OK;
-  hipLaunchKernelGGL(ema_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, t, o, ts, sdt, n, decay);
+  hipLaunchKernelGGL(ema_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, t, o, ts, sdt, n, decay, ts_lo);
   return nrse_check_launch("nrse_ema");
 }
 

@@ -84,15 +84,19 @@ __global__ __launch_bounds__(PNTHR, 2) void posconv_kernel(const nrse_gemm_param
     const int c = (lane & 7) ^ (r & 7);
     wvoff[j] = (unsigned)(((long long)r * p.b.ld + c * 8) * 2);
   }
+  // iteration t runs tap t % taps of weight segment t / taps: nseg = 2 is the split-weight mode
+  // (hi and lo bf16 planes seg_stride apart, A's window read again for the lo plane)
+  const int iters = taps * p.nseg;
   auto stage_w = [&](int t) {
     char* dst = wring + (t % WRING) * WSLOT;
-    const unsigned soff = (unsigned)(t * PCH * 2);
+    const int sg = t >= taps ? 1 : 0;
+    const unsigned soff = (unsigned)((t - sg * taps) * PCH * 2 + (long long)sg * p.b.seg_stride * 2);
 #pragma unroll
     for (int j = 0; j < 2; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void*)(dst + (wave * 2 + j) * 1024), 16, wvoff[j], soff, 0, 0);
   };
   stage_w(0);
-  if (taps > 1) stage_w(1);
+  if (iters > 1) stage_w(1);
 
   f32x4 acc[4][4];
 #pragma unroll
@@ -101,16 +105,16 @@ __global__ __launch_bounds__(PNTHR, 2) void posconv_kernel(const nrse_gemm_param
     for (int c = 0; c < 4; ++c) acc[a][c] = f32x4{0.f, 0.f, 0.f, 0.f};
 
 #pragma unroll 1
-  for (int t = 0; t < taps; ++t) {
+  for (int t = 0, tap = 0; t < iters; ++t, tap = (tap + 1 == taps ? 0 : tap + 1)) {
     // tap t's weights (and, at t = 0, the window) landed for this wave; the barrier makes every
     // wave's DMAs visible and retires the reads of the slot restaged below (tap t - 1's)
-    if (t + 1 < taps) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    if (t + 1 < iters) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // raw barrier: no fence, so tap t + 1's DMAs stay in flight across it
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (t + 2 < taps) stage_w(t + 2);
+    if (t + 2 < iters) stage_w(t + 2);
     const char* ws = wring + (t % WRING) * WSLOT;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -118,7 +122,7 @@ __global__ __launch_bounds__(PNTHR, 2) void posconv_kernel(const nrse_gemm_param
 #pragma unroll
       for (int fj = 0; fj < 4; ++fj) fb[fj] = frag7(ws, fj * 16, s, lane);
 #pragma unroll
-      for (int fi = 0; fi < 4; ++fi) fa[fi] = frag7(win, wave * 64 + fi * 16 + t, s, lane);
+      for (int fi = 0; fi < 4; ++fi) fa[fi] = frag7(win, wave * 64 + fi * 16 + tap, s, lane);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int fi = 0; fi < 4; ++fi)
@@ -313,7 +317,9 @@ bool nrse_posconv_ok(const nrse_gemm_params* p) {
   const nrse_gemm_operand& b = p->b;
   if (a.dtype != NRSE_BF16 || b.dtype != NRSE_BF16 || !a.kcontig || !b.kcontig) return false;
   if (a.chunk_shift != 6 || a.ld_chunk != a.ld || b.chunk_shift != 0) return false;
-  if (p->N != PCH || p->nseg != 1 || p->splits != 1 || p->K % PCH != 0) return false;
+  if (p->N != PCH || p->splits != 1 || p->K % PCH != 0) return false;
+  // nseg = 2: the split-weight mode (the same window against two weight planes)
+  if (p->nseg != 1 && !(p->nseg == 2 && a.seg_stride == 0 && b.seg_stride > 0)) return false;
   const int taps = p->K / PCH;
   if (taps < 1 || taps > WIN_ROWS - PBM + 1) return false;
   if (p->flags & (NRSE_EPI_ATOMIC | NRSE_EPI_COLSUM)) return false;

@@ -103,7 +103,8 @@ class Conv0Params(ctypes.Structure):
 class AdamWParams(ctypes.Structure):
     _fields_ = [("p", c_vp), ("g", c_vp), ("m", c_vp), ("v", c_vp), ("p_shadow", c_vp), ("shadow_dtype", c_int),
                 ("n", c_ll), ("lr", c_f), ("beta1", c_f), ("beta2", c_f), ("eps", c_f), ("weight_decay", c_f),
-                ("step", c_int), ("max_norm", c_f), ("sumsq", c_vp), ("grad_scale", c_f)]
+                ("step", c_int), ("max_norm", c_f), ("sumsq", c_vp), ("grad_scale", c_f),
+                ("p_shadow_lo", c_vp)]
 
 
 _P = ctypes.POINTER
@@ -145,6 +146,7 @@ _SIGNATURES = {
     "nrse_colsum": ([c_vp, c_int, c_vp, c_ll, c_int, c_vp, c_vp], c_int),
     "nrse_colsum_workspace": ([c_ll, c_int], c_ll),
     "nrse_cast": ([c_vp, c_int, c_vp, c_int, c_ll, c_vp], c_int),
+    "nrse_split_bf16": ([c_vp, c_vp, c_vp, c_ll, c_vp], c_int),
     "nrse_splitk_reduce": ([c_vp, c_vp, c_int, c_ll, c_int, c_vp], c_int),
     "nrse_rows_reduce": ([c_vp, c_ll, c_vp, c_ll, c_vp, c_ll, c_vp, c_int, c_int, c_int, c_vp], c_int),
     "nrse_swap12": ([c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
@@ -160,7 +162,7 @@ _SIGNATURES = {
     "nrse_byol_loss": ([c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_f, c_vp, c_vp], c_int),
     "nrse_sumsq": ([c_vp, c_ll, c_vp, c_vp, c_vp], c_int),
     "nrse_adamw": ([_P(AdamWParams), c_vp], c_int),
-    "nrse_ema": ([c_vp, c_vp, c_vp, c_int, c_ll, c_f, c_vp], c_int),
+    "nrse_ema": ([c_vp, c_vp, c_vp, c_int, c_ll, c_f, c_vp, c_vp], c_int),
     "nrse_health": ([c_vp, c_int, c_ll, c_vp, c_vp], c_int),
     "nrse_asp_fwd": ([c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp], c_int),
     "nrse_asp_bwd": ([c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp,

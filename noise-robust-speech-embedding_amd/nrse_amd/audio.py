@@ -6,7 +6,9 @@ in this image, so:
 
 * decoding: PCM WAV through the stdlib `wave` reader; `.flac` / `.mp3` are discovered like the
   reference but cannot be decoded here -- `load_audio` raises `AudioDecodeError`, which the
-  datasets turn into the reference's load-error path (`None`, logged once per file, retry);
+  datasets turn into the reference's load-error path (`None`, logged once per file, retry); a
+  file list in which more than half the files cannot be decoded is refused up front
+  (`check_decodable`), so such a corpus fails loudly instead of training on retries;
 * resampling: `resample` restates torchaudio.functional.resample's default method
   (`sinc_interp_hann`, lowpass_filter_width 6, rolloff 0.99; torchaudio 2.x
   `_get_sinc_resample_kernel` / `_apply_sinc_resample_kernel`): a windowed-sinc polyphase filter
@@ -44,6 +46,41 @@ def get_audio_files(path: str, exts=AUDIO_EXTS) -> list:
             if os.path.splitext(f)[1].lower() in exts:
                 out.append(os.path.join(root, f))
     return sorted(out)
+
+
+def undecodable_share(files: list, probe: int = 256) -> float:
+    """Share of `files` this build cannot decode: every file whose format has no decoder here
+    (.flac / .mp3), plus the share of broken WAV headers among up to `probe` evenly spaced WAV
+    files (their header is read, not their samples)."""
+    if not files:
+        return 0.0
+    wavs = [f for f in files if os.path.splitext(f)[1].lower() == ".wav"]
+    bad = len(files) - len(wavs)
+    if wavs:
+        step = max(1, len(wavs) // probe)
+        sample = wavs[::step]
+        broken = 0
+        for f in sample:
+            try:
+                audio_info(f)
+            except Exception:
+                broken += 1
+        bad += broken / len(sample) * len(wavs)
+    return bad / len(files)
+
+
+def check_decodable(files: list, what: str, max_share: float = 0.5) -> None:
+    """Refuse a file list mostly made of audio this build cannot decode: the reference decodes
+    any torchaudio format (audio_utils.py:27), so a FLAC / MP3 corpus would otherwise train on
+    nothing but load errors and retries (noisy_speech_dataset.py:56-76)."""
+    share = undecodable_share(files)
+    if share > max_share:
+        raise AudioDecodeError(
+            f"{what}: {share:.0%} of {len(files)} files cannot be decoded by this build (PCM WAV only; "
+            f"torchaudio and its codecs are absent). Convert the corpus to WAV.")
+    if share > 0:
+        logger.warning(f"{what}: {share:.1%} of {len(files)} files cannot be decoded and will take the "
+                       f"load-error path")
 
 
 def read_wav(path: str) -> tuple:

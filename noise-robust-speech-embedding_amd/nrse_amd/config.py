@@ -23,8 +23,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--task", type=str, default="both", choices=["categorical", "dimensional", "both"],
                    help="Which emotion recognition task to train (parsed, unused by BYOL training)")
     # MI355X additions (defaults keep the reference behaviour)
-    p.add_argument("--dtype", type=str, default="bf16", choices=["bf16", "f32"],
-                   help="compute dtype of GEMM/attention operands (f32 = exact parity mode)")
+    p.add_argument("--dtype", type=str, default="bf16", choices=["bf16", "bf16sw", "f32"],
+                   help="compute dtype of GEMM/attention operands (f32 = exact parity mode; bf16sw = bf16 "
+                        "activations x split hi+lo bf16 weights in the forward, the north-star 1e-3 mode)")
     p.add_argument("--max_steps", type=int, default=None, help="stop after this many optimizer steps")
     p.add_argument("--mock_items", type=int, default=None,
                    help="train on test/create_mock_dataset.py-style mock pairs (configs[0] plumbing)")

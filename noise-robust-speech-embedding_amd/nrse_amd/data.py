@@ -68,7 +68,8 @@ class GpuMixer:
 
 # ----------------------------------------------------------------------------- audio files
 # decoding / resampling / discovery: nrse_amd/audio.py (audio_utils.py:9-73)
-from .audio import AudioDecodeError, audio_info, get_audio_files, load_audio, read_wav  # noqa: E402,F401
+from .audio import (AudioDecodeError, audio_info, check_decodable, get_audio_files, load_audio,  # noqa: E402,F401
+                    read_wav)
 
 
 def crop_or_pad(x: np.ndarray, n: int, rng=random, random_crop: bool = True) -> np.ndarray:
@@ -98,6 +99,8 @@ class WavPairs(torch.utils.data.Dataset):
     (nrse_snr_mix status) and re-drawn by MixedLoader through `redraw` (:80-86, 94-100)."""
 
     def __init__(self, clean_files, noise_files, sample_rate, max_audio_length, snr_range):
+        check_decodable(clean_files, "clean speech files")
+        check_decodable(noise_files, "noise files")
         self.clean_files = clean_files
         self.noise_files = noise_files
         self.sr = sample_rate
@@ -476,6 +479,8 @@ class WavVarLenPairs(torch.utils.data.Dataset):
     reference's retry path."""
 
     def __init__(self, clean_files, noise_files, sample_rate, max_s, snr_range):
+        check_decodable(clean_files, "clean speech files")
+        check_decodable(noise_files, "noise files")
         self.sr, self.nmax = sample_rate, int(max_s * sample_rate)
         self.snr_range = list(snr_range)
         self.clean_files, self.lengths = [], []
@@ -502,7 +507,11 @@ class WavVarLenPairs(torch.utils.data.Dataset):
         return x if audio_valid(x) else None
 
     def __getitem__(self, idx):
-        # the loader's per-rank, per-worker seeded `random` (create_varlen_loader)
+        # the loader's per-rank, per-worker seeded `random` (create_varlen_loader). The sampler
+        # put idx in the bucket of lengths[idx]: a substitute file (an invalid clean file moves
+        # on to the next one, noisy_speech_dataset.py:56-66) is cropped / padded to that length,
+        # so the batch keeps its padded shape, and the item keeps the sampled index.
+        L, idx0 = self.lengths[idx], idx
         for attempt in range(MAX_ATTEMPTS):
             clean = self._load(self.clean_files[idx], True)
             if clean is None:
@@ -513,10 +522,9 @@ class WavVarLenPairs(torch.utils.data.Dataset):
             if noise is None:
                 logger.warning(f"Invalid noise file, trying another (attempt {attempt + 1})")
                 continue
-            # the bucket was chosen by lengths[idx]: keep the item at that length
-            clean = crop_or_pad(clean, self.lengths[idx], random_crop=False)
-            return _raw_item(clean, noise, random.choice(self.snr_range), idx, attempt + 1)
-        raise RuntimeError(f"no valid pair for item {idx} after {MAX_ATTEMPTS} attempts")
+            clean = crop_or_pad(clean, L, random_crop=False)
+            return _raw_item(clean, noise, random.choice(self.snr_range), idx0, attempt + 1)
+        raise RuntimeError(f"no valid pair for item {idx0} after {MAX_ATTEMPTS} attempts")
 
 
 def create_varlen_loader(dataset, batch_size: int, *, sample_rate: int = 16000, min_s: float = 3.0,

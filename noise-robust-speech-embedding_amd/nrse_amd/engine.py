@@ -36,6 +36,16 @@ F32 = torch.float32
 _SERIAL_TARGET = os.environ.get("NRSE_SERIAL_TARGET", "0") == "1"
 
 
+def compute_mode(name: str) -> tuple:
+    """CLI compute mode -> (compute dtype, weight_split): "bf16" (benchmarked), "bf16sw" (bf16
+    activations, split hi + lo bf16 weights in the forward GEMMs: embeddings within the
+    north-star 1e-3), "f32" (exact-f32 parity mode)."""
+    modes = {"bf16": (torch.bfloat16, False), "bf16sw": (torch.bfloat16, True), "f32": (torch.float32, False)}
+    if name not in modes:
+        raise ValueError(f"unknown compute mode {name!r} (one of {sorted(modes)})")
+    return modes[name]
+
+
 def _divisor_at_most(n: int, cap: int) -> int:
     cap = max(1, min(n, cap))
     for d in range(cap, 0, -1):
@@ -85,41 +95,72 @@ class EncoderWeights:
     and the per-step derived layouts (conv weights in implicit-GEMM order, weight-normed
     pos-conv in forward and flipped-dgrad order)."""
 
-    def __init__(self, eng: "ByolEngine", master: torch.Tensor, shadow: torch.Tensor | None):
+    def __init__(self, eng: "ByolEngine", master: torch.Tensor, shadow: torch.Tensor | None, lo_stride: int = 0):
         self.eng = eng
         self.m = eng.group_views(master, "encoder")
         self.s = eng.group_views(shadow, "encoder") if shadow is not None else self.m
+        # split-weight mode: every bf16 weight view of the forward GEMMs has its lo plane
+        # lo_stride elements further on (shadows: the [2, n] plane buffers; the derived conv /
+        # pos-conv layouts below: [2, ...] tensors, plane 0 = hi)
+        self.lo = lo_stride
         a = eng.arch
         cdt = eng.cdt
         # conv 1..6 weights [co][ci][k] -> [co][k][ci] in the compute dtype
-        self.conv_r = []
+        self.conv_r, self.conv_lo = [], []   # conv_lo[i]: lo-plane offset of conv_r[i] (0: none)
         for i in range(1, len(a.conv_dim)):
             w = self.m[f"feature_extractor.conv_layers.{i}.conv.weight"]
             co, ci, k = w.shape
-            r = torch.empty(co, k * ci, device=eng.dev, dtype=cdt)
-            K.swap12(w, r, co, ci, k)
-            self.conv_r.append(r)
+            if self.lo:
+                r32 = torch.empty(co, k * ci, device=eng.dev, dtype=F32)
+                K.swap12(w, r32, co, ci, k)
+                r2 = torch.empty(2, co, k * ci, device=eng.dev, dtype=cdt)
+                K.split_bf16(r32, r2[0], r2[1])
+                self.conv_r.append(r2[0])
+                self.conv_lo.append(r32.numel())
+            else:
+                r = torch.empty(co, k * ci, device=eng.dev, dtype=cdt)
+                K.swap12(w, r, co, ci, k)
+                self.conv_r.append(r)
+                self.conv_lo.append(0)
         # pos-conv weight norm
         H, G, pk = a.hidden, a.pos_groups, a.pos_kernel
         cpg = H // G
         pre = "encoder.pos_conv_embed.conv.parametrizations.weight."
-        self.wf = torch.empty(G, cpg, pk * cpg, device=eng.dev, dtype=cdt)
-        self.wd = torch.empty(G, cpg, pk * cpg, device=eng.dev, dtype=cdt)
         self.wn_norms = torch.empty(pk, device=eng.dev, dtype=F32)
-        K.weight_norm_fwd(self.m[pre + "original0"], self.m[pre + "original1"], self.wf, self.wd, self.wn_norms, H,
-                          cpg, pk)
+        if self.lo:
+            wf32 = torch.empty(G, cpg, pk * cpg, device=eng.dev, dtype=F32)
+            wd32 = torch.empty(G, cpg, pk * cpg, device=eng.dev, dtype=F32)
+            K.weight_norm_fwd(self.m[pre + "original0"], self.m[pre + "original1"], wf32, wd32, self.wn_norms, H,
+                              cpg, pk)
+            wf2 = torch.empty(2, G, cpg, pk * cpg, device=eng.dev, dtype=cdt)
+            K.split_bf16(wf32, wf2[0], wf2[1])
+            self.wf, self.wf_lo = wf2[0], wf32.numel()
+            self.wd = torch.empty(G, cpg, pk * cpg, device=eng.dev, dtype=cdt)
+            K.cast(wd32, self.wd)   # the backward's dgrad reads the hi plane only
+        else:
+            self.wf = torch.empty(G, cpg, pk * cpg, device=eng.dev, dtype=cdt)
+            self.wd = torch.empty(G, cpg, pk * cpg, device=eng.dev, dtype=cdt)
+            self.wf_lo = 0
+            K.weight_norm_fwd(self.m[pre + "original0"], self.m[pre + "original1"], self.wf, self.wd,
+                              self.wn_norms, H, cpg, pk)
 
 
 class ByolEngine:
     def __init__(self, arch: WavLMArch, proj_dim: int, pred_dim: int, *, device="cuda", compute_dtype=torch.bfloat16,
                  seed: int = 1234, step_cfg: StepConfig | None = None, init_flat: torch.Tensor | None = None,
-                 do_normalize: bool = True):
+                 do_normalize: bool = True, weight_split: bool = False):
         if arch.head_dim != 64:
             raise _lib.NrseError(f"head_dim {arch.head_dim} unsupported (attention kernels are head_dim 64)")
+        if weight_split and compute_dtype != torch.bfloat16:
+            raise _lib.NrseError("weight_split is a bf16-mode option")
         self.arch = arch
         self.dev = torch.device(device)
         _lib.init_device(self.dev.index or 0)
         self.cdt = compute_dtype
+        # split-weight mode (DESIGN.md §6): the forward GEMMs multiply by the weights' hi + lo bf16
+        # pair (the f32 master to ~2^-17), activations stay bf16 -- the north-star 1e-3 embedding
+        # bound at bf16 activation cost. The backward's dgrad uses the hi plane.
+        self.wsplit = bool(weight_split)
         self.cfg = step_cfg or StepConfig()
         self.layout = PR.byol_layout(arch, proj_dim, pred_dim)
         self.proj_dim, self.pred_dim = proj_dim, pred_dim
@@ -131,9 +172,18 @@ class ByolEngine:
         self.grad = torch.zeros(n, device=self.dev, dtype=F32)
         self.m = torch.zeros(n, device=self.dev, dtype=F32)
         self.v = torch.zeros(n, device=self.dev, dtype=F32)
+        self.online_lo = self.target_lo = None
         if self.cdt == F32:
             self.online_sh = None
             self.target_sh = None
+        elif self.wsplit:
+            # [2, n] planes: hi = bf16(w), lo = bf16(w - hi); a weight view's lo is n (ne) further on
+            on2 = torch.empty(2, n, device=self.dev, dtype=self.cdt)
+            tg2 = torch.empty(2, ne, device=self.dev, dtype=self.cdt)
+            self.online_sh, self.online_lo = on2[0], on2[1]
+            self.target_sh, self.target_lo = tg2[0], tg2[1]
+            K.split_bf16(self.online, self.online_sh, self.online_lo)
+            K.split_bf16(self.target, self.target_sh, self.target_lo)
         else:
             self.online_sh = torch.empty(n, device=self.dev, dtype=self.cdt)
             self.target_sh = torch.empty(ne, device=self.dev, dtype=self.cdt)
@@ -165,6 +215,19 @@ class ByolEngine:
         self._opt_events = None
         self._opt_done = None
         self._segments = self._param_segments()
+
+    def refresh_shadows(self, which=("online", "target")) -> None:
+        """Re-derive the bf16 GEMM-operand copies (and the split mode's lo planes) of the f32
+        weights after they were changed outside the fused AdamW / EMA kernels."""
+        for w in which:
+            src, sh, lo = ((self.online, self.online_sh, self.online_lo) if w == "online"
+                           else (self.target, self.target_sh, self.target_lo))
+            if sh is None:
+                continue
+            if lo is not None:
+                K.split_bf16(src, sh, lo)
+            else:
+                K.cast(src, sh)
 
     # ------------------------------------------------------------------ overlapped optimizer
     def _param_segments(self) -> list:
@@ -260,8 +323,9 @@ class ByolEngine:
             k, s, C = a.conv_kernel[i], a.conv_stride[i], a.conv_dim[i]
             Tout = (Tin - k) // s + 1
             pre_out = torch.empty(B * Tout, C, device=dev, dtype=cdt)
-            K.gemm(K.Operand(x, True, s * Cin, z1=Tin * Cin), K.Operand(W.conv_r[i - 1], True, k * Cin), pre_out,
-                   Tout, C, k * Cin, ldc=C, batch=B, c_z1=Tout * C)
+            K.gemm(K.Operand(x, True, s * Cin, z1=Tin * Cin),
+                   K.Operand(W.conv_r[i - 1], True, k * Cin, seg_stride=W.conv_lo[i - 1]), pre_out,
+                   Tout, C, k * Cin, ldc=C, batch=B, c_z1=Tout * C, nseg=2 if W.conv_lo[i - 1] else 1)
             yo = torch.empty(B * Tout, C, device=dev, dtype=cdt)
             mo = torch.empty(B * Tout, device=dev, dtype=F32)
             ro = torch.empty(B * Tout, device=dev, dtype=F32)
@@ -284,7 +348,7 @@ class ByolEngine:
         h = torch.empty(BT, H, device=dev, dtype=F32)
         pfp = a.feat_proj_dropout if train else 0.0
         K.linear_fwd(xn, Ps["feature_projection.projection.weight"], h, bias=Pm["feature_projection.projection.bias"],
-                     dropout_p=pfp, seed=R.site_seed(fseed, R.SITE_FEAT_PROJ))
+                     dropout_p=pfp, seed=R.site_seed(fseed, R.SITE_FEAT_PROJ), w_lo=W.lo)
         # -------- SpecAugment ([TF]modeling_wavlm.py:985-1011) + padded copy for the pos-conv
         pk, G = a.pos_kernel, a.pos_groups
         cpg = H // G
@@ -302,7 +366,8 @@ class ByolEngine:
         php = a.hidden_dropout if train else 0.0
         cs = int(math.log2(cpg))
         K.gemm(K.Operand(hpad, True, H, chunk_shift=cs, ld_chunk=H, z1=(T + pk) * H, z2=cpg),
-               K.Operand(W.wf, True, pk * cpg, z2=cpg * pk * cpg), h0, T, cpg, pk * cpg, ldc=H, batch=B * G, zdiv=G,
+               K.Operand(W.wf, True, pk * cpg, z2=cpg * pk * cpg, seg_stride=W.wf_lo), h0, T, cpg, pk * cpg, ldc=H,
+               batch=B * G, zdiv=G, nseg=2 if W.wf_lo else 1,
                c_z1=T * H, c_z2=cpg, bias=Pm["encoder.pos_conv_embed.conv.bias"], bias_z2=cpg,
                flags=_lib.EPI_GELU | _lib.EPI_DROP_AFTER, aux=pos_pre, ldaux=H, aux_z1=T * H, aux_z2=cpg,
                resid=h, ldr=H, r_z1=T * H, r_z2=cpg, dropout_p=php, seed=R.site_seed(fseed, R.SITE_POS))
@@ -343,7 +408,8 @@ class ByolEngine:
             r1 = torch.empty(BT, device=dev, dtype=F32)
             K.ln_fwd(hcur, Pm[p + "layer_norm.weight"], Pm[p + "layer_norm.bias"], x1, m1, r1, a.eps)
             qkv = torch.empty(BT, 3 * H, device=dev, dtype=cdt)
-            K.linear_fwd(x1, self.fused(W.s_flat, li, "qkv_w"), qkv, bias=self.fused(W.m_flat, li, "qkv_b"))
+            K.linear_fwd(x1, self.fused(W.s_flat, li, "qkv_w"), qkv, bias=self.fused(W.m_flat, li, "qkv_b"),
+                         w_lo=W.lo)
             gate = torch.empty(B, nh, T, device=dev, dtype=F32)
             at = p + "attention."
             K.gate_fwd(x1, Pm[at + "gru_rel_pos_linear.weight"], Pm[at + "gru_rel_pos_linear.bias"],
@@ -354,7 +420,7 @@ class ByolEngine:
                        bias_vec=bias_vec)
             hmid = torch.empty(BT, H, device=dev, dtype=F32)
             K.linear_fwd(ctx, Ps[at + "out_proj.weight"], hmid, bias=Pm[at + "out_proj.bias"], resid=hcur, ldr=H,
-                         dropout_p=php, seed=R.site_seed(fseed, R.site_attn_out(li)))
+                         dropout_p=php, seed=R.site_seed(fseed, R.site_attn_out(li)), w_lo=W.lo)
             x2 = torch.empty(BT, H, device=dev, dtype=cdt)
             m2 = torch.empty(BT, device=dev, dtype=F32)
             r2 = torch.empty(BT, device=dev, dtype=F32)
@@ -363,11 +429,11 @@ class ByolEngine:
             g1 = torch.empty(BT, F_, device=dev, dtype=cdt)
             K.linear_fwd(x2, Ps[p + "feed_forward.intermediate_dense.weight"], g1,
                          bias=Pm[p + "feed_forward.intermediate_dense.bias"], flags=_lib.EPI_GELU, aux=f1pre,
-                         ldaux=F_, dropout_p=pact, seed=R.site_seed(fseed, R.site_act(li)))
+                         ldaux=F_, dropout_p=pact, seed=R.site_seed(fseed, R.site_act(li)), w_lo=W.lo)
             hout = torch.empty(BT, H, device=dev, dtype=F32)
             K.linear_fwd(g1, Ps[p + "feed_forward.output_dense.weight"], hout,
                          bias=Pm[p + "feed_forward.output_dense.bias"], resid=hmid, ldr=H, dropout_p=php,
-                         seed=R.site_seed(fseed, R.site_ffn_out(li)))
+                         seed=R.site_seed(fseed, R.site_ffn_out(li)), w_lo=W.lo)
             if need_grad:
                 tape.layers.append(dict(li=li, h_in=hcur, x1=x1, m1=m1, r1=r1, qkv=qkv, gate=gate, ctx=ctx, lse=lse,
                                         hmid=hmid, x2=x2, m2=m2, r2=r2, f1pre=f1pre, g1=g1))
@@ -684,10 +750,10 @@ class ByolEngine:
         """Encoder weight views (+ the derived conv / pos-conv GEMM layouts, computed on the
         current stream). Inside forward() the caller has waited for the front-end segment."""
         if which == "online":
-            W = EncoderWeights(self, self.online, self.online_sh)
+            W = EncoderWeights(self, self.online, self.online_sh, self.online.numel() if self.wsplit else 0)
             W.m_flat, W.s_flat = self.online, (self.online_sh if self.online_sh is not None else self.online)
         else:
-            W = EncoderWeights(self, self.target, self.target_sh)
+            W = EncoderWeights(self, self.target, self.target_sh, self.target.numel() if self.wsplit else 0)
             W.m_flat, W.s_flat = self.target, (self.target_sh if self.target_sh is not None else self.target)
         return W
 
@@ -823,8 +889,8 @@ class ByolEngine:
                   step=self.step_count, max_norm=c.max_norm, sumsq_buf=self.sumsq_buf, grad_scale=grad_scale)
         ne = self.layout.ema_numel
         if not c.overlap_optimizer:
-            K.adamw(self.online, self.grad, self.m, self.v, self.online_sh, **kw)
-            K.ema(self.target, self.online[:ne], self.target_sh, c.ema_decay)
+            K.adamw(self.online, self.grad, self.m, self.v, self.online_sh, shadow_lo=self.online_lo, **kw)
+            K.ema(self.target, self.online[:ne], self.target_sh, c.ema_decay, shadow_lo=self.target_lo)
             self._opt_events = self._opt_done = None
             return
         main = torch.cuda.current_stream(self.dev)
@@ -833,16 +899,17 @@ class ByolEngine:
         st = self._opt_stream
         st.wait_stream(main)
         events = []
-        sh, tsh = self.online_sh, self.target_sh
+        sh, tsh, slo, tlo = self.online_sh, self.target_sh, self.online_lo, self.target_lo
         with torch.cuda.stream(st):
             for s, e in self._segments:
                 if e > s:
                     K.adamw(self.online[s:e], self.grad[s:e], self.m[s:e], self.v[s:e],
-                            sh[s:e] if sh is not None else None, **kw)
+                            sh[s:e] if sh is not None else None, shadow_lo=slo[s:e] if slo is not None else None,
+                            **kw)
                     te = min(e, ne)
                     if te > s:
                         K.ema(self.target[s:te], self.online[s:te], tsh[s:te] if tsh is not None else None,
-                              c.ema_decay)
+                              c.ema_decay, shadow_lo=tlo[s:te] if tlo is not None else None)
                 ev = torch.cuda.Event()
                 ev.record(st)
                 events.append(ev)

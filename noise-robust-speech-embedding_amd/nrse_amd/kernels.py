@@ -44,7 +44,14 @@ def _call(name, *args):
 # Deterministic reductions (default): the per-workgroup column sums of the gradient reductions
 # are written to a workspace of partial rows and added in a fixed order (nrse_rows_reduce)
 # instead of f32 atomics, so a step's gradients are bit-identical run to run.
-# NRSE_ATOMIC_REDUCTIONS=1 restores the atomics (timing comparisons only).
+# NRSE_ATOMIC_REDUCTIONS=1 (timing comparisons only) switches ONLY the reductions that take a
+# workspace back to f32 atomics: the GEMM COLSUM bias gradients, colsum / dropout_cast_colsum,
+# the LayerNorm dgamma / dbeta (and fused dropout column sums), ln_mean, the attention rel-pos
+# diagonals, the gate-parameter and conv0 reductions, the SpecAugment embedding, the BYOL loss and
+# the gradient sum of squares. The split-K weight gradients keep their f32 slabs + ordered
+# nrse_splitk_reduce under both settings (linear_fwd_small, linear_dgrad_small, the linear_wgrad
+# fallback, the f32 conv / pos-conv weight gradients): an A/B with the flag measures the
+# partial-row reductions only.
 DETERMINISTIC = os.environ.get("NRSE_ATOMIC_REDUCTIONS", "0") != "1"
 
 
@@ -189,13 +196,16 @@ def gemm_probe_bytes():
 
 
 # ----------------------------------------------------------------------------- linear helpers
-def linear_fwd(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, *, bias=None, flags: int = 0, **kw) -> None:
-    """out[M,N] = x[M,K] @ w[N,K]^T (+ epilogue). x, w share the compute dtype."""
+def linear_fwd(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, *, bias=None, flags: int = 0, w_lo: int = 0,
+               **kw) -> None:
+    """out[M,N] = x[M,K] @ w[N,K]^T (+ epilogue). x, w share the compute dtype. w_lo != 0: the
+    split-weight mode, w's lo plane sits w_lo elements after it and the product is
+    x @ (w_hi + w_lo)^T, two K segments of one launch (A read twice, one epilogue)."""
     M, K = x.shape
     N = w.shape[0]
     assert w.shape[1] == K and out.shape[-1] >= N
-    gemm(Operand(x, True, x.stride(0)), Operand(w, True, w.stride(0)), out, M, N, K, ldc=out.stride(0),
-         bias=bias, flags=flags, **kw)
+    gemm(Operand(x, True, x.stride(0)), Operand(w, True, w.stride(0), seg_stride=w_lo), out, M, N, K,
+         ldc=out.stride(0), nseg=2 if w_lo else 1, bias=bias, flags=flags, **kw)
 
 
 def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, dx: torch.Tensor, *, flags: int = 0, **kw) -> None:
@@ -615,16 +625,26 @@ def sumsq(x, out):
     _call("nrse_sumsq", ptr(x), x.numel(), ptr(out), ptr(ws), stream_ptr())
 
 
-def adamw(p, g, m, v, shadow, *, lr, beta1, beta2, eps, weight_decay, step, max_norm, sumsq_buf, grad_scale=1.0):
+def adamw(p, g, m, v, shadow, *, lr, beta1, beta2, eps, weight_decay, step, max_norm, sumsq_buf, grad_scale=1.0,
+          shadow_lo=None):
+    """clip + AdamW; shadow (bf16/f32) gets the updated weights, shadow_lo (bf16, with a bf16
+    shadow) the split-weight mode's lo plane bf16(p - shadow)."""
     prm = AdamWParams(ptr(p), ptr(g), ptr(m), ptr(v), ptr(shadow),
                       dtype_code(shadow) if shadow is not None else 0, p.numel(), lr, beta1, beta2, eps,
-                      weight_decay, step, max_norm, ptr(sumsq_buf), grad_scale)
+                      weight_decay, step, max_norm, ptr(sumsq_buf), grad_scale, ptr(shadow_lo))
     _call("nrse_adamw", ctypes.byref(prm), stream_ptr())
 
 
-def ema(t, o, shadow, decay):
+def ema(t, o, shadow, decay, shadow_lo=None):
     _call("nrse_ema", ptr(t), ptr(o), ptr(shadow), dtype_code(shadow) if shadow is not None else 0, t.numel(), decay,
-          stream_ptr())
+          ptr(shadow_lo), stream_ptr())
+
+
+def split_bf16(x, hi, lo):
+    """hi = bf16(x), lo = bf16(x - hi) (nrse_split_bf16)."""
+    assert x.dtype == torch.float32 and hi.dtype == lo.dtype == torch.bfloat16
+    assert hi.numel() == lo.numel() == x.numel()
+    _call("nrse_split_bf16", ptr(x), ptr(hi), ptr(lo), x.numel(), stream_ptr())
 
 
 def health(x, stats):

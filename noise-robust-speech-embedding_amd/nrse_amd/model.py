@@ -128,7 +128,7 @@ class WavLMEncoder(nn.Module):
 
 class BYOLSpeechModel(nn.Module):
     def __init__(self, config: dict, *, device=None, compute_dtype=torch.bfloat16, seed: int | None = None,
-                 arch: WavLMArch | None = None):
+                 arch: WavLMArch | None = None, weight_split: bool = False):
         super().__init__()
         m = config["model"]
         arch = arch or arch_from_name(m["name"])
@@ -139,7 +139,7 @@ class BYOLSpeechModel(nn.Module):
         seed = seed if seed is not None else int(tr.get("seed", 42))
         self.engine = ByolEngine(arch, int(m["projection_dim"]), int(m["prediction_dim"]),
                                  device=device or _device_default(), compute_dtype=compute_dtype, seed=seed,
-                                 step_cfg=cfg)
+                                 step_cfg=cfg, weight_split=weight_split)
         # the single trainable parameter: the flat online buffer (views carry the reference names)
         self.online_flat = nn.Parameter(self.engine.online, requires_grad=True)
         self._seed_counter = seed * 1000003
@@ -167,31 +167,27 @@ class BYOLSpeechModel(nn.Module):
         e.sync_optimizer()
         v = self.online_flat._version
         if v != self._shadow_version:
-            if e.online_sh is not None:
-                K.cast(e.online, e.online_sh)
+            e.refresh_shadows(("online",))
             self._shadow_version = v
 
     def _update_target_network(self) -> None:
         e = self.engine
         e.sync_optimizer()
         self._sync_shadows()
-        K.ema(e.target, e.online[:e.layout.ema_numel], e.target_sh, self.ema_decay)
+        K.ema(e.target, e.online[:e.layout.ema_numel], e.target_sh, self.ema_decay, shadow_lo=e.target_lo)
 
     def _copy_weights(self, *args) -> None:
         e = self.engine
         e.sync_optimizer()
         e.target.copy_(e.online[:e.layout.ema_numel])
-        if e.target_sh is not None:
-            K.cast(e.target, e.target_sh)
+        e.refresh_shadows(("target",))
 
     def refresh_shadows(self) -> None:
         """Re-derive the bf16 operand copies after the f32 weights were changed outside the
         fused optimizer (e.g. by torch.optim or load_state_dict)."""
         e = self.engine
         e.sync_optimizer()
-        if e.online_sh is not None:
-            K.cast(e.online, e.online_sh)
-            K.cast(e.target, e.target_sh)
+        e.refresh_shadows()
         self._shadow_version = self.online_flat._version
 
     def get_encoder(self) -> WavLMEncoder:

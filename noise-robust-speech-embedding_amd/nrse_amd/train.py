@@ -20,6 +20,7 @@ import torch
 
 from . import ddp, params as PR
 from .config import get_config
+from .engine import compute_mode
 from .data import create_dataloaders, seed_host_rng
 from .health import HealthMonitor
 from .model import BYOLSpeechModel
@@ -87,16 +88,28 @@ class FusedAdamW(torch.optim.Optimizer):
         return {"state": state, "param_groups": [group]}
 
     def load_state_dict(self, state_dict):
-        """Restore the moments, step count and lr / weight decay from `state_dict` (this class's
-        format, matched by `param_names`, or a plain AdamW state over the same tensor order)."""
+        """Restore the moments, step count and lr / weight decay from `state_dict` in this
+        class's format: each state index is matched to its tensor by `param_names`, and every
+        moment must have exactly that tensor's shape. A plain AdamW state (no `param_names`) is
+        refused: its index order is the owning module's parameter order, which the flat layout
+        does not share, and moments of equal size would load into the wrong tensors silently."""
         e = self.model.engine
         mv, vv = self._moments()
         names = list(mv)
         group = state_dict["param_groups"][0]
-        order = group.get("param_names") or names
+        order = group.get("param_names")
+        if not order:
+            raise ValueError("optimizer state has no param_names: only states written by FusedAdamW.state_dict() "
+                             "can be matched to the flat parameter layout")
         if len(order) != len(names) or set(order) != set(names):
             raise ValueError("optimizer state does not match this model's parameters")
         st = state_dict["state"]
+        for i, k in enumerate(order):
+            if i in st:
+                for moment in ("exp_avg", "exp_avg_sq"):
+                    if tuple(st[i][moment].shape) != tuple(mv[k].shape):
+                        raise ValueError(f"optimizer state {moment} of {k}: shape {tuple(st[i][moment].shape)}, "
+                                         f"expected {tuple(mv[k].shape)}")
         with torch.no_grad():
             if not st:
                 e.m.zero_()
@@ -104,8 +117,8 @@ class FusedAdamW(torch.optim.Optimizer):
                 e.step_count = 0
             for i, k in enumerate(order):
                 if i in st:
-                    mv[k].copy_(st[i]["exp_avg"].reshape(mv[k].shape))
-                    vv[k].copy_(st[i]["exp_avg_sq"].reshape(vv[k].shape))
+                    mv[k].copy_(st[i]["exp_avg"])
+                    vv[k].copy_(st[i]["exp_avg_sq"])
                     e.step_count = int(float(st[i]["step"]))
         for k in ("lr", "weight_decay", "initial_lr"):
             if k in group:
@@ -192,8 +205,8 @@ def main(argv=None):
     seed_host_rng(t.get("seed", 42), rank)
     os.makedirs(t["checkpoint_dir"], exist_ok=True)
     os.makedirs(t["log_dir"], exist_ok=True)
-    dtype = torch.float32 if config["runtime"]["dtype"] == "f32" else torch.bfloat16
-    model = BYOLSpeechModel(config, device=device, compute_dtype=dtype)
+    dtype, wsplit = compute_mode(config["runtime"]["dtype"])
+    model = BYOLSpeechModel(config, device=device, compute_dtype=dtype, weight_split=wsplit)
     train_loader, val_loader = create_dataloaders(config, device=device, rank=rank, world=world)
     optimizer = FusedAdamW(model, lr=float(t["learning_rate"]), weight_decay=float(t["weight_decay"]))
     total_steps = max(1, len(train_loader) * int(t["num_epochs"]))

@@ -83,12 +83,39 @@ def position_bias(E: torch.Tensor, T: int, nb: int, md: int) -> torch.Tensor:
 #           GEMM operand whose gradient the engine keeps in f32;
 #   _rg(x)  rounds the gradient in the backward pass: a tensor whose gradient the engine stores in
 #           bf16 as the dY operand of the dgrad / wgrad GEMMs (dv, df1, dqkv, dctx, dS, dpre ...).
+# Rounding sites (set_operand_dtype(dtype, sites=...) rounds only those; None = every site):
+#   conv     conv1-6 implicit-GEMM operands and stored outputs
+#   proj     feature-projection LN output and GEMM
+#   posconv  pos-conv operands
+#   qkv      the QKV GEMM (LN output, weights, stored q / k / v)
+#   attn     the attention core (P for P V, stored context)
+#   oproj    the out-proj GEMM
+#   ffn_up   the FFN-up GEMM (LN output, weights, stored pre-activation and GELU output)
+#   ffn_down the FFN-down GEMM weights
+SITES = ("conv", "proj", "posconv", "qkv", "attn", "oproj", "ffn_up", "ffn_down")
+# the engine's split-weight mode (bf16sw): every activation operand rounded, every weight exact
+# (the forward GEMMs multiply by the weights' hi + lo bf16 pair)
+SPLIT_WEIGHT_SITES = tuple(f"{s}:a" for s in SITES if s != "attn") + ("attn",)
 _OPERAND_DTYPE = None
+_SITES = None
 
 
-def set_operand_dtype(dtype) -> None:
-    global _OPERAND_DTYPE
+def set_operand_dtype(dtype, sites=None) -> None:
+    global _OPERAND_DTYPE, _SITES
     _OPERAND_DTYPE = None if dtype in (None, torch.float32) else dtype
+    _SITES = None if sites is None else frozenset(sites)
+    if _SITES is not None and not {x.split(":")[0] for x in _SITES} <= set(SITES):
+        raise ValueError(f"unknown rounding sites {sorted(_SITES)}")
+
+
+def _site_on(site, kind=None) -> bool:
+    """Rounding on at `site`; a sites entry "name:w" / "name:a" selects only that site's weight /
+    activation operands (kind "w" / "a")."""
+    if _OPERAND_DTYPE is None:
+        return False
+    if _SITES is None or site is None or site in _SITES:
+        return True
+    return kind is not None and f"{site}:{kind}" in _SITES
 
 
 def operand_dtype():
@@ -116,20 +143,20 @@ class _RoundGrad(torch.autograd.Function):
         return g.to(ctx.dt).to(g.dtype), None
 
 
-def _rf(x: torch.Tensor) -> torch.Tensor:
-    return x if _OPERAND_DTYPE is None else _RoundFwd.apply(x, _OPERAND_DTYPE)
+def _rf(x: torch.Tensor, site=None, kind="a") -> torch.Tensor:
+    return _RoundFwd.apply(x, _OPERAND_DTYPE) if _site_on(site, kind) else x
 
 
-def _rg(x: torch.Tensor) -> torch.Tensor:
-    return x if _OPERAND_DTYPE is None else _RoundGrad.apply(x, _OPERAND_DTYPE)
+def _rg(x: torch.Tensor, site=None) -> torch.Tensor:
+    return _RoundGrad.apply(x, _OPERAND_DTYPE) if _site_on(site, "a") else x
 
 
-def _lin(x, w, b=None, *, store=False):
+def _lin(x, w, b=None, *, store=False, site=None):
     """Linear on the GEMM path: rounded operands, f32 accumulate + bias epilogue, the output's
     gradient rounded (it is the dY operand of this GEMM's dgrad / wgrad); store=True when the
     engine also stores the output itself in bf16 (QKV, FFN-up pre-activation)."""
-    y = _rg(F.linear(_rf(x), _rf(w), b))
-    return _rf(y) if store else y
+    y = _rg(F.linear(_rf(x, site), _rf(w, site, "w"), b), site)
+    return _rf(y, site) if store else y
 
 
 # ------------------------------------------------------------------------- pieces
@@ -148,10 +175,10 @@ def conv_stack(P: dict, a, wav: torch.Tensor) -> torch.Tensor:
         if i == 0:   # direct conv from the f32 waveform (engine: conv0 kernel, f32 weights)
             x = F.conv1d(x, P[pre + "conv.weight"], stride=s)
         else:        # implicit GEMM, bf16 operands, pre-LN output stored in the compute dtype
-            x = _rf(_rg(F.conv1d(_rf(x), _rf(P[pre + "conv.weight"]), stride=s)))
+            x = _rf(_rg(F.conv1d(_rf(x, "conv"), _rf(P[pre + "conv.weight"], "conv", "w"), stride=s), "conv"), "conv")
         x = F.layer_norm(x.transpose(1, 2), (x.shape[1],), P[pre + "layer_norm.weight"], P[pre + "layer_norm.bias"],
                          a.eps).transpose(1, 2)
-        x = _rg(_rf(F.gelu(x)))
+        x = _rg(_rf(F.gelu(x), "conv"), "conv")
     return x.transpose(1, 2)
 
 
@@ -210,16 +237,16 @@ def attention(P: dict, a, li: int, x1: torch.Tensor, pbias: torch.Tensor, fseed:
     B, T, H = x1.shape
     nh, hd = a.heads, a.head_dim
     pre = f"encoder.layers.{li}.attention."
-    q = _lin(x1, P[pre + "q_proj.weight"], P[pre + "q_proj.bias"], store=True)
-    k = _lin(x1, P[pre + "k_proj.weight"], P[pre + "k_proj.bias"], store=True)
-    v = _lin(x1, P[pre + "v_proj.weight"], P[pre + "v_proj.bias"], store=True)
+    q = _lin(x1, P[pre + "q_proj.weight"], P[pre + "q_proj.bias"], store=True, site="qkv")
+    k = _lin(x1, P[pre + "k_proj.weight"], P[pre + "k_proj.bias"], store=True, site="qkv")
+    v = _lin(x1, P[pre + "v_proj.weight"], P[pre + "v_proj.bias"], store=True, site="qkv")
     q = q.view(B, T, nh, hd).transpose(1, 2)
     k = k.view(B, T, nh, hd).transpose(1, 2)
     v = v.view(B, T, nh, hd).transpose(1, 2)
     g = gate(P, pre, x1, nh)                               # [B, nh, T]
-    if _OPERAND_DTYPE is not None and not (train and a.attention_dropout > 0):
+    if _site_on("attn") and not (train and a.attention_dropout > 0):
         ctx = _FlashBf16.apply(q, k, v, g, pbias, _OPERAND_DTYPE).transpose(1, 2).reshape(B, T, H)
-        return _lin(ctx, P[pre + "out_proj.weight"], P[pre + "out_proj.bias"])
+        return _lin(ctx, P[pre + "out_proj.weight"], P[pre + "out_proj.bias"], site="oproj")
     s = (q @ k.transpose(-1, -2)) / math.sqrt(hd) + g[..., None] * pbias[None]
     p = torch.softmax(s, dim=-1)
     if train:
@@ -227,7 +254,7 @@ def attention(P: dict, a, li: int, x1: torch.Tensor, pbias: torch.Tensor, fseed:
             p = p * torch.from_numpy(masks.attn_dropout_mask(rng.site_seed(fseed, rng.site_attn_probs(li)),
                                                              a.attention_dropout, tuple(p.shape)))
     ctx = (p @ v).transpose(1, 2).reshape(B, T, H)
-    return _lin(ctx, P[pre + "out_proj.weight"], P[pre + "out_proj.bias"])
+    return _lin(ctx, P[pre + "out_proj.weight"], P[pre + "out_proj.bias"], site="oproj")
 
 
 def encoder_forward(P: dict, a, wav: torch.Tensor, *, train: bool = False, fseed: int = 0,
@@ -236,8 +263,8 @@ def encoder_forward(P: dict, a, wav: torch.Tensor, *, train: bool = False, fseed
     feats = conv_stack(P, a, wav)
     B, T, C = feats.shape
     xn = _rf(F.layer_norm(feats, (C,), P["feature_projection.layer_norm.weight"],
-                          P["feature_projection.layer_norm.bias"], a.eps))
-    h = _lin(xn, P["feature_projection.projection.weight"], P["feature_projection.projection.bias"])
+                          P["feature_projection.layer_norm.bias"], a.eps), "proj")
+    h = _lin(xn, P["feature_projection.projection.weight"], P["feature_projection.projection.bias"], site="proj")
     if train:
         h = _drop(h, a.feat_proj_dropout, rng.site_seed(fseed, rng.SITE_FEAT_PROJ))
     if train and mask_time is not None:
@@ -245,8 +272,8 @@ def encoder_forward(P: dict, a, wav: torch.Tensor, *, train: bool = False, fseed
         h = torch.where(m[..., None], P["masked_spec_embed"].view(1, 1, -1), h)
     pre = "encoder.pos_conv_embed.conv."
     w = weight_norm_w(P[pre + "parametrizations.weight.original0"], P[pre + "parametrizations.weight.original1"])
-    pc = _rg(F.conv1d(_rf(h).transpose(1, 2), _rf(w), P[pre + "bias"], padding=a.pos_kernel // 2,
-                      groups=a.pos_groups))
+    pc = _rg(F.conv1d(_rf(h, "posconv").transpose(1, 2), _rf(w, "posconv", "w"), P[pre + "bias"],
+                      padding=a.pos_kernel // 2, groups=a.pos_groups), "posconv")
     if a.pos_kernel % 2 == 0:
         pc = pc[:, :, :-1]
     h = h + F.gelu(pc).transpose(1, 2)
@@ -257,18 +284,19 @@ def encoder_forward(P: dict, a, wav: torch.Tensor, *, train: bool = False, fseed
         if train and layer_skip is not None and layer_skip[li]:
             continue
         pre = f"encoder.layers.{li}."
-        x1 = _rf(F.layer_norm(h, (h.shape[-1],), P[pre + "layer_norm.weight"], P[pre + "layer_norm.bias"], a.eps))
+        x1 = _rf(F.layer_norm(h, (h.shape[-1],), P[pre + "layer_norm.weight"], P[pre + "layer_norm.bias"], a.eps),
+                 "qkv")
         att = attention(P, a, li, x1, pbias, fseed, train)
         if train:
             att = _drop(att, a.hidden_dropout, rng.site_seed(fseed, rng.site_attn_out(li)))
         h = h + att
         x2 = _rf(F.layer_norm(h, (h.shape[-1],), P[pre + "final_layer_norm.weight"],
-                              P[pre + "final_layer_norm.bias"], a.eps))
-        f = _rf(F.gelu(_rg(F.linear(x2, _rf(P[pre + "feed_forward.intermediate_dense.weight"]),
-                                    P[pre + "feed_forward.intermediate_dense.bias"]))))
+                              P[pre + "final_layer_norm.bias"], a.eps), "ffn_up")
+        f = _rf(F.gelu(_rg(F.linear(x2, _rf(P[pre + "feed_forward.intermediate_dense.weight"], "ffn_up", "w"),
+                                    P[pre + "feed_forward.intermediate_dense.bias"]), "ffn_up")), "ffn_up")
         if train:
             f = _drop(f, a.activation_dropout, rng.site_seed(fseed, rng.site_act(li)))
-        f = _lin(f, P[pre + "feed_forward.output_dense.weight"], P[pre + "feed_forward.output_dense.bias"])
+        f = _lin(f, P[pre + "feed_forward.output_dense.weight"], P[pre + "feed_forward.output_dense.bias"], site="ffn_down")
         if train:
             f = _drop(f, a.hidden_dropout, rng.site_seed(fseed, rng.site_ffn_out(li)))
         h = h + f

@@ -11,6 +11,7 @@ import os
 import wave
 
 import numpy as np
+import pytest
 import torch
 
 from nrse_amd import audio as AU, data as D
@@ -113,3 +114,48 @@ def test_item_draws_differ_across_ranks_and_repeat_per_rank(tmp_path):
         r1 = _draws(tmp_path, 1, 2, workers)
         assert r0 == r0b, workers                # reproducible
         assert r0[0] != r1[0] and r0[1] != r1[1], workers
+
+
+def test_mostly_undecodable_corpus_is_refused(tmp_path):
+    """a corpus the build cannot decode (FLAC / MP3 without torchaudio) fails
+    loudly when the dataset is built instead of training on load errors and retries."""
+    clean = tmp_path / "clean"
+    noise = tmp_path / "noise"
+    for d in (clean, noise):
+        d.mkdir()
+    rng = np.random.default_rng(3)
+    _write_wav(clean / "a.wav", 0.1 * rng.standard_normal(16000), 16000)
+    for i in range(3):
+        (clean / f"f{i}.flac").write_bytes(b"fLaC\x00not-really")
+    _write_wav(noise / "n.wav", rng.standard_normal(16000), 16000)
+    files = AU.get_audio_files(str(clean))
+    assert AU.undecodable_share(files) == 0.75
+    with pytest.raises(AU.AudioDecodeError, match="cannot be decoded"):
+        D.WavPairs(files, AU.get_audio_files(str(noise)), 16000, 1.0, [5])
+    with pytest.raises(AU.AudioDecodeError, match="cannot be decoded"):
+        D.WavVarLenPairs(files, AU.get_audio_files(str(noise)), 16000, 12.0, [5])
+    # a broken WAV header counts as undecodable too
+    (noise / "m.wav").write_bytes(b"RIFF0000WAVEjunk")
+    (noise / "k.wav").write_bytes(b"RIFF0000WAVEjunk")
+    with pytest.raises(AU.AudioDecodeError):
+        D.WavPairs([str(clean / "a.wav")], AU.get_audio_files(str(noise)), 16000, 1.0, [5])
+
+
+def test_varlen_substitute_keeps_bucket_length(tmp_path, monkeypatch):
+    """an invalid clean file is replaced by the next one, cropped / padded to the
+    length the sampler bucketed the item by, and the item keeps the sampled index."""
+    clean = tmp_path / "clean"
+    noise = tmp_path / "noise"
+    for d in (clean, noise):
+        d.mkdir()
+    rng = np.random.default_rng(4)
+    _write_wav(clean / "a.wav", 0.1 * rng.standard_normal(16000), 16000)       # 1 s
+    _write_wav(clean / "b.wav", 0.1 * rng.standard_normal(48000), 16000)       # 3 s
+    _write_wav(noise / "n.wav", rng.standard_normal(16000), 16000)
+    vl = D.WavVarLenPairs(AU.get_audio_files(str(clean)), AU.get_audio_files(str(noise)), 16000, 12.0, [5])
+    assert vl.lengths == [16000, 48000]
+    real = vl._load
+    monkeypatch.setattr(vl, "_load", lambda p, crop: None if p.endswith("a.wav") else real(p, crop))
+    it = vl[0]                       # a.wav invalid -> b.wav (3 s) stands in, cut to a.wav's 1 s
+    assert it["clean"].shape[0] == 16000
+    assert int(it["index"]) == 0 and int(it["attempts"]) == 2

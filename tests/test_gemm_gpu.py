@@ -210,3 +210,83 @@ def test_posconv_wgrad_sliding_window(nrse_device, T, nseg, splits):
         ref = torch.einsum("bto,btip->opi", dy[..., sl], win[:, :, sl]).reshape(cpg, pk * cpg)
         assert rel(got[gi], ref) < 1e-5, gi
     assert rel(got, generic) < 1e-5
+
+
+def _split(w):
+    from nrse_amd import kernels as K
+    w2 = torch.empty((2,) + tuple(w.shape), device=w.device, dtype=torch.bfloat16)
+    K.split_bf16(w.contiguous(), w2[0], w2[1])
+    return w2
+
+
+@pytest.mark.parametrize("shape", [(12768, 1024, 1024), (300, 192, 256), (4000, 3072, 1024)])
+def test_linear_fwd_split_weights(nrse_device, shape):
+    """Split-weight mode: x @ (w_hi + w_lo)^T as two K segments of one launch
+    (A read twice, B's lo plane seg_stride further on) carries the f32 weight: the product
+    matches x_bf16 @ w_f32 to f32-accumulation level, and the bf16-weight product misses it by
+    the weight rounding."""
+    from nrse_amd import kernels as K, _lib
+    M, N, Kd = shape
+    dev = nrse_device
+    x = torch.randn(M, Kd, device=dev).to(torch.bfloat16)
+    w = torch.randn(N, Kd, device=dev) * 0.05
+    bias = torch.randn(N, device=dev)
+    w2 = _split(w)
+    hi_err = ((w2[0].double() - w.double()).abs() / w.double().abs().clamp_min(1e-30)).max().item()
+    assert hi_err <= 2 ** -8
+    assert rel(w2[0].double() + w2[1].double(), w) < 3e-5    # hi + lo: ~2^-17 relative per element
+    out = torch.empty(M, N, device=dev)
+    K.linear_fwd(x, w2[0], out, bias=bias, w_lo=w2[0].numel())
+    ref = x.double() @ w.double().t() + bias.double()
+    e_split = rel(out, ref)
+    out1 = torch.empty(M, N, device=dev)
+    K.linear_fwd(x, w2[0], out1, bias=bias)
+    e_hi = rel(out1, ref)
+    assert e_split < 2e-5, (e_split, e_hi)
+    assert e_hi > 10 * e_split, (e_split, e_hi)
+    # bf16 output + GELU epilogue (the FFN-up form)
+    pre = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    g = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    K.linear_fwd(x, w2[0], g, bias=bias, flags=_lib.EPI_GELU, aux=pre, ldaux=N, w_lo=w2[0].numel())
+    assert rel(pre.float(), ref) < 5e-3
+    assert rel(g.float(), torch.nn.functional.gelu(ref)) < 5e-3
+
+
+@pytest.mark.parametrize("T", [399, 100])
+def test_posconv_split_weights(nrse_device, T):
+    """The pos-conv sliding-window kernel with two weight planes (nseg = 2, the split-weight
+    mode's hi + lo): conv of the bf16 input with the f32 weights."""
+    from nrse_amd import kernels as K, _lib
+    dev = nrse_device
+    B, H, G, pk = 2, 1024, 16, 128
+    cpg = H // G
+    g = torch.Generator(device=dev).manual_seed(T + 1)
+    x = torch.randn(B, T, H, device=dev, generator=g)
+    hpad = torch.zeros(B, T + pk, H, device=dev, dtype=torch.bfloat16)
+    hpad[:, pk // 2:pk // 2 + T] = x.to(torch.bfloat16)
+    wf32 = torch.randn(G, cpg, pk * cpg, device=dev, generator=g) * 0.02
+    wf2 = _split(wf32)
+    bias = torch.randn(H, device=dev, generator=g) * 0.1
+    resid = torch.randn(B * T, H, device=dev, generator=g)
+    W = wf32.double().view(G, cpg, pk, cpg).permute(0, 1, 3, 2).reshape(H, cpg, pk)
+    conv = torch.nn.functional.conv1d(hpad.double().transpose(1, 2), W, groups=G)[:, :, :T].transpose(1, 2)
+    ref_pre = conv.reshape(B * T, H) + bias.double()
+    ref = torch.nn.functional.gelu(ref_pre) + resid.double()
+    out = torch.empty(B * T, H, device=dev)
+    pre = torch.empty(B * T, H, device=dev, dtype=torch.bfloat16)
+    A = K.Operand(hpad, True, H, chunk_shift=cpg.bit_length() - 1, ld_chunk=H, z1=(T + pk) * H, z2=cpg)
+    Bw = K.Operand(wf2[0], True, pk * cpg, z2=cpg * pk * cpg, seg_stride=wf32.numel())
+    K.gemm(A, Bw, out, T, cpg, pk * cpg, ldc=H, batch=B * G, zdiv=G, nseg=2, c_z1=T * H, c_z2=cpg, bias=bias,
+           bias_z2=cpg, flags=_lib.EPI_GELU | _lib.EPI_DROP_AFTER, aux=pre, ldaux=H, aux_z1=T * H, aux_z2=cpg,
+           resid=resid, ldr=H, r_z1=T * H, r_z2=cpg)
+    assert rel(out, ref) < 2e-6
+    # the same call on the generic LDS-DMA kernel agrees
+    o2 = torch.empty(B * T, H, device=dev)
+    prev = K.gemm_select(2)
+    try:
+        K.gemm(A, Bw, o2, T, cpg, pk * cpg, ldc=H, batch=B * G, zdiv=G, nseg=2, c_z1=T * H, c_z2=cpg, bias=bias,
+               bias_z2=cpg, flags=_lib.EPI_GELU | _lib.EPI_DROP_AFTER, aux=pre, ldaux=H, aux_z1=T * H,
+               aux_z2=cpg, resid=resid, ldr=H, r_z1=T * H, r_z2=cpg)
+    finally:
+        K.gemm_select(prev)
+    assert rel(o2, ref) < 2e-6

@@ -239,6 +239,23 @@ def test_adamw_clip_ema(nrse_device):
     t_ref = 0.997 * t + 0.003 * p
     K.ema(t, p, None, 0.997)
     assert rel(t, t_ref) < 1e-6
+    # split-weight mode: the AdamW / EMA kernels also write the lo plane bf16(x - hi), bit-equal to
+    # nrse_split_bf16 of the updated f32 values
+    for shadow_len in (n, 4096):
+        p2, m2, v2 = p.clone()[:shadow_len], torch.zeros(shadow_len, device=dev), torch.zeros(shadow_len, device=dev)
+        hi = torch.empty(shadow_len, device=dev, dtype=torch.bfloat16)
+        lo = torch.empty_like(hi)
+        K.adamw(p2, g[:shadow_len], m2, v2, hi, lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=1e-2,
+                step=1, max_norm=1.0, sumsq_buf=ss, shadow_lo=lo)
+        h2, l2 = torch.empty_like(hi), torch.empty_like(hi)
+        K.split_bf16(p2, h2, l2)
+        assert torch.equal(hi, h2) and torch.equal(lo, l2)
+        assert torch.equal(hi, p2.to(torch.bfloat16))
+        assert rel(hi.double() + lo.double(), p2) < 3e-5 < rel(hi.float(), p2)
+        t2 = torch.randn(shadow_len, device=dev)
+        K.ema(t2, p2, hi, 0.997, shadow_lo=lo)
+        K.split_bf16(t2, h2, l2)
+        assert torch.equal(hi, h2) and torch.equal(lo, l2)
 
 
 def test_snr_mix_matches_reference_fixture(nrse_device):

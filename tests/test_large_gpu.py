@@ -55,20 +55,20 @@ def large(request):
     return dict(z=z, arch=arch, layout=layout, flat=flat, clean=clean, noisy=noisy, tag=request.param)
 
 
-def _engine(large, dtype):
+def _engine(large, dtype, wsplit=False):
     from nrse_amd.engine import ByolEngine
     z = large["z"]
     eng = ByolEngine(large["arch"], int(z["proj_dim"]), int(z["pred_dim"]), compute_dtype=dtype,
-                     init_flat=large["flat"])
+                     init_flat=large["flat"], weight_split=wsplit)
     eng.cfg.ema_decay = float(z["ema"])
     eng.cfg.weight_decay = float(z["wd"])
     return eng
 
 
-def _run(large, dtype):
+def _run(large, dtype, wsplit=False):
     """Eval forward, last_hidden_state, one det train step; returns the measured deviations."""
     z = large["z"]
-    eng = _engine(large, dtype)
+    eng = _engine(large, dtype, wsplit)
     clean, noisy = large["clean"].cuda(), large["noisy"].cuda()
     m = {}
     pred, tproj, loss = eng.eval_forward(clean, noisy)
@@ -159,3 +159,96 @@ def test_large_bf16_deviation(nrse_device, large):
     assert m["grad_norm_rel"] < 0.25, m
     assert m["grad_sample"] < 1.0, m
     assert m["bn_running"] < 3e-2, m
+
+
+def test_large_bf16sw_matches_reference(nrse_device, large):
+    """The north-star mode at bf16 activation cost: bf16 activations, the forward
+    GEMMs against the weights' split hi + lo bf16 pair. The oracle's site ablation
+    (tools/ablate_bf16_sites.py) puts 5.1e-3 of the bf16 mode's 5.15e-3 embedding deviation on
+    the WEIGHT rounding (a perturbation shared by every frame, which the time mean keeps) and
+    0.7e-3 on the activations; with exact weights the embeddings meet the 1e-3 bound."""
+    m = _run(large, torch.bfloat16, wsplit=True)
+    _record(f"bf16sw_{large['tag']}", m)
+    assert m["eval_emb"] < 1e-3, m          # north-star bound on embeddings
+    assert m["hidden_norms"] < 1e-3, m
+    assert m["eval_pred"] < 2e-3 and m["eval_tproj"] < 2e-3, m
+    assert m["eval_loss_abs"] < 1e-3 and m["train_loss_abs"] < 1e-3, m
+    assert m["bn_running"] < 3e-3, m
+
+
+def test_large_bf16_heads_match_reference(nrse_device, large):
+    """the bf16 mode's heads, loss, head gradients and optimizer at f32-level
+    bounds against the reference. The f32-mode encoder's embeddings of both views (2-4e-7 from
+    the reference) are injected into the bf16-mode engine's projector / predictor / BYOL loss
+    and their backward, then its AdamW (with the reference's clip coefficient: the sum of squares
+    set to the reference's pre-clip norm) and EMA update the head parameters. Compared with
+    byol_large*.npz: online_pred, target_proj, loss, every head tensor's gradient norm, the
+    sampled head gradients, AdamW and EMA deltas (reference src/models/byol.py:75-128,
+    train_byol.py:62-71)."""
+    from nrse_amd import kernels as K, params as PR
+    z = large["z"]
+    clean, noisy = large["clean"].cuda(), large["noisy"].cuda()
+    e32 = _engine(large, torch.float32)
+    emb = e32.embed(clean, "online").clone()
+    temb = e32.embed(noisy, "target").clone()
+    del e32
+    torch.cuda.empty_cache()
+    assert rel(emb, z["eval_emb"]) < 1e-5
+    eng = _engine(large, torch.bfloat16)
+    eng.sync_optimizer()
+    Pon = eng.group_views(eng.online, "projector")
+    Ppr = eng.group_views(eng.online, "predictor")
+    Ptp = eng.group_views(eng.target, "projector")
+    proj, pc = eng.projector_forward(emb, Pon, "online_projector", True)
+    pred, qc = eng.predictor_forward(proj, Ppr, True)
+    tproj, _ = eng.projector_forward(temb, Ptp, "target_projector", True)
+    loss = torch.zeros(1, device=emb.device)
+    dpred = torch.empty_like(pred)
+    K.byol_loss(pred, tproj, loss, dpred)
+    eng.grad.zero_()
+    Gp = eng.group_views(eng.grad, "predictor")
+    Gj = eng.group_views(eng.grad, "projector")
+    dproj = eng.predictor_backward(dpred, qc, Ppr, Gp)
+    eng.projector_backward(dproj, pc, Pon, Gj)
+    torch.cuda.synchronize()
+    m = {"pred": rel(pred, z["train_pred"]), "tproj": rel(tproj, z["train_tproj"]),
+         "loss_abs": abs(float(loss) - float(z["train_loss"]))}
+    # head tensors: layout spec index -> reference per-tensor gradient norm
+    g = eng.grad.cpu()
+    worst, head_lo, head_hi = 0.0, None, 0
+    for i, (gname, s) in enumerate(eng.layout.specs):
+        if gname == "encoder":
+            continue
+        off, cnt, _ = eng.layout.offsets[PR.GROUP_PREFIX[gname] + s.name]
+        head_lo = off if head_lo is None else min(head_lo, off)
+        head_hi = max(head_hi, off + cnt)
+        ref_n = float(z["grad_tensor_norms"][i])
+        worst = max(worst, abs(float(g[off:off + cnt].norm()) - ref_n) / ref_n)
+    m["head_tensor_norm_worst"] = worst
+    idx = torch.from_numpy(z["grad_idx"])
+    sel = (idx >= head_lo) & (idx < head_hi)
+    m["head_samples"] = int(sel.sum())
+    m["head_grad_sample"] = rel(g[idx[sel]], z["grad_sample"][sel.numpy()])
+    # AdamW on the heads with the reference's clip coefficient, then the EMA of the target heads
+    lr = float(z["lr"])
+    eng.sumsq_buf.fill_(float(z["train_grad_norm"]) ** 2)
+    c = eng.cfg
+    K.adamw(eng.online[head_lo:head_hi], eng.grad[head_lo:head_hi], eng.m[head_lo:head_hi],
+            eng.v[head_lo:head_hi], eng.online_sh[head_lo:head_hi], lr=lr, beta1=c.betas[0], beta2=c.betas[1],
+            eps=c.eps, weight_decay=c.weight_decay, step=1, max_norm=c.max_norm, sumsq_buf=eng.sumsq_buf)
+    ne = eng.layout.ema_numel
+    K.ema(eng.target[head_lo:ne], eng.online[head_lo:ne], eng.target_sh[head_lo:ne], c.ema_decay)
+    torch.cuda.synchronize()
+    d = (eng.online.cpu()[idx[sel]] - large["flat"][idx[sel]]).numpy()
+    m["head_online_delta"] = rel(d, z["online_delta_sample"][sel.numpy()])
+    tidx = torch.from_numpy(z["target_idx"])
+    tsel = (tidx >= head_lo) & (tidx < ne)
+    dt = (eng.target.cpu()[tidx[tsel]] - large["flat"][tidx[tsel]]).numpy()
+    m["head_target_delta"] = rel(dt, z["target_delta_sample"][tsel.numpy()])
+    m["head_target_samples"] = int(tsel.sum())
+    _record(f"bf16_heads_{large['tag']}", m)
+    assert m["pred"] < 1e-3 and m["tproj"] < 1e-3, m
+    assert m["loss_abs"] < 1e-4, m
+    assert m["head_tensor_norm_worst"] < 1e-3, m
+    assert m["head_samples"] > 20 and m["head_grad_sample"] < 1e-3, m
+    assert m["head_online_delta"] < 1e-3 and m["head_target_delta"] < 1e-3, m

@@ -181,3 +181,30 @@ def test_oracle_bf16_operand_mode():
     g_rel = rel(out[torch.bfloat16][1].numpy(), out[None][1].numpy())
     assert 1e-4 < e_rel < 1e-2, e_rel      # rounded (not a no-op), but only at bf16 level
     assert g_rel < 2e-2, g_rel
+
+
+def test_oracle_split_weight_mode_meets_north_star():
+    """The split-weight mode's numerics (every activation operand in bf16, the weights exact:
+    O.SPLIT_WEIGHT_SITES) at WavLM-Large, 8 s, against the reference's own embeddings
+    (byol_large.npz): within the north-star 1e-3, while the full bf16-operand mode is not --
+    the weight rounding, shared by every frame and kept by the time mean, carries the bf16
+    mode's deviation (tools/ablate_bf16_sites.py)."""
+    from nrse_amd import arch as A, params as PR
+    z = np.load(os.path.join(GOLD, "byol_large.npz"))
+    arch = A.LARGE.deterministic()
+    layout = PR.byol_layout(arch, int(z["proj_dim"]), int(z["pred_dim"]))
+    flat = PR.init_byol_flat(layout, int(z["seed"]))
+    g = torch.Generator().manual_seed(int(z["seed"]) + 1)
+    clean = torch.randn(int(z["B"]), 1, int(z["L"]), generator=g).squeeze(1)[:2]
+    P = O.split_flat(layout, flat)["encoder"]
+    ref = z["eval_emb"][:2]
+    out = {}
+    for name, sites in (("split", O.SPLIT_WEIGHT_SITES), ("bf16", None)):
+        O.set_operand_dtype(torch.bfloat16, sites)
+        try:
+            with torch.no_grad():
+                out[name] = rel(O.encoder_forward(P, arch, clean, train=False).mean(1).numpy(), ref)
+        finally:
+            O.set_operand_dtype(None)
+    assert out["split"] < 1e-3, out
+    assert out["bf16"] > 3e-3, out
