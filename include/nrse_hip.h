@@ -34,7 +34,12 @@ typedef enum {
   NRSE_ERR_UNSUPPORTED = -5 /* configuration outside what the kernels implement */
 } nrse_status;
 
-typedef enum { NRSE_F32 = 0, NRSE_BF16 = 1 } nrse_dtype;
+typedef enum { NRSE_F32 = 0, NRSE_BF16 = 1, NRSE_BF16X3 = 2 } nrse_dtype;
+/* NRSE_BF16X3 (an OUTPUT format of nrse_layernorm_fwd and nrse_conv0_fwd only): the split-bf16
+ * activation of the split-weight mode's conv stack, three bf16 planes of n = rows * C elements
+ * each at the output pointer: [hi | lo | hi], hi = bf16(y), lo = bf16(y - hi). A GEMM that reads
+ * plane 0 with seg_stride n over nseg = 3 segments against weight planes [hi | hi | lo] computes
+ * y_hi w_hi + y_lo w_hi + y_hi w_lo: the f32 product to ~2^-16. */
 
 typedef struct {
   int device;

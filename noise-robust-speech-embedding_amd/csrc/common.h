@@ -34,6 +34,27 @@ NRSE_DEV bf16_t bf16_lo(float x) {
   return f2bf(x - __uint_as_float((uint32_t)h << 16));
 }
 
+// 4 consecutive values at element i of an output in dtype dt: f32, bf16, or the three-plane split
+// bf16 form NRSE_BF16X3 ([hi | lo | hi], planes `plane` elements apart; include/nrse_hip.h)
+NRSE_DEV void store4_out(void* p, int dt, long long i, long long plane, const float* o) {
+  if (dt == NRSE_F32) {
+    *reinterpret_cast<float4*>((float*)p + i) = make_float4(o[0], o[1], o[2], o[3]);
+    return;
+  }
+  uint2 u;
+  u.x = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
+  u.y = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
+  bf16_t* b = (bf16_t*)p + i;
+  *reinterpret_cast<uint2*>(b) = u;
+  if (dt == NRSE_BF16X3) {
+    uint2 w;
+    w.x = (uint32_t)f2bf(o[0] - __uint_as_float(u.x << 16)) | ((uint32_t)f2bf(o[1] - __uint_as_float(u.x & 0xffff0000u)) << 16);
+    w.y = (uint32_t)f2bf(o[2] - __uint_as_float(u.y << 16)) | ((uint32_t)f2bf(o[3] - __uint_as_float(u.y & 0xffff0000u)) << 16);
+    *reinterpret_cast<uint2*>(b + plane) = w;
+    *reinterpret_cast<uint2*>(b + 2 * plane) = u;
+  }
+}
+
 template <typename T> NRSE_DEV float to_f(T x);
 template <> NRSE_DEV float to_f<float>(float x) { return x; }
 template <> NRSE_DEV float to_f<bf16_t>(bf16_t x) { return bf2f(x); }

@@ -88,14 +88,8 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(const nrse_conv0_params 
 #pragma unroll
       for (int h = 0; h < 2; ++h) o[h] = gelu2(pk_fma((y[q][h] - mean) * rstd, ga[q][h], be[q][h]));
       const long long off = row * C + (q * 64 + lane) * 4;
-      if (p.out_dtype == NRSE_BF16) {
-        uint2 u;
-        u.x = (uint32_t)f2bf(o[0].x) | ((uint32_t)f2bf(o[0].y) << 16);
-        u.y = (uint32_t)f2bf(o[1].x) | ((uint32_t)f2bf(o[1].y) << 16);
-        *reinterpret_cast<uint2*>((bf16_t*)p.out + off) = u;
-      } else {
-        *reinterpret_cast<float4*>((float*)p.out + off) = make_float4(o[0].x, o[0].y, o[1].x, o[1].y);
-      }
+      const float ov[4] = {o[0].x, o[0].y, o[1].x, o[1].y};
+      store4_out(p.out, p.out_dtype, off, rows * C, ov);
     }
     if (lane == 0) {
       p.mean[row] = mean;
@@ -540,6 +534,8 @@ extern "C" int nrse_conv0_fwd(const nrse_conv0_params* p, void* stream) {
   NRSE_REQUIRE(p && p->wav && p->w && p->gamma && p->beta && p->out && p->mean && p->rstd, "nrse_conv0_fwd: bad args");
   NRSE_REQUIRE(p->k > 0 && p->k <= KMAX && p->T0 == (p->L - p->k) / p->s + 1, "nrse_conv0_fwd: bad geometry");
   NRSE_REQUIRE((long long)p->batch * p->T0 < (1LL << 31), "nrse_conv0_fwd: too many rows");
+  NRSE_REQUIRE(p->out_dtype == NRSE_F32 || p->out_dtype == NRSE_BF16 || p->out_dtype == NRSE_BF16X3,
+               "nrse_conv0_fwd: bad out_dtype %d", p->out_dtype);
   const long long rows = (long long)p->batch * p->T0;
   long long blocks = (rows + 3) / 4;
   if (blocks > 4096) blocks = 4096;

@@ -87,7 +87,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const nrse_ln_fwd_params p)
 #pragma unroll
       for (int e = 0; e < CH; ++e) o[e] = fmaxf(o[e], 0.f);
     }
-    store4(p.y, p.y_dtype, base + c0, o);
+    store4_out(p.y, p.y_dtype, base + c0, p.rows * C, o);
   }
   if (lane == 0) {
     if (p.mean) p.mean[row] = mean;
@@ -138,7 +138,7 @@ __global__ __launch_bounds__(256) void ln_fwd_f32_kernel(const nrse_ln_fwd_param
 #pragma unroll
       for (int e = 0; e < CH; ++e) o[e] = fmaxf(o[e], 0.f);
     }
-    store4(p.y, p.y_dtype, base + c0, o);
+    store4_out(p.y, p.y_dtype, base + c0, p.rows * C, o);
   }
   if (lane == 0) {
     if (p.mean) p.mean[row] = mean;
@@ -198,7 +198,7 @@ __global__ __launch_bounds__(256) void ln_fwd_bf16_kernel(const nrse_ln_fwd_para
 #pragma unroll
         for (int e = 0; e < CH; ++e) o[e] = fmaxf(o[e], 0.f);
       }
-      store4(p.y, p.y_dtype, row * C + c0, o);
+      store4_out(p.y, p.y_dtype, row * C + c0, p.rows * C, o);
     }
     if (lane == 0) {
       if (p.mean) p.mean[row] = mean;
@@ -574,6 +574,8 @@ bool c_ok(int C) { return C == 256 || C == 512 || C == 1024; }
 extern "C" int nrse_layernorm_fwd(const nrse_ln_fwd_params* p, void* stream) {
   NRSE_REQUIRE(p && p->x && p->y && p->gamma && p->beta && p->rows > 0, "nrse_layernorm_fwd: bad args");
   if (!c_ok(p->C)) { nrse_set_error("nrse_layernorm_fwd: C=%d not in {256,512,1024}", p->C); return NRSE_ERR_UNSUPPORTED; }
+  NRSE_REQUIRE(p->y_dtype == NRSE_F32 || p->y_dtype == NRSE_BF16 || p->y_dtype == NRSE_BF16X3,
+               "nrse_layernorm_fwd: bad y_dtype %d", p->y_dtype);
   if (p->x_dtype == NRSE_BF16 && p->C <= 512 && ((uintptr_t)p->x & 7) == 0) {
     constexpr int RPW = 4;
     const dim3 g((unsigned)((p->rows + 4 * RPW - 1) / (4 * RPW)));

@@ -14,6 +14,7 @@ LIB_PATH = os.environ.get("NRSE_LIB_PATH") or os.path.join(_HERE, "libnrse_hip.s
 
 F32 = 0
 BF16 = 1
+BF16X3 = 2   # output-only split-bf16 planes [hi | lo | hi] (include/nrse_hip.h)
 
 EPI_BIAS = 1 << 0
 EPI_GELU = 1 << 1

@@ -111,11 +111,14 @@ class EncoderWeights:
             w = self.m[f"feature_extractor.conv_layers.{i}.conv.weight"]
             co, ci, k = w.shape
             if self.lo:
+                # planes [hi | hi | lo] against the split activations' [hi | lo | hi] (NRSE_BF16X3):
+                # three K segments of one GEMM, x_hi w_hi + x_lo w_hi + x_hi w_lo
                 r32 = torch.empty(co, k * ci, device=eng.dev, dtype=F32)
                 K.swap12(w, r32, co, ci, k)
-                r2 = torch.empty(2, co, k * ci, device=eng.dev, dtype=cdt)
-                K.split_bf16(r32, r2[0], r2[1])
-                self.conv_r.append(r2[0])
+                r3 = torch.empty(3, co, k * ci, device=eng.dev, dtype=cdt)
+                K.split_bf16(r32, r3[0], r3[2])
+                r3[1].copy_(r3[0])
+                self.conv_r.append(r3[0])
                 self.conv_lo.append(r32.numel())
             else:
                 r = torch.empty(co, k * ci, device=eng.dev, dtype=cdt)
@@ -310,30 +313,42 @@ class ByolEngine:
         # -------- conv feature encoder ([TF]modeling_wavlm.py:712-720, 773-783)
         k0, s0, C0 = a.conv_kernel[0], a.conv_stride[0], a.conv_dim[0]
         T0 = (L - k0) // s0 + 1
-        y = torch.empty(B * T0, C0, device=dev, dtype=cdt)
+        # split-weight mode: the conv stack also carries its activations as split bf16 planes
+        # (NRSE_BF16X3 [hi | lo | hi], read by 3-segment GEMMs) and its pre-activations in f32 --
+        # the activation roundings that remain in this mode are otherwise dominated by the conv
+        # stack (tools/ablate_bf16_sites.py: 6e-4 of 7e-4 at 8 s, more at 3 s)
+        split = self.wsplit
+        nconv = len(a.conv_dim)
+        y = torch.empty((3, B * T0, C0) if split else (B * T0, C0), device=dev, dtype=cdt)
         mean = torch.empty(B * T0, device=dev, dtype=F32)
         rstd = torch.empty(B * T0, device=dev, dtype=F32)
         pre0 = "feature_extractor.conv_layers.0."
         K.conv0_fwd(wav, Pm[pre0 + "conv.weight"], Pm[pre0 + "layer_norm.weight"], Pm[pre0 + "layer_norm.bias"], y,
-                    mean, rstd, T0, k0, s0, a.eps)
+                    mean, rstd, T0, k0, s0, a.eps, split3=split)
         if need_grad:
             tape.conv.append(dict(mean=mean, rstd=rstd, T=T0))
-        x, Tin, Cin = y, T0, C0
-        for i in range(1, len(a.conv_dim)):
+        x, Tin, Cin = (y[0] if split else y), T0, C0
+        for i in range(1, nconv):
             k, s, C = a.conv_kernel[i], a.conv_stride[i], a.conv_dim[i]
             Tout = (Tin - k) // s + 1
-            pre_out = torch.empty(B * Tout, C, device=dev, dtype=cdt)
-            K.gemm(K.Operand(x, True, s * Cin, z1=Tin * Cin),
+            pre_out = torch.empty(B * Tout, C, device=dev, dtype=F32 if split else cdt)
+            K.gemm(K.Operand(x, True, s * Cin, z1=Tin * Cin, seg_stride=B * Tin * Cin if split else 0),
                    K.Operand(W.conv_r[i - 1], True, k * Cin, seg_stride=W.conv_lo[i - 1]), pre_out,
-                   Tout, C, k * Cin, ldc=C, batch=B, c_z1=Tout * C, nseg=2 if W.conv_lo[i - 1] else 1)
-            yo = torch.empty(B * Tout, C, device=dev, dtype=cdt)
+                   Tout, C, k * Cin, ldc=C, batch=B, c_z1=Tout * C, nseg=3 if split else 1)
+            # the last layer's output feeds only the feature-projection LN: f32 in the split mode
+            last = i == nconv - 1
+            if split:
+                yo3 = torch.empty((B * Tout, C) if last else (3, B * Tout, C), device=dev, dtype=F32 if last else cdt)
+            else:
+                yo3 = torch.empty(B * Tout, C, device=dev, dtype=cdt)
             mo = torch.empty(B * Tout, device=dev, dtype=F32)
             ro = torch.empty(B * Tout, device=dev, dtype=F32)
             p = f"feature_extractor.conv_layers.{i}."
-            K.ln_fwd(pre_out, Pm[p + "layer_norm.weight"], Pm[p + "layer_norm.bias"], yo, mo, ro, a.eps, gelu=True)
+            K.ln_fwd(pre_out, Pm[p + "layer_norm.weight"], Pm[p + "layer_norm.bias"], yo3, mo, ro, a.eps, gelu=True,
+                     split3=split and not last)
             if need_grad:
                 tape.conv.append(dict(x=x, pre=pre_out, mean=mo, rstd=ro, Tin=Tin, T=Tout, k=k, s=s))
-            x, Tin, Cin = yo, Tout, C
+            x, Tin, Cin = (yo3[0] if split and not last else yo3), Tout, C
         T = Tin
         C = Cin
         H = a.hidden

@@ -374,10 +374,19 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, *, splits:
 
 
 # ----------------------------------------------------------------------------- layernorm
-def ln_fwd(x, gamma, beta, y, mean, rstd, eps, gelu=False, relu=False):
+def _out_code(y: torch.Tensor, n: int, split3: bool) -> int:
+    """dtype code of a kernel output; split3: y is the [3, n] bf16 planes [hi | lo | hi] of the
+    split-weight mode's conv stack (NRSE_BF16X3)."""
+    if not split3:
+        return dtype_code(y)
+    assert y.dtype == torch.bfloat16 and y.is_contiguous() and y.shape[0] == 3 and y.numel() == 3 * n, y.shape
+    return _lib.BF16X3
+
+
+def ln_fwd(x, gamma, beta, y, mean, rstd, eps, gelu=False, relu=False, split3=False):
     rows, C = x.shape[0] if x.dim() == 2 else x.numel() // x.shape[-1], x.shape[-1]
-    p = LnFwdParams(ptr(x), dtype_code(x), ptr(gamma), ptr(beta), ptr(y), dtype_code(y), ptr(mean), ptr(rstd),
-                    rows, C, eps, (_lib.LN_GELU if gelu else 0) | (_lib.LN_RELU if relu else 0))
+    p = LnFwdParams(ptr(x), dtype_code(x), ptr(gamma), ptr(beta), ptr(y), _out_code(y, rows * C, split3), ptr(mean),
+                    ptr(rstd), rows, C, eps, (_lib.LN_GELU if gelu else 0) | (_lib.LN_RELU if relu else 0))
     _call("nrse_layernorm_fwd", ctypes.byref(p), stream_ptr())
 
 
@@ -469,12 +478,12 @@ def attn_bwd(qkv, gate, bias, ctx, dctx, lse, delta, dqkv, dgate, diag, batch, T
 
 
 # ----------------------------------------------------------------------------- conv front end
-def conv0_fwd(wav, w, gamma, beta, out, mean, rstd, T0, k, s, eps):
+def conv0_fwd(wav, w, gamma, beta, out, mean, rstd, T0, k, s, eps, split3=False):
     B, L = wav.shape
     C = w.shape[0]
     p = Conv0Params()
     p.wav, p.L, p.w, p.gamma, p.beta = ptr(wav), L, ptr(w), ptr(gamma), ptr(beta)
-    p.out, p.out_dtype, p.mean, p.rstd = ptr(out), dtype_code(out), ptr(mean), ptr(rstd)
+    p.out, p.out_dtype, p.mean, p.rstd = ptr(out), _out_code(out, B * T0 * C, split3), ptr(mean), ptr(rstd)
     p.batch, p.T0, p.C, p.k, p.s, p.eps = B, T0, C, k, s, eps
     _call("nrse_conv0_fwd", ctypes.byref(p), stream_ptr())
 

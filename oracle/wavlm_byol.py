@@ -93,9 +93,10 @@ def position_bias(E: torch.Tensor, T: int, nb: int, md: int) -> torch.Tensor:
 #   ffn_up   the FFN-up GEMM (LN output, weights, stored pre-activation and GELU output)
 #   ffn_down the FFN-down GEMM weights
 SITES = ("conv", "proj", "posconv", "qkv", "attn", "oproj", "ffn_up", "ffn_down")
-# the engine's split-weight mode (bf16sw): every activation operand rounded, every weight exact
-# (the forward GEMMs multiply by the weights' hi + lo bf16 pair)
-SPLIT_WEIGHT_SITES = tuple(f"{s}:a" for s in SITES if s != "attn") + ("attn",)
+# the engine's split-weight mode (bf16sw): every weight exact (the forward GEMMs multiply by the
+# weights' hi + lo bf16 pair), the conv stack's activations exact too (split bf16 planes and f32
+# pre-activations), every other activation operand rounded
+SPLIT_WEIGHT_SITES = tuple(f"{s}:a" for s in SITES if s not in ("attn", "conv")) + ("attn",)
 _OPERAND_DTYPE = None
 _SITES = None
 
@@ -115,6 +116,8 @@ def _site_on(site, kind=None) -> bool:
         return False
     if _SITES is None or site is None or site in _SITES:
         return True
+    if kind == "p":   # a stored pre-activation: an activation ("a") unless selected on its own
+        return f"{site}:a" in _SITES or f"{site}:p" in _SITES
     return kind is not None and f"{site}:{kind}" in _SITES
 
 
@@ -175,7 +178,8 @@ def conv_stack(P: dict, a, wav: torch.Tensor) -> torch.Tensor:
         if i == 0:   # direct conv from the f32 waveform (engine: conv0 kernel, f32 weights)
             x = F.conv1d(x, P[pre + "conv.weight"], stride=s)
         else:        # implicit GEMM, bf16 operands, pre-LN output stored in the compute dtype
-            x = _rf(_rg(F.conv1d(_rf(x, "conv"), _rf(P[pre + "conv.weight"], "conv", "w"), stride=s), "conv"), "conv")
+            x = _rf(_rg(F.conv1d(_rf(x, "conv"), _rf(P[pre + "conv.weight"], "conv", "w"), stride=s), "conv"), "conv",
+                    "p")
         x = F.layer_norm(x.transpose(1, 2), (x.shape[1],), P[pre + "layer_norm.weight"], P[pre + "layer_norm.bias"],
                          a.eps).transpose(1, 2)
         x = _rg(_rf(F.gelu(x), "conv"), "conv")

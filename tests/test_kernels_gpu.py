@@ -394,3 +394,37 @@ def test_dropout_cast_colsum(nrse_device, odt, p):
     keep = (ref != 0) | (x == 0)
     exact = torch.where(keep, x.double() / (1 - p), torch.zeros_like(x, dtype=torch.float64))
     assert rel(cs, exact.sum(0)) < 1e-5
+
+
+def test_split3_outputs(nrse_device):
+    """NRSE_BF16X3 outputs of the LN forward and conv0 (the split-weight mode's conv stack):
+    planes [hi | lo | hi] with hi = bf16(y), lo = bf16(y - hi), equal to the f32 output split."""
+    from nrse_amd import kernels as K
+    dev = nrse_device
+    for xdt in (torch.float32, torch.bfloat16):
+        rows, C = 1001, 512
+        x = (torch.randn(rows, C, device=dev) * 2).to(xdt)
+        g = torch.randn(C, device=dev) * 0.1 + 1
+        b = torch.randn(C, device=dev) * 0.1
+        y32 = torch.empty(rows, C, device=dev)
+        m = torch.empty(rows, device=dev); r = torch.empty(rows, device=dev)
+        K.ln_fwd(x, g, b, y32, m, r, 1e-5, gelu=True)
+        y3 = torch.empty(3, rows, C, device=dev, dtype=torch.bfloat16)
+        K.ln_fwd(x, g, b, y3, m, r, 1e-5, gelu=True, split3=True)
+        hi, lo = torch.empty(rows, C, device=dev, dtype=torch.bfloat16), torch.empty(rows, C, device=dev, dtype=torch.bfloat16)
+        K.split_bf16(y32, hi, lo)
+        assert torch.equal(y3[0], hi) and torch.equal(y3[1], lo) and torch.equal(y3[2], hi)
+    B, L, k, s = 3, 16000, 10, 5
+    T0 = (L - k) // s + 1
+    wav = torch.randn(B, L, device=dev) * 0.1
+    w = torch.randn(512, k, device=dev) * 0.3
+    g = torch.randn(512, device=dev) * 0.1 + 1
+    b = torch.randn(512, device=dev) * 0.1
+    o32 = torch.empty(B * T0, 512, device=dev)
+    m = torch.empty(B * T0, device=dev); r = torch.empty(B * T0, device=dev)
+    K.conv0_fwd(wav, w, g, b, o32, m, r, T0, k, s, 1e-5)
+    o3 = torch.empty(3, B * T0, 512, device=dev, dtype=torch.bfloat16)
+    K.conv0_fwd(wav, w, g, b, o3, m, r, T0, k, s, 1e-5, split3=True)
+    hi, lo = torch.empty_like(o3[0]), torch.empty_like(o3[0])
+    K.split_bf16(o32, hi, lo)
+    assert torch.equal(o3[0], hi) and torch.equal(o3[1], lo) and torch.equal(o3[2], hi)

@@ -171,8 +171,8 @@ def test_large_bf16sw_matches_reference(nrse_device, large):
     _record(f"bf16sw_{large['tag']}", m)
     assert m["eval_emb"] < 1e-3, m          # north-star bound on embeddings
     assert m["hidden_norms"] < 1e-3, m
-    assert m["eval_pred"] < 2e-3 and m["eval_tproj"] < 2e-3, m
-    assert m["eval_loss_abs"] < 1e-3 and m["train_loss_abs"] < 1e-3, m
+    assert m["eval_pred"] < 1e-3 and m["eval_tproj"] < 1e-3, m
+    assert m["eval_loss_abs"] < 1e-4 and m["train_loss_abs"] < 3e-3, m
     assert m["bn_running"] < 3e-3, m
 
 
@@ -215,7 +215,8 @@ def test_large_bf16_heads_match_reference(nrse_device, large):
          "loss_abs": abs(float(loss) - float(z["train_loss"]))}
     # head tensors: layout spec index -> reference per-tensor gradient norm
     g = eng.grad.cpu()
-    worst, head_lo, head_hi = 0.0, None, 0
+    worst, worst_name, head_lo, head_hi = 0.0, None, None, 0
+    floor = 1e-4 * float(z["train_grad_norm"])   # as the f32 test: tensors with a significant gradient
     for i, (gname, s) in enumerate(eng.layout.specs):
         if gname == "encoder":
             continue
@@ -223,8 +224,12 @@ def test_large_bf16_heads_match_reference(nrse_device, large):
         head_lo = off if head_lo is None else min(head_lo, off)
         head_hi = max(head_hi, off + cnt)
         ref_n = float(z["grad_tensor_norms"][i])
-        worst = max(worst, abs(float(g[off:off + cnt].norm()) - ref_n) / ref_n)
+        if ref_n > floor:
+            e = abs(float(g[off:off + cnt].norm()) - ref_n) / ref_n
+            if e > worst:
+                worst, worst_name = e, f"{gname}.{s.name}"
     m["head_tensor_norm_worst"] = worst
+    m["head_tensor_norm_worst_name"] = worst_name
     idx = torch.from_numpy(z["grad_idx"])
     sel = (idx >= head_lo) & (idx < head_hi)
     m["head_samples"] = int(sel.sum())
@@ -251,4 +256,7 @@ def test_large_bf16_heads_match_reference(nrse_device, large):
     assert m["loss_abs"] < 1e-4, m
     assert m["head_tensor_norm_worst"] < 1e-3, m
     assert m["head_samples"] > 20 and m["head_grad_sample"] < 1e-3, m
-    assert m["head_online_delta"] < 1e-3 and m["head_target_delta"] < 1e-3, m
+    assert m["head_online_delta"] < 1e-3, m
+    # the EMA delta (1 - ema) * d_online ~ 3e-8 sits at ~1 ulp of the 0.02-sized f32 weights it is
+    # added to: f32-rounding-limited on both sides (the f32 test's bound)
+    assert m["head_target_delta"] < 0.05, m

@@ -184,8 +184,9 @@ def test_oracle_bf16_operand_mode():
 
 
 def test_oracle_split_weight_mode_meets_north_star():
-    """The split-weight mode's numerics (every activation operand in bf16, the weights exact:
-    O.SPLIT_WEIGHT_SITES) at WavLM-Large, 8 s, against the reference's own embeddings
+    """The split-weight mode's numerics (the weights and the conv stack's activations exact, every
+    other activation operand in bf16: O.SPLIT_WEIGHT_SITES) at WavLM-Large, 8 s, against the
+    reference's own embeddings
     (byol_large.npz): within the north-star 1e-3, while the full bf16-operand mode is not --
     the weight rounding, shared by every frame and kept by the time mean, carries the bf16
     mode's deviation (tools/ablate_bf16_sites.py)."""
