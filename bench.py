@@ -278,21 +278,42 @@ def main():
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
+    # N > 1: events around each step's all-reduce wait (end of backward -> every exchange done)
+    eng.ar_timing = world > 1
+    eng.ar_events = []
     executed = [0, 0]
     probe = []
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    sent = 0
     for i in range(args.steps):
         step(args.warmup + i)
         executed[0] += eng.executed_layers[0]
         executed[1] += eng.executed_layers[1]
+        sent += allreduce.issued_elems if allreduce is not None else 0
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     dt = time.perf_counter() - t0
+    ddp_stats = None
     if world > 1:
+        # multi-rank readiness record: each rank's time per step, the exposed
+        # all-reduce wait (last backward kernel -> all exchanges done, device events on the main
+        # stream), and the bytes the gradient exchange puts on the wire per step
+        exposed = [e0.elapsed_time(e1) for e0, e1 in eng.ar_events]
+        eng.ar_timing = False
+        mine = torch.tensor([dt / args.steps * 1e3, sum(exposed) / max(len(exposed), 1)], device=dev, dtype=torch.float64)
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        torch.distributed.all_gather(allr, mine)
+        esz = 2 if args.wire == "bf16" else 4
+        buf_bytes = sent * esz // args.steps   # LayerDrop-skipped layers are not sent
+        ddp_stats = {"rank_ms_per_step": [round(float(t[0]), 2) for t in allr],
+                     "allreduce_exposed_ms": [round(float(t[1]), 3) for t in allr],
+                     "wire": args.wire, "grad_bytes_per_step": buf_bytes,
+                     "ring_bytes_per_rank_per_step": int(2 * (world - 1) / world * buf_bytes),
+                     "backend": torch.distributed.get_backend()}
         tt = torch.tensor([dt], device=dev)
         torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
         dt = float(tt)
@@ -388,6 +409,7 @@ def main():
                                                 "concurrent streams",
                                         "gemm_share_of_step": round(gms / probe_step_ms, 3)}},
         "step_tflops": round(fpp * value / world / 1e12, 1),
+        **({"ddp": ddp_stats} if ddp_stats is not None else {}),
         "loss_last": round(loss, 5), "snr_mix_ok": st_ok,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

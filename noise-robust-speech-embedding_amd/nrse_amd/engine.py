@@ -218,6 +218,10 @@ class ByolEngine:
         self._opt_events = None
         self._opt_done = None
         self._segments = self._param_segments()
+        # ar_timing: record (end of backward, all exchanges done) events per step on the main
+        # stream (bench.py reports the exposed all-reduce time from them)
+        self.ar_timing = False
+        self.ar_events = []
 
     def refresh_shadows(self, which=("online", "target")) -> None:
         """Re-derive the bf16 GEMM-operand copies (and the split mode's lo planes) of the f32
@@ -472,10 +476,16 @@ class ByolEngine:
         return emb, tape, executed
 
     # ------------------------------------------------------------------ encoder backward
-    def encoder_backward(self, tape: Tape, demb: torch.Tensor, Gv: dict, W: EncoderWeights, on_layer=None) -> None:
+    def encoder_backward(self, tape: Tape, demb: torch.Tensor, Gv: dict, W: EncoderWeights, on_layer=None,
+                         on_front=None) -> None:
         """Accumulate d(loss)/d(encoder params) into the grad views Gv given d(loss)/d(emb).
         on_layer(li), if given, is called once layer li's gradients are all enqueued (main and
-        side stream) and no later kernel writes them (layer 0 excepted: rel_attn_embed)."""
+        side stream) and no later kernel writes them (layer 0 excepted: rel_attn_embed).
+        on_front(name), if given, likewise for the front-end groups of _grad_groups(): "rel",
+        "posconv", "proj", "conv6" .. "conv1", "conv0" (in that order)."""
+        def front(name):
+            if on_front is not None:
+                on_front(name)
         a = self.arch
         cdt = self.cdt
         dev = self.dev
@@ -566,6 +576,7 @@ class ByolEngine:
         tape.layers = []
         main.wait_stream(self._bwd_side_stream())
         K.rel_bias_bwd(diag, *self.bucket_runs(T), Gv["encoder.layers.0.attention.rel_attn_embed.weight"], nh, T)
+        front("rel")
         # positional conv block: h0 = drop(h + gelu(conv(hpad) + b))
         pk, G = a.pos_kernel, a.pos_groups
         cpg = H // G
@@ -602,6 +613,7 @@ class ByolEngine:
             K.weight_norm_bwd(dWf, Pm[pre + "original0"], Pm[pre + "original1"], W.wn_norms, Gv[pre + "original0"],
                               Gv[pre + "original1"], wn_scratch, H, cpg, pk)
             del dWf
+            front("posconv")
         # dgrad: ds += conv_transpose(dpre) (flipped taps, dypad has pk/2-1 leading zero rows)
         K.gemm(K.Operand(dypad, True, H, chunk_shift=cs, ld_chunk=H, z1=(T + pk) * H, z2=cpg),
                K.Operand(W.wd, True, pk * cpg, z2=cpg * pk * cpg), ds, T, cpg, pk * cpg, ldc=H, batch=B * G, zdiv=G,
@@ -623,6 +635,7 @@ class ByolEngine:
         K.ln_bwd(dxn, tape.feats, Pm["feature_projection.layer_norm.weight"], tape.fp_mean, tape.fp_rstd, dfeat,
                  dgamma=Gv["feature_projection.layer_norm.weight"], dbeta=Gv["feature_projection.layer_norm.bias"])
         del dxn
+        front("proj")
         tape.feats = tape.xn = tape.hpad = tape.pos_pre = None
         # conv stack backward (LN+GELU bwd with col2im of the next layer's dgrad GEMM)
         dy_src, col = dfeat, None
@@ -660,6 +673,7 @@ class ByolEngine:
                     K.gemm_slab(A_op, B_op, dWr, Cc, k * Cin, Tout, nseg=B // S, splits=S, accumulate=False)
                 K.swap12(dWr, Gv[p + "conv.weight"], Cc, k, Cin, accumulate=True)
                 del dWr
+                front(f"conv{i}")
             # dgrad -> G [B*Tout, k*Cin] (col2im folded into the next LN backward)
             Gd = torch.empty(B * Tout, k * Cin, device=dev, dtype=cdt)
             K.gemm(K.Operand(dpre, True, Cc), K.Operand(W.conv_r[i - 1], False, k * Cin), Gd, B * Tout, k * Cin, Cc,
@@ -672,6 +686,7 @@ class ByolEngine:
         K.conv0_bwd(tape.wav, Pm[p + "conv.weight"], Pm[p + "layer_norm.weight"], Pm[p + "layer_norm.bias"],
                     c0["mean"], c0["rstd"], dy_src, Gv[p + "conv.weight"], Gv[p + "layer_norm.weight"],
                     Gv[p + "layer_norm.bias"], c0["T"], a.conv_kernel[0], a.conv_stride[0], col[:3])
+        front("conv0")
         tape.conv = []
         main.wait_stream(self._bwd_side_stream())  # every gradient written before clip / AdamW
 
@@ -853,37 +868,64 @@ class ByolEngine:
         """[start, end) of transformer layer li's parameters in the flat buffers."""
         return PR.layer_range(self.layout, self.arch, li)
 
+    def _grad_groups(self) -> dict:
+        """The units of the overlapped gradient all-reduce (params.grad_groups)."""
+        if getattr(self, "_groups", None) is None:
+            self._groups = PR.grad_groups(self.layout, self.arch)
+        return self._groups
+
     def backward(self, dpred: torch.Tensor, ctx: dict, allreduce=None) -> None:
         """Accumulate all online-parameter gradients into self.grad from d(loss)/d(pred).
-        With a GradAllReduce, each transformer layer's gradient range (except layer 0's) is
-        all-reduced as soon as backward has finished it, overlapping the exchange with the
-        remaining layers; the rest of the buffer goes when backward ends. Layers LayerDrop
+        With a GradAllReduce, every unit of _grad_groups() is all-reduced as soon as backward
+        has finished writing it, so the exchange overlaps the rest of backward: the heads right
+        after their backward (before the encoder's), each transformer layer when its backward
+        (main-stream LN / bias / gate gradients and side-stream weight gradients) is done, the
+        final LN with the top layer, layer 0 without its rel_attn_embed row (sent after the
+        rel-pos bias backward), then the front end group by group as its weight gradients land
+        (pos-conv, feature projection, conv 6 .. 1, conv 0): only conv 0's 5k parameters and
+        the exchanges still in flight remain after the last backward kernel. Layers LayerDrop
         skipped hold zero gradient on every rank (rank-shared decisions) and are not sent."""
         Gp = self.group_views(self.grad, "predictor")
         Gj = self.group_views(self.grad, "projector")
         Ge = self.group_views(self.grad, "encoder")
+        on = allreduce is not None and allreduce.active()
+        main = torch.cuda.current_stream(self.dev)
+        groups = self._grad_groups() if on else None
+
+        def send(key):
+            # the unit's producers ran on main and/or the backward side stream: enqueue the
+            # exchange on the side stream behind both
+            side = main if _SERIAL_TARGET else self._bwd_side_stream()
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                for s, e in groups[key]:
+                    allreduce.issue(self.grad[s:e])
+
+        if on:
+            allreduce.start()
         dproj = self.predictor_backward(dpred, ctx["qc"], ctx["Ppr"], Gp)
         demb = self.projector_backward(dproj, ctx["pc"], ctx["Pon"], Gj)
-        on_layer = None
-        if allreduce is not None and allreduce.active():
-            allreduce.start()
-            main = torch.cuda.current_stream(self.dev)
+        if on:
+            send("heads")
+        top = max((L_["li"] for L_ in ctx["tape"].layers), default=None)
 
-            def on_layer(li):
-                if li == 0:
-                    return  # rel_attn_embed is written after the layer loop
-                s, e = self.layer_range(li)
-                side = main if _SERIAL_TARGET else self._bwd_side_stream()
-                side.wait_stream(main)  # the layer's main-stream gradients (LN, biases, gate)
-                with torch.cuda.stream(side):
-                    allreduce.issue(self.grad[s:e])
-        self.encoder_backward(ctx["tape"], demb, Ge, ctx["W"], on_layer=on_layer)
-        if on_layer is not None:
-            s1, _ = self.layer_range(1)
-            _, e_last = self.layer_range(self.arch.layers - 1)
-            allreduce.issue(self.grad[:s1])          # conv / projection / pos-conv / layer 0
-            allreduce.issue(self.grad[e_last:])      # final LN + heads
+        def on_layer(li):
+            send(("layer", li))
+            if li == top:
+                send("final")   # written by the first kernel of the encoder backward
+        self.encoder_backward(ctx["tape"], demb, Ge, ctx["W"], on_layer=on_layer if on else None,
+                              on_front=send if on else None)
+        if on:
+            if top is None:
+                send("final")
+            if self.ar_timing:
+                ev0 = torch.cuda.Event(enable_timing=True)
+                ev0.record(main)
             allreduce.finish()
+            if self.ar_timing:
+                ev1 = torch.cuda.Event(enable_timing=True)
+                ev1.record(main)
+                self.ar_events.append((ev0, ev1))
 
     def optimizer_step(self, lr: float, grad_scale: float = 1.0) -> None:
         """clip_grad_norm_(1.0) + AdamW + target EMA (train_byol.py:67-71), no host sync.

@@ -239,3 +239,41 @@ def layer_range(layout: ByolLayout, arch: WavLMArch, li: int) -> tuple:
     nxt = (f"encoder.layers.{li + 1}.attention.q_proj.weight" if li + 1 < arch.layers else "encoder.layer_norm.weight")
     return start, layout.offsets[pre + nxt][0]
 
+
+
+def grad_groups(layout: ByolLayout, arch: WavLMArch) -> dict:
+    """The flat gradient cut into the units the overlapped all-reduce sends (nrse_amd/engine.py
+    backward), each a list of [start, end) ranges; together they tile the buffer exactly once.
+    "heads" = projector + predictor, "final" = the final LN, ("layer", li) = transformer layer li
+    (layer 0 without its rel_attn_embed, which is "rel"), "posconv", "proj" = the feature
+    projection, its LN and the SpecAugment embedding, "conv<i>" = conv layer i's weight and LN."""
+    pre = GROUP_PREFIX["encoder"]
+    off = lambda name: layout.offsets[pre + name][0]   # noqa: E731
+    starts = sorted(v[0] for v in layout.offsets.values())
+    head0 = min(v[0] for k, v in layout.offsets.items() if not k.startswith(pre))
+    g = {"heads": [(head0, layout.numel)], "final": [(off("encoder.layer_norm.weight"), head0)]}
+    rel = off("encoder.layers.0.attention.rel_attn_embed.weight")
+    rel_end = next(o for o in starts if o > rel)
+    for li in range(arch.layers):
+        s, e = layer_range(layout, arch, li)
+        g[("layer", li)] = [(s, rel), (rel_end, e)] if li == 0 else [(s, e)]
+    g["rel"] = [(rel, rel_end)]
+    pos0 = off("encoder.pos_conv_embed.conv.bias")
+    g["posconv"] = [(pos0, layer_range(layout, arch, 0)[0])]
+    conv = [off(f"feature_extractor.conv_layers.{i}.conv.weight") for i in range(len(arch.conv_dim))]
+    fp0 = off("feature_projection.layer_norm.weight")
+    g["proj"] = [(fp0, pos0)] + ([(0, conv[0])] if conv[0] > 0 else [])
+    for i in range(len(conv)):
+        g[f"conv{i}"] = [(conv[i], conv[i + 1] if i + 1 < len(conv) else fp0)]
+    return g
+
+
+def grad_group_order(arch: WavLMArch) -> list:
+    """The order the engine's backward sends grad_groups() when no layer is skipped."""
+    order = ["heads"]
+    for li in reversed(range(arch.layers)):
+        order.append(("layer", li))
+        if li == arch.layers - 1:
+            order.append("final")
+    order += ["rel", "posconv", "proj"] + [f"conv{i}" for i in reversed(range(1, len(arch.conv_dim)))] + ["conv0"]
+    return order
