@@ -234,6 +234,11 @@ typedef struct {
   float scale;                    /* 1/sqrt(head_dim) */
   float dropout_p; uint32_t seed;
   const float* bias_vec;          /* [H, 2T-1] (bf16 MFMA path); bias [H, T, Tb] is the f32 path's */
+  uint16_t* drop_mask;            /* optional (bf16 MFMA path, dropout_p > 0): the keep bits of the
+                                     probability dropout, [B*H][ntiles][4][Tp] u16 (ntiles = Tp/64,
+                                     Tp = T rounded up to 64): word (bh, key tile kt, g, query q) bit
+                                     4t + r = keep(q, key 64 kt + 16 t + 4 g + r); the backward reads
+                                     them instead of re-hashing (nrse_attn_mask_elems) */
 } nrse_attn_fwd_params;
 
 typedef struct {
@@ -248,6 +253,7 @@ typedef struct {
   int batch, T, H, head_dim;
   float scale; float dropout_p; uint32_t seed;
   const float* bias_vec;               /* [H, 2T-1] (bf16 MFMA path) */
+  const uint16_t* drop_mask;           /* optional: the forward's keep bits (nrse_attn_fwd_params) */
   float* diag_part;                    /* optional: f32 workspace of nrse_attn_bwd_workspace(p)
                                           floats; the per-block diag rows are then added in a fixed
                                           order (deterministic) instead of by f32 atomics */
@@ -256,6 +262,7 @@ typedef struct {
 int nrse_attn_fwd(const nrse_attn_fwd_params* p, void* stream);
 int nrse_attn_bwd(const nrse_attn_bwd_params* p, void* stream);
 long long nrse_attn_bwd_workspace(const nrse_attn_bwd_params* p);  /* floats for p->diag_part */
+long long nrse_attn_mask_elems(int batch, int T, int H);           /* u16 words of drop_mask */
 
 /* ------------------------------------------------------------------------------------------
  * Conv feature encoder front end and the positional-conv weight norm.

@@ -195,6 +195,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
   const uint32_t thr = dropout_threshold16(p.dropout_p);
   constexpr bool drop = DROP;
   const float dsc = drop ? 1.f / (1.f - p.dropout_p) : 1.f;
+  const int Tp = ntiles * 64;
   // this lane's query row: key pair (kb + 16t + 4g)/2 + rp holds elements r = 2rp, 2rp + 1
   const uint32_t rowpair = (uint32_t)(bh * T + qi) * (uint32_t)((T + 1) >> 1) + (uint32_t)(2 * g);
   // Lazy rescaling in the base-2 domain: mref is the row's reference maximum, and a tile's scores
@@ -283,17 +284,22 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
 #pragma unroll
     for (int t = 0; t < 4; ++t) lpart2 += f32x2{pd[t][0], pd[t][1]} + f32x2{pd[t][2], pd[t][3]};
     if constexpr (DROP) {
+      uint32_t mb = 0;  // this lane's 16 keep bits of the tile: bit 4t + r = key kb + 16t + 4g + r
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int rp = 0; rp < 2; ++rp) {
           const uint32_t hh = mix32((rowpair + (uint32_t)((kb >> 1) + 8 * t + rp)) ^ key);
-          pd[t][2 * rp] = attn_half_keep(hh, 0, thr) ? pd[t][2 * rp] : 0.f;
-          pd[t][2 * rp + 1] = attn_half_keep(hh, 1, thr) ? pd[t][2 * rp + 1] : 0.f;
+          const bool k0 = attn_half_keep(hh, 0, thr), k1 = attn_half_keep(hh, 1, thr);
+          pd[t][2 * rp] = k0 ? pd[t][2 * rp] : 0.f;
+          pd[t][2 * rp + 1] = k1 ? pd[t][2 * rp + 1] : 0.f;
+          mb |= (k0 ? 1u << (4 * t + 2 * rp) : 0u) | (k1 ? 2u << (4 * t + 2 * rp) : 0u);
           // opaque to the optimiser: otherwise it pushes the bf16 conversion into each select
           // (16 conversions + 8 v_perm per tile instead of 8 packed conversions)
           asm("" : "+v"(pd[t][2 * rp]), "+v"(pd[t][2 * rp + 1]));
         }
+      // the backward reads the bits instead of re-hashing: [bh][key tile][g][Tp] u16
+      if (p.drop_mask && qv) p.drop_mask[((bh * ntiles + it) * 4 + g) * Tp + qi] = (uint16_t)mb;
     }
     // O^T = V^T P^T (V in the A slot): lane (g, i16) holds O[its query][16 dt + 4g + r], so the
     // rescale by its own row's alpha needs no cross-lane broadcast
@@ -325,8 +331,11 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
 }
 
 // ------------------------------------------------------------------------------ bwd: dQ, dgate
-template <bool DROP>
+// DM: dropout mode, 0 none, 1 re-hashed keep bits, 2 the forward's recorded bits (drop_mask);
+// one specialisation each (both paths in one kernel cost 20 VGPRs and a wave per SIMD)
+template <int DM>
 __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_params p) {
+  constexpr bool DROP = DM != 0;
   extern __shared__ __attribute__((aligned(16))) char dyn[];
   char* const kv0 = dyn;  // [2 buffers][K tile, V tile], LDS-DMA double buffer as in the forward
   float* const bv = reinterpret_cast<float*>(dyn + 4 * TILE_B);
@@ -384,6 +393,12 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
   constexpr bool drop = DROP;
   const float dsc = drop ? 1.f / (1.f - p.dropout_p) : 1.f;
   const uint32_t rowpair = (uint32_t)(bh * T + qi) * (uint32_t)((T + 1) >> 1) + (uint32_t)(2 * g);  // as fwd
+  // the forward's keep bits (if recorded): word (bh, key tile, g, qi), bit 4t + r for key 16t + 4g + r;
+  // tile it+1's word is loaded while tile it computes (the top-of-tile vmcnt(0) covers it)
+  const int Tp = ntiles * 64;
+  constexpr bool use_mask = DM == 2;
+  const uint16_t* mrow = use_mask ? p.drop_mask + (bh * ntiles * 4 + g) * (long long)Tp + (qv ? qi : 0) : nullptr;
+  uint32_t mnext = use_mask ? (uint32_t)mrow[0] : 0u;
   float dgate = 0.f;
   f32x4 dq[4];
 #pragma unroll
@@ -395,10 +410,12 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    const uint32_t mcur = mnext;
     if (it + 1 < ntiles) {
       char* const Kn = kv0 + ((it + 1) & 1) * 2 * TILE_B;
       kv_dma_issue(kd, Kn, kb + 64, w);
       kv_dma_issue(vd, Kn + TILE_B, kb + 64, w);
+      if (use_mask) mnext = mrow[(long long)(it + 1) * 4 * Tp];
     }
     const int nt16 = min(4, (T - kb + 15) >> 4);
     f32x4 s[4], dp[4];
@@ -422,16 +439,23 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
       bb[t][0] = v4.x; bb[t][1] = v4.y; bb[t][2] = v4.z; bb[t][3] = v4.w;
     }
     if constexpr (DROP) {
+      if constexpr (use_mask) {
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
-        if (t < nt16) {
+        for (int t = 0; t < 4; ++t)
 #pragma unroll
-          for (int rp = 0; rp < 2; ++rp) {
-            const uint32_t hh = mix32((rowpair + (uint32_t)((kb >> 1) + 8 * t + rp)) ^ key);
-            dp[t][2 * rp] = attn_half_keep(hh, 0, thr) ? dp[t][2 * rp] * dsc : 0.f;
-            dp[t][2 * rp + 1] = attn_half_keep(hh, 1, thr) ? dp[t][2 * rp + 1] * dsc : 0.f;
+          for (int r = 0; r < 4; ++r) dp[t][r] = (mcur >> (4 * t + r)) & 1u ? dp[t][r] * dsc : 0.f;
+      } else {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          if (t < nt16) {
+#pragma unroll
+            for (int rp = 0; rp < 2; ++rp) {
+              const uint32_t hh = mix32((rowpair + (uint32_t)((kb >> 1) + 8 * t + rp)) ^ key);
+              dp[t][2 * rp] = attn_half_keep(hh, 0, thr) ? dp[t][2 * rp] * dsc : 0.f;
+              dp[t][2 * rp + 1] = attn_half_keep(hh, 1, thr) ? dp[t][2 * rp + 1] * dsc : 0.f;
+            }
           }
-        }
+      }
     }
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -479,6 +503,8 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
 // ------------------------------------------------------------------------------ bwd: dK, dV, diag
 // 3 waves per SIMD (<= 168 VGPRs; LDS ~50 KB at T = 399 -> 3 workgroups per CU): the element
 // loops are long dependency chains, latency-bound at 2 waves per SIMD
+// DM: dropout mode as attn_bwd_q_kernel's
+template <int DM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void attn_bwd_kv_kernel(
     const nrse_attn_bwd_params p) {
   extern __shared__ __attribute__((aligned(16))) char dyn[];
@@ -490,6 +516,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   const int bvl = bv_len(T);
   float* const diag = rbv + 4 * bvl;                                  // [diag_len(T)]
   float* const dtmp = diag + diag_len(T);                             // [4 waves][4 lane rows][64]
+  // [2 buffers][4 g][64 queries] u16: the forward's keep bits of this key block for the query
+  // tile, staged by LDS-DMA beside Q / dO (wave 0, lanes 0-31: 512 B)
+  char* const mtile0 = reinterpret_cast<char*>(dtmp + 1024);
   const long long ld3 = 3LL * Hd;
   const BlockPos bp = block_pos((p.T + 63) / 64, p.H);
   const int b = bp.b, h = bp.h;
@@ -505,9 +534,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   const KvDma qd = kv_dma_init(qkv, T, ld3, h * D * 2, w, lane);
   const KvDma od = kv_dma_init(dctx, T, Hd, h * D * 2, w, lane);
   const int ntiles = (T + 63) / 64;
+  const long long bh = (long long)b * H + h;
+  constexpr bool use_mask = DM == 2;
+  // mask DMA: lane l < 32 of wave 0 moves 16 B = 8 queries of row g_f = l >> 3
+  __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(use_mask ? p.drop_mask + (bh * ntiles + bp.blk) * 4 * (long long)(ntiles * 64) : nullptr), 0,
+      use_mask ? ntiles * 64 * 4 * 2 : 0, 0x00020000);
+  const unsigned mvoff = (unsigned)(((lane >> 3) * ntiles * 64 + (lane & 7) * 8) * 2);
+  auto mask_issue = [&](char* dst, int q0) {
+    if (use_mask && w == 0 && lane < 32)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(mrs, (lds_void_t*)dst, 16, mvoff + (unsigned)q0 * 2, 0, 0, 0);
+  };
   kv_dma_issue(qd, qo0, 0, w);
   kv_dma_issue(od, qo0 + TILE_B, 0, w);
-  const long long bh = (long long)b * H + h;
+  mask_issue(mtile0, 0);
   for (int q = tid; q < Tp; q += 256) {
     const bool ok = q < T;
     rowall[q] = ok ? p.lse[bh * T + q] * LOG2E : 0.f;
@@ -581,7 +621,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   const int par = kj & 1;
   const uint32_t tp2 = (uint32_t)((T + 1) >> 1);
   const uint32_t colpair = (uint32_t)(kj >> 1);
-  const bool drop = p.dropout_p > 0.f;
+  constexpr bool drop = DM != 0;
   const float dsc = drop ? 1.f / (1.f - p.dropout_p) : 1.f;
   const int kl = w * 16 + i16;  // key within the 64-key block
   const int u00 = 63 - kl + 4 * g;
@@ -603,6 +643,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
       char* const Qn = qo0 + ((it + 1) & 1) * 2 * TILE_B;
       kv_dma_issue(qd, Qn, qb + 64, w);
       kv_dma_issue(od, Qn + TILE_B, qb + 64, w);
+      mask_issue(mtile0 + ((it + 1) & 1) * 512, qb + 64);
     }
     f32x4 s[4], dp[4];
 #pragma unroll
@@ -632,7 +673,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
       ds[t][2] = exp2_(fmaf(s[t][2], c1, g4.z * b4.z) - l4.z);
       ds[t][3] = exp2_(fmaf(s[t][3], c1, g4.w * b4.w) - l4.w);
     }
-    if (drop) {
+    if constexpr (use_mask) {
+      // element (t, r) = (query qb + 16t + 4g + r, key 16w + i16 of the block): the forward's word
+      // (that query, g_f = i16 >> 2), bit 4w + (i16 & 3)
+      const char* mt = mtile0 + (it & 1) * 512 + (i16 >> 2) * 128;
+      const int sh = 4 * w + (i16 & 3);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const uint2 mw = *reinterpret_cast<const uint2*>(mt + (16 * t + 4 * g) * 2);
+        const uint32_t bits[4] = {mw.x >> sh, mw.x >> (16 + sh), mw.y >> sh, mw.y >> (16 + sh)};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool keep = bits[r] & 1u;
+          pd[t][r] = keep ? ds[t][r] : 0.f;
+          dp[t][r] = keep ? dp[t][r] * dsc : 0.f;
+        }
+      }
+    } else if constexpr (drop) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const uint32_t qa = (uint32_t)(bh * T + qb + 16 * t + 4 * g + 2 * par);
@@ -764,15 +821,19 @@ int nrse_attn_bwd_mfma(const nrse_attn_bwd_params* p, hipStream_t st) {
   const size_t bvl = (size_t)bv_len(p->T);
   const size_t lds_q = 4 * TILE_B + 4 * bvl * sizeof(float);
   const size_t lds_kv =
-      4 * TILE_B + (3 * (size_t)((p->T + 63) & ~63) + 4 * bvl + (size_t)(((p->T + 63) & ~63) + 80) + 1024) * sizeof(float);
+      4 * TILE_B + (3 * (size_t)((p->T + 63) & ~63) + 4 * bvl + (size_t)(((p->T + 63) & ~63) + 80) + 1024) * sizeof(float) +
+      2 * 512;  // the double-buffered keep-bit tile
   if (lds_kv > 160 * 1024) {
     nrse_set_error("nrse_attn_bwd: T=%d too long for the LDS bias copies / diagonal accumulator", p->T);
     return NRSE_ERR_UNSUPPORTED;
   }
   // the dQ kernel also produces delta = rowsum(dO * O), which the dK/dV kernel reads
-  if (p->dropout_p > 0.f) hipLaunchKernelGGL(attn_bwd_q_kernel<true>, grid, dim3(256), lds_q, st, *p);
-  else hipLaunchKernelGGL(attn_bwd_q_kernel<false>, grid, dim3(256), lds_q, st, *p);
-  hipLaunchKernelGGL(attn_bwd_kv_kernel, grid, dim3(256), lds_kv, st, *p);
+  if (p->dropout_p > 0.f && p->drop_mask) hipLaunchKernelGGL(attn_bwd_q_kernel<2>, grid, dim3(256), lds_q, st, *p);
+  else if (p->dropout_p > 0.f) hipLaunchKernelGGL(attn_bwd_q_kernel<1>, grid, dim3(256), lds_q, st, *p);
+  else hipLaunchKernelGGL(attn_bwd_q_kernel<0>, grid, dim3(256), lds_q, st, *p);
+  if (p->dropout_p > 0.f && p->drop_mask) hipLaunchKernelGGL(attn_bwd_kv_kernel<2>, grid, dim3(256), lds_kv, st, *p);
+  else if (p->dropout_p > 0.f) hipLaunchKernelGGL(attn_bwd_kv_kernel<1>, grid, dim3(256), lds_kv, st, *p);
+  else hipLaunchKernelGGL(attn_bwd_kv_kernel<0>, grid, dim3(256), lds_kv, st, *p);
   const int rc = nrse_check_launch("nrse_attn_bwd(mfma)");
   if (rc || !p->diag || !p->diag_part) return rc;
   const int ntiles = (p->T + 63) / 64;
@@ -780,3 +841,9 @@ int nrse_attn_bwd_mfma(const nrse_attn_bwd_params* p, hipStream_t st) {
                           st);
 }
 
+
+extern "C" long long nrse_attn_mask_elems(int batch, int T, int H) {
+  if (batch <= 0 || T <= 0 || H <= 0) return 0;
+  const long long nt = (T + 63) / 64;
+  return (long long)batch * H * nt * 4 * nt * 64;
+}

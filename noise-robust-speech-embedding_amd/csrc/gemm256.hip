@@ -9,22 +9,27 @@
 //    accumulators of 16x16) doubles the MFMAs per LDS byte read.
 //  - one K-tile (BK = 64) is 4 half-tiles of 16 KiB: A-lo = A rows {0-63,128-191}, A-hi = A rows
 //    {64-127,192-255}, B-lo = B cols {wn*64 + 0..31}, B-hi = B cols {wn*64 + 32..63}. Each wave
-//    computes its 128x64 output as 4 quadrants (64x32, 16 MFMAs) in 4 phases: p0 (A-lo,B-lo),
-//    p1 (A-lo,B-hi), p2 (A-hi,B-hi), p3 (A-hi,B-lo), reading A-lo and B-lo in p0, B-hi in p1,
-//    A-hi in p2 and keeping fragments in registers for their second use.
+//    computes its 128x64 output as 4 quadrants (64x32, 16 MFMAs) in 2 phases per K-tile:
+//    phase 0 reads A-lo, B-lo, B-hi and runs quadrants (A-lo,B-lo), (A-lo,B-hi); phase 1 reads
+//    A-hi into the A-lo registers and runs (A-hi,B-hi), (A-hi,B-lo) with the B fragments kept.
+//    (r04: the r03 loop ran 4 phases of 16 MFMAs, 8 barriers per K-tile; 2 phases of 32 MFMAs
+//    halve the barrier syncs, and a phase-0 read burst of 16 ds_read_b128 per wave (64 KiB per
+//    CU, ~256 LDS cycles) still fits beside the partner's 512-cycle MFMA segment.)
 //  - LDS is a ring of 10 half-tile slots (160 KiB). Half-tiles are numbered in first-read order
-//    (seq = 4t + {A-lo, B-lo, B-hi, A-hi}), seq n lives in slot n % 10, and phase P stages
-//    seq P + 8 (K-tile t+2): every DMA has >= 6 phases (~1.3 us at full MFMA rate, more than the
-//    ~1.1 us issue-to-landed latency of LDS-DMA under load) before its data is needed.
+//    (seq = 4t + {A-lo, B-lo, B-hi, A-hi}), seq n lives in slot n % 10; phase 0 of K-tile t
+//    stages seq 4t+8, 4t+9 and phase 1 seq 4t+10, 4t+11 (K-tile t+2): every DMA has >= 3 phases
+//    (~1.5 us) before its data is needed.
 //  - ping-pong: the waves with wm = 1 run one barrier behind those with wm = 0, so each SIMD
-//    alternates one wave's 16-MFMA segment with the other wave's read+stage segment.
+//    alternates one wave's 32-MFMA segment with the other wave's read+stage segment.
 //    With the barriers numbered globally, group 0's phase P reads in (#2P-1, #2P) and its
 //    MFMAs run in (#2P, #2P+1); group 1 is shifted by one. Hand-off rules that follow:
 //      RAW: data read in phase Q is waited for (vmcnt) by every issuing wave before the FIRST
-//           barrier of phase Q-1: vmcnt(12) there leaves the 6 youngest half-tiles (seq
-//           P+3..P+8) in flight and retires seq <= P+2, which covers phase P+1's reads.
-//      WAR: a slot is restaged >= 2 phases after its last read: seq n is staged in phase n-8
-//           into the slot of seq n-10, last read in phase <= n-10.
+//           barrier of phase Q-1: vmcnt(12) in phase 0 retires A-hi(t), vmcnt(10) in phase 1
+//           retires A-lo, B-lo, B-hi of K-tile t+1.
+//      WAR: a slot is restaged one or two phases after its last read. Every read of the old
+//           contents (both groups) was issued before the barrier that precedes the restaging
+//           DMA's issue, and a ds_read issued before an LDS-DMA write lands returns the old
+//           bytes (MI355X_MICROARCH.md, two waves per SIMD, item 7).
 //    No wait is vmcnt(0) and the barriers are raw s_barrier (no fence), so DMAs stay in flight
 //    across them.
 //  - tiles are numbered XCD-aware (consecutive tile ids on one XCD, T1) and grouped 8 M-tiles
@@ -425,7 +430,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
     for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // prologue: K-tiles 0 and 1 (half-tile sequence numbers 0..7, slot = seq % 10), then wait for
-  // the two read in phase 0 (6 younger half-tiles = 12 DMAs may stay in flight)
+  // the three read in phase 0 (A-lo, B-lo, B-hi; 5 younger half-tiles = 10 DMAs may stay in flight)
   {
     const TilePos q0 = tile_pos(0), q1 = tile_pos(1);
 #pragma unroll
@@ -433,7 +438,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
 #pragma unroll
     for (int j = 0; j < 4; ++j) stage(j, q1, 4 + j);
   }
-  asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
   NRSE_BAR();
   NRSE_STAMP(1);
 
@@ -458,8 +463,10 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
   _Pragma("unroll") for (int fj = 0; fj < 2; ++fj)                                     \
     NRSE_MFMA(acc[(MH) * 4 + fi][(NH) * 2 + fj], fa[fi][s], FB[fj][s]);                  \
   __builtin_amdgcn_s_setprio(0);
-// the wait before each phase's first barrier retires every half-tile the NEXT phase reads
-#define NRSE_WAIT() asm volatile("s_waitcnt vmcnt(12)" ::: "memory")
+// the wait before each phase's first barrier retires every half-tile the NEXT phase reads:
+// phase 0 of K-tile t leaves the 6 youngest half-tiles in flight (retiring A-hi(t)), phase 1
+// the 5 youngest (retiring A-lo, B-lo, B-hi of K-tile t+1)
+#define NRSE_WAIT(N) asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory")
 
   // ping-pong start: group 1 falls one barrier behind (schedule and hand-off rules: header)
   if (wm == 1) __builtin_amdgcn_s_barrier();
@@ -471,45 +478,35 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
 #pragma unroll 1
   for (int t = 0; t < ntiles; ++t) {
     const int s0 = base, s1 = wrap(base + 1), s2 = wrap(base + 2), s3 = wrap(base + 3);
-    // phase p stages half-tile j = p of K-tile t+2 (sequence 4t+8+p) into slot (4t+8+p) % 10
+    // K-tile t+2 is staged over the two phases of K-tile t: A-lo, B-lo in phase 0 (sequence
+    // 4t+8, 4t+9), B-hi, A-hi in phase 1 (4t+10, 4t+11)
     const TilePos q2 = tile_pos_at(t + 2 < ntiles, u_sg, u_k);
     if (++u_k == tps) { u_k = 0; ++u_sg; }
-    // phase 0: quadrant (M-half 0, N-half 0) from A-lo, B-lo
+    // phase 0: quadrants (M-half 0, N-half 0) and (0, 1) from A-lo, B-lo, B-hi
     NRSE_READ_A(s0, 4)
     NRSE_READ_B(s1, fbl)
+    NRSE_READ_B(s2, fbh)
     stage(0, q2, wrap(base + 8));
-    NRSE_WAIT();
+    stage(1, q2, wrap(base + 9));
+    NRSE_WAIT(12);
     NRSE_BAR();
     NRSE_PSTAMP(0);
     NRSE_QUAD(0, 0, fbl)
-    NRSE_BAR();
-    NRSE_PSTAMP(1);
-    // phase 1: (0, 1) from B-hi
-    NRSE_READ_B(s2, fbh)
-    stage(1, q2, wrap(base + 9));
-    NRSE_WAIT();
-    NRSE_BAR();
-    NRSE_PSTAMP(2);
     NRSE_QUAD(0, 1, fbh)
     NRSE_BAR();
-    NRSE_PSTAMP(3);
-    // phase 2: (1, 1) from A-hi
+    NRSE_PSTAMP(1);
+    // phase 1: quadrants (1, 1) and (1, 0) from A-hi (into the A-lo registers) and the B
+    // fragments still in registers
     NRSE_READ_A(s3, NFI_HI)
     stage(2, q2, base);  // (4t + 10) % 10
-    NRSE_WAIT();
-    NRSE_BAR();
-    NRSE_PSTAMP(4);
-    NRSE_QUAD(1, 1, fbh)
-    NRSE_BAR();
-    NRSE_PSTAMP(5);
-    // phase 3: (1, 0) from registers
     stage(3, q2, s1);    // (4t + 11) % 10
-    NRSE_WAIT();
+    NRSE_WAIT(10);
     NRSE_BAR();
-    NRSE_PSTAMP(6);
+    NRSE_PSTAMP(2);
+    NRSE_QUAD(1, 1, fbh)
     NRSE_QUAD(1, 0, fbl)
     NRSE_BAR();
-    NRSE_PSTAMP(7);
+    NRSE_PSTAMP(3);
     base = wrap(base + 4);
   }
   if (wm == 0) __builtin_amdgcn_s_barrier();

@@ -82,14 +82,14 @@ class LnBwdParams(ctypes.Structure):
 class AttnFwdParams(ctypes.Structure):
     _fields_ = [("qkv", c_vp), ("dtype", c_int), ("gate", c_vp), ("bias", c_vp), ("ctx", c_vp), ("lse", c_vp),
                 ("batch", c_int), ("T", c_int), ("H", c_int), ("head_dim", c_int), ("scale", c_f),
-                ("dropout_p", c_f), ("seed", c_u32), ("bias_vec", c_vp)]
+                ("dropout_p", c_f), ("seed", c_u32), ("bias_vec", c_vp), ("drop_mask", c_vp)]
 
 
 class AttnBwdParams(ctypes.Structure):
     _fields_ = [("qkv", c_vp), ("dtype", c_int), ("gate", c_vp), ("bias", c_vp), ("ctx", c_vp), ("dctx", c_vp),
                 ("lse", c_vp), ("delta", c_vp), ("dqkv", c_vp), ("dgate", c_vp), ("diag", c_vp),
                 ("batch", c_int), ("T", c_int), ("H", c_int), ("head_dim", c_int), ("scale", c_f),
-                ("dropout_p", c_f), ("seed", c_u32), ("bias_vec", c_vp), ("diag_part", c_vp)]
+                ("dropout_p", c_f), ("seed", c_u32), ("bias_vec", c_vp), ("drop_mask", c_vp), ("diag_part", c_vp)]
 
 
 class Conv0Params(ctypes.Structure):
@@ -134,6 +134,7 @@ _SIGNATURES = {
     "nrse_attn_fwd": ([_P(AttnFwdParams), c_vp], c_int),
     "nrse_attn_bwd": ([_P(AttnBwdParams), c_vp], c_int),
     "nrse_attn_bwd_workspace": ([_P(AttnBwdParams)], c_ll),
+    "nrse_attn_mask_elems": ([c_int, c_int, c_int], c_ll),
     "nrse_conv0_fwd": ([_P(Conv0Params), c_vp], c_int),
     "nrse_conv0_bwd": ([_P(Conv0Params), c_vp], c_int),
     "nrse_conv0_bwd_workspace": ([_P(Conv0Params)], c_ll),

@@ -435,8 +435,11 @@ class ByolEngine:
                        Pm[at + "gru_rel_pos_const"], gate, B, T, nh)
             ctx = torch.empty(BT, H, device=dev, dtype=cdt)
             lse = torch.empty(B, nh, T, device=dev, dtype=F32)
+            # the probability-dropout keep bits, recorded for the backward (bf16 path)
+            dmask = (torch.empty(K.attn_mask_elems(B, T, nh), device=dev, dtype=torch.int16)
+                     if need_grad and pat > 0 and bias_vec is not None else None)
             K.attn_fwd(qkv, gate, bias_tab, ctx, lse, B, T, nh, pat, R.site_seed(fseed, R.site_attn_probs(li)),
-                       bias_vec=bias_vec)
+                       bias_vec=bias_vec, drop_mask=dmask)
             hmid = torch.empty(BT, H, device=dev, dtype=F32)
             K.linear_fwd(ctx, Ps[at + "out_proj.weight"], hmid, bias=Pm[at + "out_proj.bias"], resid=hcur, ldr=H,
                          dropout_p=php, seed=R.site_seed(fseed, R.site_attn_out(li)), w_lo=W.lo)
@@ -455,7 +458,7 @@ class ByolEngine:
                          seed=R.site_seed(fseed, R.site_ffn_out(li)), w_lo=W.lo)
             if need_grad:
                 tape.layers.append(dict(li=li, h_in=hcur, x1=x1, m1=m1, r1=r1, qkv=qkv, gate=gate, ctx=ctx, lse=lse,
-                                        hmid=hmid, x2=x2, m2=m2, r2=r2, f1pre=f1pre, g1=g1))
+                                        hmid=hmid, x2=x2, m2=m2, r2=r2, f1pre=f1pre, g1=g1, dmask=dmask))
             hcur = hout
         self._param_wait(a.layers)  # final LN (+ the heads that follow)
         if hidden_dtype is not None:
@@ -552,7 +555,8 @@ class ByolEngine:
             dqkv = torch.empty(BT, 3 * H, device=dev, dtype=cdt)
             dgate = torch.empty(B, nh, T, device=dev, dtype=F32)
             K.attn_bwd(L_["qkv"], L_["gate"], tape.bias_tab, L_["ctx"], dctx, L_["lse"], delta, dqkv, dgate, diag, B,
-                       T, nh, pat, R.site_seed(fseed, R.site_attn_probs(li)), bias_vec=tape.bias_vec)
+                       T, nh, pat, R.site_seed(fseed, R.site_attn_probs(li)), bias_vec=tape.bias_vec,
+                       drop_mask=L_["dmask"])
             del dctx
             with self._wgrad_stream(main, dqkv, L_["x1"]):
                 K.linear_wgrad(dqkv, L_["x1"], self.fused(self.grad_flat_for(Gv), li, "qkv_w"))

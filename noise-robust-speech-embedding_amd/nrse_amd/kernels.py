@@ -458,18 +458,26 @@ def gate_bwd(x1, W, b, c, dgate, dx1, dW, db, dc, batch, T, H):
           ptr(dc), batch, T, H, ptr(ws), stream_ptr())
 
 
-def attn_fwd(qkv, gate, bias, ctx, lse, batch, T, H, dropout_p=0.0, seed=0, bias_vec=None):
-    """bias: [H, T, Tb] table (f32 parity path), bias_vec: [H, 2T-1] Toeplitz vector (bf16 path)."""
+def attn_mask_elems(batch, T, H) -> int:
+    """u16 words of the forward's dropout keep-bit mask (nrse_attn_fwd_params.drop_mask)."""
+    return int(_lib.lib().nrse_attn_mask_elems(batch, T, H))
+
+
+def attn_fwd(qkv, gate, bias, ctx, lse, batch, T, H, dropout_p=0.0, seed=0, bias_vec=None, drop_mask=None):
+    """bias: [H, T, Tb] table (f32 parity path), bias_vec: [H, 2T-1] Toeplitz vector (bf16 path);
+    drop_mask (optional, int16 [attn_mask_elems]): the keep bits for the backward."""
+    if drop_mask is not None:
+        assert drop_mask.dtype == torch.int16 and drop_mask.numel() >= attn_mask_elems(batch, T, H)
     p = AttnFwdParams(ptr(qkv), dtype_code(qkv), ptr(gate), ptr(bias), ptr(ctx), ptr(lse), batch, T, H, 64,
-                      0.125, dropout_p, seed & 0xFFFFFFFF, ptr(bias_vec))
+                      0.125, dropout_p, seed & 0xFFFFFFFF, ptr(bias_vec), ptr(drop_mask))
     _call("nrse_attn_fwd", ctypes.byref(p), stream_ptr())
 
 
 def attn_bwd(qkv, gate, bias, ctx, dctx, lse, delta, dqkv, dgate, diag, batch, T, H, dropout_p=0.0, seed=0,
-             bias_vec=None):
+             bias_vec=None, drop_mask=None):
     p = AttnBwdParams(ptr(qkv), dtype_code(qkv), ptr(gate), ptr(bias), ptr(ctx), ptr(dctx), ptr(lse), ptr(delta),
                       ptr(dqkv), ptr(dgate), ptr(diag), batch, T, H, 64, 0.125, dropout_p, seed & 0xFFFFFFFF,
-                      ptr(bias_vec))
+                      ptr(bias_vec), ptr(drop_mask))
     ws = None
     if DETERMINISTIC and diag is not None:
         ws = workspace(_lib.lib().nrse_attn_bwd_workspace(ctypes.byref(p)))

@@ -86,3 +86,46 @@ def test_attention_fwd_bwd(nrse_device, dtype, T, p):
         ref_diag[h].index_add_(0, idx, dbias[h].reshape(-1))
     e = ((diag.double() - ref_diag).norm() / ref_diag.norm()).item()
     assert e < 3 * tol, ("diag", e)
+
+
+@pytest.mark.parametrize("T", [49, 399, 599])
+def test_attention_recorded_dropout_mask(nrse_device, T):
+    """The forward records the probability-dropout keep bits (drop_mask, [B*H][key tile][4][Tp]
+    u16) and the backward reads them instead of re-hashing: the bits are the counter hash's
+    (oracle/masks.py attn_keep_mask), and the mask-reading backward equals the re-hashing one
+    bit for bit."""
+    from nrse_amd import kernels as K
+    dev = nrse_device
+    B, H, p, seed = 2, 4, 0.1, 123
+    torch.manual_seed(T + 5)
+    qkv = (torch.randn(B * T, 3 * H * 64, device=dev) * 0.5).to(torch.bfloat16)
+    gate = torch.rand(B, H, T, device=dev) + 1.0
+    vec, bias = toeplitz_bias(H, T, dev)
+    ctx = torch.empty(B * T, H * 64, device=dev, dtype=torch.bfloat16)
+    ctx2 = torch.empty_like(ctx)
+    lse = torch.empty(B, H, T, device=dev)
+    mask = torch.zeros(K.attn_mask_elems(B, T, H), device=dev, dtype=torch.int16)
+    K.attn_fwd(qkv, gate, None, ctx, lse, B, T, H, p, seed, bias_vec=vec, drop_mask=mask)
+    K.attn_fwd(qkv, gate, None, ctx2, lse, B, T, H, p, seed, bias_vec=vec)
+    assert torch.equal(ctx, ctx2)
+    # decode: word (bh, kt, g, q) bit 4t + r <-> key 64 kt + 16 t + 4 g + r
+    nt = (T + 63) // 64
+    Tp = nt * 64
+    w = mask.view(B * H, nt, 4, Tp).to(torch.int32).cpu() & 0xFFFF
+    bits = torch.stack([(w >> b) & 1 for b in range(16)], -1)          # [bh, kt, g, q, 4t + r]
+    bits = bits.view(B * H, nt, 4, Tp, 4, 4).permute(0, 3, 1, 4, 2, 5)  # [bh, q, kt, t, g, r]
+    keep = bits.reshape(B * H, Tp, nt * 64)[:, :T, :T].bool().numpy()
+    ref = MK.attn_dropout_mask(seed, p, (B, H, T, T)).reshape(B * H, T, T) > 0
+    assert (keep == ref).all()
+    dctx = (torch.randn(B * T, H * 64, device=dev) * 0.5).to(torch.bfloat16)
+    outs = []
+    for m in (None, mask):
+        dqkv = torch.empty_like(qkv)
+        dgate = torch.empty(B, H, T, device=dev)
+        diag = torch.zeros(H, 2 * T - 1, device=dev)
+        delta = torch.empty(B, H, T, device=dev)
+        K.attn_bwd(qkv, gate, None, ctx, dctx, lse, delta, dqkv, dgate, diag, B, T, H, p, seed, bias_vec=vec,
+                   drop_mask=m)
+        outs.append((dqkv, dgate, diag))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
