@@ -456,6 +456,9 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
   _Pragma("unroll") for (int fj = 0; fj < 2; ++fj)                                     \
   _Pragma("unroll") for (int s = 0; s < 2; ++s)                                        \
     FB[fj][s] = NRSE_FRAG(BKC, smem + (SLOT) * HALF, wn * 32 + fj * 16, s, lane);
+// per-segment priority flips (r04: a static s_setprio 1 for the younger half instead,
+// MI355X_MICROARCH.md two waves per SIMD item 4, measured 6 % slower on the step: 537-540 vs
+// 507-508 pairs/s same box)
 #define NRSE_QUAD(MH, NH, FB)                                                            \
   __builtin_amdgcn_s_setprio(1);                                                         \
   _Pragma("unroll") for (int s = 0; s < 2; ++s)                                        \

@@ -35,3 +35,12 @@ for p in (0.0, 0.1):
     tbn = timeit(lambda: K.attn_bwd(qkv, gate, bias, ctx, dctx, lse, delta, dqkv, dgate, None, B, T, H, p, 1, bias_vec=bvec))
     fl = 4.0 * B * H * T * T * 64
     print(f"p={p}: fwd {tf*1e3:.1f}us ({fl/tf/1e9:.0f} TF) | bwd {tb*1e3:.1f}us ({2.5*fl/tb/1e9:.0f} TF) | bwd no-diag {tbn*1e3:.1f}us", flush=True)
+
+# the step's form: the forward records the dropout keep bits, the backward reads them
+mask = torch.empty(K.attn_mask_elems(B, T, H), device=dev, dtype=torch.int16)
+p = 0.1
+tf = timeit(lambda: K.attn_fwd(qkv, gate, bias, ctx, lse, B, T, H, p, 1, bias_vec=bvec, drop_mask=mask))
+tb = timeit(lambda: K.attn_bwd(qkv, gate, bias, ctx, dctx, lse, delta, dqkv, dgate, diag, B, T, H, p, 1, bias_vec=bvec,
+                               drop_mask=mask))
+fl = 4.0 * B * H * T * T * 64
+print(f"p={p} recorded mask: fwd {tf*1e3:.1f}us ({fl/tf/1e9:.0f} TF) | bwd {tb*1e3:.1f}us ({2.5*fl/tb/1e9:.0f} TF)", flush=True)

@@ -43,9 +43,12 @@ if what in ("all", "attn"):
     dqkv = torch.empty_like(qkv)
     dgate = torch.empty(B, H, T, device=dev)
     diag = torch.zeros(H, 2 * T - 1, device=dev)
+    # the step's form: the forward records the dropout keep bits, the backward reads them
+    mask = torch.empty(K.attn_mask_elems(B, T, H), device=dev, dtype=torch.int16)
     for _ in range(reps):
-        K.attn_fwd(qkv, gate, bias, ctx, lse, B, T, H, 0.1, 123, bias_vec=bvec)
-        K.attn_bwd(qkv, gate, bias, ctx, dctx, lse, delta, dqkv, dgate, diag, B, T, H, 0.1, 123, bias_vec=bvec)
+        K.attn_fwd(qkv, gate, bias, ctx, lse, B, T, H, 0.1, 123, bias_vec=bvec, drop_mask=mask)
+        K.attn_bwd(qkv, gate, bias, ctx, dctx, lse, delta, dqkv, dgate, diag, B, T, H, 0.1, 123, bias_vec=bvec,
+                   drop_mask=mask)
 if what == "conv0":
     # conv0 (1 -> 512, k10 s5) + LN + GELU forward, and its backward with dy = the col2im fold
     # of conv1's dgrad [32 x 12799, 3 x 512] (bf16), as in the step
