@@ -15,6 +15,12 @@
 // image stay (nearly) conflict-free.
 #include "common.h"
 
+// NRSE_ATTN_FWD_CHAINS: 1 = attn_fwd_kernel (4 waves x 16 queries), 2 = attn_fwd2_kernel (2 waves
+// x 2 chains of 16 queries)
+#ifndef NRSE_ATTN_FWD_CHAINS
+#define NRSE_ATTN_FWD_CHAINS 1
+#endif
+
 namespace {
 
 constexpr int D = 64;
@@ -116,6 +122,27 @@ NRSE_DEV KvDma kv_dma_init(const bf16_t* utt_base, int T, long long ld, int col_
     d.voff[j] = (unsigned)row * d.ld_b + (unsigned)col_b + (unsigned)chunk * 16;
   }
   return d;
+}
+
+// the two-wave form: 4 wave-instructions per tile per wave (rows (4 wave + j) * 8 .. +7)
+struct KvDma2 {
+  struct {
+    __amdgpu_buffer_rsrc_t rs;
+    unsigned voff[4];
+    unsigned ld_b;
+  } d;
+};
+NRSE_DEV KvDma2 kv_dma_init2(const bf16_t* utt_base, int T, long long ld, int col_b, int wave, int lane) {
+  KvDma2 k;
+  k.d.ld_b = (unsigned)(ld * 2);
+  k.d.rs = __builtin_amdgcn_make_buffer_rsrc((void*)utt_base, 0, (int)((long long)T * ld * 2), 0x00020000);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = (wave * 4 + j) * 8 + (lane >> 3);
+    const int chunk = (lane & 7) ^ (((row >> 1) & 3) << 1);
+    k.d.voff[j] = (unsigned)row * k.d.ld_b + (unsigned)col_b + (unsigned)chunk * 16;
+  }
+  return k;
 }
 
 // stage rows row0 .. row0+63 into the tile at `tile` (wave-uniform LDS address)
@@ -328,6 +355,201 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
     }
   }
   if (g == 0 && qv) p.lse[bh * T + qi] = (m + __builtin_amdgcn_logf(l)) * LN2;
+}
+
+// ------------------------------------------------------------------------------ forward, two chains
+// The same computation with 2 waves per workgroup and TWO independent 16-query chains per wave
+// (wave w: queries q0 + 32w + 16c + i16, c = 0, 1): each wave issues both chains' QK^T MFMAs
+// before either softmax, so one chain's exp / max / hash work overlaps the other's MFMAs inside
+// the wave instead of relying on other waves to cover the dependency stalls (r03 PMC: 39 % of
+// wave-cycles stalled on dependencies). Results are bit-identical to attn_fwd_kernel's (same
+// per-element arithmetic and order).
+template <typename DD>
+NRSE_DEV void kv_dma_issue2(const DD& d, char* tile, int row0, int wave) {
+  const unsigned roff = (unsigned)row0 * d.ld_b;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(d.rs, (lds_void_t*)(tile + (wave * 4 + j) * 1024), 16, d.voff[j] + roff,
+                                             0, 0, 0);
+}
+template <bool DROP>
+__global__ __launch_bounds__(128) void attn_fwd2_kernel(const nrse_attn_fwd_params p) {
+  extern __shared__ __attribute__((aligned(16))) char dyn[];
+  char* const kv0 = dyn;
+  float* const bv = reinterpret_cast<float*>(dyn + 4 * TILE_B);
+  const int T = p.T, H = p.H, Hd = H * D;
+  const long long ld3 = 3LL * Hd;
+  const BlockPos bp = block_pos((p.T + 63) / 64, p.H);
+  const int b = bp.b, h = bp.h;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, i16 = lane & 15;
+  const int q0 = bp.blk * 64;
+  const bf16_t* qkv = (const bf16_t*)p.qkv + (long long)b * T * ld3;
+  const KvDma2 kd = kv_dma_init2(qkv, T, ld3, (Hd + h * D) * 2, w, lane);
+  const KvDma2 vd = kv_dma_init2(qkv, T, ld3, (2 * Hd + h * D) * 2, w, lane);
+  const int ntiles = (T + 63) / 64;
+  const int Tp = ntiles * 64;
+  kv_dma_issue2(kd.d, kv0, 0, w);
+  kv_dma_issue2(vd.d, kv0 + TILE_B, 0, w);
+  {
+    const int len = bv_len(T), nd = 2 * T - 1;
+    const int e_lo = T - 1 - q0 - 63;
+    const float* vec = p.bias_vec + (long long)h * (2 * T - 1);
+    for (int j = tid; j < len; j += 128) {
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const int e = e_lo + j + s4;
+        bv[s4 * len + j] = (e >= 0 && e < nd) ? vec[e] : 0.f;
+      }
+    }
+  }
+  const long long bh = (long long)b * H + h;
+  const float c1 = p.scale * LOG2E;
+  const int bvl = bv_len(T);
+  const uint32_t key = site_key(p.seed);
+  const uint32_t thr = dropout_threshold16(p.dropout_p);
+  constexpr bool drop = DROP;
+  const float dsc = drop ? 1.f / (1.f - p.dropout_p) : 1.f;
+  constexpr float RESCALE_TAU = 8.f;
+  int qi[2];
+  bool qv[2];
+  bf16x8 qf[2][2];
+  float gl[2], mref[2];
+  const float* bvl_base[2];
+  uint32_t rowpair[2];
+  f32x2 lpart2[2];
+  f32x4 o[2][4];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    qi[c] = q0 + 32 * w + 16 * c + i16;
+    qv[c] = qi[c] < T;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      uint4 u = make_uint4(0, 0, 0, 0);
+      if (qv[c]) u = *reinterpret_cast<const uint4*>(qkv + (long long)qi[c] * ld3 + h * D + 8 * g + 32 * s);
+      qf[c][s] = __builtin_bit_cast(bf16x8, u);
+    }
+    gl[c] = (qv[c] ? p.gate[bh * T + qi[c]] : 0.f) * LOG2E;
+    const int u00 = 4 * g + 63 - (32 * w + 16 * c + i16);
+    const int bsel = u00 & 3;
+    bvl_base[c] = bv + bsel * bvl + (u00 - bsel);
+    rowpair[c] = (uint32_t)(bh * T + qi[c]) * (uint32_t)((T + 1) >> 1) + (uint32_t)(2 * g);
+    mref[c] = 0.f;
+    lpart2[c] = f32x2{0.f, 0.f};
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[c][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  for (int it = 0; it < ntiles; ++it) {
+    const int kb = it * 64;
+    char* const Kt = kv0 + (it & 1) * 2 * TILE_B;
+    char* const Vt = Kt + TILE_B;
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (it + 1 < ntiles) {
+      char* const Kn = kv0 + ((it + 1) & 1) * 2 * TILE_B;
+      kv_dma_issue2(kd.d, Kn, kb + 64, w);
+      kv_dma_issue2(vd.d, Kn + TILE_B, kb + 64, w);
+    }
+    // both chains' S^T = K Q^T first
+    f32x4 sc[2][4];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        sc[c][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss)
+          sc[c][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rd_row(Kt, 16 * t + i16, 4 * ss + g), qf[c][ss], sc[c][t], 0, 0, 0);
+      }
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      float v[4][4];
+      const f32x2 c12 = {c1, c1}, gl2 = {gl[c], gl[c]}, nm2 = {-mref[c], -mref[c]};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const float4 bb = *reinterpret_cast<const float4*>(bvl_base[c] + kb + 16 * t);
+        const f32x2 r0 = pk_fma(f32x2{sc[c][t][0], sc[c][t][1]}, c12, pk_fma(gl2, f32x2{bb.x, bb.y}, nm2));
+        const f32x2 r1 = pk_fma(f32x2{sc[c][t][2], sc[c][t][3]}, c12, pk_fma(gl2, f32x2{bb.z, bb.w}, nm2));
+        v[t][0] = r0.x; v[t][1] = r0.y; v[t][2] = r1.x; v[t][3] = r1.y;
+      }
+      if (kb + 64 > T) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[t][r] = (kb + 16 * t + 4 * g + r < T) ? v[t][r] : -INFINITY;
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) mx = fmaxf(mx, fmaxf(fmaxf(v[t][0], v[t][1]), fmaxf(v[t][2], v[t][3])));
+      mx = xor32_max(xor16_max(mx));
+      if (it == 0 || __builtin_amdgcn_ballot_w64(mx > RESCALE_TAU)) {
+        const float sh = it == 0 ? mx : fmaxf(mx, 0.f);
+        const float alpha = it == 0 ? 1.f : exp2_(-sh);
+        mref[c] += sh;
+        const f32x2 sh2 = {sh, sh}, al2 = {alpha, alpha};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const f32x2 a0 = f32x2{v[t][0], v[t][1]} - sh2, a1 = f32x2{v[t][2], v[t][3]} - sh2;
+          v[t][0] = a0.x; v[t][1] = a0.y; v[t][2] = a1.x; v[t][3] = a1.y;
+        }
+        lpart2[c] *= al2;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          const f32x2 o0 = f32x2{o[c][dt][0], o[c][dt][1]} * al2, o1 = f32x2{o[c][dt][2], o[c][dt][3]} * al2;
+          o[c][dt] = f32x4{o0.x, o0.y, o1.x, o1.y};
+        }
+      }
+      float pd[4][4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pd[t][r] = exp2_(v[t][r]);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) lpart2[c] += f32x2{pd[t][0], pd[t][1]} + f32x2{pd[t][2], pd[t][3]};
+      if constexpr (DROP) {
+        uint32_t mb = 0;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int rp = 0; rp < 2; ++rp) {
+            const uint32_t hh = mix32((rowpair[c] + (uint32_t)((kb >> 1) + 8 * t + rp)) ^ key);
+            const bool k0 = attn_half_keep(hh, 0, thr), k1 = attn_half_keep(hh, 1, thr);
+            pd[t][2 * rp] = k0 ? pd[t][2 * rp] : 0.f;
+            pd[t][2 * rp + 1] = k1 ? pd[t][2 * rp + 1] : 0.f;
+            mb |= (k0 ? 1u << (4 * t + 2 * rp) : 0u) | (k1 ? 2u << (4 * t + 2 * rp) : 0u);
+            asm("" : "+v"(pd[t][2 * rp]), "+v"(pd[t][2 * rp + 1]));
+          }
+        if (p.drop_mask && qv[c]) p.drop_mask[((bh * ntiles + it) * 4 + g) * Tp + qi[c]] = (uint16_t)mb;
+      }
+#pragma unroll
+      for (int cc = 0; cc < 2; ++cc) {
+        const bf16x8 pa = pack8(pd[2 * cc], pd[2 * cc + 1]);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+          o[c][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rd_tr(Vt, 32 * cc, 32 * cc + 16, 16 * dt, lane), pa, o[c][dt], 0, 0, 0);
+      }
+    }
+  }
+  bf16_t* ctx = (bf16_t*)p.ctx;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const float l = xor32_sum(xor16_sum(lpart2[c].x + lpart2[c].y));
+    if (qv[c]) {
+      const float inv = dsc / l;
+      bf16_t* crow = ctx + ((long long)b * T + qi[c]) * Hd + h * D + 4 * g;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        uint2 u;
+        u.x = (uint32_t)f2bf(o[c][dt][0] * inv) | ((uint32_t)f2bf(o[c][dt][1] * inv) << 16);
+        u.y = (uint32_t)f2bf(o[c][dt][2] * inv) | ((uint32_t)f2bf(o[c][dt][3] * inv) << 16);
+        *reinterpret_cast<uint2*>(crow + 16 * dt) = u;
+      }
+      if (g == 0) p.lse[bh * T + qi[c]] = (mref[c] + __builtin_amdgcn_logf(l)) * LN2;
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------ bwd: dQ, dgate
@@ -807,8 +1029,13 @@ int nrse_attn_fwd_mfma(const nrse_attn_fwd_params* p, hipStream_t st) {
     nrse_set_error("nrse_attn_fwd: T=%d too long for the LDS bias copies", p->T);
     return NRSE_ERR_UNSUPPORTED;
   }
+#if NRSE_ATTN_FWD_CHAINS == 2
+  if (p->dropout_p > 0.f) hipLaunchKernelGGL(attn_fwd2_kernel<true>, grid, dim3(128), lds, st, *p);
+  else hipLaunchKernelGGL(attn_fwd2_kernel<false>, grid, dim3(128), lds, st, *p);
+#else
   if (p->dropout_p > 0.f) hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(256), lds, st, *p);
   else hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(256), lds, st, *p);
+#endif
   return nrse_check_launch("nrse_attn_fwd(mfma)");
 }
 

@@ -10,6 +10,7 @@ for i in 1 2; do
     [ "$lib" = "-" ] && lib=""
     echo "== [${lib:-in-tree}]"
     NRSE_LIB_PATH=$lib timeout -k 10 180 python -u tools/bench_gemm_fwd.py 2>&1 | grep -v amdgpu.ids || exit 1
+    NRSE_LIB_PATH=$lib timeout -k 10 120 python -u tools/bench_attn.py 2>&1 | grep -v amdgpu.ids || exit 1
   done
 done
 for i in 1 2; do
