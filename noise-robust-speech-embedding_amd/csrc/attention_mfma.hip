@@ -1031,7 +1031,7 @@ int nrse_attn_fwd_mfma(const nrse_attn_fwd_params* p, hipStream_t st) {
   }
 #if NRSE_ATTN_FWD_CHAINS == 2
   if (p->dropout_p > 0.f) hipLaunchKernelGGL(attn_fwd2_kernel<true>, grid, dim3(128), lds, st, *p);
-  else hipLaunchKernelGGL(attn_fwd2_kernel<false>, grid, dim3(128), lds, st, *p);
+  else hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(256), lds, st, *p);
 #else
   if (p->dropout_p > 0.f) hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(256), lds, st, *p);
   else hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(256), lds, st, *p);

@@ -48,11 +48,6 @@
 #ifndef NRSE_G3_STAMPS
 #define NRSE_G3_STAMPS 0
 #endif
-// NRSE_G3_VARIANT (A/B builds only): 1 = each phase's DMAs issued before its fragment reads,
-// 2 = phase 0's B-hi fragments read between the computing wave's own MFMAs
-#ifndef NRSE_G3_VARIANT
-#define NRSE_G3_VARIANT 0
-#endif
 #if NRSE_G3_STAMPS
 #define NRSE_STAMP(I)                                                                                 \
   do {                                                                                                \
@@ -491,41 +486,23 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
     const TilePos q2 = tile_pos_at(t + 2 < ntiles, u_sg, u_k);
     if (++u_k == tps) { u_k = 0; ++u_sg; }
     // phase 0: quadrants (M-half 0, N-half 0) and (0, 1) from A-lo, B-lo, B-hi
-#if NRSE_G3_VARIANT == 1
-    stage(0, q2, wrap(base + 8));
-    stage(1, q2, wrap(base + 9));
-#endif
     NRSE_READ_A(s0, 4)
     NRSE_READ_B(s1, fbl)
-#if NRSE_G3_VARIANT != 2
     NRSE_READ_B(s2, fbh)
-#endif
-#if NRSE_G3_VARIANT != 1
     stage(0, q2, wrap(base + 8));
     stage(1, q2, wrap(base + 9));
-#endif
     NRSE_WAIT(12);
     NRSE_BAR();
     NRSE_PSTAMP(0);
     NRSE_QUAD(0, 0, fbl)
-#if NRSE_G3_VARIANT == 2
-    // B-hi read by the computing wave between its own MFMAs (the read interval carries 12 reads)
-    NRSE_READ_B(s2, fbh)
-#endif
     NRSE_QUAD(0, 1, fbh)
     NRSE_BAR();
     NRSE_PSTAMP(1);
     // phase 1: quadrants (1, 1) and (1, 0) from A-hi (into the A-lo registers) and the B
     // fragments still in registers
-#if NRSE_G3_VARIANT == 1
-    stage(2, q2, base);
-    stage(3, q2, s1);
-#endif
     NRSE_READ_A(s3, NFI_HI)
-#if NRSE_G3_VARIANT != 1
     stage(2, q2, base);  // (4t + 10) % 10
     stage(3, q2, s1);    // (4t + 11) % 10
-#endif
     NRSE_WAIT(10);
     NRSE_BAR();
     NRSE_PSTAMP(2);

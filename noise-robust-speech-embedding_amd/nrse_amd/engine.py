@@ -66,11 +66,6 @@ class StepConfig:
     # wait per layer (see ByolEngine.optimizer_step). Same kernels, same per-element arithmetic:
     # parameters are bit-identical to the serial order (tests/test_engine_gpu.py).
     overlap_optimizer: bool = False
-    # Run the step's main chain (forward of the online view, the dgrad / attention chain of the
-    # backward) on a high-priority stream, so the hardware dispatcher hands freed CUs to it before
-    # the side streams' work (target view, weight gradients, optimizer segments). NRSE_PRIO_CHAIN=1
-    # turns it on by default (A/B measurements).
-    priority_chain: bool = os.environ.get("NRSE_PRIO_CHAIN", "0") == "1"
 
 
 @dataclass
@@ -986,32 +981,10 @@ class ByolEngine:
         """Pre-clip global gradient norm of the last step (host sync)."""
         return float(self.sumsq_buf.sqrt()) / world_size
 
-    def _hi_stream(self) -> torch.cuda.Stream:
-        if getattr(self, "_hi", None) is None:
-            _, greatest = torch.cuda.Stream.priority_range()
-            self._hi = torch.cuda.Stream(self.dev, priority=greatest)
-        return self._hi
-
     def train_step(self, clean: torch.Tensor, noisy: torch.Tensor, *, lr: float, step_seed: int, rank: int = 0,
                    allreduce=None, world_size: int = 1) -> torch.Tensor:
         """One iteration of train_one_epoch (train_byol.py:47-77): forward, loss, backward,
         clip, AdamW, EMA. Returns the device-resident loss (no sync)."""
-        if not self.cfg.priority_chain:
-            return self._train_step(clean, noisy, lr=lr, step_seed=step_seed, rank=rank, allreduce=allreduce,
-                                    world_size=world_size)
-        caller = torch.cuda.current_stream(self.dev)
-        hs = self._hi_stream()
-        hs.wait_stream(caller)
-        clean.record_stream(hs)
-        noisy.record_stream(hs)
-        with torch.cuda.stream(hs):
-            out = self._train_step(clean, noisy, lr=lr, step_seed=step_seed, rank=rank, allreduce=allreduce,
-                                   world_size=world_size)
-        caller.wait_stream(hs)
-        return out
-
-    def _train_step(self, clean: torch.Tensor, noisy: torch.Tensor, *, lr: float, step_seed: int, rank: int = 0,
-                    allreduce=None, world_size: int = 1) -> torch.Tensor:
         B = clean.shape[0]
         self.health_buf.zero_()   # rows: clean, noisy, online_pred, target_proj (nrse_amd/health.py)
         K.health(clean, self.health_buf[0])
