@@ -733,14 +733,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   char* const qo0 = dyn;  // [2 buffers][Q tile, dO tile], LDS-DMA double buffer
   const int T = p.T, H = p.H, Hd = H * D;
   const int Tp = (T + 63) & ~63;
-  float* const rowall = reinterpret_cast<float*>(dyn + 4 * TILE_B);  // lse*log2e [Tp], delta [Tp], gate [Tp]
-  float* const rbv = rowall + 3 * Tp;                                 // 4 reversed bias copies
+  // [2 buffers][lse, delta, gate][64 queries] f32 of the query tile, staged by LDS-DMA beside Q / dO
+  // (waves 1-3, one 256-B piece each; queries past T land as zeros)
+  float* const rows0 = reinterpret_cast<float*>(dyn + 4 * TILE_B);
+  float* const rbv = rows0 + 2 * 3 * 64;                              // 4 reversed bias copies
   const int bvl = bv_len(T);
   float* const diag = rbv + 4 * bvl;                                  // [diag_len(T)]
-  float* const dtmp = diag + diag_len(T);                             // [4 waves][4 lane rows][64]
+  float* const dtmp = diag + diag_len(T);                             // [2 buffers][4 waves][4 lane rows][64]
   // [2 buffers][4 g][64 queries] u16: the forward's keep bits of this key block for the query
   // tile, staged by LDS-DMA beside Q / dO (wave 0, lanes 0-31: 512 B)
-  char* const mtile0 = reinterpret_cast<char*>(dtmp + 1024);
+  char* const mtile0 = reinterpret_cast<char*>(dtmp + 2 * 1024);
   const long long ld3 = 3LL * Hd;
   const BlockPos bp = block_pos((p.T + 63) / 64, p.H);
   const int b = bp.b, h = bp.h;
@@ -767,15 +769,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     if (use_mask && w == 0 && lane < 32)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(mrs, (lds_void_t*)dst, 16, mvoff + (unsigned)q0 * 2, 0, 0, 0);
   };
+  // per-query rows: wave w in 1..3 moves row array w - 1 (lse, delta, gate) with lanes 0-15
+  const float* rsrc = w == 1 ? p.lse : (w == 2 ? p.delta : p.gate);
+  const __amdgpu_buffer_rsrc_t rrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(rsrc + bh * T), 0, T * 4, 0x00020000);
+  auto rows_issue = [&](float* dst, int q0) {
+    if (w > 0 && lane < 16)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rrs, (lds_void_t*)(dst + (w - 1) * 64), 16,
+                                               (unsigned)(lane * 16 + q0 * 4), 0, 0, 0);
+  };
   kv_dma_issue(qd, qo0, 0, w);
   kv_dma_issue(od, qo0 + TILE_B, 0, w);
   mask_issue(mtile0, 0);
-  for (int q = tid; q < Tp; q += 256) {
-    const bool ok = q < T;
-    rowall[q] = ok ? p.lse[bh * T + q] * LOG2E : 0.f;
-    rowall[Tp + q] = ok ? p.delta[bh * T + q] : 0.f;
-    rowall[2 * Tp + q] = ok ? p.gate[bh * T + q] : 0.f;
-  }
+  rows_issue(rows0, 0);
   // bias of (query q, key kj) = vec[kj - q + T - 1]: reversed copies, copy s index j holds
   // log2e * vec[e_hi - j - s], e_hi = kb0 + 63 + T - 1; element (q, kj) sits at segment index
   // u = 63 - kl + q, so a lane's 4 consecutive queries are one aligned float4 of copy (u & 3).
@@ -813,11 +819,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   const int ndiag = diag_len(T);
   const int DPAD = diag_pad(T);
   for (int e = tid; e < ndiag; e += 256) diag[e] = 0.f;
-  float* const tw = dtmp + (w * 4 + g) * 64;
-  // fold the staged tile of relative diagonals r = 16 w + (slot - 48) - 4 g into diag[cb + r]
-  auto fold = [&](int cb) {
-    __syncthreads();
+  // fold the staged tile of relative diagonals r = 16 w + (slot - 48) - 4 g of staging buffer
+  // `buf` into diag[cb + r]. Double-buffered: tile it's staging is folded after the NEXT tile's
+  // top barrier (no barrier of its own; r03 had one per tile)
+  auto fold = [&](int buf, int cb) {
     if (tid < 124) {
+      const float* st = dtmp + buf * 1024;
       const int r = tid - 60;
       float s = 0.f;
 #pragma unroll
@@ -825,7 +832,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 #pragma unroll
         for (int gg = 0; gg < 4; ++gg) {
           const int slot = r - 16 * wv + 4 * gg + 48;
-          if (slot >= 0 && slot < 64) s += dtmp[(wv * 4 + gg) * 64 + slot];
+          if (slot >= 0 && slot < 64) s += st[(wv * 4 + gg) * 64 + slot];
         }
       diag[cb + r] += s;
     }
@@ -866,7 +873,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
       kv_dma_issue(qd, Qn, qb + 64, w);
       kv_dma_issue(od, Qn + TILE_B, qb + 64, w);
       mask_issue(mtile0 + ((it + 1) & 1) * 512, qb + 64);
+      rows_issue(rows0 + ((it + 1) & 1) * 192, qb + 64);
     }
+    if (p.diag && it > 0) fold((it - 1) & 1, kb0 - (qb - 64) - dbase);
+    const float* const rows = rows0 + (it & 1) * 192;  // lse [64], delta [64], gate [64]
     f32x4 s[4], dp[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -886,14 +896,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     float pd[4][4], ds[4][4], gv[4][4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const int ql = qb + 16 * t + 4 * g;
-      const float4 l4 = *reinterpret_cast<const float4*>(rowall + ql);
-      const float4 g4 = *reinterpret_cast<const float4*>(rowall + 2 * Tp + ql);
+      const int ql = 16 * t + 4 * g;
+      const float4 l4 = *reinterpret_cast<const float4*>(rows + ql);
+      const float4 g4 = *reinterpret_cast<const float4*>(rows + 128 + ql);
       const float4 b4 = *reinterpret_cast<const float4*>(rb_base + qb + 16 * t);
-      ds[t][0] = exp2_(fmaf(s[t][0], c1, g4.x * b4.x) - l4.x);  // P (log2 domain)
-      ds[t][1] = exp2_(fmaf(s[t][1], c1, g4.y * b4.y) - l4.y);
-      ds[t][2] = exp2_(fmaf(s[t][2], c1, g4.z * b4.z) - l4.z);
-      ds[t][3] = exp2_(fmaf(s[t][3], c1, g4.w * b4.w) - l4.w);
+      // P (log2 domain; lse in natural-log units)
+      ds[t][0] = exp2_(fmaf(l4.x, -LOG2E, fmaf(s[t][0], c1, g4.x * b4.x)));
+      ds[t][1] = exp2_(fmaf(l4.y, -LOG2E, fmaf(s[t][1], c1, g4.y * b4.y)));
+      ds[t][2] = exp2_(fmaf(l4.z, -LOG2E, fmaf(s[t][2], c1, g4.z * b4.z)));
+      ds[t][3] = exp2_(fmaf(l4.w, -LOG2E, fmaf(s[t][3], c1, g4.w * b4.w)));
     }
     if constexpr (use_mask) {
       // element (t, r) = (query qb + 16t + 4g + r, key 16w + i16 of the block): the forward's word
@@ -936,9 +947,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     }
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const int ql = qb + 16 * t + 4 * g;
-      const float4 d4 = *reinterpret_cast<const float4*>(rowall + Tp + ql);
-      const float4 g4 = *reinterpret_cast<const float4*>(rowall + 2 * Tp + ql);
+      const int ql = 16 * t + 4 * g;
+      const float4 d4 = *reinterpret_cast<const float4*>(rows + 64 + ql);
+      const float4 g4 = *reinterpret_cast<const float4*>(rows + 128 + ql);
       ds[t][0] *= dp[t][0] - d4.x; gv[t][0] = ds[t][0] * (g4.x * kvf);
       ds[t][1] *= dp[t][1] - d4.y; gv[t][1] = ds[t][1] * (g4.y * kvf);
       ds[t][2] *= dp[t][2] - d4.z; gv[t][2] = ds[t][2] * (g4.z * kvf);
@@ -952,12 +963,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
         diag_rot<2>(gv[t][2], wlo[1], whi[1], dacc[t], dacc[t + 1]);
         diag_rot<3>(gv[t][3], wlo[2], whi[2], dacc[t], dacc[t + 1]);
       }
-      // diagonals i16 - 4g - 16j + 16w (j < 4) relative to kb0 - qb are complete: stage, fold
+      // diagonals i16 - 4g - 16j + 16w (j < 4) relative to kb0 - qb are complete: stage them
+      // (folded after the next tile's top barrier)
+      float* const tw = dtmp + (it & 1) * 1024 + (w * 4 + g) * 64;
 #pragma unroll
       for (int j = 0; j < 4; ++j) tw[i16 - 16 * j + 48] = dacc[j];
       dacc[0] = dacc[4];
       dacc[1] = dacc[2] = dacc[3] = dacc[4] = 0.f;
-      fold(kb0 - qb - dbase);
     }
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
@@ -986,12 +998,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
       *reinterpret_cast<uint2*>(krow + 2 * Hd + 16 * dt) = uv;
     }
   }
-  if (p.diag) {  // the carried accumulator: diagonals i16 - 4g + 16w relative to kb0 - (last qb + 64)
-    const int qend = ((T + 63) / 64) * 64;
-    __syncthreads();  // the last tile's fold has read the staging area
+  if (p.diag) {
+    const int qend = ntiles * 64;
+    __syncthreads();  // the last tile's staging is written
+    fold((ntiles - 1) & 1, kb0 - (qend - 64) - dbase);
+    // the carried accumulator: diagonals i16 - 4g + 16w relative to kb0 - qend, staged in the
+    // other buffer (its last fold ran before the last tile's top barrier)
+    float* const tw = dtmp + (ntiles & 1) * 1024 + (w * 4 + g) * 64;
     tw[i16 + 48] = dacc[0];
     tw[i16 + 32] = tw[i16 + 16] = tw[i16] = 0.f;
-    fold(kb0 - qend - dbase);
+    __syncthreads();
+    fold(ntiles & 1, kb0 - qend - dbase);
   }
   __syncthreads();
   if (p.diag) {
@@ -1047,9 +1064,11 @@ int nrse_attn_bwd_mfma(const nrse_attn_bwd_params* p, hipStream_t st) {
   const dim3 grid((unsigned)((p->T + 63) / 64 * p->H * p->batch));
   const size_t bvl = (size_t)bv_len(p->T);
   const size_t lds_q = 4 * TILE_B + 4 * bvl * sizeof(float);
-  const size_t lds_kv =
-      4 * TILE_B + (3 * (size_t)((p->T + 63) & ~63) + 4 * bvl + (size_t)(((p->T + 63) & ~63) + 80) + 1024) * sizeof(float) +
-      2 * 512;  // the double-buffered keep-bit tile
+  // Q / dO tiles, per-query rows, bias copies, diagonals, fold staging, keep-bit tiles (all x2
+  // buffers where double-buffered): 53.8 KB at T = 399, 3 workgroups per CU
+  const size_t lds_kv = 4 * TILE_B +
+                        (2 * 3 * 64 + 4 * bvl + (size_t)(((p->T + 63) & ~63) + 80) + 2 * 1024) * sizeof(float) +
+                        2 * 512;
   if (lds_kv > 160 * 1024) {
     nrse_set_error("nrse_attn_bwd: T=%d too long for the LDS bias copies / diagonal accumulator", p->T);
     return NRSE_ERR_UNSUPPORTED;
