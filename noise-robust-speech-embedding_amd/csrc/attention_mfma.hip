@@ -9,17 +9,12 @@
 //   bwd_kv: grid (k-blocks, H, B); S = Q K^T (lane = key); dV += Pd^T dO, dK += dS^T Q with the
 //           accumulator tiles used as MFMA A operands; sum_b gate*dS accumulated per diagonal
 //           j-i in LDS (rel_attn_embed gradient) then one atomic per diagonal per workgroup.
-//   bwd_q : grid (q-blocks, H, B); dQ += dS K (K by transposed LDS read), dgate = sum_j dS*bias.
+//   bwd_q : grid (q-blocks, H, B); dQ^T += K^T dS^T (K by transposed LDS read; lane = query, so
+//           dQ leaves in 8-byte runs), dgate = sum_j dS*bias.
 // LDS tiles are [64 rows][64 bf16] (128-byte rows) with the 16-byte chunk XOR-swizzled by
 // ((row>>1)&3)<<1 so both ds_read_b128 row reads and ds_read_b64_tr_b16 column reads of one
 // image stay (nearly) conflict-free.
 #include "common.h"
-
-// NRSE_ATTN_FWD_CHAINS: 1 = attn_fwd_kernel (4 waves x 16 queries), 2 = attn_fwd2_kernel (2 waves
-// x 2 chains of 16 queries)
-#ifndef NRSE_ATTN_FWD_CHAINS
-#define NRSE_ATTN_FWD_CHAINS 1
-#endif
 
 namespace {
 
@@ -122,27 +117,6 @@ NRSE_DEV KvDma kv_dma_init(const bf16_t* utt_base, int T, long long ld, int col_
     d.voff[j] = (unsigned)row * d.ld_b + (unsigned)col_b + (unsigned)chunk * 16;
   }
   return d;
-}
-
-// the two-wave form: 4 wave-instructions per tile per wave (rows (4 wave + j) * 8 .. +7)
-struct KvDma2 {
-  struct {
-    __amdgpu_buffer_rsrc_t rs;
-    unsigned voff[4];
-    unsigned ld_b;
-  } d;
-};
-NRSE_DEV KvDma2 kv_dma_init2(const bf16_t* utt_base, int T, long long ld, int col_b, int wave, int lane) {
-  KvDma2 k;
-  k.d.ld_b = (unsigned)(ld * 2);
-  k.d.rs = __builtin_amdgcn_make_buffer_rsrc((void*)utt_base, 0, (int)((long long)T * ld * 2), 0x00020000);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int row = (wave * 4 + j) * 8 + (lane >> 3);
-    const int chunk = (lane & 7) ^ (((row >> 1) & 3) << 1);
-    k.d.voff[j] = (unsigned)row * k.d.ld_b + (unsigned)col_b + (unsigned)chunk * 16;
-  }
-  return k;
 }
 
 // stage rows row0 .. row0+63 into the tile at `tile` (wave-uniform LDS address)
@@ -357,201 +331,6 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
   if (g == 0 && qv) p.lse[bh * T + qi] = (m + __builtin_amdgcn_logf(l)) * LN2;
 }
 
-// ------------------------------------------------------------------------------ forward, two chains
-// The same computation with 2 waves per workgroup and TWO independent 16-query chains per wave
-// (wave w: queries q0 + 32w + 16c + i16, c = 0, 1): each wave issues both chains' QK^T MFMAs
-// before either softmax, so one chain's exp / max / hash work overlaps the other's MFMAs inside
-// the wave instead of relying on other waves to cover the dependency stalls (r03 PMC: 39 % of
-// wave-cycles stalled on dependencies). Results are bit-identical to attn_fwd_kernel's (same
-// per-element arithmetic and order).
-template <typename DD>
-NRSE_DEV void kv_dma_issue2(const DD& d, char* tile, int row0, int wave) {
-  const unsigned roff = (unsigned)row0 * d.ld_b;
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(d.rs, (lds_void_t*)(tile + (wave * 4 + j) * 1024), 16, d.voff[j] + roff,
-                                             0, 0, 0);
-}
-template <bool DROP>
-__global__ __launch_bounds__(128) void attn_fwd2_kernel(const nrse_attn_fwd_params p) {
-  extern __shared__ __attribute__((aligned(16))) char dyn[];
-  char* const kv0 = dyn;
-  float* const bv = reinterpret_cast<float*>(dyn + 4 * TILE_B);
-  const int T = p.T, H = p.H, Hd = H * D;
-  const long long ld3 = 3LL * Hd;
-  const BlockPos bp = block_pos((p.T + 63) / 64, p.H);
-  const int b = bp.b, h = bp.h;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = lane >> 4, i16 = lane & 15;
-  const int q0 = bp.blk * 64;
-  const bf16_t* qkv = (const bf16_t*)p.qkv + (long long)b * T * ld3;
-  const KvDma2 kd = kv_dma_init2(qkv, T, ld3, (Hd + h * D) * 2, w, lane);
-  const KvDma2 vd = kv_dma_init2(qkv, T, ld3, (2 * Hd + h * D) * 2, w, lane);
-  const int ntiles = (T + 63) / 64;
-  const int Tp = ntiles * 64;
-  kv_dma_issue2(kd.d, kv0, 0, w);
-  kv_dma_issue2(vd.d, kv0 + TILE_B, 0, w);
-  {
-    const int len = bv_len(T), nd = 2 * T - 1;
-    const int e_lo = T - 1 - q0 - 63;
-    const float* vec = p.bias_vec + (long long)h * (2 * T - 1);
-    for (int j = tid; j < len; j += 128) {
-#pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) {
-        const int e = e_lo + j + s4;
-        bv[s4 * len + j] = (e >= 0 && e < nd) ? vec[e] : 0.f;
-      }
-    }
-  }
-  const long long bh = (long long)b * H + h;
-  const float c1 = p.scale * LOG2E;
-  const int bvl = bv_len(T);
-  const uint32_t key = site_key(p.seed);
-  const uint32_t thr = dropout_threshold16(p.dropout_p);
-  constexpr bool drop = DROP;
-  const float dsc = drop ? 1.f / (1.f - p.dropout_p) : 1.f;
-  constexpr float RESCALE_TAU = 8.f;
-  int qi[2];
-  bool qv[2];
-  bf16x8 qf[2][2];
-  float gl[2], mref[2];
-  const float* bvl_base[2];
-  uint32_t rowpair[2];
-  f32x2 lpart2[2];
-  f32x4 o[2][4];
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    qi[c] = q0 + 32 * w + 16 * c + i16;
-    qv[c] = qi[c] < T;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      uint4 u = make_uint4(0, 0, 0, 0);
-      if (qv[c]) u = *reinterpret_cast<const uint4*>(qkv + (long long)qi[c] * ld3 + h * D + 8 * g + 32 * s);
-      qf[c][s] = __builtin_bit_cast(bf16x8, u);
-    }
-    gl[c] = (qv[c] ? p.gate[bh * T + qi[c]] : 0.f) * LOG2E;
-    const int u00 = 4 * g + 63 - (32 * w + 16 * c + i16);
-    const int bsel = u00 & 3;
-    bvl_base[c] = bv + bsel * bvl + (u00 - bsel);
-    rowpair[c] = (uint32_t)(bh * T + qi[c]) * (uint32_t)((T + 1) >> 1) + (uint32_t)(2 * g);
-    mref[c] = 0.f;
-    lpart2[c] = f32x2{0.f, 0.f};
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) o[c][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-
-  for (int it = 0; it < ntiles; ++it) {
-    const int kb = it * 64;
-    char* const Kt = kv0 + (it & 1) * 2 * TILE_B;
-    char* const Vt = Kt + TILE_B;
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (it + 1 < ntiles) {
-      char* const Kn = kv0 + ((it + 1) & 1) * 2 * TILE_B;
-      kv_dma_issue2(kd.d, Kn, kb + 64, w);
-      kv_dma_issue2(vd.d, Kn + TILE_B, kb + 64, w);
-    }
-    // both chains' S^T = K Q^T first
-    f32x4 sc[2][4];
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        sc[c][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ss = 0; ss < 2; ++ss)
-          sc[c][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rd_row(Kt, 16 * t + i16, 4 * ss + g), qf[c][ss], sc[c][t], 0, 0, 0);
-      }
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      float v[4][4];
-      const f32x2 c12 = {c1, c1}, gl2 = {gl[c], gl[c]}, nm2 = {-mref[c], -mref[c]};
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const float4 bb = *reinterpret_cast<const float4*>(bvl_base[c] + kb + 16 * t);
-        const f32x2 r0 = pk_fma(f32x2{sc[c][t][0], sc[c][t][1]}, c12, pk_fma(gl2, f32x2{bb.x, bb.y}, nm2));
-        const f32x2 r1 = pk_fma(f32x2{sc[c][t][2], sc[c][t][3]}, c12, pk_fma(gl2, f32x2{bb.z, bb.w}, nm2));
-        v[t][0] = r0.x; v[t][1] = r0.y; v[t][2] = r1.x; v[t][3] = r1.y;
-      }
-      if (kb + 64 > T) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[t][r] = (kb + 16 * t + 4 * g + r < T) ? v[t][r] : -INFINITY;
-      }
-      float mx = -INFINITY;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) mx = fmaxf(mx, fmaxf(fmaxf(v[t][0], v[t][1]), fmaxf(v[t][2], v[t][3])));
-      mx = xor32_max(xor16_max(mx));
-      if (it == 0 || __builtin_amdgcn_ballot_w64(mx > RESCALE_TAU)) {
-        const float sh = it == 0 ? mx : fmaxf(mx, 0.f);
-        const float alpha = it == 0 ? 1.f : exp2_(-sh);
-        mref[c] += sh;
-        const f32x2 sh2 = {sh, sh}, al2 = {alpha, alpha};
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const f32x2 a0 = f32x2{v[t][0], v[t][1]} - sh2, a1 = f32x2{v[t][2], v[t][3]} - sh2;
-          v[t][0] = a0.x; v[t][1] = a0.y; v[t][2] = a1.x; v[t][3] = a1.y;
-        }
-        lpart2[c] *= al2;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-          const f32x2 o0 = f32x2{o[c][dt][0], o[c][dt][1]} * al2, o1 = f32x2{o[c][dt][2], o[c][dt][3]} * al2;
-          o[c][dt] = f32x4{o0.x, o0.y, o1.x, o1.y};
-        }
-      }
-      float pd[4][4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) pd[t][r] = exp2_(v[t][r]);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) lpart2[c] += f32x2{pd[t][0], pd[t][1]} + f32x2{pd[t][2], pd[t][3]};
-      if constexpr (DROP) {
-        uint32_t mb = 0;
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int rp = 0; rp < 2; ++rp) {
-            const uint32_t hh = mix32((rowpair[c] + (uint32_t)((kb >> 1) + 8 * t + rp)) ^ key);
-            const bool k0 = attn_half_keep(hh, 0, thr), k1 = attn_half_keep(hh, 1, thr);
-            pd[t][2 * rp] = k0 ? pd[t][2 * rp] : 0.f;
-            pd[t][2 * rp + 1] = k1 ? pd[t][2 * rp + 1] : 0.f;
-            mb |= (k0 ? 1u << (4 * t + 2 * rp) : 0u) | (k1 ? 2u << (4 * t + 2 * rp) : 0u);
-            asm("" : "+v"(pd[t][2 * rp]), "+v"(pd[t][2 * rp + 1]));
-          }
-        if (p.drop_mask && qv[c]) p.drop_mask[((bh * ntiles + it) * 4 + g) * Tp + qi[c]] = (uint16_t)mb;
-      }
-#pragma unroll
-      for (int cc = 0; cc < 2; ++cc) {
-        const bf16x8 pa = pack8(pd[2 * cc], pd[2 * cc + 1]);
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt)
-          o[c][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rd_tr(Vt, 32 * cc, 32 * cc + 16, 16 * dt, lane), pa, o[c][dt], 0, 0, 0);
-      }
-    }
-  }
-  bf16_t* ctx = (bf16_t*)p.ctx;
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const float l = xor32_sum(xor16_sum(lpart2[c].x + lpart2[c].y));
-    if (qv[c]) {
-      const float inv = dsc / l;
-      bf16_t* crow = ctx + ((long long)b * T + qi[c]) * Hd + h * D + 4 * g;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        uint2 u;
-        u.x = (uint32_t)f2bf(o[c][dt][0] * inv) | ((uint32_t)f2bf(o[c][dt][1] * inv) << 16);
-        u.y = (uint32_t)f2bf(o[c][dt][2] * inv) | ((uint32_t)f2bf(o[c][dt][3] * inv) << 16);
-        *reinterpret_cast<uint2*>(crow + 16 * dt) = u;
-      }
-      if (g == 0) p.lse[bh * T + qi[c]] = (mref[c] + __builtin_amdgcn_logf(l)) * LN2;
-    }
-  }
-}
-
 // ------------------------------------------------------------------------------ bwd: dQ, dgate
 // DM: dropout mode, 0 none, 1 re-hashed keep bits, 2 the forward's recorded bits (drop_mask);
 // one specialisation each (both paths in one kernel cost 20 VGPRs and a wave per SIMD)
@@ -705,19 +484,20 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
       const bf16x8 da = pack8(ds[2 * c], ds[2 * c + 1]);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt)
-        dq[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, rd_tr(Kt, 32 * c, 32 * c + 16, 16 * dt, lane), dq[dt], 0, 0, 0);
+        dq[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rd_tr(Kt, 32 * c, 32 * c + 16, 16 * dt, lane), da, dq[dt], 0, 0, 0);
     }
   }
   dgate = xor32_sum(xor16_sum(dgate));
   if (g == 0 && qv) p.dgate[bh * T + qi] = dgate;
-  bf16_t* dqkv = (bf16_t*)p.dqkv + (long long)b * T * ld3;
-  const int qrow0 = q0 + w * 16;
+  // dQ^T accumulated (K^T in the A slot): lane (g, i16) holds query qi, dims 16 dt + 4g .. + 3
+  if (qv) {
+    bf16_t* qrow = (bf16_t*)p.dqkv + ((long long)b * T + qi) * ld3 + h * D + 4 * g;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int q = qrow0 + 4 * g + r;
-    if (q < T) {
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) dqkv[(long long)q * ld3 + h * D + 16 * dt + i16] = f2bf(dq[dt][r] * p.scale);
+    for (int dt = 0; dt < 4; ++dt) {
+      uint2 u;
+      u.x = (uint32_t)f2bf(dq[dt][0] * p.scale) | ((uint32_t)f2bf(dq[dt][1] * p.scale) << 16);
+      u.y = (uint32_t)f2bf(dq[dt][2] * p.scale) | ((uint32_t)f2bf(dq[dt][3] * p.scale) << 16);
+      *reinterpret_cast<uint2*>(qrow + 16 * dt) = u;
     }
   }
 }
@@ -733,16 +513,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   char* const qo0 = dyn;  // [2 buffers][Q tile, dO tile], LDS-DMA double buffer
   const int T = p.T, H = p.H, Hd = H * D;
   const int Tp = (T + 63) & ~63;
-  // [2 buffers][lse, delta, gate][64 queries] f32 of the query tile, staged by LDS-DMA beside Q / dO
-  // (waves 1-3, one 256-B piece each; queries past T land as zeros)
-  float* const rows0 = reinterpret_cast<float*>(dyn + 4 * TILE_B);
-  float* const rbv = rows0 + 2 * 3 * 64;                              // 4 reversed bias copies
+  float* const rowall = reinterpret_cast<float*>(dyn + 4 * TILE_B);  // lse*log2e [Tp], delta [Tp], gate [Tp]
+  float* const rbv = rowall + 3 * Tp;                                 // 4 reversed bias copies
   const int bvl = bv_len(T);
   float* const diag = rbv + 4 * bvl;                                  // [diag_len(T)]
-  float* const dtmp = diag + diag_len(T);                             // [2 buffers][4 waves][4 lane rows][64]
+  float* const dtmp = diag + diag_len(T);                             // [4 waves][4 lane rows][64]
   // [2 buffers][4 g][64 queries] u16: the forward's keep bits of this key block for the query
   // tile, staged by LDS-DMA beside Q / dO (wave 0, lanes 0-31: 512 B)
-  char* const mtile0 = reinterpret_cast<char*>(dtmp + 2 * 1024);
+  char* const mtile0 = reinterpret_cast<char*>(dtmp + 1024);
   const long long ld3 = 3LL * Hd;
   const BlockPos bp = block_pos((p.T + 63) / 64, p.H);
   const int b = bp.b, h = bp.h;
@@ -769,19 +547,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     if (use_mask && w == 0 && lane < 32)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(mrs, (lds_void_t*)dst, 16, mvoff + (unsigned)q0 * 2, 0, 0, 0);
   };
-  // per-query rows: wave w in 1..3 moves row array w - 1 (lse, delta, gate) with lanes 0-15
-  const float* rsrc = w == 1 ? p.lse : (w == 2 ? p.delta : p.gate);
-  const __amdgpu_buffer_rsrc_t rrs =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(rsrc + bh * T), 0, T * 4, 0x00020000);
-  auto rows_issue = [&](float* dst, int q0) {
-    if (w > 0 && lane < 16)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rrs, (lds_void_t*)(dst + (w - 1) * 64), 16,
-                                               (unsigned)(lane * 16 + q0 * 4), 0, 0, 0);
-  };
   kv_dma_issue(qd, qo0, 0, w);
   kv_dma_issue(od, qo0 + TILE_B, 0, w);
   mask_issue(mtile0, 0);
-  rows_issue(rows0, 0);
+  for (int q = tid; q < Tp; q += 256) {
+    const bool ok = q < T;
+    rowall[q] = ok ? p.lse[bh * T + q] * LOG2E : 0.f;
+    rowall[Tp + q] = ok ? p.delta[bh * T + q] : 0.f;
+    rowall[2 * Tp + q] = ok ? p.gate[bh * T + q] : 0.f;
+  }
   // bias of (query q, key kj) = vec[kj - q + T - 1]: reversed copies, copy s index j holds
   // log2e * vec[e_hi - j - s], e_hi = kb0 + 63 + T - 1; element (q, kj) sits at segment index
   // u = 63 - kl + q, so a lane's 4 consecutive queries are one aligned float4 of copy (u & 3).
@@ -819,12 +593,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   const int ndiag = diag_len(T);
   const int DPAD = diag_pad(T);
   for (int e = tid; e < ndiag; e += 256) diag[e] = 0.f;
-  // fold the staged tile of relative diagonals r = 16 w + (slot - 48) - 4 g of staging buffer
-  // `buf` into diag[cb + r]. Double-buffered: tile it's staging is folded after the NEXT tile's
-  // top barrier (no barrier of its own; r03 had one per tile)
-  auto fold = [&](int buf, int cb) {
+  float* const tw = dtmp + (w * 4 + g) * 64;
+  // fold the staged tile of relative diagonals r = 16 w + (slot - 48) - 4 g into diag[cb + r]
+  auto fold = [&](int cb) {
+    __syncthreads();
     if (tid < 124) {
-      const float* st = dtmp + buf * 1024;
       const int r = tid - 60;
       float s = 0.f;
 #pragma unroll
@@ -832,7 +605,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 #pragma unroll
         for (int gg = 0; gg < 4; ++gg) {
           const int slot = r - 16 * wv + 4 * gg + 48;
-          if (slot >= 0 && slot < 64) s += st[(wv * 4 + gg) * 64 + slot];
+          if (slot >= 0 && slot < 64) s += dtmp[(wv * 4 + gg) * 64 + slot];
         }
       diag[cb + r] += s;
     }
@@ -873,10 +646,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
       kv_dma_issue(qd, Qn, qb + 64, w);
       kv_dma_issue(od, Qn + TILE_B, qb + 64, w);
       mask_issue(mtile0 + ((it + 1) & 1) * 512, qb + 64);
-      rows_issue(rows0 + ((it + 1) & 1) * 192, qb + 64);
     }
-    if (p.diag && it > 0) fold((it - 1) & 1, kb0 - (qb - 64) - dbase);
-    const float* const rows = rows0 + (it & 1) * 192;  // lse [64], delta [64], gate [64]
     f32x4 s[4], dp[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -896,15 +666,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     float pd[4][4], ds[4][4], gv[4][4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const int ql = 16 * t + 4 * g;
-      const float4 l4 = *reinterpret_cast<const float4*>(rows + ql);
-      const float4 g4 = *reinterpret_cast<const float4*>(rows + 128 + ql);
+      const int ql = qb + 16 * t + 4 * g;
+      const float4 l4 = *reinterpret_cast<const float4*>(rowall + ql);
+      const float4 g4 = *reinterpret_cast<const float4*>(rowall + 2 * Tp + ql);
       const float4 b4 = *reinterpret_cast<const float4*>(rb_base + qb + 16 * t);
-      // P (log2 domain; lse in natural-log units)
-      ds[t][0] = exp2_(fmaf(l4.x, -LOG2E, fmaf(s[t][0], c1, g4.x * b4.x)));
-      ds[t][1] = exp2_(fmaf(l4.y, -LOG2E, fmaf(s[t][1], c1, g4.y * b4.y)));
-      ds[t][2] = exp2_(fmaf(l4.z, -LOG2E, fmaf(s[t][2], c1, g4.z * b4.z)));
-      ds[t][3] = exp2_(fmaf(l4.w, -LOG2E, fmaf(s[t][3], c1, g4.w * b4.w)));
+      ds[t][0] = exp2_(fmaf(s[t][0], c1, g4.x * b4.x) - l4.x);  // P (log2 domain)
+      ds[t][1] = exp2_(fmaf(s[t][1], c1, g4.y * b4.y) - l4.y);
+      ds[t][2] = exp2_(fmaf(s[t][2], c1, g4.z * b4.z) - l4.z);
+      ds[t][3] = exp2_(fmaf(s[t][3], c1, g4.w * b4.w) - l4.w);
     }
     if constexpr (use_mask) {
       // element (t, r) = (query qb + 16t + 4g + r, key 16w + i16 of the block): the forward's word
@@ -947,9 +716,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     }
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const int ql = 16 * t + 4 * g;
-      const float4 d4 = *reinterpret_cast<const float4*>(rows + 64 + ql);
-      const float4 g4 = *reinterpret_cast<const float4*>(rows + 128 + ql);
+      const int ql = qb + 16 * t + 4 * g;
+      const float4 d4 = *reinterpret_cast<const float4*>(rowall + Tp + ql);
+      const float4 g4 = *reinterpret_cast<const float4*>(rowall + 2 * Tp + ql);
       ds[t][0] *= dp[t][0] - d4.x; gv[t][0] = ds[t][0] * (g4.x * kvf);
       ds[t][1] *= dp[t][1] - d4.y; gv[t][1] = ds[t][1] * (g4.y * kvf);
       ds[t][2] *= dp[t][2] - d4.z; gv[t][2] = ds[t][2] * (g4.z * kvf);
@@ -963,13 +732,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
         diag_rot<2>(gv[t][2], wlo[1], whi[1], dacc[t], dacc[t + 1]);
         diag_rot<3>(gv[t][3], wlo[2], whi[2], dacc[t], dacc[t + 1]);
       }
-      // diagonals i16 - 4g - 16j + 16w (j < 4) relative to kb0 - qb are complete: stage them
-      // (folded after the next tile's top barrier)
-      float* const tw = dtmp + (it & 1) * 1024 + (w * 4 + g) * 64;
+      // diagonals i16 - 4g - 16j + 16w (j < 4) relative to kb0 - qb are complete: stage, fold
 #pragma unroll
       for (int j = 0; j < 4; ++j) tw[i16 - 16 * j + 48] = dacc[j];
       dacc[0] = dacc[4];
       dacc[1] = dacc[2] = dacc[3] = dacc[4] = 0.f;
+      fold(kb0 - qb - dbase);
     }
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
@@ -998,17 +766,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
       *reinterpret_cast<uint2*>(krow + 2 * Hd + 16 * dt) = uv;
     }
   }
-  if (p.diag) {
-    const int qend = ntiles * 64;
-    __syncthreads();  // the last tile's staging is written
-    fold((ntiles - 1) & 1, kb0 - (qend - 64) - dbase);
-    // the carried accumulator: diagonals i16 - 4g + 16w relative to kb0 - qend, staged in the
-    // other buffer (its last fold ran before the last tile's top barrier)
-    float* const tw = dtmp + (ntiles & 1) * 1024 + (w * 4 + g) * 64;
+  if (p.diag) {  // the carried accumulator: diagonals i16 - 4g + 16w relative to kb0 - (last qb + 64)
+    const int qend = ((T + 63) / 64) * 64;
+    __syncthreads();  // the last tile's fold has read the staging area
     tw[i16 + 48] = dacc[0];
     tw[i16 + 32] = tw[i16 + 16] = tw[i16] = 0.f;
-    __syncthreads();
-    fold(ntiles & 1, kb0 - qend - dbase);
+    fold(kb0 - qend - dbase);
   }
   __syncthreads();
   if (p.diag) {
@@ -1046,13 +809,8 @@ int nrse_attn_fwd_mfma(const nrse_attn_fwd_params* p, hipStream_t st) {
     nrse_set_error("nrse_attn_fwd: T=%d too long for the LDS bias copies", p->T);
     return NRSE_ERR_UNSUPPORTED;
   }
-#if NRSE_ATTN_FWD_CHAINS == 2
-  if (p->dropout_p > 0.f) hipLaunchKernelGGL(attn_fwd2_kernel<true>, grid, dim3(128), lds, st, *p);
-  else hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(256), lds, st, *p);
-#else
   if (p->dropout_p > 0.f) hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(256), lds, st, *p);
   else hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(256), lds, st, *p);
-#endif
   return nrse_check_launch("nrse_attn_fwd(mfma)");
 }
 
@@ -1064,11 +822,9 @@ int nrse_attn_bwd_mfma(const nrse_attn_bwd_params* p, hipStream_t st) {
   const dim3 grid((unsigned)((p->T + 63) / 64 * p->H * p->batch));
   const size_t bvl = (size_t)bv_len(p->T);
   const size_t lds_q = 4 * TILE_B + 4 * bvl * sizeof(float);
-  // Q / dO tiles, per-query rows, bias copies, diagonals, fold staging, keep-bit tiles (all x2
-  // buffers where double-buffered): 53.8 KB at T = 399, 3 workgroups per CU
-  const size_t lds_kv = 4 * TILE_B +
-                        (2 * 3 * 64 + 4 * bvl + (size_t)(((p->T + 63) & ~63) + 80) + 2 * 1024) * sizeof(float) +
-                        2 * 512;
+  const size_t lds_kv =
+      4 * TILE_B + (3 * (size_t)((p->T + 63) & ~63) + 4 * bvl + (size_t)(((p->T + 63) & ~63) + 80) + 1024) * sizeof(float) +
+      2 * 512;  // the double-buffered keep-bit tile
   if (lds_kv > 160 * 1024) {
     nrse_set_error("nrse_attn_bwd: T=%d too long for the LDS bias copies / diagonal accumulator", p->T);
     return NRSE_ERR_UNSUPPORTED;

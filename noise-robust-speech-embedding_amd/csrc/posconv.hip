@@ -292,8 +292,11 @@ __global__ __launch_bounds__(PNTHR, 2) void posconv_wgrad_kernel(const nrse_gemm
     }
   }
 
-  // f32 atomics into dWf (zeroed by the caller; nshare partial sums per element)
-  float* cbase = (float*)p.c + (long long)g * p.c_z1;
+  // c_split > 0: share sh's partial sums stored whole into slab sh (16-byte stores, summed in
+  // slab order by the caller); else f32 atomics into dWf (zeroed by the caller; nshare partial
+  // sums per element). The atomics cost 32 B of write traffic per 4-byte add.
+  const bool slabs = p.c_split != 0;
+  float* cbase = (float*)p.c + (long long)g * p.c_z1 + (slabs ? (long long)sh * p.c_split : 0);
   const int q = lane >> 4, i = lane & 15;
 #pragma unroll
   for (int tl = 0; tl < 2; ++tl) {
@@ -303,8 +306,13 @@ __global__ __launch_bounds__(PNTHR, 2) void posconv_wgrad_kernel(const nrse_gemm
 #pragma unroll
       for (int fj = 0; fj < 4; ++fj) {
         float* dst = cbase + (long long)(fi * 16 + i) * p.ldc + n0 + fj * 16 + 4 * q;
+        if (slabs) {
+          *reinterpret_cast<float4*>(dst) =
+              make_float4(acc[tl][fi][fj][0], acc[tl][fi][fj][1], acc[tl][fi][fj][2], acc[tl][fi][fj][3]);
+        } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) atomicAdd(dst + e, acc[tl][fi][fj][e]);
+          for (int e = 0; e < 4; ++e) atomicAdd(dst + e, acc[tl][fi][fj][e]);
+        }
       }
   }
 }
@@ -346,10 +354,14 @@ bool nrse_posconv_wgrad_ok(const nrse_gemm_params* p) {
   if (a.dtype != NRSE_BF16 || b.dtype != NRSE_BF16 || a.kcontig || b.kcontig) return false;
   if (a.chunk_shift != 0 || b.chunk_shift != 6 || b.ld_chunk != b.ld) return false;
   if (p->M != PCH || p->N % (WTB * PCH) != 0 || p->K < 1 || p->zdiv != 1) return false;
-  // the kernel adds two partial sums per element straight into C (the caller zeroes it): per-split
-  // slabs (c_split > 0) are not supported here and take the generic path
-  if (p->flags != NRSE_EPI_ATOMIC || p->c_dtype != NRSE_F32 || p->ldc < p->N || p->alpha != 1.f) return false;
-  if (p->c_split != 0) return false;
+  // either two partial sums per element added straight into C (EPI_ATOMIC; the caller zeroes it)
+  // or, with splits = 2 and per-split slabs (c_split > 0), each split's sum stored into its slab
+  if (p->c_dtype != NRSE_F32 || p->ldc < p->N || p->alpha != 1.f || (p->ldc & 3) || (p->c_z1 & 3)) return false;
+  if (p->c_split == 0 ? p->flags != NRSE_EPI_ATOMIC
+                      : (p->flags != 0 || p->splits != 2 || (p->c_split & 3) ||
+                         p->c_split < (long long)(p->batch - 1) * p->c_z1 + (long long)(p->M - 1) * p->ldc + p->N))
+    return false;
+  if (((uintptr_t)p->c) & 15) return false;
   if (a.ld % 8 || b.ld % 8 || a.seg_stride % 8 || b.seg_stride % 8 || a.z1 % 8 || b.z1 % 8) return false;
   if (b.seg_stride % b.ld != 0 || b.seg_stride / b.ld < (long long)p->K + p->N / PCH - 1) return false;
   if ((((uintptr_t)a.ptr) | ((uintptr_t)b.ptr)) & 15) return false;
@@ -365,7 +377,8 @@ int nrse_posconv_wgrad(const nrse_gemm_params* p, hipStream_t st) {
   const int nseg_total = p->nseg * p->splits;
   // two shares of the segments: 2 workgroups per CU at 16 groups x 16 tap blocks, and with two
   // partial sums per element onto the zeroed dWf the atomic result is order-independent
-  const int nshare = nseg_total >= 2 ? 2 : 1;
+  // (slab mode: one share per split, splits = 2)
+  const int nshare = p->c_split != 0 ? 2 : nseg_total >= 2 ? 2 : 1;
   const int ktiles = nrse_cdiv(p->K, 64);
   const long long b_rows = p->b.seg_stride / p->b.ld;
   const long long total = (long long)p->batch * nshare * ntb;

@@ -594,18 +594,27 @@ class ByolEngine:
         # backward) on the side stream, beside the dgrad chain down the front end
         with self._wgrad_stream(main, dypad, tape.hpad):
             K.colsum(dypad, Gv["encoder.pos_conv_embed.conv.bias"])
-            dWf = torch.zeros(G, cpg, pk * cpg, device=dev, dtype=F32)
             S = _divisor_at_most(B, 8)
             off = (pk // 2 - 1) * H
             A_op = K.Operand(dypad, False, H, offset=off, seg_stride=(T + pk) * H, z1=cpg)
             B_op = K.Operand(tape.hpad, False, H, chunk_shift=cs, ld_chunk=H, seg_stride=(T + pk) * H, z1=cpg)
-            if S <= 2 or (cdt == torch.bfloat16 and cpg == 64):
-                # at most two partial sums per element onto the zeroed dWf (the bf16 pos-conv wgrad
-                # kernel of posconv.hip, 64-channel groups, adds two shares): an order-independent,
+            if cdt == torch.bfloat16 and cpg == 64 and B % 2 == 0:
+                # the bf16 pos-conv wgrad kernel of posconv.hip (64-channel groups): two halves of
+                # the utterances, each stored whole into its slab, summed in slab order
+                dWf = torch.empty(G, cpg, pk * cpg, device=dev, dtype=F32)
+                slab = torch.empty(2, G, cpg, pk * cpg, device=dev, dtype=F32)
+                K.gemm(A_op, B_op, slab, cpg, pk * cpg, T, ldc=pk * cpg, nseg=B // 2, splits=2, batch=G,
+                       c_z1=cpg * pk * cpg, c_split=dWf.numel())
+                K.splitk_reduce(dWf, slab, 2, accumulate=False)
+                del slab
+            elif S <= 2 or (cdt == torch.bfloat16 and cpg == 64):
+                # at most two partial sums per element onto the zeroed dWf: an order-independent,
                 # deterministic f32 sum
+                dWf = torch.zeros(G, cpg, pk * cpg, device=dev, dtype=F32)
                 K.gemm(A_op, B_op, dWf, cpg, pk * cpg, T, ldc=pk * cpg, nseg=B // S, splits=S, batch=G,
                        c_z1=cpg * pk * cpg, flags=_lib.EPI_ATOMIC)
             else:
+                dWf = torch.empty(G, cpg, pk * cpg, device=dev, dtype=F32)
                 # other shapes (generic kernels): split slabs added in split order
                 slab = torch.empty(S, G, cpg, pk * cpg, device=dev, dtype=F32)
                 K.gemm(A_op, B_op, slab, cpg, pk * cpg, T, ldc=pk * cpg, nseg=B // S, splits=S, batch=G,

@@ -212,6 +212,44 @@ def test_posconv_wgrad_sliding_window(nrse_device, T, nseg, splits):
     assert rel(got, generic) < 1e-5
 
 
+@pytest.mark.parametrize("T,nseg", [(399, 2), (100, 1)])
+def test_posconv_wgrad_slabs(nrse_device, T, nseg):
+    """The engine's form of the pos-conv weight gradient (engine.py encoder_backward): splits = 2
+    with per-split f32 slabs stored whole by posconv_wgrad_kernel, then summed in slab order by
+    nrse_splitk_reduce. Bit-identical to the two-share atomic form (two partial sums onto zeros),
+    and within f32 accumulation of a float64 einsum."""
+    from nrse_amd import kernels as K, _lib
+    dev = nrse_device
+    B, H, G, pk = 2 * nseg, 1024, 16, 128
+    cpg = H // G
+    cs = cpg.bit_length() - 1
+    g = torch.Generator(device=dev).manual_seed(T + 7)
+    hpad = torch.zeros(B, T + pk, H, device=dev, dtype=torch.bfloat16)
+    hpad[:, pk // 2:pk // 2 + T] = torch.randn(B, T, H, device=dev, generator=g).to(torch.bfloat16)
+    lead = pk // 2 - 1
+    dypad = torch.zeros(B, T + pk, H, device=dev, dtype=torch.bfloat16)
+    dypad[:, lead:lead + T] = torch.randn(B, T, H, device=dev, generator=g).to(torch.bfloat16)
+    A_op = K.Operand(dypad, False, H, offset=lead * H, seg_stride=(T + pk) * H, z1=cpg)
+    B_op = K.Operand(hpad, False, H, chunk_shift=cs, ld_chunk=H, seg_stride=(T + pk) * H, z1=cpg)
+    n = G * cpg * pk * cpg
+    slab = torch.full((2, n), float("nan"), device=dev)
+    K.gemm(A_op, B_op, slab, cpg, pk * cpg, T, ldc=pk * cpg, nseg=nseg, splits=2, batch=G,
+           c_z1=cpg * pk * cpg, c_split=n)
+    got = torch.empty(n, device=dev)
+    K.splitk_reduce(got, slab, 2, accumulate=False)
+    atom = torch.zeros(n, device=dev)
+    K.gemm(A_op, B_op, atom, cpg, pk * cpg, T, ldc=pk * cpg, nseg=nseg, splits=2, batch=G,
+           c_z1=cpg * pk * cpg, flags=_lib.EPI_ATOMIC)
+    assert torch.equal(got, atom)
+    dy = dypad[:, lead:lead + T].double()
+    win = hpad.double().unfold(1, pk, 1)[:, :T]
+    got = got.view(G, cpg, pk * cpg)
+    for gi in (0, G - 1):
+        sl = slice(gi * cpg, (gi + 1) * cpg)
+        ref = torch.einsum("bto,btip->opi", dy[..., sl], win[:, :, sl]).reshape(cpg, pk * cpg)
+        assert rel(got[gi], ref) < 1e-5, gi
+
+
 def _split(w):
     from nrse_amd import kernels as K
     w2 = torch.empty((2,) + tuple(w.shape), device=w.device, dtype=torch.bfloat16)
