@@ -598,15 +598,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   auto fold = [&](int cb) {
     __syncthreads();
     if (tid < 124) {
+      // branch-free: all 16 reads issued back to back (an out-of-range slot reads slot 0 and
+      // adds zero), summed in the fixed (wave, row) order
       const int r = tid - 60;
-      float s = 0.f;
+      float v[16];
 #pragma unroll
       for (int wv = 0; wv < 4; ++wv)
 #pragma unroll
         for (int gg = 0; gg < 4; ++gg) {
           const int slot = r - 16 * wv + 4 * gg + 48;
-          if (slot >= 0 && slot < 64) s += dtmp[(wv * 4 + gg) * 64 + slot];
+          const bool ok = (unsigned)slot < 64u;
+          const float x = dtmp[(wv * 4 + gg) * 64 + (ok ? slot : 0)];
+          v[wv * 4 + gg] = ok ? x : 0.f;
         }
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s += v[i];
       diag[cb + r] += s;
     }
   };
