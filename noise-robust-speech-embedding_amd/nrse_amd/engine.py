@@ -194,6 +194,7 @@ class ByolEngine:
             K.cast(self.target, self.target_sh)
         self.step_count = 0
         self._offsets = {}
+        self._view_cache = {}
         for gname, s in self.layout.specs:
             off, cnt, shp = self.layout.offsets[PR.GROUP_PREFIX[gname] + s.name]
             self._offsets.setdefault(gname, {})[s.name] = (off, cnt, shp)
@@ -263,9 +264,21 @@ class ByolEngine:
 
     # ------------------------------------------------------------------ views
     def group_views(self, flat: torch.Tensor, group: str) -> dict:
+        """name -> view of `flat` for every parameter of `group`. Cached per (buffer object,
+        group): building the encoder's ~400 views costs ~1.5 ms of host time, and the step asks
+        for them five times (both views' master and shadow weights, the gradient), which delayed
+        the enqueue of each step's first kernels. The cache holds the buffer itself and is keyed
+        on its identity, so a replaced buffer (load_state_dict) gets fresh views."""
+        key = (id(flat), group)
+        hit = self._view_cache.get(key)
+        if hit is not None and hit[0] is flat:
+            return hit[1]
         out = {}
         for name, (off, cnt, shp) in self._offsets[group].items():
             out[name] = flat[off:off + cnt].view(shp)
+        if len(self._view_cache) >= 32:   # callers passing transient buffers: stay bounded
+            self._view_cache.clear()
+        self._view_cache[key] = (flat, out)
         return out
 
     def fused(self, flat: torch.Tensor, layer: int, kind: str) -> torch.Tensor:
