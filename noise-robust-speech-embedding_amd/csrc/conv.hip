@@ -28,7 +28,9 @@ NRSE_DEV void load_wT(float* wT, const float* w, int C, int k) {
 
 // conv0 forward: VALU-bound (10-tap conv, LN, GELU per element), so channel pairs run as
 // packed FP32 (v_pk_fma_f32 / v_pk_mul_f32): lane owns 4*NQ channels as 2*NQ pairs.
-template <int NQ>
+// K10: the model's geometry (k = KMAX = 10) as a compile-time constant -- with a runtime k every
+// tap load is conditional, a branch per tap per row
+template <int NQ, bool K10>
 __global__ __launch_bounds__(256) void conv0_fwd_kernel(const nrse_conv0_params p) {
   __shared__ __attribute__((aligned(16))) float wT[KMAX * 512];
   const int lane = threadIdx.x & 63;
@@ -56,7 +58,7 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(const nrse_conv0_params 
     const float* x = p.wav + (long long)b * p.L + (long long)t * p.s;
     float xs[KMAX];
 #pragma unroll
-    for (int j = 0; j < KMAX; ++j) xs[j] = j < p.k ? x[j] : 0.f;
+    for (int j = 0; j < KMAX; ++j) xs[j] = (K10 || j < p.k) ? x[j] : 0.f;
     f32x2 y[NQ][2];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
@@ -131,14 +133,14 @@ struct C0Row {
   bool v0, v1;
 };
 
-template <bool BF>
+template <bool BF, bool K10>
 NRSE_DEV void c0_load(const nrse_conv0_params& p, const UDiv31& dT0, const UDiv31& dS, long long row, int c0,
                       bool col2, C0Row<BF>& r) {
   const long long b = dT0.div((unsigned)row);  // rows < 2^31 (host check)
   const int t = (int)((unsigned)row - (unsigned)b * (unsigned)p.T0);
   const float* x = p.wav + b * p.L + (long long)t * p.s;
 #pragma unroll
-  for (int j = 0; j < KMAX; ++j) r.xs[j] = j < p.k ? ldg(x + j) : 0.f;
+  for (int j = 0; j < KMAX; ++j) r.xs[j] = (K10 || j < p.k) ? ldg(x + j) : 0.f;
   r.mean = ldg(p.mean + row);
   r.rstd = ldg(p.rstd + row);
   long long o0 = row * p.C, o1 = 0;
@@ -190,7 +192,8 @@ NRSE_DEV f32x4 c0_dy_generic(const nrse_conv0_params& p, long long row, int c0) 
   return d;
 }
 
-template <int WPR, bool BF>
+// K10: k = KMAX and a two-tap col2im (col_k <= 2 col_s): unconditional tap loads, no generic fold
+template <int WPR, bool BF, bool K10>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void conv0_bwd_kernel(const nrse_conv0_params p) {
   constexpr int RPB = 4 / WPR;  // rows in flight per block
   __shared__ __attribute__((aligned(16))) float wT[KMAX * 512];
@@ -218,7 +221,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
   const long long first = (long long)blockIdx.x * RPB;
   // uniform trip count over the block (the row exchange is a block barrier)
   const long long iters = first < rows ? (rows - first + stride - 1) / stride : 0;
-  const bool generic = p.dy_mode == NRSE_DY_COL2IM && p.col_k > 2 * p.col_s;
+  const bool generic = !K10 && p.dy_mode == NRSE_DY_COL2IM && p.col_k > 2 * p.col_s;
   UDiv31 dT0, dS;
   dT0.init((unsigned)p.T0);
   dS.init(p.col_s > 0 ? (unsigned)p.col_s : 1u);
@@ -226,7 +229,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
 
   auto step = [&](const C0Row<BF>& cur, C0Row<BF>& nxt, long long it, long long row) {
     const long long rn = row + stride;
-    c0_load<BF>(p, dT0, dS, rn < last ? rn : last, c0, !generic, nxt);
+    c0_load<BF, K10>(p, dT0, dS, rn < last ? rn : last, c0, !generic, nxt);
     __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this row's math
     const bool live = row < rows;
     f32x2 xh[2], g[2];
@@ -292,7 +295,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
 
   C0Row<BF> ra, rb;
   long long row = first + rg;
-  if (iters > 0) c0_load<BF>(p, dT0, dS, row < last ? row : last, c0, !generic, ra);
+  if (iters > 0) c0_load<BF, K10>(p, dT0, dS, row < last ? row : last, c0, !generic, ra);
   for (long long it = 0; it < iters; it += 2) {  // two row buffers, alternated (no copies)
     step(ra, rb, it, row);
     row += stride;
@@ -301,14 +304,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
     row += stride;
   }
   // block reduce: dw (k x C), dgamma, dbeta (the RPB row groups hold disjoint rows)
-  for (int j = 0; j < p.k + 2; ++j) {
+  const int kk = K10 ? KMAX : p.k;
+  for (int j = 0; j < kk + 2; ++j) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       f32x2 v = dbe[h];
 #pragma unroll
       for (int jj = 0; jj < KMAX; ++jj)
         if (jj == j) v = dw[jj][h];
-      if (j == p.k) v = dga[h];
+      if (j == kk) v = dga[h];
       red[rg][c0 + 2 * h] = v.x;
       red[rg][c0 + 2 * h + 1] = v.y;
     }
@@ -317,9 +321,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
       float v = 0.f;
 #pragma unroll
       for (int q = 0; q < RPB; ++q) v += red[q][c];
-      if (p.part) p.part[((long long)blockIdx.x * (p.k + 2) + j) * C + c] = v;  // row [dw | dgamma | dbeta]
-      else if (j < p.k) atomicAdd(p.dw + (long long)j * C + c, v);  // [k][C]: 256-B atomic wave-instructions
-      else if (j == p.k) atomicAdd(p.dgamma + c, v);
+      if (p.part) p.part[((long long)blockIdx.x * (kk + 2) + j) * C + c] = v;  // row [dw | dgamma | dbeta]
+      else if (j < kk) atomicAdd(p.dw + (long long)j * C + c, v);  // [k][C]: 256-B atomic wave-instructions
+      else if (j == kk) atomicAdd(p.dgamma + c, v);
       else atomicAdd(p.dbeta + c, v);
     }
     __syncthreads();
@@ -540,9 +544,16 @@ extern "C" int nrse_conv0_fwd(const nrse_conv0_params* p, void* stream) {
   long long blocks = (rows + 3) / 4;
   if (blocks > 4096) blocks = 4096;
   hipStream_t st = (hipStream_t)stream;
+  const bool k10 = p->k == KMAX;
   switch (p->C) {
-    case 256: hipLaunchKernelGGL(conv0_fwd_kernel<1>, dim3(blocks), dim3(256), 0, st, *p); break;
-    case 512: hipLaunchKernelGGL(conv0_fwd_kernel<2>, dim3(blocks), dim3(256), 0, st, *p); break;
+    case 256:
+      if (k10) hipLaunchKernelGGL((conv0_fwd_kernel<1, true>), dim3(blocks), dim3(256), 0, st, *p);
+      else hipLaunchKernelGGL((conv0_fwd_kernel<1, false>), dim3(blocks), dim3(256), 0, st, *p);
+      break;
+    case 512:
+      if (k10) hipLaunchKernelGGL((conv0_fwd_kernel<2, true>), dim3(blocks), dim3(256), 0, st, *p);
+      else hipLaunchKernelGGL((conv0_fwd_kernel<2, false>), dim3(blocks), dim3(256), 0, st, *p);
+      break;
     default: nrse_set_error("nrse_conv0_fwd: C=%d unsupported", p->C); return NRSE_ERR_UNSUPPORTED;
   }
   return nrse_check_launch("nrse_conv0_fwd");
@@ -567,17 +578,21 @@ extern "C" int nrse_conv0_bwd(const nrse_conv0_params* p, void* stream) {
   const bool bf = p->dy_dtype == NRSE_BF16;
   const long long blocks = conv0_bwd_blocks(p);
   hipStream_t st = (hipStream_t)stream;
+  // the model's geometry (k = 10, two-tap col2im) specialised; anything else takes the generic form
+  const bool k10 = p->k == KMAX && (p->dy_mode != NRSE_DY_COL2IM || p->col_k <= 2 * p->col_s);
+#define NRSE_C0B(W, B, K) hipLaunchKernelGGL((conv0_bwd_kernel<W, B, K>), dim3(blocks), dim3(256), 0, st, *p)
   switch (p->C) {
     case 256:
-      if (bf) hipLaunchKernelGGL((conv0_bwd_kernel<1, true>), dim3(blocks), dim3(256), 0, st, *p);
-      else hipLaunchKernelGGL((conv0_bwd_kernel<1, false>), dim3(blocks), dim3(256), 0, st, *p);
+      if (k10) { if (bf) NRSE_C0B(1, true, true); else NRSE_C0B(1, false, true); }
+      else { if (bf) NRSE_C0B(1, true, false); else NRSE_C0B(1, false, false); }
       break;
     case 512:  // 2 waves per row
-      if (bf) hipLaunchKernelGGL((conv0_bwd_kernel<2, true>), dim3(blocks), dim3(256), 0, st, *p);
-      else hipLaunchKernelGGL((conv0_bwd_kernel<2, false>), dim3(blocks), dim3(256), 0, st, *p);
+      if (k10) { if (bf) NRSE_C0B(2, true, true); else NRSE_C0B(2, false, true); }
+      else { if (bf) NRSE_C0B(2, true, false); else NRSE_C0B(2, false, false); }
       break;
     default: nrse_set_error("nrse_conv0_bwd: C=%d unsupported", p->C); return NRSE_ERR_UNSUPPORTED;
   }
+#undef NRSE_C0B
   const int rc = nrse_check_launch("nrse_conv0_bwd");
   if (rc || !p->part) return rc;
   return nrse_rows_reduce(p->dw, (long long)p->k * p->C, p->dgamma, p->C, p->dbeta, p->C, p->part, (int)blocks, 1, 1,

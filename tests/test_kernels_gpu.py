@@ -111,11 +111,13 @@ def test_layernorm_bwd_col2im_and_bcast(nrse_device, C, k, s):
     assert rel(dx, xr.grad) < 1e-6
 
 
-@pytest.mark.parametrize("C", [256, 512])
-def test_conv0_fwd_bwd(nrse_device, C):
+@pytest.mark.parametrize("C,k", [(256, 10), (512, 10), (512, 8)])
+def test_conv0_fwd_bwd(nrse_device, C, k):
+    """conv0 + LN + GELU forward / backward against float64 autograd: the model's k = 10 (the
+    compile-time-geometry kernels) and k = 8 (the runtime-k form)."""
     from nrse_amd import kernels as K
     dev = nrse_device
-    B, L, k, s = 2, 4001, 10, 5
+    B, L, s = 2, 4001, 5
     T0 = (L - k) // s + 1
     wav = torch.randn(B, L, device=dev)
     w = torch.randn(C, 1, k, device=dev) * 0.3
