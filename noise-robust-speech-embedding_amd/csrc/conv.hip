@@ -6,9 +6,18 @@
 // conv0 has K = 10: vector-ALU work, HBM-bound on its [B*T0, C] output (the largest activation
 // of the step). One wave per output row; the [k][C] weight is held in LDS (read as float4 per
 // tap), lane owns 4*NQ channels.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
+
+// NRSE_CONV0_MFMA=0 keeps the VALU forward for bf16 outputs too (A/B measurements)
+bool conv0_mfma_on() {
+  static int v = -1;
+  if (v < 0) v = getenv("NRSE_CONV0_MFMA") ? atoi(getenv("NRSE_CONV0_MFMA")) : 1;
+  return v != 0;
+}
 
 constexpr int KMAX = 10;
 
@@ -94,6 +103,155 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(const nrse_conv0_params 
       store4_out(p.out, p.out_dtype, off, rows * C, ov);
     }
     if (lane == 0) {
+      p.mean[row] = mean;
+      p.rstd[row] = rstd;
+    }
+  }
+}
+
+// conv0 forward on the matrix cores, for bf16 and split-bf16 (NRSE_BF16X3) outputs at k = 10:
+// one wave = 16 rows x C channels per step. The 10-tap contraction is an MFMA 16x16x32 bf16 per
+// 16-channel block with both operands split into bf16 hi + lo parts packed along K,
+//   K = [x_hi . w_hi | x_lo . w_hi | x_hi . w_lo | 0 0]   (3 x 10 products, relative error ~2^-16),
+// X3 adds x_lo . w_lo in a second MFMA (the three-plane output carries ~16 bits). The product is
+// formed transposed (D = W'^T X'^T), so lane (g, l) holds row l of the block and, in channel
+// block n, channels ch(n, 4g + r) = 32 (n >> 1) + 8 g + 4 (n & 1) + r: the row's LayerNorm sums
+// are lane-local over 4 C / 16 values plus two lane swaps (the VALU kernel above paid two wave
+// reductions per row), and each lane stores 8 consecutive channels (16 B) per block pair. The
+// weight fragments live in LDS in fragment order (one conflict-free ds_read_b128 per block).
+// Exact f32 outputs (the parity mode) keep conv0_fwd_kernel.
+template <int NB, bool X3>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void conv0_fwd_mfma_kernel(
+    const nrse_conv0_params p) {
+  constexpr int C = NB * 16, NF = X3 ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) bf16x8 wimg[NF * NB * 64];
+  __shared__ __attribute__((aligned(16))) float gb[2 * C];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int g = lane >> 4, l = lane & 15;
+  // weight fragments: fragment m, block n, lane (g', l') holds W'[k = 8 g' + e][ch(n, l')]
+  for (int idx = tid; idx < NF * NB * 64; idx += 256) {
+    const int m = idx / (NB * 64), rem = idx - m * (NB * 64);
+    const int n = rem >> 6, gg = (rem >> 4) & 3, ll = rem & 15;
+    const int ch = 32 * (n >> 1) + 8 * (ll >> 2) + 4 * (n & 1) + (ll & 3);
+    bf16x8 v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = 8 * gg + e;
+      float wv = 0.f;
+      if (m == 0 && k < 30) {
+        const float w = p.w[ch * KMAX + k % 10];
+        const float hi = bf2f(f2bf(w));
+        wv = k < 20 ? hi : w - hi;  // [w_hi | w_hi | w_lo]; w_lo rounds to bf16 below
+      } else if (m == 1 && k < 10) {
+        const float w = p.w[ch * KMAX + k];
+        wv = w - bf2f(f2bf(w));
+      }
+      v[e] = (__bf16)wv;
+    }
+    wimg[idx] = v;
+  }
+  for (int c = tid; c < C; c += 256) {
+    gb[c] = p.gamma[c];
+    gb[C + c] = p.beta[c];
+  }
+  __syncthreads();
+
+  // this lane's K positions: element e is k = 8g + e -> tap k % 10, part k / 10 (0 hi, 1 lo, 2 hi, 3 zero)
+  int tap[8], part[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int k = 8 * g + e;
+    tap[e] = k < 30 ? k % 10 : 0;
+    part[e] = k / 10;
+  }
+  const long long rows = (long long)p.batch * p.T0;
+  const long long nblk = (rows + 15) >> 4;
+  const long long wstride = (long long)gridDim.x * 4;
+  UDiv31 dT0;
+  dT0.init((unsigned)p.T0);
+  const float invC = 1.f / C;
+  auto load_x = [&](long long blk, float (&xs)[8]) {
+    long long row = blk * 16 + l;
+    row = row < rows ? row : rows - 1;
+    const unsigned b = dT0.div((unsigned)row);
+    const int t = (int)((unsigned)row - b * (unsigned)p.T0);
+    const float* x = p.wav + (long long)b * p.L + (long long)t * p.s;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) xs[e] = ldg(x + tap[e]);
+  };
+  long long blk = (long long)blockIdx.x * 4 + (tid >> 6);
+  float xn[8];
+  if (blk < nblk) load_x(blk, xn);
+  for (; blk < nblk; blk += wstride) {
+    bf16x8 xf, xf2;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float hi = bf2f(f2bf(xn[e]));
+      const float lo = xn[e] - hi;
+      xf[e] = (__bf16)(part[e] == 1 ? lo : (part[e] == 3 ? 0.f : hi));
+      xf2[e] = (__bf16)(8 * g + e < 10 ? lo : 0.f);
+    }
+    if (blk + wstride < nblk) load_x(blk + wstride, xn);  // next block's samples in flight
+    f32x4 acc[NB];
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wimg[n * 64 + lane], xf, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      if constexpr (X3) acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wimg[(NB + n) * 64 + lane], xf2, acc[n], 0, 0, 0);
+    }
+    // LayerNorm over the row's C channels: this lane's 4 NB values + the lanes l ^ 16, l ^ 32
+    f32x2 s2 = f32x2{0.f, 0.f};
+#pragma unroll
+    for (int n = 0; n < NB; ++n) s2 += f32x2{acc[n][0], acc[n][1]} + f32x2{acc[n][2], acc[n][3]};
+    const float mean = xor32_sum(xor16_sum(s2.x + s2.y)) * invC;
+    f32x2 v2 = f32x2{0.f, 0.f};
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      const f32x2 d0 = f32x2{acc[n][0], acc[n][1]} - mean, d1 = f32x2{acc[n][2], acc[n][3]} - mean;
+      acc[n] = f32x4{d0.x, d0.y, d1.x, d1.y};
+      v2 = pk_fma(d0, d0, pk_fma(d1, d1, v2));
+    }
+    const float rstd = rsqrtf(xor32_sum(xor16_sum(v2.x + v2.y)) * invC + p.eps);
+    const long long row = blk * 16 + l;
+    const bool ok = row < rows;
+    const f32x2 rs2 = f32x2{rstd, rstd};
+#pragma unroll
+    for (int q = 0; q < NB / 2; ++q) {
+      const int c0 = 32 * q + 8 * g;
+      float o[8];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const float4 ga = *reinterpret_cast<const float4*>(gb + c0 + 4 * h);
+        const float4 be = *reinterpret_cast<const float4*>(gb + C + c0 + 4 * h);
+        const f32x4 a = acc[2 * q + h];
+        const f32x2 z0 = pk_fma(f32x2{a[0], a[1]} * rs2, f32x2{ga.x, ga.y}, f32x2{be.x, be.y});
+        const f32x2 z1 = pk_fma(f32x2{a[2], a[3]} * rs2, f32x2{ga.z, ga.w}, f32x2{be.z, be.w});
+        const f32x2 y0 = gelu2(z0), y1 = gelu2(z1);
+        o[4 * h + 0] = y0.x; o[4 * h + 1] = y0.y; o[4 * h + 2] = y1.x; o[4 * h + 3] = y1.y;
+      }
+      uint4 u;
+      u.x = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
+      u.y = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
+      u.z = (uint32_t)f2bf(o[4]) | ((uint32_t)f2bf(o[5]) << 16);
+      u.w = (uint32_t)f2bf(o[6]) | ((uint32_t)f2bf(o[7]) << 16);
+      bf16_t* dst = (bf16_t*)p.out + row * C + c0;
+      if (ok) {
+        *reinterpret_cast<uint4*>(dst) = u;
+        if constexpr (X3) {
+          const unsigned uw[4] = {u.x, u.y, u.z, u.w};
+          unsigned lw[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            lw[e] = (uint32_t)f2bf(o[2 * e] - __uint_as_float(uw[e] << 16)) |
+                    ((uint32_t)f2bf(o[2 * e + 1] - __uint_as_float(uw[e] & 0xffff0000u)) << 16);
+          *reinterpret_cast<uint4*>(dst + rows * C) = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+          *reinterpret_cast<uint4*>(dst + 2 * rows * C) = u;
+        }
+      }
+      // one block pair at a time: hoisting every pair's gamma / beta reads to the top of the
+      // loop (what the scheduler does otherwise) spilled the accumulators
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (g == 0 && ok) {
       p.mean[row] = mean;
       p.rstd[row] = rstd;
     }
@@ -545,6 +703,21 @@ extern "C" int nrse_conv0_fwd(const nrse_conv0_params* p, void* stream) {
   if (blocks > 4096) blocks = 4096;
   hipStream_t st = (hipStream_t)stream;
   const bool k10 = p->k == KMAX;
+  if (k10 && p->out_dtype != NRSE_F32 && (p->C == 512 || p->C == 256) && conv0_mfma_on()) {
+    // matrix-core form (bf16 / split-bf16 outputs): 2 workgroups per CU, waves loop over 16-row blocks
+    const long long nblk = (rows + 15) / 16;
+    long long wg = (nblk + 3) / 4;
+    if (wg > 1024) wg = 1024;
+    const bool x3 = p->out_dtype == NRSE_BF16X3;
+    if (p->C == 512) {
+      if (x3) hipLaunchKernelGGL((conv0_fwd_mfma_kernel<32, true>), dim3(wg), dim3(256), 0, st, *p);
+      else hipLaunchKernelGGL((conv0_fwd_mfma_kernel<32, false>), dim3(wg), dim3(256), 0, st, *p);
+    } else {
+      if (x3) hipLaunchKernelGGL((conv0_fwd_mfma_kernel<16, true>), dim3(wg), dim3(256), 0, st, *p);
+      else hipLaunchKernelGGL((conv0_fwd_mfma_kernel<16, false>), dim3(wg), dim3(256), 0, st, *p);
+    }
+    return nrse_check_launch("nrse_conv0_fwd");
+  }
   switch (p->C) {
     case 256:
       if (k10) hipLaunchKernelGGL((conv0_fwd_kernel<1, true>), dim3(blocks), dim3(256), 0, st, *p);

@@ -173,7 +173,10 @@ NRSE_DEV void ld_issue(const Ld& o, char* dst, int wave, int hh, unsigned soff, 
 // one per M-half mh of both M-waves (128 image rows; an f32 image is 130 KB, a bf16 one leaves
 // room for the pre-activation image). The dropout mask index is the general epilogue's.
 // Other flag sets (atomic, accumulate, ReLU, tanh, f32 aux, ...) take the general epilogue.
-enum : int { FE_BIAS = 1, FE_GELU = 2, FE_GELUB = 4, FE_DROP = 8, FE_RESID = 16, FE_OBF = 32, FE_RBF = 64 };
+// FE_NOAUX: GELU without the pre-activation image (the target view's FFN-up keeps no tape; it
+// had fallen to the general epilogue's four f32 passes)
+enum : int { FE_BIAS = 1, FE_GELU = 2, FE_GELUB = 4, FE_DROP = 8, FE_RESID = 16, FE_OBF = 32, FE_RBF = 64,
+             FE_NOAUX = 128 };
 
 // compile-time mode of the flag set, or -1 (general epilogue)
 NRSE_DEV int fast_epi_mode(const nrse_gemm_params& p) {
@@ -183,7 +186,9 @@ NRSE_DEV int fast_epi_mode(const nrse_gemm_params& p) {
   int m = 0;
   if (f & NRSE_EPI_BIAS) m |= FE_BIAS;
   if (f & NRSE_EPI_GELU) {
-    if (!p.aux || p.aux_dtype != NRSE_BF16 || p.c_dtype != NRSE_BF16) return -1;
+    if (p.c_dtype != NRSE_BF16) return -1;
+    if (!p.aux) m |= FE_NOAUX;
+    else if (p.aux_dtype != NRSE_BF16) return -1;
     m |= FE_GELU;
   }
   if (f & NRSE_EPI_GELU_BWD) {
@@ -205,6 +210,7 @@ NRSE_DEV void fast_epilogue(const nrse_gemm_params& p, const f32x4 (&acc)[8][4],
                             const float4 (&bpre)[4], int z, int mt) {
   constexpr bool BIAS = FE & FE_BIAS, GELU = FE & FE_GELU, GELUB = FE & FE_GELUB, DROP = FE & FE_DROP;
   constexpr bool RESID = FE & FE_RESID, OBF = FE & FE_OBF;
+  constexpr bool GAUX = GELU && !(FE & FE_NOAUX);  // pre-activation image + stores
   constexpr int NFI_HI = (BMT / 2 - 64) / 16;
   constexpr int ES = OBF ? 2 : 4;
   constexpr int PITCH = 256 * ES + 16;               // image row pitch (bytes), bank-spread
@@ -244,10 +250,12 @@ NRSE_DEV void fast_epilogue(const nrse_gemm_params& p, const f32x4 (&acc)[8][4],
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = fmaf(acc[a][fn][e], p.alpha, BIAS ? bias4[fn][e] : 0.f);
         if constexpr (GELU) {
-          uint2 u;
-          u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-          u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-          *reinterpret_cast<uint2*>(aimg + prow * APITCH + tcol * 2) = u;
+          if constexpr (GAUX) {
+            uint2 u;
+            u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+            u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+            *reinterpret_cast<uint2*>(aimg + prow * APITCH + tcol * 2) = u;
+          }
           {  // packed FP32 pairs (FFN-up 773-775 -> 781-789 TF isolated; step neutral)
             const f32x2 g0 = gelu2(f32x2{v[0], v[1]}), g1 = gelu2(f32x2{v[2], v[3]});
             v[0] = g0.x; v[1] = g0.y; v[2] = g1.x; v[3] = g1.y;
@@ -321,7 +329,7 @@ NRSE_DEV void fast_epilogue(const nrse_gemm_params& p, const f32x4 (&acc)[8][4],
       if (m >= p.M || n >= p.N) continue;
       const uint4 u = *reinterpret_cast<const uint4*>(oimg + prow * PITCH + ch * 16);
       *reinterpret_cast<uint4*>((char*)p.c + (epi.cbase + (long long)m * p.ldc + n) * ES) = u;
-      if constexpr (GELU) {
+      if constexpr (GAUX) {
         const uint4 w = *reinterpret_cast<const uint4*>(aimg + prow * APITCH + ch * 16);
         *reinterpret_cast<uint4*>((bf16_t*)p.aux + epi.abase + (long long)m * p.ldaux + n) = w;
       }
@@ -541,6 +549,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
         NRSE_FE(FE_OBF | FE_BIAS)
         NRSE_FE(FE_BIAS)
         NRSE_FE(FE_OBF | FE_BIAS | FE_GELU)
+        NRSE_FE(FE_OBF | FE_BIAS | FE_GELU | FE_NOAUX)
+        NRSE_FE(FE_BIAS | FE_DROP)
         NRSE_FE(FE_BIAS | FE_RESID)
         NRSE_FE(FE_BIAS | FE_RESID | FE_DROP)
         default: break;
@@ -551,6 +561,14 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
         NRSE_FE(0)
         NRSE_FE(FE_OBF | FE_GELUB)
         NRSE_FE(FE_OBF | FE_GELUB | FE_DROP)
+        default: break;
+      }
+    } else {
+      // weight gradients (both operands row-contiguous): plain f32 slab / bf16 stores; they had
+      // taken the general epilogue's four LDS passes
+      switch (fe) {
+        NRSE_FE(0)
+        NRSE_FE(FE_OBF)
         default: break;
       }
     }

@@ -358,3 +358,44 @@ def test_conv_gemm_split_activations(nrse_device):
            nseg=3)
     ref = torch.nn.functional.conv1d(x.double().transpose(1, 2), w.double(), stride=s).transpose(1, 2).reshape(-1, C)
     assert rel(y, ref) < 2e-5
+
+
+@pytest.mark.parametrize("shape", [(12768, 4096, 1024), (300, 256, 128)])
+def test_gelu_without_preactivation_matches(nrse_device, shape):
+    """The FFN-up epilogue without a pre-activation output (the target view keeps no tape) gives
+    the same bf16 output as the taped form, bit for bit, and the taped pre-activation matches
+    float64."""
+    from nrse_amd import kernels as K, _lib
+    M, N, Kd = shape
+    dev = nrse_device
+    x = torch.randn(M, Kd, device=dev).to(torch.bfloat16)
+    w = (torch.randn(N, Kd, device=dev) * 0.05).to(torch.bfloat16)
+    b = torch.randn(N, device=dev)
+    pre = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    y1 = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    y2 = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    K.linear_fwd(x, w, y1, bias=b, flags=_lib.EPI_GELU, aux=pre, ldaux=N)
+    K.linear_fwd(x, w, y2, bias=b, flags=_lib.EPI_GELU)
+    assert torch.equal(y1, y2)
+    ref_pre = x.double() @ w.double().t() + b.double()
+    assert rel(pre, ref_pre) < 5e-3
+    assert rel(y2, torch.nn.functional.gelu(ref_pre)) < 5e-3
+
+
+def test_bias_dropout_f32_matches_residual_form(nrse_device):
+    """bias + dropout with an f32 output (the feature projection) equals the bias + dropout +
+    residual form with a zero residual, bit for bit (same keep mask, same rounding)."""
+    from nrse_amd import kernels as K
+    M, N, Kd = 12768, 1024, 512
+    dev = nrse_device
+    x = torch.randn(M, Kd, device=dev).to(torch.bfloat16)
+    w = (torch.randn(N, Kd, device=dev) * 0.05).to(torch.bfloat16)
+    b = torch.randn(N, device=dev)
+    zero = torch.zeros(M, N, device=dev)
+    y1 = torch.empty(M, N, device=dev)
+    y2 = torch.empty(M, N, device=dev)
+    K.linear_fwd(x, w, y1, bias=b, dropout_p=0.1, seed=7)
+    K.linear_fwd(x, w, y2, bias=b, resid=zero, ldr=N, dropout_p=0.1, seed=7)
+    assert torch.equal(y1, y2)
+    kept = (y1 != 0).float().mean().item()
+    assert abs(kept - 0.9) < 0.01

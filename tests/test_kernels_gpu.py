@@ -137,6 +137,36 @@ def test_conv0_fwd_bwd(nrse_device, C, k):
     assert rel(dg, gr.grad) < 1e-5 and rel(db, br.grad) < 1e-5
 
 
+@pytest.mark.parametrize("C", [512, 256])
+@pytest.mark.parametrize("split3", [False, True])
+def test_conv0_fwd_mfma_bf16_outputs(nrse_device, C, split3):
+    """conv0 forward with bf16 / split-bf16 outputs (the matrix-core kernel: split-bf16 operands,
+    transposed product) against float64: the output within its storage precision, mean / rstd
+    within the split contraction's ~2^-16."""
+    from nrse_amd import kernels as K
+    dev = nrse_device
+    B, L, k, s = 3, 8001, 10, 5
+    T0 = (L - k) // s + 1  # 1599 rows per utterance: the last 16-row block is partial
+    wav = torch.randn(B, L, device=dev) * 0.2
+    w = torch.randn(C, 1, k, device=dev) * 0.3
+    g = torch.randn(C, device=dev) * 0.1 + 1; b = torch.randn(C, device=dev) * 0.1
+    rows = B * T0
+    out = torch.empty((3, rows, C) if split3 else (rows, C), device=dev, dtype=torch.bfloat16)
+    mean = torch.empty(rows, device=dev); rstd = torch.empty_like(mean)
+    K.conv0_fwd(wav, w.view(C, k), g, b, out, mean, rstd, T0, k, s, 1e-5, split3=split3)
+    y = F.conv1d(wav.double()[:, None], w.double(), stride=s).transpose(1, 2).reshape(rows, C)
+    mu = y.mean(1); var = y.var(1, unbiased=False)
+    ref = F.gelu((y - mu[:, None]) / torch.sqrt(var[:, None] + 1e-5) * g.double() + b.double())
+    assert rel(mean, mu) < 1e-5
+    assert rel(rstd, 1 / torch.sqrt(var + 1e-5)) < 1e-5
+    if split3:
+        assert torch.equal(out[0], out[2])
+        got = out[0].double() + out[1].double()
+        assert rel(got, ref) < 5e-5
+    else:
+        assert rel(out, ref) < 4e-3
+
+
 @pytest.mark.parametrize("C,ck,cs,dt", [(512, 3, 2, torch.bfloat16), (512, 2, 2, torch.float32),
                                          (256, 3, 2, torch.float32), (512, 4, 1, torch.float32)])
 def test_conv0_bwd_col2im(nrse_device, C, ck, cs, dt):

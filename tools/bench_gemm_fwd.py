@@ -25,8 +25,12 @@ def timeit(fn, iters=20):
 
 M = int(os.environ.get("M", 12768))
 gens = [int(g) for g in os.environ.get("GENS", "0").split(",")]
-for name, N, Kd, epi in (("qkv", 3072, 1024, "bias"), ("out", 1024, 1024, "resid"), ("ffn1", 4096, 1024, "gelu"),
-                         ("ffn2", 1024, 4096, "resid")):
+SHAPES = (("qkv", 3072, 1024, "bias"), ("out", 1024, 1024, "resid"), ("ffn1", 4096, 1024, "gelu"),
+          ("ffn2", 1024, 4096, "resid"), ("ffn1t", 4096, 1024, "gelu_noaux"), ("fproj", 1024, 512, "bias_drop"))
+only = os.environ.get("SHAPES")
+for name, N, Kd, epi in SHAPES:
+    if only and name not in only.split(","):
+        continue
     x = torch.randn(M, Kd, device=dev).to(torch.bfloat16)
     w = (torch.randn(N, Kd, device=dev) * 0.05).to(torch.bfloat16)
     b = torch.randn(N, device=dev)
@@ -41,6 +45,12 @@ for name, N, Kd, epi in (("qkv", 3072, 1024, "bias"), ("out", 1024, 1024, "resid
         if epi == "gelu":
             y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
             return lambda: K.linear_fwd(x, w, y, bias=b, flags=_lib.EPI_GELU, aux=pre, ldaux=N), y
+        if epi == "gelu_noaux":  # the target view's FFN-up (no tape)
+            y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            return lambda: K.linear_fwd(x, w, y, bias=b, flags=_lib.EPI_GELU), y
+        if epi == "bias_drop":  # the feature projection (f32 out)
+            y = torch.empty(M, N, device=dev)
+            return lambda: K.linear_fwd(x, w, y, bias=b, dropout_p=0.1, seed=5), y
         y = torch.empty(M, N, device=dev)
         return lambda: K.linear_fwd(x, w, y, bias=b, flags=_lib.EPI_RESID, resid=r, ldr=N, dropout_p=0.1,
                                     seed=5), y

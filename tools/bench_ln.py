@@ -69,6 +69,10 @@ o0 = torch.empty(32 * T0, 512, device=dev, dtype=torch.bfloat16)
 m0 = torch.empty(32 * T0, device=dev); r0 = torch.empty(32 * T0, device=dev)
 us = timeit(lambda: K.conv0_fwd(wav, w0, g0, b0, o0, m0, r0, T0, 10, 5, 1e-5), iters=10)
 print(f"conv0 fwd 819168x512 (bf16 out): {us:.1f} us  {32 * T0 * 512 * 2 / us / 1e3:.0f} GB/s", flush=True)
+o3 = torch.empty(3, 32 * T0, 512, device=dev, dtype=torch.bfloat16)
+us = timeit(lambda: K.conv0_fwd(wav, w0, g0, b0, o3, m0, r0, T0, 10, 5, 1e-5, split3=True), iters=10)
+print(f"conv0 fwd 819168x512 (bf16x3 out): {us:.1f} us  {3 * 32 * T0 * 512 * 2 / us / 1e3:.0f} GB/s", flush=True)
+del o3
 col0 = torch.randn(32 * Tin, 3 * 512, device=dev).to(torch.bfloat16)
 dw0 = torch.zeros(512, 10, device=dev); dg0 = torch.zeros(512, device=dev); db0 = torch.zeros(512, device=dev)
 us = timeit(lambda: K.conv0_bwd(wav, w0, g0, b0, m0, r0, col0, dw0, dg0, db0, T0, 10, 5, (3, 2, Tin)), iters=10)
