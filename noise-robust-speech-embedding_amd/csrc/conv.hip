@@ -469,7 +469,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
       f32x2 v = dbe[h];
 #pragma unroll
       for (int jj = 0; jj < KMAX; ++jj)
-        if (jj == j) v = dw[jj][h];
+        if (jj == j && jj < kk) v = dw[jj][h];  // rows kk, kk + 1 are dgamma, dbeta
       if (j == kk) v = dga[h];
       red[rg][c0 + 2 * h] = v.x;
       red[rg][c0 + 2 * h + 1] = v.y;

@@ -563,15 +563,10 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
         NRSE_FE(FE_OBF | FE_GELUB | FE_DROP)
         default: break;
       }
-    } else {
-      // weight gradients (both operands row-contiguous): plain f32 slab / bf16 stores; they had
-      // taken the general epilogue's four LDS passes
-      switch (fe) {
-        NRSE_FE(0)
-        NRSE_FE(FE_OBF)
-        default: break;
-      }
     }
+    // (the weight gradients, both operands row-contiguous, keep the general epilogue: its 1-KB
+    // row sweeps of the f32 slab measured 1-3 % faster than the register form's 64-B row pieces,
+    // r04 same box: qkv / out / ffn1 / ffn2 wgrad 722 / 476 / 722 / 706 vs 709 / 461 / 714 / 685 TF)
 #undef NRSE_FE
   }
 
