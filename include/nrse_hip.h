@@ -177,6 +177,12 @@ typedef struct {
   /* optional f32 workspace of nrse_layernorm_bwd_workspace(p) floats: the column sums (dgamma,
    * dbeta, dv_colsum) are then added in a fixed order (deterministic) instead of by f32 atomics */
   float* part;
+  /* optional (the encoder form: resid given, x / dy / resid f32, dy direct): the gated rel-pos
+   * attention's gate-path gradient added to dy on the fly, so nrse_gate_bwd_dp need not
+   * read-modify-write the LN1 gradient: dy[r, 64 h + d] += gate_dp[r, h, 0] * sum_{i<4} gate_w[i, d]
+   * + gate_dp[r, h, 1] * sum_{i>=4} gate_w[i, d]; gate_dp [rows, C / 64, 2] f32 (8-byte aligned),
+   * gate_w [8, 64] (gru_rel_pos_linear.weight, [TF]modeling_wavlm.py:164-176) */
+  const float* gate_dp; const float* gate_w;
 } nrse_ln_bwd_params;
 
 int nrse_layernorm_fwd(const nrse_ln_fwd_params* p, void* stream);
@@ -221,6 +227,11 @@ int nrse_gate_fwd(const void* x1, int x_dtype, const float* W, const float* bvec
  * bias), dc [H] (gru_rel_pos_const). x1, dx1 16-byte aligned. */
 int nrse_gate_bwd(const void* x1, int x_dtype, const float* W, const float* bvec, const float* c, const float* dgate,
                   float* dx1, float* dW, float* db, float* dc, int batch, int T, int H, float* part, void* stream);
+/* The same with the gate-path gradient left for the LN backward to add (nrse_ln_bwd_params.gate_dp):
+ * dp [B*T, H, 2] f32 receives (dpa, dpb) per (row, head); dx1 is not touched. */
+int nrse_gate_bwd_dp(const void* x1, int x_dtype, const float* W, const float* bvec, const float* c,
+                     const float* dgate, float* dp, float* dW, float* db, float* dc, int batch, int T, int H,
+                     float* part, void* stream);
 /* part (optional): f32 workspace of nrse_gate_bwd_workspace(H) floats; the per-workgroup
  * parameter gradients are then added in a fixed order (deterministic) instead of by atomics */
 long long nrse_gate_bwd_workspace(int H);

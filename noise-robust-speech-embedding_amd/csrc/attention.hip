@@ -139,9 +139,12 @@ __global__ __launch_bounds__(256) void gate_fwd_kernel(const void* __restrict__ 
 //   dc[h] += sum_{n of head h} dgate * a * b.
 // The grid is a multiple of H workgroups, so the item stride (8 per wave per step) is a
 // multiple of H and every 8-lane group keeps one head for the whole loop.
+// DP (nrse_gate_bwd_dp): instead of the dx1 read-modify-write (104 MB per layer at WavLM-Large),
+// store the item's (dpa, dpb) to dp[n] (float2); the encoder LayerNorm backward that reads dx1
+// next adds dpa * wa + dpb * wb itself (nrse_ln_bwd_params.gate_dp).
 constexpr int GATE_BWD_BLOCKS_PER_HEAD = 16;
 constexpr int GATE_BU = 4;
-template <typename T>
+template <typename T, bool DP>
 __global__ __launch_bounds__(256) void gate_bwd_kernel(const void* __restrict__ x1, const float* __restrict__ W,
                                                        const float* __restrict__ bv, const float* __restrict__ c,
                                                        const float* __restrict__ dgate, float* __restrict__ dx1,
@@ -175,9 +178,11 @@ __global__ __launch_bounds__(256) void gate_bwd_kernel(const void* __restrict__ 
       const int row = nc / H;
       const int bi = row / Tn, t = row - bi * Tn;
       dgv[j] = dgate[((long long)bi * H + h) * Tn + t];
-      const float4* d = reinterpret_cast<const float4*>(dx1 + (long long)nc * HD + 8 * sub);
-      du[j] = d[0];
-      dw[j] = d[1];
+      if constexpr (!DP) {
+        const float4* d = reinterpret_cast<const float4*>(dx1 + (long long)nc * HD + 8 * sub);
+        du[j] = d[0];
+        dw[j] = d[1];
+      }
     }
 #pragma unroll
     for (int j = 0; j < GATE_BU; ++j) {
@@ -188,7 +193,9 @@ __global__ __launch_bounds__(256) void gate_bwd_kernel(const void* __restrict__ 
       const float dg = ok ? dgv[j] : 0.f;
       const float dpa = dg * (b * ch - 1.f) * a * (1.f - a);
       const float dpb = dg * a * ch * b * (1.f - b);
-      if (ok) {
+      if constexpr (DP) {
+        if (ok && sub == 0) *reinterpret_cast<float2*>(dx1 + 2LL * n) = make_float2(dpa, dpb);
+      } else if (ok) {
         float4 u = du[j], v = dw[j];
         u.x += dpa * gw.wa[0] + dpb * gw.wb[0]; u.y += dpa * gw.wa[1] + dpb * gw.wb[1];
         u.z += dpa * gw.wa[2] + dpb * gw.wb[2]; u.w += dpa * gw.wa[3] + dpb * gw.wb[3];
@@ -566,12 +573,33 @@ extern "C" int nrse_gate_bwd(const void* x1, int x_dtype, const float* W, const 
   NRSE_REQUIRE(!part || H <= 256 - 2 * HD - 8, "nrse_gate_bwd: H too large for the partial-row form");
   dim3 grid((unsigned)(gate_bwd_bph() * H));
   if (x_dtype == NRSE_BF16)
-    hipLaunchKernelGGL(gate_bwd_kernel<bf16_t>, grid, dim3(256), 0, st, x1, W, bvec, c, dgate, dx1, dW, db, dc, batch,
-                       T, H, part);
+    hipLaunchKernelGGL((gate_bwd_kernel<bf16_t, false>), grid, dim3(256), 0, st, x1, W, bvec, c, dgate, dx1, dW, db, dc,
+                       batch, T, H, part);
   else
-    hipLaunchKernelGGL(gate_bwd_kernel<float>, grid, dim3(256), 0, st, x1, W, bvec, c, dgate, dx1, dW, db, dc, batch,
-                       T, H, part);
+    hipLaunchKernelGGL((gate_bwd_kernel<float, false>), grid, dim3(256), 0, st, x1, W, bvec, c, dgate, dx1, dW, db, dc,
+                       batch, T, H, part);
   const int rc = nrse_check_launch("nrse_gate_bwd");
+  if (rc || !part) return rc;
+  return nrse_rows_reduce(dW, 8 * HD, db, 8, dc, H, part, (int)grid.x, 1, 1, st);
+}
+
+extern "C" int nrse_gate_bwd_dp(const void* x1, int x_dtype, const float* W, const float* bvec, const float* c,
+                                const float* dgate, float* dp, float* dW, float* db, float* dc, int batch, int T, int H,
+                                float* part, void* stream) {
+  NRSE_REQUIRE(x1 && W && bvec && c && dgate && dp && dW && db && dc && batch > 0 && T > 0 && H > 0,
+               "nrse_gate_bwd_dp: bad args");
+  NRSE_REQUIRE(((uintptr_t)x1 & 15) == 0 && ((uintptr_t)dp & 7) == 0, "nrse_gate_bwd_dp: x1 / dp misaligned");
+  NRSE_REQUIRE((long long)batch * T * H < (1LL << 31) - (1LL << 24), "nrse_gate_bwd_dp: too many items");
+  NRSE_REQUIRE(!part || H <= 256 - 2 * HD - 8, "nrse_gate_bwd_dp: H too large for the partial-row form");
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid((unsigned)(gate_bwd_bph() * H));
+  if (x_dtype == NRSE_BF16)
+    hipLaunchKernelGGL((gate_bwd_kernel<bf16_t, true>), grid, dim3(256), 0, st, x1, W, bvec, c, dgate, dp, dW, db, dc,
+                       batch, T, H, part);
+  else
+    hipLaunchKernelGGL((gate_bwd_kernel<float, true>), grid, dim3(256), 0, st, x1, W, bvec, c, dgate, dp, dW, db, dc,
+                       batch, T, H, part);
+  const int rc = nrse_check_launch("nrse_gate_bwd_dp");
   if (rc || !part) return rc;
   return nrse_rows_reduce(dW, 8 * HD, db, 8, dc, H, part, (int)grid.x, 1, 1, st);
 }

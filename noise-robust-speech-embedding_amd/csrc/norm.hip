@@ -253,6 +253,7 @@ template <int NK, bool RES, bool COL, bool BF>
 struct LnRow {
   float x[BF ? 1 : NK][CH], dy[BF ? 1 : NK][CH], r[RES ? NK : 1][CH], dy2[COL && !BF ? NK : 1][CH];
   uint2 xr[BF ? NK : 1], dyr[BF ? NK : 1], dy2r[COL && BF ? NK : 1];
+  float gd[RES ? NK : 1][2];  // GT: the row's gate-path (dpa, dpb) of this lane's head per k
   float mean, rstd;
   bool v0, v1;  // BF: col2im taps present (their loads are issued regardless, from a valid address)
 };
@@ -280,11 +281,21 @@ NRSE_DEV void col_taps(const nrse_ln_bwd_params& p, const ColDiv& cd, long long 
 
 // FD (encoder form, RES): x, dy and the residual all f32, dy direct: three unconditional 16-B
 // loads per word, no dtype / mode branches (each of which had made the compiler wait for the load)
-template <int NK, bool RES, bool COL, bool BF, bool FD>
+template <int NK, bool RES, bool COL, bool BF, bool FD, bool GT>
 NRSE_DEV void ln_bwd_load(const nrse_ln_bwd_params& p, const ColDiv& cd, long long row, int lane,
                           LnRow<NK, RES, COL, BF>& b) {
   b.mean = p.mean[row];
   b.rstd = p.rstd[row];
+  if constexpr (GT) {
+    // head of channel (k * 64 + lane) * CH: 4k + lane / 16 of the row's C / 64
+    const float* gp = p.gate_dp + (row * (p.C >> 6) + (lane >> 4)) * 2;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      const float2 v = *reinterpret_cast<const float2*>(gp + 8 * k);
+      b.gd[k][0] = v.x;
+      b.gd[k][1] = v.y;
+    }
+  }
   if constexpr (FD) {
     const float* xr = (const float*)p.x + row * p.C;
     const float* dr = (const float*)p.dy + row * p.C;
@@ -339,8 +350,10 @@ NRSE_DEV void ln_bwd_load(const nrse_ln_bwd_params& p, const ColDiv& cd, long lo
 
 // RES: the encoder-layer form (residual input, fused dropout-cast consumer); !RES (conv / feature
 // projection LNs) drops their registers: 137 -> fewer VGPRs, more waves for the long row sweeps
-template <int NK, bool RES, bool COL, bool BF, bool FD = false>
+// GT (with FD): dy += the gate path's gradient, nrse_ln_bwd_params.gate_dp
+template <int NK, bool RES, bool COL, bool BF, bool FD = false, bool GT = false>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const nrse_ln_bwd_params p) {
+  static_assert(!GT || FD, "the gate term rides on the encoder form");
   constexpr bool GBL = RES && !FD;  // gamma / beta read from global memory per row
   __shared__ float red[4][NK * 64 * CH];
   // gamma / beta staged once: read per row from LDS (lgkmcnt), not global memory, whose per-row
@@ -358,6 +371,18 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const nrse_ln_bwd_params p)
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: row math (col2im divisions) on the SALU
   const int C = p.C;
   const bool fuse = RES && p.dv != nullptr;
+  // GT: the pair-summed gate weights of this lane's head dims d = 4 (lane % 16) + e (the same for
+  // every k), summed in gate_bwd's order
+  float gwa[CH], gwb[CH];
+#pragma unroll
+  for (int e = 0; e < CH; ++e) {
+    gwa[e] = gwb[e] = 0.f;
+    if constexpr (GT) {
+      const int d = (lane & 15) * CH + e;
+      gwa[e] = p.gate_w[d] + p.gate_w[64 + d] + p.gate_w[128 + d] + p.gate_w[192 + d];
+      gwb[e] = p.gate_w[256 + d] + p.gate_w[320 + d] + p.gate_w[384 + d] + p.gate_w[448 + d];
+    }
+  }
   const uint32_t key = site_key(p.dv_seed);
   const uint32_t thr = dropout_threshold(p.dv_p);
   const float dsc = p.dv_p > 0.f ? 1.f / (1.f - p.dv_p) : 1.f;
@@ -402,6 +427,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const nrse_ln_bwd_params p)
         for (int e = 0; e < CH; ++e) {
           xv[e] = b.x[k][e];
           dv0[e] = b.dy[k][e];
+          if constexpr (GT) dv0[e] += b.gd[RES ? k : 0][0] * gwa[e] + b.gd[RES ? k : 0][1] * gwb[e];
           if constexpr (COL) dv1[e] = b.dy2[k][e];
         }
       }
@@ -454,24 +480,24 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const nrse_ln_bwd_params p)
   }
   LnRow<NK, RES, COL, BF> ba, bb;
   const long long last = p.rows - 1;
-  if (row < p.rows) ln_bwd_load<NK, RES, COL, BF, FD>(p, cd, row, lane, ba);
+  if (row < p.rows) ln_bwd_load<NK, RES, COL, BF, FD, GT>(p, cd, row, lane, ba);
   for (; row < p.rows; row += 2 * nw) {
     const long long rb = row + nw;
     // BF: unconditional (clamped) prefetch, fenced from the scheduler, which otherwise sinks the
     // loads below part of the current row's math to save registers (and then waits for them)
     if (BF || FD) {
-      ln_bwd_load<NK, RES, COL, BF, FD>(p, cd, rb < last ? rb : last, lane, bb);
+      ln_bwd_load<NK, RES, COL, BF, FD, GT>(p, cd, rb < last ? rb : last, lane, bb);
       __builtin_amdgcn_sched_barrier(0);
     } else if (rb < p.rows) {
-      ln_bwd_load<NK, RES, COL, BF, FD>(p, cd, rb, lane, bb);
+      ln_bwd_load<NK, RES, COL, BF, FD, GT>(p, cd, rb, lane, bb);
     }
     compute(ba, row);
     if (rb >= p.rows) break;
     if (BF || FD) {
-      ln_bwd_load<NK, RES, COL, BF, FD>(p, cd, rb + nw < last ? rb + nw : last, lane, ba);
+      ln_bwd_load<NK, RES, COL, BF, FD, GT>(p, cd, rb + nw < last ? rb + nw : last, lane, ba);
       __builtin_amdgcn_sched_barrier(0);
     } else if (rb + nw < p.rows) {
-      ln_bwd_load<NK, RES, COL, BF, FD>(p, cd, rb + nw, lane, ba);
+      ln_bwd_load<NK, RES, COL, BF, FD, GT>(p, cd, rb + nw, lane, ba);
     }
     compute(bb, rb);
   }
@@ -635,8 +661,11 @@ extern "C" int nrse_layernorm_bwd(const nrse_ln_bwd_params* p, void* stream) {
   const bool fd = res && p->resid && p->x_dtype == NRSE_F32 && p->dy_dtype == NRSE_F32 &&
                   p->dy_mode == NRSE_DY_DIRECT &&
                   ((((uintptr_t)p->x) | ((uintptr_t)p->dy) | ((uintptr_t)p->resid)) & 15) == 0;
+  NRSE_REQUIRE(!p->gate_dp || (fd && p->gate_w && p->C % 64 == 0 && ((uintptr_t)p->gate_dp & 7) == 0),
+               "nrse_layernorm_bwd: gate_dp needs the encoder form (resid, f32 x / dy / resid, dy direct) and gate_w");
 #define NRSE_LN_BWD_NK(NK)                                                                          \
-  if (fd) hipLaunchKernelGGL((ln_bwd_kernel<NK, true, false, false, true>), grid, dim3(256), 0, st, *p); \
+  if (fd && p->gate_dp) hipLaunchKernelGGL((ln_bwd_kernel<NK, true, false, false, true, true>), grid, dim3(256), 0, st, *p); \
+  else if (fd) hipLaunchKernelGGL((ln_bwd_kernel<NK, true, false, false, true>), grid, dim3(256), 0, st, *p); \
   else if (res) hipLaunchKernelGGL((ln_bwd_kernel<NK, true, false, false>), grid, dim3(256), 0, st, *p);    \
   else if (bf && col2) hipLaunchKernelGGL((ln_bwd_kernel<NK, false, true, true>), grid, dim3(256), 0, st, *p); \
   else if (bf) hipLaunchKernelGGL((ln_bwd_kernel<NK, false, false, true>), grid, dim3(256), 0, st, *p); \

@@ -76,7 +76,7 @@ class LnBwdParams(ctypes.Structure):
                 ("dx", c_vp), ("dx_dtype", c_int), ("resid", c_vp), ("dgamma", c_vp), ("dbeta", c_vp),
                 ("rows", c_ll), ("C", c_int), ("flags", c_int),
                 ("dv", c_vp), ("dv_dtype", c_int), ("dv_colsum", c_vp), ("dv_p", c_f), ("dv_seed", c_u32),
-                ("part", c_vp)]
+                ("part", c_vp), ("gate_dp", c_vp), ("gate_w", c_vp)]
 
 
 class AttnFwdParams(ctypes.Structure):
@@ -131,6 +131,8 @@ _SIGNATURES = {
     "nrse_gate_bwd_workspace": ([c_int], c_ll),
     "nrse_gate_bwd": ([c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp],
                       c_int),
+    "nrse_gate_bwd_dp": ([c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp,
+                          c_vp], c_int),
     "nrse_attn_fwd": ([_P(AttnFwdParams), c_vp], c_int),
     "nrse_attn_bwd": ([_P(AttnBwdParams), c_vp], c_int),
     "nrse_attn_bwd_workspace": ([_P(AttnBwdParams)], c_ll),

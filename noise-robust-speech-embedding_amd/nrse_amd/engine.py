@@ -54,6 +54,11 @@ def _divisor_at_most(n: int, cap: int) -> int:
     return 1
 
 
+# the gate path's dx1 contribution added by the LN1 backward (nrse_gate_bwd_dp + gate_dp) instead
+# of a read-modify-write of dx1 by nrse_gate_bwd; NRSE_GATE_INTO_LN=0 restores the latter (A/B)
+_GATE_INTO_LN = os.environ.get("NRSE_GATE_INTO_LN", "1") != "0"
+
+
 @dataclass
 class StepConfig:
     lr: float = 1e-5
@@ -571,21 +576,30 @@ class ByolEngine:
                        T, nh, pat, R.site_seed(fseed, R.site_attn_probs(li)), bias_vec=tape.bias_vec,
                        drop_mask=L_["dmask"])
             del dctx
+            # the gate path's backward: its parameter gradients and each (row, head)'s (dpa, dpb),
+            # which the LN1 backward below adds to dx1 as it reads it (no dx1 read-modify-write)
+            gdp = torch.empty(BT, nh, 2, device=dev, dtype=F32) if _GATE_INTO_LN else None
+            if gdp is not None:
+                K.gate_bwd_dp(L_["x1"], Pm[at + "gru_rel_pos_linear.weight"], Pm[at + "gru_rel_pos_linear.bias"],
+                              Pm[at + "gru_rel_pos_const"], dgate, gdp, Gv[at + "gru_rel_pos_linear.weight"],
+                              Gv[at + "gru_rel_pos_linear.bias"], Gv[at + "gru_rel_pos_const"], B, T, nh)
             with self._wgrad_stream(main, dqkv, L_["x1"]):
                 K.linear_wgrad(dqkv, L_["x1"], self.fused(self.grad_flat_for(Gv), li, "qkv_w"))
                 K.colsum(dqkv, self.fused(self.grad_flat_for(Gv), li, "qkv_b"))
             dx1 = torch.empty(BT, H, device=dev, dtype=F32)
             K.linear_dgrad(dqkv, self.fused(W.s_flat, li, "qkv_w"), dx1)
             del dqkv
-            K.gate_bwd(L_["x1"], Pm[at + "gru_rel_pos_linear.weight"], Pm[at + "gru_rel_pos_linear.bias"],
-                       Pm[at + "gru_rel_pos_const"], dgate, dx1, Gv[at + "gru_rel_pos_linear.weight"],
-                       Gv[at + "gru_rel_pos_linear.bias"], Gv[at + "gru_rel_pos_const"], B, T, nh)
+            if gdp is None:  # the read-modify-write form (NRSE_GATE_INTO_LN=0, A/B)
+                K.gate_bwd(L_["x1"], Pm[at + "gru_rel_pos_linear.weight"], Pm[at + "gru_rel_pos_linear.bias"],
+                           Pm[at + "gru_rel_pos_const"], dgate, dx1, Gv[at + "gru_rel_pos_linear.weight"],
+                           Gv[at + "gru_rel_pos_linear.bias"], Gv[at + "gru_rel_pos_const"], B, T, nh)
             dhin = torch.empty(BT, H, device=dev, dtype=F32)
             # + the next (lower) layer's FFN output-dropout backward, fused
             dv2_next, kw = ffn_out_dropout(j + 1)
             K.ln_bwd(dx1, L_["h_in"], Pm[p + "layer_norm.weight"], L_["m1"], L_["r1"], dhin, resid=dhmid,
-                     dgamma=Gv[p + "layer_norm.weight"], dbeta=Gv[p + "layer_norm.bias"], **kw)
-            del dx1, dhmid
+                     dgamma=Gv[p + "layer_norm.weight"], dbeta=Gv[p + "layer_norm.bias"], gate_dp=gdp,
+                     gate_w=Pm[at + "gru_rel_pos_linear.weight"] if gdp is not None else None, **kw)
+            del dx1, dhmid, gdp
             L_.clear()
             dh = dhin
             if on_layer is not None:

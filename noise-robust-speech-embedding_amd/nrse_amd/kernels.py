@@ -392,9 +392,10 @@ def ln_fwd(x, gamma, beta, y, mean, rstd, eps, gelu=False, relu=False, split3=Fa
 
 def ln_bwd(dy, x, gamma, mean, rstd, dx, *, beta=None, gelu=False, relu=False, resid=None, dgamma=None, dbeta=None,
            mode=_lib.DY_DIRECT, col=(0, 0, 0, 0), bcast_t=0, dy_scale=1.0, rows=None,
-           dv=None, dv_colsum=None, dv_p=0.0, dv_seed=0):
+           dv=None, dv_colsum=None, dv_p=0.0, dv_seed=0, gate_dp=None, gate_w=None):
     """LayerNorm backward; with `dv`, also the fused dropout_cast_colsum of dx: dv = dropout(dx)
-    (cast to dv's dtype), dv_colsum += column sums of dv."""
+    (cast to dv's dtype), dv_colsum += column sums of dv. gate_dp / gate_w (encoder form): dy plus
+    the gate path's gradient from gate_bwd_dp's (dpa, dpb) and gru_rel_pos_linear.weight."""
     C = x.shape[-1]
     rows = rows if rows is not None else x.numel() // C
     p = LnBwdParams()
@@ -411,6 +412,9 @@ def ln_bwd(dy, x, gamma, mean, rstd, dx, *, beta=None, gelu=False, relu=False, r
         assert dv.numel() == rows * C and (dv_colsum is None or dv_colsum.dtype == torch.float32)
         p.dv, p.dv_dtype, p.dv_colsum = ptr(dv), dtype_code(dv), ptr(dv_colsum)
         p.dv_p, p.dv_seed = dv_p, dv_seed & 0xFFFFFFFF
+    if gate_dp is not None:
+        assert gate_dp.dtype == torch.float32 and gate_dp.numel() == rows * (C // 64) * 2 and gate_w is not None
+        p.gate_dp, p.gate_w = ptr(gate_dp), ptr(gate_w)
     ws = None
     if DETERMINISTIC and (dgamma is not None or (dv is not None and dv_colsum is not None)):
         ws = workspace(_lib.lib().nrse_layernorm_bwd_workspace(ctypes.byref(p)))
@@ -455,6 +459,16 @@ def gate_bwd(x1, W, b, c, dgate, dx1, dW, db, dc, batch, T, H):
     assert dx1.dtype == torch.float32 and dW.dtype == db.dtype == dc.dtype == torch.float32
     ws = workspace(_lib.lib().nrse_gate_bwd_workspace(H)) if DETERMINISTIC else None
     _call("nrse_gate_bwd", ptr(x1), dtype_code(x1), ptr(W), ptr(b), ptr(c), ptr(dgate), ptr(dx1), ptr(dW), ptr(db),
+          ptr(dc), batch, T, H, ptr(ws), stream_ptr())
+
+
+def gate_bwd_dp(x1, W, b, c, dgate, dp, dW, db, dc, batch, T, H):
+    """The gate backward without the dx1 read-modify-write: dp [B*T, H, 2] f32 receives each
+    (row, head)'s (dpa, dpb) for the LN backward (ln_bwd(gate_dp=dp, gate_w=W)); dW/db/dc as gate_bwd."""
+    assert dp.dtype == torch.float32 and dp.numel() == batch * T * H * 2
+    assert dW.dtype == db.dtype == dc.dtype == torch.float32
+    ws = workspace(_lib.lib().nrse_gate_bwd_workspace(H)) if DETERMINISTIC else None
+    _call("nrse_gate_bwd_dp", ptr(x1), dtype_code(x1), ptr(W), ptr(b), ptr(c), ptr(dgate), ptr(dp), ptr(dW), ptr(db),
           ptr(dc), batch, T, H, ptr(ws), stream_ptr())
 
 
