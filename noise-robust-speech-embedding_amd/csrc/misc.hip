@@ -525,23 +525,28 @@ extern "C" int nrse_gelu_bwd_pad(const float* dy, const void* pre, int pdt, void
 // Row groups of `batch` (slab [batch][S][n], dst_j + b * n_j): per-utterance sums.
 struct RowsDst { float* d[3]; long long n[3]; };
 
+// RG row groups x (1024 / RG) column quads per workgroup: RG = 16 (256 columns) by default; RG =
+// 64 (64 columns) when that grid would leave most CUs idle (r04: the encoder LayerNorm's 512
+// partial rows x 3072 columns ran on 12 workgroups at ~1 TB/s)
+template <int RG>
 __global__ __launch_bounds__(1024) void rows_reduce_kernel(RowsDst dst, const float* __restrict__ slab, int S,
                                                            long long n, int acc) {
-  __shared__ float4 red[16][64];
-  const int q = threadIdx.x & 63, r = threadIdx.x >> 6;
-  const long long col = (long long)blockIdx.x * 256 + 4 * q;
+  constexpr int NQ = 1024 / RG;
+  __shared__ float4 red[RG][NQ];
+  const int q = threadIdx.x % NQ, r = threadIdx.x / NQ;
+  const long long col = (long long)blockIdx.x * (4 * NQ) + 4 * q;
   const float* sl = slab + (long long)blockIdx.y * S * n;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   if (col < n) {
     int k = r;
-    for (; k + 112 < S; k += 128) {
+    for (; k + 7 * RG < S; k += 8 * RG) {
       float4 v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(sl + (long long)(k + 16 * u) * n + col);
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(sl + (long long)(k + RG * u) * n + col);
 #pragma unroll
       for (int u = 0; u < 8; ++u) { s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w; }
     }
-    for (; k < S; k += 16) {
+    for (; k < S; k += RG) {
       const float4 v = *reinterpret_cast<const float4*>(sl + (long long)k * n + col);
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
@@ -551,7 +556,7 @@ __global__ __launch_bounds__(1024) void rows_reduce_kernel(RowsDst dst, const fl
   if (r == 0 && col < n) {
     float4 t = red[0][q];
 #pragma unroll
-    for (int i = 1; i < 16; ++i) { t.x += red[i][q].x; t.y += red[i][q].y; t.z += red[i][q].z; t.w += red[i][q].w; }
+    for (int i = 1; i < RG; ++i) { t.x += red[i][q].x; t.y += red[i][q].y; t.z += red[i][q].z; t.w += red[i][q].w; }
     int j = 0;
     long long c = col;
     while (j < 2 && c >= dst.n[j]) { c -= dst.n[j]; ++j; }
@@ -608,8 +613,11 @@ extern "C" int nrse_rows_reduce(float* d0, long long n0, float* d1, long long n1
   const long long n = dst.n[0] + dst.n[1] + dst.n[2];
   const bool vec = n0 % 4 == 0 && dst.n[1] % 4 == 0 && dst.n[2] % 4 == 0 && al16(d0) && (!d1 || al16(d1)) &&
                    (!d2 || al16(d2)) && al16(slab);
-  if (vec)
-    hipLaunchKernelGGL(rows_reduce_kernel, dim3((unsigned)((n + 255) / 256), (unsigned)batch), dim3(1024), 0,
+  if (vec && S >= 128 && ((n + 255) / 256) * batch < 128)
+    hipLaunchKernelGGL(rows_reduce_kernel<64>, dim3((unsigned)((n + 63) / 64), (unsigned)batch), dim3(1024), 0,
+                       (hipStream_t)stream, dst, slab, S, n, accumulate);
+  else if (vec)
+    hipLaunchKernelGGL(rows_reduce_kernel<16>, dim3((unsigned)((n + 255) / 256), (unsigned)batch), dim3(1024), 0,
                        (hipStream_t)stream, dst, slab, S, n, accumulate);
   else
     hipLaunchKernelGGL(rows_reduce1_kernel, dim3((unsigned)((n + 63) / 64), (unsigned)batch), dim3(1024), 0,

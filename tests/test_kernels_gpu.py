@@ -505,3 +505,25 @@ def test_split3_outputs(nrse_device):
     assert torch.equal(o3[0], o3[2])
     assert rel(o3[0].double() + o3[1].double(), o32) < 3e-5
     assert (o3[1].float().abs() <= o3[0].float().abs() * 2 ** -8 + 1e-30).all()
+
+
+@pytest.mark.parametrize("S,n,batch,acc", [(512, 3072, 1, False), (512, 3072, 1, True), (64, 4096, 1, False),
+                                           (224, 796, 16, False), (130, 520, 2, True)])
+def test_rows_reduce(nrse_device, S, n, batch, acc):
+    """nrse_rows_reduce against float64 in both workgroup shapes (256-column groups; 64-column
+    groups when the grid is small), into three destinations, accumulating or not, and the same
+    bits on a second run."""
+    from nrse_amd import kernels as K
+    dev = nrse_device
+    slab = torch.randn(batch, S, n, device=dev)
+    n0, n1 = n // 2, n // 4
+    n2 = n - n0 - n1
+    base = [torch.randn(batch, m, device=dev) if acc else torch.zeros(batch, m, device=dev) for m in (n0, n1, n2)]
+    outs = []
+    for _ in range(2):
+        d = [x.clone() for x in base]
+        K.rows_reduce(slab, S, *d, batch=batch, accumulate=acc)
+        outs.append(torch.cat(d, 1))
+    ref = slab.double().sum(1) + torch.cat(base, 1).double()
+    assert rel(outs[0], ref) < 1e-6
+    assert torch.equal(outs[0], outs[1])
