@@ -2,15 +2,15 @@
 # Round-4 evidence on one box: SQ/GRBM/TCC counter passes of the isolated hot kernels
 # (tools/pmc_sq.sh), HBM traffic of the step's GEMMs (tools/pmc_gemm.sh), the default bench line
 # (with the CPU baseline), and its serial rocprofv3 kernel-trace summary.
-# Usage (on the GPU box): bash tools/gpu_r04_evidence.sh TAG
+# Usage (on the GPU box): bash tools/gpu_evidence.sh TAG
+# (gpurun merges gpurun_out/ back: copy ${TAG}_sq_p1_table.json / ${TAG}_traffic.json into profiles/
+# as the round's SQ table / GEMM traffic files, which bench.py reads)
 set -o pipefail
 TAG=${1:-r04e}
 mkdir -p gpurun_out
 bash tools/pmc_sq.sh ${TAG}_sq all > gpurun_out/${TAG}_sq.txt 2>&1 || { tail -20 gpurun_out/${TAG}_sq.txt; exit 1; }
 grep -E "gemm256|attn" gpurun_out/${TAG}_sq.txt | head -20
-cp gpurun_out/${TAG}_sq_p1_table.json profiles/r04_pmc_sq_table.json
 bash tools/pmc_gemm.sh ${TAG} || exit 1
-cp gpurun_out/${TAG}_traffic.json profiles/r04_gemm_traffic.json
 timeout -k 10 400 python -u bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || { tail -30 gpurun_out/${TAG}_bench.err; exit 1; }
 python -c "import json; d=json.load(open('gpurun_out/${TAG}_bench.json')); print(d['value'], d['ms_per_step'], d['roofline'], d['cpu_baseline'])"
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT

@@ -1,14 +1,14 @@
 #!/bin/bash
 # r04 session 2 evidence on one box: the full GPU suite, the r04 evidence pass
-# (tools/gpu_r04_evidence.sh: SQ table, GEMM traffic, default bench with the CPU baseline, serial
+# (tools/gpu_evidence.sh: SQ table, GEMM traffic, default bench with the CPU baseline, serial
 # kernel stats), the conv0 counter pass and the in-step kernel stats.
-# Usage (on the GPU box): bash tools/gpu_r04g.sh TAG
+# Usage (on the GPU box): bash tools/gpu_evidence_full.sh TAG
 set -o pipefail
 TAG=${1:-r04g}
 mkdir -p gpurun_out
 timeout -k 10 1100 python -u -m pytest tests -m gpu -x -q --timeout 400 --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1 || { echo "tests failed"; tail -40 gpurun_out/${TAG}_tests.log; exit 1; }
 tail -2 gpurun_out/${TAG}_tests.log
-bash tools/gpu_r04_evidence.sh ${TAG}e || exit 1
+bash tools/gpu_evidence.sh ${TAG}e || exit 1
 bash tools/pmc_sq.sh ${TAG}_c0 conv0 > gpurun_out/${TAG}_c0.txt 2>&1 || { tail -20 gpurun_out/${TAG}_c0.txt; exit 1; }
 grep -E "conv0" gpurun_out/${TAG}_c0.txt | head
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
