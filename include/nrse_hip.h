@@ -250,6 +250,9 @@ typedef struct {
                                      Tp = T rounded up to 64): word (bh, key tile kt, g, query q) bit
                                      4t + r = keep(q, key 64 kt + 16 t + 4 g + r); the backward reads
                                      them instead of re-hashing (nrse_attn_mask_elems) */
+  int drop_mask_in;               /* nonzero (bf16 MFMA path): drop_mask already holds the keep bits
+                                     (nrse_attn_dropout_mask, the same function of seed and position)
+                                     and the forward reads them instead of hashing */
 } nrse_attn_fwd_params;
 
 typedef struct {
@@ -274,6 +277,12 @@ int nrse_attn_fwd(const nrse_attn_fwd_params* p, void* stream);
 int nrse_attn_bwd(const nrse_attn_bwd_params* p, void* stream);
 long long nrse_attn_bwd_workspace(const nrse_attn_bwd_params* p);  /* floats for p->diag_part */
 long long nrse_attn_mask_elems(int batch, int T, int H);           /* u16 words of drop_mask */
+/* The attention-probability dropout keep bits of one layer in the drop_mask layout, computed ahead
+ * of the forward (a data-independent pure-VALU kernel that needs no LDS and few VGPRs, so its waves
+ * run beside the 256x256 GEMMs' on the same SIMDs); the forward then reads them
+ * (drop_mask_in = 1). Words of queries q >= T are zero. */
+int nrse_attn_dropout_mask(uint16_t* drop_mask, int batch, int T, int H, float dropout_p, uint32_t seed,
+                           void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Conv feature encoder front end and the positional-conv weight norm.

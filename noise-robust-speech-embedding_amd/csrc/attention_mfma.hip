@@ -152,10 +152,14 @@ NRSE_DEV void bv_stage(float* bv, const float* vec, int T, int q0, int tid) {
 // One workgroup = 64 queries (4 waves x 16) of one (b, h); K/V tiles double-buffered in LDS by
 // LDS-DMA, the next tile in flight while the current one is computed (one barrier per tile);
 // the gated bias gate[b,h,i] * vec[h, j-i+T-1] from the LDS Toeplitz copies.
-// DROP: dropout on (a compile-time branch: the runtime one made the compiler copy every
-// probability register across it, 16 v_mov per key tile)
-template <bool DROP>
+// DM: dropout mode, a compile-time branch (the runtime one made the compiler copy every
+// probability register across it, 16 v_mov per key tile): 0 none, 1 the pair hash in the kernel
+// (and its keep bits recorded to drop_mask if given), 2 the keep bits read from drop_mask
+// (nrse_attn_dropout_mask computed them ahead, beside the GEMMs: the hash and the bit assembly
+// were about half of this VALU-bound loop's issue cycles)
+template <int DM>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_params p) {
+  constexpr bool DROP = DM != 0;
   extern __shared__ __attribute__((aligned(16))) char dyn[];
   char* const kv0 = dyn;                       // [2 buffers][K tile, V tile]
   float* const bv = reinterpret_cast<float*>(dyn + 4 * TILE_B);
@@ -199,6 +203,11 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
   const int Tp = ntiles * 64;
   // this lane's query row: key pair (kb + 16t + 4g)/2 + rp holds elements r = 2rp, 2rp + 1
   const uint32_t rowpair = (uint32_t)(bh * T + qi) * (uint32_t)((T + 1) >> 1) + (uint32_t)(2 * g);
+  // DM 2: word (bh, key tile, g, qi) of the precomputed bits, the next tile's word loaded while the
+  // current tile computes (the top-of-tile vmcnt(0) covers it)
+  const uint16_t* mrow = DM == 2 ? p.drop_mask + (bh * ntiles * 4 + g) * (long long)(ntiles * 64) + (qv ? qi : 0)
+                                 : nullptr;
+  uint32_t mnext = DM == 2 ? (uint32_t)mrow[0] : 0u;
   // Lazy rescaling in the base-2 domain: mref is the row's reference maximum, and a tile's scores
   // are formed relative to it in two packed fmas, v = s * c1 + (gl * bias - mref) (no separate
   // subtract before the exponential). Only when some lane of the wave sees a score more than
@@ -225,10 +234,12 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     // prefetch tile it+1 into the other buffer (its last readers finished before this barrier)
+    const uint32_t mcur = mnext;
     if (it + 1 < ntiles) {
       char* const Kn = kv0 + ((it + 1) & 1) * 2 * TILE_B;
       kv_dma_issue(kd, Kn, kb + 64, w);
       kv_dma_issue(vd, Kn + TILE_B, kb + 64, w);
+      if (DM == 2) mnext = mrow[(long long)(it + 1) * 4 * (ntiles * 64)];
     }
     // the MFMAs run on every sub-tile (a conditional MFMA makes the compiler stage its result
     // through AGPRs)
@@ -284,7 +295,15 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
       for (int r = 0; r < 4; ++r) pd[t][r] = exp2_(v[t][r]);
 #pragma unroll
     for (int t = 0; t < 4; ++t) lpart2 += f32x2{pd[t][0], pd[t][1]} + f32x2{pd[t][2], pd[t][3]};
-    if constexpr (DROP) {
+    if constexpr (DM == 2) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pd[t][r] = (mcur >> (4 * t + r)) & 1u ? pd[t][r] : 0.f;
+          asm("" : "+v"(pd[t][r]));  // keep the packed bf16 conversions (see DM 1)
+        }
+    } else if constexpr (DROP) {
       uint32_t mb = 0;  // this lane's 16 keep bits of the tile: bit 4t + r = key kb + 16t + 4g + r
 #pragma unroll
       for (int t = 0; t < 4; ++t)
@@ -816,8 +835,10 @@ int nrse_attn_fwd_mfma(const nrse_attn_fwd_params* p, hipStream_t st) {
     nrse_set_error("nrse_attn_fwd: T=%d too long for the LDS bias copies", p->T);
     return NRSE_ERR_UNSUPPORTED;
   }
-  if (p->dropout_p > 0.f) hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(256), lds, st, *p);
-  else hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(256), lds, st, *p);
+  if (p->dropout_p > 0.f && p->drop_mask && p->drop_mask_in)
+    hipLaunchKernelGGL(attn_fwd_kernel<2>, grid, dim3(256), lds, st, *p);
+  else if (p->dropout_p > 0.f) hipLaunchKernelGGL(attn_fwd_kernel<1>, grid, dim3(256), lds, st, *p);
+  else hipLaunchKernelGGL(attn_fwd_kernel<0>, grid, dim3(256), lds, st, *p);
   return nrse_check_launch("nrse_attn_fwd(mfma)");
 }
 
@@ -850,6 +871,63 @@ int nrse_attn_bwd_mfma(const nrse_attn_bwd_params* p, hipStream_t st) {
                           st);
 }
 
+
+namespace {
+// One thread per mask word (bh, key tile kt, g, q): the forward's 8 pair hashes of that word
+// (attn_fwd_kernel DM 1), bit 4t + 2rp + e = keep(q, key 64 kt + 16 t + 4 g + 2 rp + e).
+__global__ __launch_bounds__(256) void attn_mask_kernel(uint16_t* __restrict__ mask, int T, int ntiles, int rows,
+                                                        uint32_t seed, uint32_t thr) {
+  // one wave per mask row ((bh, key tile, g): Tp words, lane-strided), waves grid-strided over the
+  // rows: the launch is sized to sit beside the GEMMs it overlaps (a few waves per CU), not to fill
+  // the chip
+  const uint32_t key = site_key(seed);
+  const int lane = threadIdx.x & 63;
+  const int nw = gridDim.x * 4;
+  const int Tp = ntiles * 64;
+  const uint32_t tp2 = (uint32_t)((T + 1) >> 1);
+  for (int r = blockIdx.x * 4 + (threadIdx.x >> 6); r < rows; r += nw) {
+    const int g = r & 3;
+    const int kt = (r >> 2) % ntiles;
+    const int bh = (r >> 2) / ntiles;
+    const int kb = kt * 64;
+    uint16_t* out = mask + (long long)r * Tp;
+    for (int q = lane; q < Tp; q += 64) {
+      uint32_t mb = 0;
+      if (q < T) {
+        const uint32_t rowpair = (uint32_t)(bh * T + q) * tp2 + (uint32_t)(2 * g);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int rp = 0; rp < 2; ++rp) {
+            const uint32_t hh = mix32((rowpair + (uint32_t)((kb >> 1) + 8 * t + rp)) ^ key);
+            mb |= (attn_half_keep(hh, 0, thr) ? 1u : 0u) << (4 * t + 2 * rp);
+            mb |= (attn_half_keep(hh, 1, thr) ? 1u : 0u) << (4 * t + 2 * rp + 1);
+          }
+      }
+      out[q] = (uint16_t)mb;
+    }
+  }
+}
+}  // namespace
+
+extern "C" int nrse_attn_dropout_mask(uint16_t* drop_mask, int batch, int T, int H, float dropout_p, uint32_t seed,
+                                      void* stream) {
+  NRSE_REQUIRE(drop_mask && batch > 0 && T > 0 && H > 0 && dropout_p > 0.f && dropout_p < 1.f,
+               "nrse_attn_dropout_mask: bad args");
+  NRSE_REQUIRE((long long)batch * H * T < (1LL << 31), "nrse_attn_dropout_mask: too many rows");
+  const int ntiles = (T + 63) / 64;
+  const int rows = batch * H * ntiles * 4;
+  // workgroups (4 waves each): NRSE_MASK_WGS, default 256 (one wave per SIMD) -- the kernel runs
+  // on a side stream under the layer's LN1 / QKV GEMM and must leave their waves room
+  static const int wgs_env = [] {
+    const char* e = getenv("NRSE_MASK_WGS");
+    return e ? atoi(e) : 0;
+  }();
+  const int wgs = std::max(1, std::min(wgs_env > 0 ? wgs_env : 256, (rows + 3) / 4));
+  hipLaunchKernelGGL(attn_mask_kernel, dim3((unsigned)wgs), dim3(256), 0, (hipStream_t)stream, drop_mask, T, ntiles,
+                     rows, seed, dropout_threshold16(dropout_p));
+  return nrse_check_launch("nrse_attn_dropout_mask");
+}
 
 extern "C" long long nrse_attn_mask_elems(int batch, int T, int H) {
   if (batch <= 0 || T <= 0 || H <= 0) return 0;

@@ -82,7 +82,8 @@ class LnBwdParams(ctypes.Structure):
 class AttnFwdParams(ctypes.Structure):
     _fields_ = [("qkv", c_vp), ("dtype", c_int), ("gate", c_vp), ("bias", c_vp), ("ctx", c_vp), ("lse", c_vp),
                 ("batch", c_int), ("T", c_int), ("H", c_int), ("head_dim", c_int), ("scale", c_f),
-                ("dropout_p", c_f), ("seed", c_u32), ("bias_vec", c_vp), ("drop_mask", c_vp)]
+                ("dropout_p", c_f), ("seed", c_u32), ("bias_vec", c_vp), ("drop_mask", c_vp),
+                ("drop_mask_in", c_int)]
 
 
 class AttnBwdParams(ctypes.Structure):
@@ -133,6 +134,7 @@ _SIGNATURES = {
                       c_int),
     "nrse_gate_bwd_dp": ([c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp,
                           c_vp], c_int),
+    "nrse_attn_dropout_mask": ([c_vp, c_int, c_int, c_int, c_f, c_u32, c_vp], c_int),
     "nrse_attn_fwd": ([_P(AttnFwdParams), c_vp], c_int),
     "nrse_attn_bwd": ([_P(AttnBwdParams), c_vp], c_int),
     "nrse_attn_bwd_workspace": ([_P(AttnBwdParams)], c_ll),

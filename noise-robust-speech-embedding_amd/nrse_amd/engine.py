@@ -57,6 +57,10 @@ def _divisor_at_most(n: int, cap: int) -> int:
 # the gate path's dx1 contribution added by the LN1 backward (nrse_gate_bwd_dp + gate_dp) instead
 # of a read-modify-write of dx1 by nrse_gate_bwd; NRSE_GATE_INTO_LN=0 restores the latter (A/B)
 _GATE_INTO_LN = os.environ.get("NRSE_GATE_INTO_LN", "1") != "0"
+# the attention-probability dropout bits computed ahead on a mask stream and read by the forward
+# (nrse_attn_dropout_mask); opt-in with NRSE_MASK_AHEAD=1: the mask kernel (29 us) costs more
+# than the forward saves (73 -> 58 us) when the two views already overlap (step 552 vs 554 pairs/s)
+_MASK_AHEAD = os.environ.get("NRSE_MASK_AHEAD", "0") == "1"
 
 
 @dataclass
@@ -440,6 +444,23 @@ class ByolEngine:
                 continue
             executed += 1
             p = f"encoder.layers.{li}."
+            # the probability-dropout keep bits of this layer (bf16 path): computed ahead on a mask
+            # stream, beside this layer's LN1 / QKV GEMM (a pure-VALU kernel whose waves fit on the
+            # GEMM's SIMDs), then read by the attention forward instead of hashed in it; the online
+            # view keeps them for the backward
+            dmask, mask_ev = None, None
+            if pat > 0 and bias_vec is not None:
+                dmask = torch.empty(K.attn_mask_elems(B, T, nh), device=dev, dtype=torch.int16)
+                if _MASK_AHEAD:
+                    cur = torch.cuda.current_stream(dev)
+                    ms = self._mask_stream(cur)
+                    ms.wait_stream(cur)
+                    with torch.cuda.stream(ms):
+                        K.attn_dropout_mask(dmask, B, T, nh, pat, R.site_seed(fseed, R.site_attn_probs(li)))
+                        mask_ev = torch.cuda.Event()
+                        mask_ev.record(ms)
+                elif not need_grad:
+                    dmask = None  # hashed in the forward, not recorded
             x1 = torch.empty(BT, H, device=dev, dtype=cdt)
             m1 = torch.empty(BT, device=dev, dtype=F32)
             r1 = torch.empty(BT, device=dev, dtype=F32)
@@ -453,11 +474,11 @@ class ByolEngine:
                        Pm[at + "gru_rel_pos_const"], gate, B, T, nh)
             ctx = torch.empty(BT, H, device=dev, dtype=cdt)
             lse = torch.empty(B, nh, T, device=dev, dtype=F32)
-            # the probability-dropout keep bits, recorded for the backward (bf16 path)
-            dmask = (torch.empty(K.attn_mask_elems(B, T, nh), device=dev, dtype=torch.int16)
-                     if need_grad and pat > 0 and bias_vec is not None else None)
+            if mask_ev is not None:
+                torch.cuda.current_stream(dev).wait_event(mask_ev)
+            # (without the mask stream the forward hashes and, for the online view, records the bits)
             K.attn_fwd(qkv, gate, bias_tab, ctx, lse, B, T, nh, pat, R.site_seed(fseed, R.site_attn_probs(li)),
-                       bias_vec=bias_vec, drop_mask=dmask)
+                       bias_vec=bias_vec, drop_mask=dmask, mask_in=mask_ev is not None)
             hmid = torch.empty(BT, H, device=dev, dtype=F32)
             K.linear_fwd(ctx, Ps[at + "out_proj.weight"], hmid, bias=Pm[at + "out_proj.bias"], resid=hcur, ldr=H,
                          dropout_p=php, seed=R.site_seed(fseed, R.site_attn_out(li)), w_lo=W.lo)
@@ -846,6 +867,15 @@ class ByolEngine:
             t.record_stream(side)
         with torch.cuda.stream(side):
             yield
+
+    def _mask_stream(self, view_stream: torch.cuda.Stream) -> torch.cuda.Stream:
+        """One dropout-mask stream per view stream (the two views' forwards run concurrently)."""
+        if getattr(self, "_mask_streams", None) is None:
+            self._mask_streams = {}
+        key = view_stream.cuda_stream
+        if key not in self._mask_streams:
+            self._mask_streams[key] = torch.cuda.Stream(self.dev)
+        return self._mask_streams[key]
 
     def _side_stream(self) -> torch.cuda.Stream:
         if getattr(self, "_side", None) is None:

@@ -477,13 +477,23 @@ def attn_mask_elems(batch, T, H) -> int:
     return int(_lib.lib().nrse_attn_mask_elems(batch, T, H))
 
 
-def attn_fwd(qkv, gate, bias, ctx, lse, batch, T, H, dropout_p=0.0, seed=0, bias_vec=None, drop_mask=None):
+def attn_dropout_mask(mask, batch, T, H, dropout_p, seed):
+    """The probability-dropout keep bits of one attention layer (drop_mask layout), computed ahead
+    of attn_fwd(..., drop_mask=mask, mask_in=True) by a pure-VALU kernel (nrse_attn_dropout_mask)."""
+    assert mask.dtype == torch.int16 and mask.numel() >= attn_mask_elems(batch, T, H)
+    _call("nrse_attn_dropout_mask", ptr(mask), batch, T, H, dropout_p, seed & 0xFFFFFFFF, stream_ptr())
+
+
+def attn_fwd(qkv, gate, bias, ctx, lse, batch, T, H, dropout_p=0.0, seed=0, bias_vec=None, drop_mask=None,
+             mask_in=False):
     """bias: [H, T, Tb] table (f32 parity path), bias_vec: [H, 2T-1] Toeplitz vector (bf16 path);
-    drop_mask (optional, int16 [attn_mask_elems]): the keep bits for the backward."""
+    drop_mask (optional, int16 [attn_mask_elems]): the keep bits for the backward, recorded by the
+    forward, or (mask_in) read by it (attn_dropout_mask wrote them)."""
     if drop_mask is not None:
         assert drop_mask.dtype == torch.int16 and drop_mask.numel() >= attn_mask_elems(batch, T, H)
     p = AttnFwdParams(ptr(qkv), dtype_code(qkv), ptr(gate), ptr(bias), ptr(ctx), ptr(lse), batch, T, H, 64,
-                      0.125, dropout_p, seed & 0xFFFFFFFF, ptr(bias_vec), ptr(drop_mask))
+                      0.125, dropout_p, seed & 0xFFFFFFFF, ptr(bias_vec), ptr(drop_mask),
+                      1 if (mask_in and drop_mask is not None) else 0)
     _call("nrse_attn_fwd", ctypes.byref(p), stream_ptr())
 
 

@@ -129,3 +129,32 @@ def test_attention_recorded_dropout_mask(nrse_device, T):
         outs.append((dqkv, dgate, diag))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("T", [49, 399, 599])
+def test_attention_precomputed_dropout_mask(nrse_device, T):
+    """nrse_attn_dropout_mask writes exactly the keep bits the forward records (every word of a
+    valid query), and the forward that reads them (mask_in) gives the hashing forward's ctx and
+    lse bit for bit."""
+    from nrse_amd import kernels as K
+    dev = nrse_device
+    B, H, p, seed = 2, 4, 0.1, 77
+    torch.manual_seed(T + 9)
+    qkv = (torch.randn(B * T, 3 * H * 64, device=dev) * 0.5).to(torch.bfloat16)
+    gate = torch.rand(B, H, T, device=dev) + 1.0
+    vec, _ = toeplitz_bias(H, T, dev)
+    ctx1 = torch.empty(B * T, H * 64, device=dev, dtype=torch.bfloat16)
+    ctx2 = torch.empty_like(ctx1)
+    lse1 = torch.empty(B, H, T, device=dev)
+    lse2 = torch.empty_like(lse1)
+    rec = torch.zeros(K.attn_mask_elems(B, T, H), device=dev, dtype=torch.int16)
+    K.attn_fwd(qkv, gate, None, ctx1, lse1, B, T, H, p, seed, bias_vec=vec, drop_mask=rec)
+    pre = torch.full_like(rec, -1)
+    K.attn_dropout_mask(pre, B, T, H, p, seed)
+    nt = (T + 63) // 64
+    Tp = nt * 64
+    valid = (torch.arange(Tp, device=dev) < T).view(1, 1, 1, Tp).expand(B * H, nt, 4, Tp).reshape(-1)
+    assert torch.equal(pre[valid], rec[valid])
+    assert (pre[~valid] == 0).all()
+    K.attn_fwd(qkv, gate, None, ctx2, lse2, B, T, H, p, seed, bias_vec=vec, drop_mask=pre, mask_in=True)
+    assert torch.equal(ctx1, ctx2) and torch.equal(lse1, lse2)

@@ -44,3 +44,8 @@ tb = timeit(lambda: K.attn_bwd(qkv, gate, bias, ctx, dctx, lse, delta, dqkv, dga
                                drop_mask=mask))
 fl = 4.0 * B * H * T * T * 64
 print(f"p={p} recorded mask: fwd {tf*1e3:.1f}us ({fl/tf/1e9:.0f} TF) | bwd {tb*1e3:.1f}us ({2.5*fl/tb/1e9:.0f} TF)", flush=True)
+# the mask computed ahead by its own kernel (alone here; in the step it runs beside the GEMMs) and
+# read by the forward
+tm = timeit(lambda: K.attn_dropout_mask(mask, B, T, H, p, 1))
+tf2 = timeit(lambda: K.attn_fwd(qkv, gate, bias, ctx, lse, B, T, H, p, 1, bias_vec=bvec, drop_mask=mask, mask_in=True))
+print(f"p={p} precomputed mask: mask kernel {tm*1e3:.1f}us | fwd {tf2*1e3:.1f}us ({fl/tf2/1e9:.0f} TF)", flush=True)
