@@ -440,6 +440,16 @@ typedef struct {
   float grad_scale;                       /* extra multiplier on g (e.g. 1/world_size) */
   void* p_shadow_lo;                      /* optional (bf16 shadow only): lo = bf16(p - shadow), the
                                              split-weight mode's second weight plane */
+  /* optional target EMA fused into the update (src/models/byol.py:62-73, as nrse_ema on the
+   * updated p): for i < ema_n, ema_t[i] = ema_decay * ema_t[i] + (1 - ema_decay) * p_new[i], its
+   * shadow (ema_shadow_dtype, and the bf16 lo plane) written alongside; saves nrse_ema's re-read
+   * of p and its launch. ema_t null: no EMA. ema_n <= n. */
+  float* ema_t;
+  void* ema_shadow;
+  void* ema_shadow_lo;
+  int ema_shadow_dtype;
+  float ema_decay;
+  long long ema_n;
 } nrse_adamw_params;
 int nrse_adamw(const nrse_adamw_params* p, void* stream);
 /* t_shadow_lo: optional, as nrse_adamw_params.p_shadow_lo */

@@ -57,6 +57,18 @@ __global__ __launch_bounds__(256) void sum_parts_kernel(const double* __restrict
   if (threadIdx.x == 0) *out += red[0] + red[1] + red[2] + red[3];
 }
 
+// t' = decay t + (1 - decay) o with one explicit rounding order at every EMA site (ema_kernel and
+// the fused form in adamw_kernel), so the two forms agree bit for bit whatever the contraction
+NRSE_DEV float ema_mix(float t, float o, float decay, float om) { return fmaf(decay, t, om * o); }
+
+// one element of the fused target EMA (nrse_adamw_params.ema_t), as ema_kernel's scalar tail
+NRSE_DEV void ema_one(const nrse_adamw_params& p, long long i, float pn, float eom) {
+  const float t = ema_mix(p.ema_t[i], pn, p.ema_decay, eom);
+  p.ema_t[i] = t;
+  if (p.ema_shadow) store_from_f(p.ema_shadow, p.ema_shadow_dtype, i, t);
+  if (p.ema_shadow_lo) ((bf16_t*)p.ema_shadow_lo)[i] = bf16_lo(t);
+}
+
 __global__ __launch_bounds__(256) void adamw_kernel(const nrse_adamw_params p) {
   const double ss = p.sumsq ? *p.sumsq : 0.0;
   float coef = 1.f;
@@ -73,6 +85,8 @@ __global__ __launch_bounds__(256) void adamw_kernel(const nrse_adamw_params p) {
   const float bc2s = sqrtf(bc2);
   const float decay = 1.f - p.lr * p.weight_decay;
   const long long n4 = p.n / 4;
+  const long long e4 = p.ema_n / 4;  // whole quads of the fused EMA range
+  const float eom = 1.f - p.ema_decay;
   for (long long q = (long long)blockIdx.x * 256 + threadIdx.x; q < n4; q += (long long)gridDim.x * 256) {
     float4 pv = reinterpret_cast<float4*>(p.p)[q];
     const float4 gv = reinterpret_cast<const float4*>(p.g)[q];
@@ -98,6 +112,24 @@ __global__ __launch_bounds__(256) void adamw_kernel(const nrse_adamw_params p) {
         reinterpret_cast<float4*>(p.p_shadow)[q] = pv;
       }
     }
+    if (p.ema_t) {
+      if (q < e4) {
+        float4 tv = reinterpret_cast<float4*>(p.ema_t)[q];
+        tv.x = ema_mix(tv.x, pv.x, p.ema_decay, eom); tv.y = ema_mix(tv.y, pv.y, p.ema_decay, eom);
+        tv.z = ema_mix(tv.z, pv.z, p.ema_decay, eom); tv.w = ema_mix(tv.w, pv.w, p.ema_decay, eom);
+        reinterpret_cast<float4*>(p.ema_t)[q] = tv;
+        if (p.ema_shadow) {
+          if (p.ema_shadow_dtype == NRSE_BF16) store_bf16x4(p.ema_shadow, p.ema_shadow_lo, q, &tv.x);
+          else reinterpret_cast<float4*>(p.ema_shadow)[q] = tv;
+        }
+      } else if (q == e4) {
+        // the quad holding the EMA range's end: its first ema_n - 4 q elements, from this thread's
+        // updated registers
+#pragma unroll
+        for (int e = 0; e < 3; ++e)
+          if (4 * q + e < p.ema_n) ema_one(p, 4 * q + e, pa[e], eom);
+      }
+    }
   }
   for (long long i = n4 * 4 + (long long)blockIdx.x * 256 + threadIdx.x; i < p.n; i += (long long)gridDim.x * 256) {
     const float g = p.g[i] * coef;
@@ -108,6 +140,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(const nrse_adamw_params p) {
     p.p[i] = w - step_size * p.m[i] / denom;
     if (p.p_shadow) store_from_f(p.p_shadow, p.shadow_dtype, i, p.p[i]);
     if (p.p_shadow_lo) ((bf16_t*)p.p_shadow_lo)[i] = bf16_lo(p.p[i]);
+    if (p.ema_t && i < p.ema_n) ema_one(p, i, p.p[i], eom);
   }
 }
 
@@ -119,8 +152,8 @@ __global__ __launch_bounds__(256) void ema_kernel(float* __restrict__ t, const f
   for (long long q = (long long)blockIdx.x * 256 + threadIdx.x; q < n4; q += (long long)gridDim.x * 256) {
     float4 tv = reinterpret_cast<float4*>(t)[q];
     const float4 ov = reinterpret_cast<const float4*>(o)[q];
-    tv.x = decay * tv.x + om * ov.x; tv.y = decay * tv.y + om * ov.y;
-    tv.z = decay * tv.z + om * ov.z; tv.w = decay * tv.w + om * ov.w;
+    tv.x = ema_mix(tv.x, ov.x, decay, om); tv.y = ema_mix(tv.y, ov.y, decay, om);
+    tv.z = ema_mix(tv.z, ov.z, decay, om); tv.w = ema_mix(tv.w, ov.w, decay, om);
     reinterpret_cast<float4*>(t)[q] = tv;
     if (ts) {
       if (sdt == NRSE_BF16) {
@@ -131,7 +164,7 @@ __global__ __launch_bounds__(256) void ema_kernel(float* __restrict__ t, const f
     }
   }
   for (long long i = n4 * 4 + (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
-    t[i] = decay * t[i] + om * o[i];
+    t[i] = ema_mix(t[i], o[i], decay, om);
     if (ts) store_from_f(ts, sdt, i, t[i]);
     if (tlo) ((bf16_t*)tlo)[i] = bf16_lo(t[i]);
   }
@@ -189,6 +222,11 @@ extern "C" int nrse_adamw(const nrse_adamw_params* p, void* stream) {
                "nrse_adamw: buffers must be 16-byte aligned");
   NRSE_REQUIRE(!p->p_shadow_lo || (p->p_shadow && p->shadow_dtype == NRSE_BF16 && ((uintptr_t)p->p_shadow_lo & 7) == 0),
                "nrse_adamw: p_shadow_lo needs a bf16 p_shadow and 8-byte alignment");
+  NRSE_REQUIRE(!p->ema_t || (p->ema_n >= 0 && p->ema_n <= p->n && ((uintptr_t)p->ema_t & 15) == 0),
+               "nrse_adamw: ema_t needs ema_n <= n and 16-byte alignment");
+  NRSE_REQUIRE(!p->ema_shadow_lo ||
+                   (p->ema_shadow && p->ema_shadow_dtype == NRSE_BF16 && ((uintptr_t)p->ema_shadow_lo & 7) == 0),
+               "nrse_adamw: ema_shadow_lo needs a bf16 ema_shadow and 8-byte alignment");
   if (p->n == 0) return NRSE_OK;
   hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(p->n)), dim3(256), 0, (hipStream_t)stream, *p);
   return nrse_check_launch("nrse_adamw");

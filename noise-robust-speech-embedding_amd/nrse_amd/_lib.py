@@ -106,7 +106,8 @@ class AdamWParams(ctypes.Structure):
     _fields_ = [("p", c_vp), ("g", c_vp), ("m", c_vp), ("v", c_vp), ("p_shadow", c_vp), ("shadow_dtype", c_int),
                 ("n", c_ll), ("lr", c_f), ("beta1", c_f), ("beta2", c_f), ("eps", c_f), ("weight_decay", c_f),
                 ("step", c_int), ("max_norm", c_f), ("sumsq", c_vp), ("grad_scale", c_f),
-                ("p_shadow_lo", c_vp)]
+                ("p_shadow_lo", c_vp), ("ema_t", c_vp), ("ema_shadow", c_vp), ("ema_shadow_lo", c_vp),
+                ("ema_shadow_dtype", c_int), ("ema_decay", c_f), ("ema_n", c_ll)]
 
 
 _P = ctypes.POINTER

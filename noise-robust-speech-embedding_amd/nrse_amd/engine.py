@@ -61,6 +61,9 @@ _GATE_INTO_LN = os.environ.get("NRSE_GATE_INTO_LN", "1") != "0"
 # (nrse_attn_dropout_mask); opt-in with NRSE_MASK_AHEAD=1: the mask kernel (29 us) costs more
 # than the forward saves (73 -> 58 us) when the two views already overlap (step 552 vs 554 pairs/s)
 _MASK_AHEAD = os.environ.get("NRSE_MASK_AHEAD", "0") == "1"
+# the target EMA in the AdamW pass (nrse_adamw_params.ema_t) instead of a second pass re-reading
+# the updated weights (nrse_ema); NRSE_FUSED_EMA=0 restores the two launches (A/B)
+_FUSED_EMA = os.environ.get("NRSE_FUSED_EMA", "1") != "0"
 
 
 @dataclass
@@ -1016,8 +1019,13 @@ class ByolEngine:
                   step=self.step_count, max_norm=c.max_norm, sumsq_buf=self.sumsq_buf, grad_scale=grad_scale)
         ne = self.layout.ema_numel
         if not c.overlap_optimizer:
-            K.adamw(self.online, self.grad, self.m, self.v, self.online_sh, shadow_lo=self.online_lo, **kw)
-            K.ema(self.target, self.online[:ne], self.target_sh, c.ema_decay, shadow_lo=self.target_lo)
+            if _FUSED_EMA:
+                K.adamw(self.online, self.grad, self.m, self.v, self.online_sh, shadow_lo=self.online_lo,
+                        ema_t=self.target, ema_shadow=self.target_sh, ema_shadow_lo=self.target_lo,
+                        ema_decay=c.ema_decay, **kw)
+            else:
+                K.adamw(self.online, self.grad, self.m, self.v, self.online_sh, shadow_lo=self.online_lo, **kw)
+                K.ema(self.target, self.online[:ne], self.target_sh, c.ema_decay, shadow_lo=self.target_lo)
             self._opt_events = self._opt_done = None
             return
         main = torch.cuda.current_stream(self.dev)
@@ -1030,11 +1038,15 @@ class ByolEngine:
         with torch.cuda.stream(st):
             for s, e in self._segments:
                 if e > s:
+                    te = min(e, ne)
+                    fuse = _FUSED_EMA and te > s
                     K.adamw(self.online[s:e], self.grad[s:e], self.m[s:e], self.v[s:e],
                             sh[s:e] if sh is not None else None, shadow_lo=slo[s:e] if slo is not None else None,
-                            **kw)
-                    te = min(e, ne)
-                    if te > s:
+                            ema_t=self.target[s:te] if fuse else None,
+                            ema_shadow=tsh[s:te] if fuse and tsh is not None else None,
+                            ema_shadow_lo=tlo[s:te] if fuse and tlo is not None else None,
+                            ema_decay=c.ema_decay, **kw)
+                    if te > s and not fuse:
                         K.ema(self.target[s:te], self.online[s:te], tsh[s:te] if tsh is not None else None,
                               c.ema_decay, shadow_lo=tlo[s:te] if tlo is not None else None)
                 ev = torch.cuda.Event()

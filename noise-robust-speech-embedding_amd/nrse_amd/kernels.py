@@ -667,12 +667,18 @@ def sumsq(x, out):
 
 
 def adamw(p, g, m, v, shadow, *, lr, beta1, beta2, eps, weight_decay, step, max_norm, sumsq_buf, grad_scale=1.0,
-          shadow_lo=None):
+          shadow_lo=None, ema_t=None, ema_shadow=None, ema_shadow_lo=None, ema_decay=0.0):
     """clip + AdamW; shadow (bf16/f32) gets the updated weights, shadow_lo (bf16, with a bf16
-    shadow) the split-weight mode's lo plane bf16(p - shadow)."""
+    shadow) the split-weight mode's lo plane bf16(p - shadow). ema_t (f32, numel <= p's): the
+    target EMA of the first ema_t.numel() updated weights in the same pass (as ema() after)."""
+    if ema_t is not None:
+        assert ema_t.dtype == torch.float32 and ema_t.numel() <= p.numel()
     prm = AdamWParams(ptr(p), ptr(g), ptr(m), ptr(v), ptr(shadow),
                       dtype_code(shadow) if shadow is not None else 0, p.numel(), lr, beta1, beta2, eps,
-                      weight_decay, step, max_norm, ptr(sumsq_buf), grad_scale, ptr(shadow_lo))
+                      weight_decay, step, max_norm, ptr(sumsq_buf), grad_scale, ptr(shadow_lo),
+                      ptr(ema_t), ptr(ema_shadow), ptr(ema_shadow_lo),
+                      dtype_code(ema_shadow) if ema_shadow is not None else 0, ema_decay,
+                      ema_t.numel() if ema_t is not None else 0)
     _call("nrse_adamw", ctypes.byref(prm), stream_ptr())
 
 

@@ -290,6 +290,39 @@ def test_adamw_clip_ema(nrse_device):
         assert torch.equal(hi, h2) and torch.equal(lo, l2)
 
 
+def test_adamw_fused_ema_matches_two_passes(nrse_device):
+    """The target EMA fused into the AdamW pass (nrse_adamw_params.ema_t) equals nrse_adamw followed
+    by nrse_ema on the updated weights, bit for bit, with the EMA range ending inside a float4 quad,
+    on a quad boundary, and in the scalar tail; shadows (bf16 and split-plane) included."""
+    from nrse_amd import kernels as K
+    dev = nrse_device
+    n = 100_003
+    g = torch.randn(n, device=dev) * 3
+    ss = torch.zeros(1, device=dev, dtype=torch.float64)
+    K.sumsq(g, ss)
+    kw = dict(lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=1e-2, step=3, max_norm=1.0, sumsq_buf=ss)
+    base = torch.randn(n, device=dev)
+    m0, v0 = torch.randn(n, device=dev) * 0.1, torch.rand(n, device=dev) * 0.01
+    t0 = torch.randn(n, device=dev)
+    for ne, split in ((n, False), (n - 1, True), (4 * 11111, False), (4 * 11111 + 3, True), (4 * 25000 + 2, False)):
+        outs = []
+        for fused in (False, True):
+            p, m, v, t = base.clone(), m0.clone(), v0.clone(), t0[:ne].clone()
+            sh = torch.empty(n, device=dev, dtype=torch.bfloat16)
+            tsh = torch.empty(ne, device=dev, dtype=torch.bfloat16)
+            lo = torch.empty_like(sh) if split else None
+            tlo = torch.empty_like(tsh) if split else None
+            if fused:
+                K.adamw(p, g, m, v, sh, shadow_lo=lo, ema_t=t, ema_shadow=tsh, ema_shadow_lo=tlo, ema_decay=0.997,
+                        **kw)
+            else:
+                K.adamw(p, g, m, v, sh, shadow_lo=lo, **kw)
+                K.ema(t, p[:ne], tsh, 0.997, shadow_lo=tlo)
+            outs.append((p, m, v, t, sh, tsh) + ((lo, tlo) if split else ()))
+        for a, b in zip(*outs):
+            assert torch.equal(a, b), (ne, split)
+
+
 def test_snr_mix_matches_reference_fixture(nrse_device):
     from nrse_amd import kernels as K
     z = np.load(os.path.join(GOLD, "snr_mix.npz"))
