@@ -21,13 +21,13 @@ clean = clean.cuda()
 
 
 def b_loss():
-    pred, tproj, _ = eb.forward(clean, noisy, train=True, step_seed=100, need_grad=True)
+    pred, tproj, ctx = eb.forward(clean, noisy, train=True, step_seed=100, need_grad=True)
     loss = torch.zeros(1, device="cuda")
     K.byol_loss(pred, tproj, loss, torch.empty_like(pred), None)
-    return loss
+    return loss, pred, tproj, ctx["emb"]
 
 
-ref = b_loss().clone()
+ref = [t.clone() for t in b_loss()]
 torch.cuda.synchronize()
 trials = int(os.environ.get("TRIALS", "8"))
 for mode in os.environ.get("MODES", "default,ovl,sync,serial").split(","):
@@ -38,9 +38,11 @@ for mode in os.environ.get("MODES", "default,ovl,sync,serial").split(","):
         if mode in ("sync", "syncserial"):
             ea.sync_optimizer(); torch.cuda.synchronize()
         E._SERIAL_TARGET = mode in ("serial", "syncserial")
-        lb = b_loss()
+        out = b_loss()
         E._SERIAL_TARGET = False
         torch.cuda.synchronize()
-        if not torch.equal(lb, ref):
-            bad.append(float(lb) - float(ref))
-    print(f"{mode}: {len(bad)} of {trials} differ {bad[:4]}", flush=True)
+        if not torch.equal(out[0], ref[0]):
+            # which view: online pred / online embedding (main stream), target projection (side)
+            bad.append("".join(n for n, a, r in zip(("P", "T", "E"), out[1:], ref[1:]) if not torch.equal(a, r)))
+    print(f"{mode}: {len(bad)} of {trials} differ {bad[:8]} (P online pred, T target proj, E online emb)",
+          flush=True)
