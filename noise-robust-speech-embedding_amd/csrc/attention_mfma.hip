@@ -136,6 +136,15 @@ NRSE_DEV void kv_dma_issue(const KvDma& d, char* tile, int row0, int wave) {
 // Tp + 64 entries cover every read (Tp = T rounded up to the 64-key tile); the fwd kernel's LDS
 // is then 32 KB of K/V tiles + 4 (Tp + 64) floats = 40 KB at T = 399: 4 workgroups per CU.
 __host__ __device__ inline int bv_len(int T) { return ((T + 63) & ~63) + 64; }
+// Inside copy s, segment element j sits at bv_pos(j, s): rotated by 16 s within its 64-float
+// block (a 256-B bank row). One ds_read_b128 lane group reads 3 aligned positions 4-12 floats
+// apart from all 4 copies; with the copies one bank row apart and unrotated, the 4 copies of a
+// position were 4 addresses on the same 4 banks, a 4-way conflict. Rotated by 4 slots per copy,
+// the 12 addresses take 12 distinct 16-B slots (PMC, profiles/r04_s3_attn_lds_pmc.txt:
+// SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE 0.368 -> 0.0 forward, 0.296 -> 0.0 dQ, 0.302 -> 0.19
+// dK/dV; time unchanged, the kernels are VALU-bound). An aligned float4 never straddles a block,
+// and bv_pos(j + 64 m, s) = bv_pos(j, s) + 64 m: a lane keeps one offset per 16-key sub-tile.
+__host__ __device__ inline int bv_pos(int j, int s) { return (j & ~63) | ((j + 16 * s) & 63); }
 NRSE_DEV void bv_stage(float* bv, const float* vec, int T, int q0, int tid) {
   const int len = bv_len(T), nd = 2 * T - 1;
   const int e_lo = T - 1 - q0 - 63;
@@ -143,7 +152,7 @@ NRSE_DEV void bv_stage(float* bv, const float* vec, int T, int q0, int tid) {
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int e = e_lo + j + s;
-      bv[s * len + j] = (e >= 0 && e < nd) ? vec[e] : 0.f;
+      bv[s * len + bv_pos(j, s)] = (e >= 0 && e < nd) ? vec[e] : 0.f;
     }
   }
 }
@@ -195,7 +204,10 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
   const int bvl = bv_len(T);
   const int u00 = 4 * g + 63 - (w * 16 + i16);
   const int bsel = u00 & 3;
-  const float* bvl_base = bv + bsel * bvl + (u00 - bsel);
+  const float* bvl_base = bv + bsel * bvl;  // copy bsel, rotated as bv_pos
+  int boff[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) boff[t] = bv_pos(u00 - bsel + 16 * t, bsel);
   const uint32_t key = site_key(p.seed);
   const uint32_t thr = dropout_threshold16(p.dropout_p);
   constexpr bool drop = DROP;
@@ -254,7 +266,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
     const f32x2 c12 = {c1, c1}, gl2 = {gl, gl}, nm2 = {-mref, -mref};
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const float4 bb = *reinterpret_cast<const float4*>(bvl_base + kb + 16 * t);
+      const float4 bb = *reinterpret_cast<const float4*>(bvl_base + kb + boff[t]);
       const f32x2 r0 = pk_fma(f32x2{s[t][0], s[t][1]}, c12, pk_fma(gl2, f32x2{bb.x, bb.y}, nm2));
       const f32x2 r1 = pk_fma(f32x2{s[t][2], s[t][3]}, c12, pk_fma(gl2, f32x2{bb.z, bb.w}, nm2));
       v[t][0] = r0.x; v[t][1] = r0.y; v[t][2] = r1.x; v[t][3] = r1.y;
@@ -407,7 +419,10 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
   const int bvl = bv_len(T);
   const int u00 = 4 * g + 63 - (w * 16 + i16);
   const int bsel = u00 & 3;
-  const float* bvl_base = bv + bsel * bvl + (u00 - bsel);
+  const float* bvl_base = bv + bsel * bvl;  // copy bsel, rotated as bv_pos
+  int boff[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) boff[t] = bv_pos(u00 - bsel + 16 * t, bsel);
   const uint32_t key = site_key(p.seed);
   const uint32_t thr = dropout_threshold16(p.dropout_p);
   constexpr bool drop = DROP;
@@ -455,7 +470,7 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
     float ds[4][4], bb[4][4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const float4 v4 = *reinterpret_cast<const float4*>(bvl_base + kb + 16 * t);
+      const float4 v4 = *reinterpret_cast<const float4*>(bvl_base + kb + boff[t]);
       bb[t][0] = v4.x; bb[t][1] = v4.y; bb[t][2] = v4.z; bb[t][3] = v4.w;
     }
     if constexpr (DROP) {
@@ -577,7 +592,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   }
   // bias of (query q, key kj) = vec[kj - q + T - 1]: reversed copies, copy s index j holds
   // log2e * vec[e_hi - j - s], e_hi = kb0 + 63 + T - 1; element (q, kj) sits at segment index
-  // u = 63 - kl + q, so a lane's 4 consecutive queries are one aligned float4 of copy (u & 3).
+  // u = 63 - kl + q, so a lane's 4 consecutive queries are one aligned float4 of copy (u & 3)
+  // (stored at bv_pos(j, s) within the copy, as the forward's copies).
   {
     const float* vec = p.bias_vec + (long long)h * (2 * T - 1);
     const int nd = 2 * T - 1, e_hi = kb0 + 63 + T - 1;
@@ -585,7 +601,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 #pragma unroll
       for (int s4 = 0; s4 < 4; ++s4) {
         const int e = e_hi - j - s4;
-        rbv[s4 * bvl + j] = (e >= 0 && e < nd) ? vec[e] * LOG2E : 0.f;
+        rbv[s4 * bvl + bv_pos(j, s4)] = (e >= 0 && e < nd) ? vec[e] * LOG2E : 0.f;
       }
     }
   }
@@ -654,7 +670,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   const int kl = w * 16 + i16;  // key within the 64-key block
   const int u00 = 63 - kl + 4 * g;
   const int bsel = u00 & 3;
-  const float* rb_base = rbv + bsel * bvl + (u00 - bsel);
+  const float* rb_base = rbv + bsel * bvl;  // copy bsel, rotated as bv_pos
+  int boff[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) boff[t] = bv_pos(u00 - bsel + 16 * t, bsel);
   f32x4 dk[4], dv[4];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) dk[dt] = dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -695,7 +714,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
       const int ql = qb + 16 * t + 4 * g;
       const float4 l4 = *reinterpret_cast<const float4*>(rowall + ql);
       const float4 g4 = *reinterpret_cast<const float4*>(rowall + 2 * Tp + ql);
-      const float4 b4 = *reinterpret_cast<const float4*>(rb_base + qb + 16 * t);
+      const float4 b4 = *reinterpret_cast<const float4*>(rb_base + qb + boff[t]);
       ds[t][0] = exp2_(fmaf(s[t][0], c1, g4.x * b4.x) - l4.x);  // P (log2 domain)
       ds[t][1] = exp2_(fmaf(s[t][1], c1, g4.y * b4.y) - l4.y);
       ds[t][2] = exp2_(fmaf(s[t][2], c1, g4.z * b4.z) - l4.z);
