@@ -132,9 +132,9 @@ long long nrse_gemm_colsum_workspace(const nrse_gemm_params* p);  /* floats for 
  * staged 128x128, 2 = LDS-DMA 128x128, 3 = LDS-DMA 256x256 (falls back when a problem does not
  * fit it). Process-wide; for tests and benchmarks. Returns the previous setting. */
 int nrse_gemm_select(int generation);
-/* Tile rows of the 256-column LDS-DMA kernel: 0 = automatic (224 when that needs no more tile
- * waves than 256, e.g. M = 12768 = 57 x 224), 256 or 224 to pin one. Process-wide; for tests and
- * benchmarks. Returns the previous setting. */
+/* Tile rows of the 256-column LDS-DMA kernel: 256 (the default) or 224 pins one, 0 = automatic
+ * (224 when that needs no more tile waves than 256, e.g. M = 12768 = 57 x 224: faster alone, slower
+ * beside concurrent streams). Process-wide; for tests and benchmarks. Returns the previous setting. */
 int nrse_gemm_tile_rows(int rows);
 
 /* ------------------------------------------------------------------------------------------

@@ -642,15 +642,23 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
   NRSE_STAMP(7);
 }
 
-// Tile rows for this problem: 224 when it needs no more waves of 256 workgroups (one per CU)
-// than 256-row tiles do -- its tiles are 7/8 the work, so the same number of waves finishes
-// sooner (M = 12768: N = 1024 -> 228 instead of 200 tiles, both one wave). NRSE_GEMM_BM=256 or
-// 224 forces one (A/B measurements).
+// Tile rows: 256 by default. The automatic choice (NRSE_GEMM_BM=0) takes 224 when a problem
+// needs no more waves of 256 workgroups (one per CU) than 256-row tiles do -- its tiles are 7/8
+// the work, so alone on the chip the same number of waves finishes sooner (M = 12768, N = 1024:
+// 228 instead of 200 tiles, both one wave; isolated forward / dgrad / wgrad 3-9 % faster). In the
+// step the GEMMs share the chip with the other view's or stream's kernels, and the fewer, larger
+// tiles leave those CUs: 570.1 / 570.7 vs 553.0 / 553.2 pairs/s same box
+// (profiles/r04_s3_tile_rows_ab.txt). NRSE_GEMM_BM=224 pins the other; nrse_gemm_tile_rows too.
 int g_tile_rows = -1;  // -1: not read yet, 0: automatic, 256 / 224: pinned
 
+int tile_rows_setting() {
+  if (g_tile_rows < 0) g_tile_rows = getenv("NRSE_GEMM_BM") ? atoi(getenv("NRSE_GEMM_BM")) : 256;
+  return g_tile_rows;
+}
+
 int bm_choice(const nrse_gemm_params* p) {
-  if (g_tile_rows < 0) g_tile_rows = getenv("NRSE_GEMM_BM") ? atoi(getenv("NRSE_GEMM_BM")) : 0;
-  if (g_tile_rows == 256 || g_tile_rows == 224) return g_tile_rows;
+  const int pinned = tile_rows_setting();
+  if (pinned == 256 || pinned == 224) return pinned;
   const long long per = (long long)nrse_cdiv(p->N, BN) * p->batch * p->splits;
   const long long w256 = (nrse_cdiv(p->M, 256) * per + 255) / 256;
   const long long w224 = (nrse_cdiv(p->M, 224) * per + 255) / 256;
@@ -672,7 +680,7 @@ int launch(const nrse_gemm_params* p, hipStream_t st) {
 }  // namespace
 
 extern "C" int nrse_gemm_tile_rows(int rows) {
-  const int prev = g_tile_rows < 0 ? 0 : g_tile_rows;
+  const int prev = tile_rows_setting();
   g_tile_rows = (rows == 256 || rows == 224) ? rows : 0;
   return prev;
 }
