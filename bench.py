@@ -112,6 +112,26 @@ def gemm_mfma_busy():
         return None
 
 
+def north_star_parity():
+    """Embedding / prediction rel-L2 of the bf16sw mode against the reference's own outputs at 3 / 8 /
+    12 s (tests/test_large_gpu.py::test_large_bf16sw_matches_reference records, committed under
+    profiles/): the newest round's files."""
+    out = {}
+    for tag in ("3s", "8s", "12s"):
+        for rnd in ("r05", "r04"):
+            path = os.path.join(ROOT, "profiles", f"{rnd}_large_parity_bf16sw_{tag}.json")
+            try:
+                with open(path) as fh:
+                    m = json.load(fh)
+            except (OSError, ValueError):
+                continue
+            out[tag] = {"eval_emb_rel_l2": m.get("eval_emb"), "eval_pred_rel_l2": m.get("eval_pred"),
+                        "eval_tproj_rel_l2": m.get("eval_tproj"), "source": f"profiles/{os.path.basename(path)}"}
+            break
+    out["bound"] = 1e-3
+    return out
+
+
 def bench_emotion(args):
     """configs[3]: one dimensional-emotion fine-tune iteration over the frozen WavLM-Large encoder
     (default_wavlm-large_emotion_dim_ft.yaml: batch 36, 5 s, hidden 1024, dropout 0.3, AdamW
@@ -195,6 +215,8 @@ def main():
                     help="bf16 (the metric's mode), bf16sw (bf16 activations x split hi+lo bf16 weights in the "
                          "forward: embeddings within the north-star 1e-3), f32 (exact parity mode)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-north-star", action="store_true",
+                    help="skip the north-star mode's (bf16sw) second timed run after the bf16 one (N = 1, fixed)")
     ap.add_argument("--detail", default=None, help="write per-shape GEMM timings here (json)")
     ap.add_argument("--serial-optimizer", action="store_true",
                     help="clip/AdamW/EMA on the main stream after backward (default: overlapped per layer "
@@ -225,11 +247,6 @@ def main():
     arch = A.LARGE
     B = args.batch
     L = int(args.seconds * 16000)
-    cdt, wsplit = compute_mode(args.dtype)
-    eng = ByolEngine(arch, 1024, 2048, device=dev, compute_dtype=cdt, seed=1234, weight_split=wsplit,
-                     step_cfg=StepConfig(ema_decay=0.997, overlap_optimizer=not args.serial_optimizer))
-    allreduce = (ddp.GradAllReduce(wire_dtype=torch.bfloat16 if args.wire == "bf16" else None)
-                 if world > 1 else None)
 
     # synthetic pairs resident in HBM: clean ~ N(0, 0.1^2), noise ~ N(0, 1), SNR from the YAML
     gen = torch.Generator(device=dev)
@@ -247,11 +264,6 @@ def main():
     def lr_at(step):  # CosineAnnealingLR(T_max) stepped per iteration (train_byol.py:149-150)
         return 0.5 * 1e-5 * (1 + math.cos(math.pi * step / total_steps))
 
-    def step(i):
-        K.snr_mix(clean_raw, noise_raw, noise_len, snr, clean_iv, noisy_iv, status, kscale, K.SNR_PEAK_ZMUV)
-        return eng.train_step(clean_iv, noisy_iv, lr=lr_at(i), step_seed=i, rank=rank, allreduce=allreduce,
-                              world_size=world)
-
     varlen_batches = None
     if args.workload == "varlen":
         # configs[4]: every step a different length-bucketed batch of 3-12 s pairs, all staged in
@@ -268,6 +280,22 @@ def main():
         if len(varlen_batches) < args.steps + args.warmup:
             raise SystemExit("varlen: not enough bucketed batches for the requested steps")
 
+    def make_engine(mode):
+        cdt, wsplit = compute_mode(mode)
+        # fused_zero_grad: the AdamW pass clears the gradient for the next step (no fill kernel)
+        eng = ByolEngine(arch, 1024, 2048, device=dev, compute_dtype=cdt, seed=1234, weight_split=wsplit,
+                         step_cfg=StepConfig(ema_decay=0.997, overlap_optimizer=not args.serial_optimizer,
+                                             fused_zero_grad=True))
+        return eng, cdt
+
+    def make_step(eng):
+        if varlen_batches is None:
+            def step(i):
+                K.snr_mix(clean_raw, noise_raw, noise_len, snr, clean_iv, noisy_iv, status, kscale, K.SNR_PEAK_ZMUV)
+                return eng.train_step(clean_iv, noisy_iv, lr=lr_at(i), step_seed=i, rank=rank, allreduce=allreduce,
+                                      world_size=world)
+            return step
+
         def step(i):  # noqa: F811
             r = varlen_batches[i % len(varlen_batches)]
             Lb = r["clean"].shape[1]
@@ -275,29 +303,63 @@ def main():
             n = torch.empty(B, Lb, device=dev)
             K.snr_mix(r["clean"], r["noise"], r["noise_len"], r["snr"].float(), c, n, status, kscale, K.SNR_PEAK_ZMUV)
             return eng.train_step(c, n, lr=lr_at(i), step_seed=i, rank=rank, allreduce=allreduce, world_size=world)
+        return step
 
-    for i in range(args.warmup):
+    def serial_probe(eng, step, i):
+        """Roofline probe: the timed region runs GEMMs on up to three streams at once, so its event
+        durations include time shared with the other streams' kernels. One extra step after the
+        timed region runs with the streams serialised (target view, weight gradients and the
+        optimizer on the main stream) and brackets every GEMM launch with HIP events on its launch
+        stream: per-launch durations of the kernels alone, whose sum stays below the step time."""
+        from nrse_amd import engine as E
+        serial_prev, overlap_prev = E._SERIAL_TARGET, eng.cfg.overlap_optimizer
+        E._SERIAL_TARGET, eng.cfg.overlap_optimizer = True, False
+        eng.sync_optimizer()
+        torch.cuda.synchronize()
+        sprobe = []
+        ts0 = time.perf_counter()
+        K.set_gemm_probe(sprobe)
         step(i)
-    torch.cuda.synchronize()
-    # N > 1: events around each step's all-reduce wait (end of backward -> every exchange done)
-    eng.ar_timing = world > 1
-    eng.ar_events = []
-    executed = [0, 0]
-    probe = []
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    sent = 0
-    for i in range(args.steps):
-        step(args.warmup + i)
-        executed[0] += eng.executed_layers[0]
-        executed[1] += eng.executed_layers[1]
-        sent += allreduce.issued_elems if allreduce is not None else 0
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    dt = time.perf_counter() - t0
+        K.set_gemm_probe(None)
+        torch.cuda.synchronize()
+        sdt_ms = (time.perf_counter() - ts0) * 1e3
+        sbytes = K.gemm_probe_bytes()
+        E._SERIAL_TARGET, eng.cfg.overlap_optimizer = serial_prev, overlap_prev
+        s_gflops = sum(f for f, _, _, _ in sprobe)
+        s_ms = sum(e0.elapsed_time(e1) for _, e0, e1, _ in sprobe)
+        return dict(gflops=s_gflops, ms=s_ms, bytes=sum(sbytes), launches=len(sprobe), step_ms=sdt_ms)
+
+    def timed(eng, step):
+        """W untimed warm-up steps, then EXACTLY K steps bracketed by a barrier + device sync on both
+        sides (max over ranks for N > 1)."""
+        for i in range(args.warmup):
+            step(i)
+        torch.cuda.synchronize()
+        # N > 1: events around each step's all-reduce wait (end of backward -> every exchange done)
+        eng.ar_timing = world > 1
+        eng.ar_events = []
+        executed = [0, 0]
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        sent = 0
+        for i in range(args.steps):
+            step(args.warmup + i)
+            executed[0] += eng.executed_layers[0]
+            executed[1] += eng.executed_layers[1]
+            sent += allreduce.issued_elems if allreduce is not None else 0
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        dt = time.perf_counter() - t0
+        return dt, executed, sent
+
+    allreduce = (ddp.GradAllReduce(wire_dtype=torch.bfloat16 if args.wire == "bf16" else None)
+                 if world > 1 else None)
+    eng, cdt = make_engine(args.dtype)
+    step = make_step(eng)
+    dt, executed, sent = timed(eng, step)
     ddp_stats = None
     if world > 1:
         # multi-rank readiness record (VERDICT r03 #6): each rank's time per step, the exposed
@@ -321,6 +383,7 @@ def main():
     # In-step GEMM durations: one extra step after the timed region, streams overlapped as in the
     # timed steps, with HIP events around every GEMM launch (kept out of the timed region: the
     # event records cost ~2 % of a step when every launch is bracketed)
+    probe = []
     tp0 = time.perf_counter()
     K.set_gemm_probe(probe)
     step(args.warmup + args.steps)
@@ -329,30 +392,10 @@ def main():
     probe_step_ms = (time.perf_counter() - tp0) * 1e3
     loss = float(eng.loss_buf)
     st_ok = int((status == 0).sum())
-    # Roofline probe: the timed region runs GEMMs on up to three streams at once, so its event
-    # durations include time shared with the other streams' kernels. One extra step after the
-    # timed region runs with the streams serialised (target view, weight gradients and the
-    # optimizer on the main stream) and brackets every GEMM launch with HIP events on its launch
-    # stream: per-launch durations of the kernels alone, whose sum stays below the step time.
-    from nrse_amd import engine as E
-    serial_prev, overlap_prev = E._SERIAL_TARGET, eng.cfg.overlap_optimizer
-    E._SERIAL_TARGET, eng.cfg.overlap_optimizer = True, False
-    eng.sync_optimizer()
-    torch.cuda.synchronize()
-    sprobe = []
-    ts0 = time.perf_counter()
-    K.set_gemm_probe(sprobe)
-    step(args.warmup + args.steps + 1)
-    K.set_gemm_probe(None)
-    torch.cuda.synchronize()
-    sdt_ms = (time.perf_counter() - ts0) * 1e3
-    sbytes = K.gemm_probe_bytes()
-    E._SERIAL_TARGET, eng.cfg.overlap_optimizer = serial_prev, overlap_prev
-    s_gflops = sum(f for f, _, _, _ in sprobe)
-    s_ms = sum(e0.elapsed_time(e1) for _, e0, e1, _ in sprobe)
+    sp = serial_probe(eng, step, args.warmup + args.steps + 1)
+    s_gflops, s_ms, sdt_ms = sp["gflops"], sp["ms"], sp["step_ms"]
     # live roofline of the dominant kernel family (nrse_gemm, MFMA-bound)
     gflops = sum(f for f, _, _, _ in probe)
-    gbytes = sum(b for b in K.gemm_probe_bytes())
     gms = sum(e0.elapsed_time(e1) for _, e0, e1, _ in probe)
     n_launch = len(probe)
     achieved_tfs = gflops / (gms * 1e-3) / 1e12 if gms > 0 else 0.0
@@ -398,8 +441,8 @@ def main():
                      "achieved": round(s_achieved, 1), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(s_achieved / peak, 4),
                      "traffic": gemm_traffic(), "traffic_unit": f"HBM bytes per GEMM launch (PMC, profiles/{TRAFFIC_FILE})",
-                     "algorithmic_bytes_per_launch": round(sum(sbytes) / max(len(sprobe), 1)),
-                     "avg_launch_ms": round(s_ms / max(len(sprobe), 1), 4), "launches": len(sprobe),
+                     "algorithmic_bytes_per_launch": round(sp["bytes"] / max(sp["launches"], 1)),
+                     "avg_launch_ms": round(s_ms / max(sp["launches"], 1), 4), "launches": sp["launches"],
                      "gemm_tflop_per_step": round(s_gflops / 1e12, 3), "gemm_ms_per_step": round(s_ms, 3),
                      "probe_step_ms": round(sdt_ms, 2), "gemm_share_of_step": round(s_ms / sdt_ms, 3),
                      "mfma_busy_pmc": gemm_mfma_busy(),
@@ -413,6 +456,33 @@ def main():
         **({"ddp": ddp_stats} if ddp_stats is not None else {}),
         "loss_last": round(loss, 5), "snr_mix_ok": st_ok,
     }
+    if (world == 1 and varlen_batches is None and args.dtype == "bf16" and not args.no_north_star):
+        # the north-star mode (embeddings within 1e-3 of the reference) timed by the
+        # same process, same steps and warm-up, after the metric's bf16 run
+        del eng, step, probe
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        eng2, _ = make_engine("bf16sw")
+        step2 = make_step(eng2)
+        dt2, executed2, _ = timed(eng2, step2)
+        sp2 = serial_probe(eng2, step2, args.warmup + args.steps)
+        a2 = sp2["gflops"] / (sp2["ms"] * 1e-3) / 1e12 if sp2["ms"] > 0 else 0.0
+        result["north_star_mode"] = {
+            "dtype": "bf16sw", "value": round(pairs / dt2, 3), "unit": "pairs/s",
+            "ms_per_step": round(dt2 / args.steps * 1e3, 2), "steps": args.steps, "warmup": args.warmup,
+            "what": "bf16 activations; forward GEMMs against the split weight: bf16 hi plane + the fp8 correction "
+                    "x8 (w - w_hi)8 2^-e on the MX-scaled fp8 MFMA (layers' QKV / FFN), bf16 lo plane elsewhere "
+                    "(DESIGN.md §6)" if eng2.online_lo8 is not None else
+                    "bf16 activations; forward GEMMs against the split hi + lo bf16 weight planes (DESIGN.md §6)",
+            "roofline": {"bound": "mfma", "achieved": round(a2, 1), "peak": BF16_DENSE_PEAK_TFS, "unit": "TFLOP/s",
+                         "frac": round(a2 / BF16_DENSE_PEAK_TFS, 4), "launches": sp2["launches"],
+                         "gemm_tflop_per_step_bf16_equivalent": round(sp2["gflops"] / 1e12, 3),
+                         "gemm_ms_per_step": round(sp2["ms"], 3), "probe_step_ms": round(sp2["step_ms"], 2),
+                         "note": "serial probe as the main line's; fp8 segments count half their FLOPs (2x the bf16 "
+                                 "MFMA rate)"},
+            "parity_vs_reference": north_star_parity(),
+            "loss_last": round(float(eng2.loss_buf), 5),
+        }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(A.LARGE)
     if rank == 0:

@@ -34,7 +34,9 @@ typedef enum {
   NRSE_ERR_UNSUPPORTED = -5 /* configuration outside what the kernels implement */
 } nrse_status;
 
-typedef enum { NRSE_F32 = 0, NRSE_BF16 = 1, NRSE_BF16X3 = 2 } nrse_dtype;
+typedef enum { NRSE_F32 = 0, NRSE_BF16 = 1, NRSE_BF16X3 = 2, NRSE_FP8 = 3 } nrse_dtype;
+/* NRSE_FP8 (ABI 6): OCP fp8 e4m3fn (gfx950's native fp8), one byte per element, saturated at +-448;
+ * the split-weight mode's correction operands (nrse_gemm_params.a8 / b8). */
 /* NRSE_BF16X3 (an OUTPUT format of nrse_layernorm_fwd and nrse_conv0_fwd only): the split-bf16
  * activation of the split-weight mode's conv stack, three bf16 planes of n = rows * C elements
  * each at the output pointer: [hi | lo | hi], hi = bf16(y), lo = bf16(y - hi). A GEMM that reads
@@ -124,6 +126,21 @@ typedef struct {
   /* optional f32 workspace of nrse_gemm_colsum_workspace(p) floats (COLSUM): the
    * per-tile column sums are then added in a fixed order (deterministic) instead of by atomics */
   float* colsum_part;
+  /* ABI 6, the split-weight mode's fp8 correction segments: after the nseg bf16 segments, nseg8
+   * more K segments of K elements each whose operands a8 / b8 are NRSE_FP8, k-contiguous (ld,
+   * seg_stride, z1, z2 in bytes = elements), multiplied on the MX-scaled MFMA
+   * (v_mfma_scale_f32_16x16x128_f8f6f4, 2x the bf16 rate) with B scaled by 2^-b8_exp:
+   *   C[m,n] = epilogue( alpha * (sum_bf16 + 2^-b8_exp * sum_{s<nseg8, k<K} a8(m,k) b8(n,k)) ).
+   * Requires the 256x256 kernel's conditions, K % 128 == 0, splits == 1, 16-byte aligned a8 / b8
+   * with ld, seg_stride, z1, z2 multiples of 16; nseg8 = 0 (or zeroed trailing fields): none. */
+  nrse_gemm_operand a8, b8;
+  int nseg8;
+  int b8_exp;
+  /* ABI 6: optional fp8 copy of a bf16 output, written beside C by the register epilogues of the
+   * 256x256 kernel: c8[m * ldc8 + n] = fp8(bf16 C[m, n]) (the next GEMM's a8 operand: FFN-up's
+   * GELU output feeding FFN-down's correction segment). ldc8 % 16 == 0, 16-byte aligned. */
+  void* c8;
+  long long ldc8;
 } nrse_gemm_params;
 
 int nrse_gemm(const nrse_gemm_params* p, void* stream);
@@ -157,6 +174,9 @@ typedef struct {
   void* y; int y_dtype;
   float* mean; float* rstd;
   long long rows; int C; float eps; int flags;
+  /* ABI 6, optional (bf16 y): y8 [rows, C] NRSE_FP8 = fp8(bf16 y), the next GEMM's a8 operand
+   * (split-weight mode); 16-byte aligned */
+  void* y8;
 } nrse_ln_fwd_params;
 
 typedef struct {
@@ -267,10 +287,11 @@ typedef struct {
   int batch, T, H, head_dim;
   float scale; float dropout_p; uint32_t seed;
   const float* bias_vec;               /* [H, 2T-1] (bf16 MFMA path) */
-  const uint16_t* drop_mask;           /* optional: the forward's keep bits (nrse_attn_fwd_params) */
   float* diag_part;                    /* optional: f32 workspace of nrse_attn_bwd_workspace(p)
                                           floats; the per-block diag rows are then added in a fixed
                                           order (deterministic) instead of by f32 atomics */
+  const uint16_t* drop_mask;           /* optional (ABI 6: trailing, after diag_part): the forward's
+                                          keep bits (nrse_attn_fwd_params.drop_mask); NULL re-hashes */
 } nrse_attn_bwd_params;
 
 int nrse_attn_fwd(const nrse_attn_fwd_params* p, void* stream);
@@ -357,6 +378,13 @@ int nrse_cast(const void* x, int x_dtype, void* y, int y_dtype, long long n, voi
 /* split-bf16 pair of an f32 tensor: hi = bf16(x), lo = bf16(x - hi) (the split-weight mode's GEMM
  * operand planes: x @ (hi + lo) carries the f32 weight to ~2^-17 relative) */
 int nrse_split_bf16(const float* x, void* hi, void* lo, long long n, void* stream);
+/* ABI 6: the fp8 correction plane of the same split: lo8[i] = fp8((x[i] - bf16(x[i])) * 2^lo8_exp)
+ * (NRSE_FP8, saturated), as nrse_adamw_params.p_shadow_lo8 writes it */
+int nrse_split_lo8(const float* x, void* lo8, int lo8_exp, long long n, void* stream);
+/* ABI 6: y8[i] = fp8(x[i]) of a bf16 / f32 tensor (NRSE_FP8, saturated at +-448), n elements */
+int nrse_cast_fp8(const void* x, int x_dtype, void* y8, long long n, void* stream);
+/* ABI 6: dst[i] = 0 for i < n floats (the step's small accumulators: no torch fill kernel) */
+int nrse_zero(float* dst, long long n, void* stream);
 /* Split-K reduction of a weight gradient (the Linear wgrads of the backward, train_byol.py:65):
  * dst[i] (+)= sum_s slabs[s * n + i], s = 0 .. splits-1, in split order (deterministic); f32;
  * accumulate = 0 overwrites dst. The partial slabs are written by nrse_gemm with c_split = n. */
@@ -450,6 +478,15 @@ typedef struct {
   int ema_shadow_dtype;
   float ema_decay;
   long long ema_n;
+  /* ABI 6, optional: the split-weight mode's fp8 correction planes (NRSE_FP8, one byte per weight):
+   * p_shadow_lo8[i] = fp8((p_new[i] - bf16(p_new[i])) * 2^lo8_exp), ema_shadow_lo8 likewise for the
+   * EMA target (i < ema_n); the nrse_gemm b8 operand with b8_exp = lo8_exp */
+  void* p_shadow_lo8;
+  void* ema_shadow_lo8;
+  int lo8_exp;
+  /* ABI 6, optional: nonzero stores 0 to every g[i] after reading it, so the gradient buffer is
+   * zeroed for the next step's accumulation inside this pass (no separate fill over g) */
+  int zero_grad;
 } nrse_adamw_params;
 int nrse_adamw(const nrse_adamw_params* p, void* stream);
 /* t_shadow_lo: optional, as nrse_adamw_params.p_shadow_lo */

@@ -55,6 +55,35 @@ NRSE_DEV void store4_out(void* p, int dt, long long i, long long plane, const fl
   }
 }
 
+// OCP fp8 e4m3fn (NRSE_FP8, gfx950's native fp8): v_cvt_pk_fp8_f32 rounds to nearest even; the
+// inputs are clamped to the largest finite value first (+-448), so out-of-range values saturate
+// instead of becoming NaN. fp8x4 packs a, b, c, d into bytes 0..3 (little-endian element order).
+NRSE_DEV uint32_t fp8x4(float a, float b, float c, float d) {
+  a = __builtin_amdgcn_fmed3f(a, -448.f, 448.f);
+  b = __builtin_amdgcn_fmed3f(b, -448.f, 448.f);
+  c = __builtin_amdgcn_fmed3f(c, -448.f, 448.f);
+  d = __builtin_amdgcn_fmed3f(d, -448.f, 448.f);
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+  return (uint32_t)w;
+}
+NRSE_DEV unsigned char fp8_1(float a) { return (unsigned char)(fp8x4(a, 0.f, 0.f, 0.f) & 0xffu); }
+// the split-weight mode's fp8 correction of x (nrse_split_lo8): (x - bf16(x)) * sc, sc = 2^lo8_exp
+NRSE_DEV float lo_resid(float x) { return x - __uint_as_float((uint32_t)f2bf(x) << 16); }
+// fp8 of 4 values as they are stored in bf16 (the a8 operand is fp8(bf16 y), one rounding path)
+NRSE_DEV uint32_t fp8x4_of_bf(const float* o) {
+  return fp8x4(bf2f(f2bf(o[0])), bf2f(f2bf(o[1])), bf2f(f2bf(o[2])), bf2f(f2bf(o[3])));
+}
+// 8 packed bf16 (a 16-B row chunk) -> 8 fp8 bytes
+NRSE_DEV uint2 fp8x8_from_bf16x8(uint4 u) {
+  uint2 r;
+  r.x = fp8x4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+              __uint_as_float(u.y & 0xffff0000u));
+  r.y = fp8x4(__uint_as_float(u.z << 16), __uint_as_float(u.z & 0xffff0000u), __uint_as_float(u.w << 16),
+              __uint_as_float(u.w & 0xffff0000u));
+  return r;
+}
+
 template <typename T> NRSE_DEV float to_f(T x);
 template <> NRSE_DEV float to_f<float>(float x) { return x; }
 template <> NRSE_DEV float to_f<bf16_t>(bf16_t x) { return bf2f(x); }

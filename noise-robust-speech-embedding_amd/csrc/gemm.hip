@@ -25,6 +25,7 @@ int nrse_posconv(const nrse_gemm_params* p, hipStream_t st);
 bool nrse_posconv_wgrad_ok(const nrse_gemm_params* p);
 int nrse_posconv_wgrad(const nrse_gemm_params* p, hipStream_t st);
 bool nrse_gemm256_ok(const nrse_gemm_params* p);         // gemm256.hip
+bool nrse_gemm256_f8_ok(const nrse_gemm_params* p);
 long long nrse_gemm256_tiles(const nrse_gemm_params* p);
 int nrse_gemm256(const nrse_gemm_params* p, hipStream_t st);
 int nrse_gemm256_rows(const nrse_gemm_params* p);           // its tile rows for p (256 or 224)
@@ -398,10 +399,31 @@ extern "C" int nrse_gemm(const nrse_gemm_params* p, void* stream) {
   const bool big = nrse_gemm256_tiles(p) >= 128 && !(p->flags & NRSE_EPI_ATOMIC);
   // the grouped pos-conv pattern (sliding-window A operand, N = 64): its own kernel unless a
   // generation is pinned (NRSE_GEMM_GEN=1|2|3 benchmarks the generic kernels on it)
-  if ((gen == 0 || gen == 4) && nrse_posconv_ok(p)) return nrse_posconv(p, st);
-  if ((gen == 0 || gen == 4) && nrse_posconv_wgrad_ok(p)) return nrse_posconv_wgrad(p, st);
+  const bool f8 = p->nseg8 != 0 || p->c8;  // ABI 6 fields: the 256x256 kernel only (below)
+  if (!f8 && (gen == 0 || gen == 4) && nrse_posconv_ok(p)) return nrse_posconv(p, st);
+  if (!f8 && (gen == 0 || gen == 4) && nrse_posconv_wgrad_ok(p)) return nrse_posconv_wgrad(p, st);
   const bool part = (p->flags & NRSE_EPI_COLSUM) && p->colsum_part;
   int rc, mt;
+  if (f8) {
+    // ABI 6 (split-weight mode): fp8 correction segments / fp8 output copy -- the 256x256
+    // kernel only; no other kernel implements them, so anything else is refused, never dropped
+    NRSE_REQUIRE(p->nseg8 >= 0, "nrse_gemm: nseg8 < 0");
+    if (!nrse_gemm256_ok(p) || (p->nseg8 > 0 && !nrse_gemm256_f8_ok(p))) {
+      nrse_set_error("nrse_gemm: fp8 correction segments need the 256x256 kernel's layout, K %% 128 == 0, "
+                     "splits == 1 and 16-byte aligned NRSE_FP8 k-contiguous a8 / b8 (M=%d N=%d K=%d)",
+                     p->M, p->N, p->K);
+      return NRSE_ERR_UNSUPPORTED;
+    }
+    if (p->c8 && (p->c_dtype != NRSE_BF16 || p->batch != 1 || p->splits != 1 || ((uintptr_t)p->c8 & 7) ||
+                  (p->ldc8 & 7) || p->ldc8 < p->N)) {
+      nrse_set_error("nrse_gemm: c8 needs a bf16 C, batch == splits == 1, 8-byte aligned c8 and ldc8 >= N");
+      return NRSE_ERR_UNSUPPORTED;
+    }
+    rc = nrse_gemm256(p, st);
+    mt = nrse_cdiv(p->M, nrse_gemm256_rows(p));
+    if (rc || !part) return rc;
+    return nrse_rows_reduce(p->colsum, p->N, nullptr, 0, nullptr, 0, p->colsum_part, 2 * mt, 1, 1, stream);
+  }
   if (gen != 1 && gen != 2 && nrse_gemm256_ok(p) && (gen == 3 || big)) {
     rc = nrse_gemm256(p, st);
     mt = nrse_cdiv(p->M, nrse_gemm256_rows(p));

@@ -37,6 +37,7 @@
 //  - the 256x256 f32 result leaves through LDS in four 64-row passes with the same fused
 //    epilogue as gemm_dma.hip (epi8).
 #include <cstdlib>
+#include <type_traits>
 
 #include "gemm_common.h"
 
@@ -161,6 +162,50 @@ NRSE_DEV void ld_issue(const Ld& o, char* dst, int wave, int hh, unsigned soff, 
     if (krem < BK) voff = o.kpos[hh][j] < krem ? voff : OOB;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(dst + (wave * 2 + j) * 1024), 16, voff, soff, 0, 0);
   }
+}
+
+// fp8 correction-segment loader (ABI 6, nrse_gemm_params.a8 / b8): k-contiguous [row][k] bytes
+// with the bf16 operand's element pitch (a8.ld == a.ld, a multiple of 64). One fp8 K-tile is 128 k
+// = 128 bytes per row, the bf16 K-tile's bytes, so the LDS image, its swizzle, the ring and the
+// fragment reads are the bf16 loader's, and so are the per-lane source offsets up to the pitch:
+// bf16 row r, chunk c sits at 2 r ld + 16 c (2 r ld a multiple of 128), fp8 at r ld + 16 c. The fp8
+// offsets are derived from the bf16 loader's at issue (no registers held for them). No K tail
+// (the host requires K % 128 == 0).
+struct Ld8 {
+  __amdgpu_buffer_rsrc_t rs;
+  long long seg;
+};
+
+NRSE_DEV void ld8_init(Ld8& o, const nrse_gemm_operand& d, const char* base) {
+  o.rs = make_rsrc(base);
+  o.seg = d.seg_stride;
+}
+
+NRSE_DEV unsigned ld8_soff(const Ld8& o, int sg, int ki) { return (unsigned)((long long)sg * o.seg + (long long)ki * 128); }
+
+NRSE_DEV void ld8_issue(const Ld8& o, const Ld& l16, char* dst, int wave, int hh, unsigned soff, bool live = true) {
+  const __amdgpu_buffer_rsrc_t rs = live ? o.rs : l16.dead;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const unsigned v = l16.voff[hh][j];
+    const unsigned v8 = v >= OOB ? OOB : ((v & ~127u) >> 1) + (v & 127u);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(dst + (wave * 2 + j) * 1024), 16, v8, soff, 0, 0);
+  }
+}
+
+typedef int i32x4v __attribute__((ext_vector_type(4)));
+typedef int i32x8v __attribute__((ext_vector_type(8)));
+// both 32-deep fragments of a 64-deep bf16 K-tile (k-substeps 0, 1) as one 8-register tuple, which
+// is also the operand of the fp8 MFMA over the same 128 bytes: A and B lanes read the same byte
+// positions, so every byte of a row meets its partner whatever k the hardware assigns it
+NRSE_DEV i32x8v frag2(const char* lds, int base, int lane) {
+  const i32x4v a = __builtin_bit_cast(i32x4v, frag<true>(lds, base, 0, lane));
+  const i32x4v b = __builtin_bit_cast(i32x4v, frag<true>(lds, base, 1, lane));
+  return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+NRSE_DEV bf16x8 frag_half(i32x8v v, int s) {
+  return s == 0 ? __builtin_bit_cast(bf16x8, __builtin_shufflevector(v, v, 0, 1, 2, 3))
+                : __builtin_bit_cast(bf16x8, __builtin_shufflevector(v, v, 4, 5, 6, 7));
 }
 
 // ------------------------------------------------------------------ register epilogue
@@ -329,6 +374,10 @@ NRSE_DEV void fast_epilogue(const nrse_gemm_params& p, const f32x4 (&acc)[8][4],
       if (m >= p.M || n >= p.N) continue;
       const uint4 u = *reinterpret_cast<const uint4*>(oimg + prow * PITCH + ch * 16);
       *reinterpret_cast<uint4*>((char*)p.c + (epi.cbase + (long long)m * p.ldc + n) * ES) = u;
+      if constexpr (OBF) {
+        // the fp8 copy of the stored bf16 values (ABI 6 c8: the next GEMM's correction operand)
+        if (p.c8) *reinterpret_cast<uint2*>((unsigned char*)p.c8 + (long long)m * p.ldc8 + n) = fp8x8_from_bf16x8(u);
+      }
       if constexpr (GAUX) {
         const uint4 w = *reinterpret_cast<const uint4*>(aimg + prow * APITCH + ch * 16);
         *reinterpret_cast<uint4*>((bf16_t*)p.aux + epi.abase + (long long)m * p.ldaux + n) = w;
@@ -352,9 +401,11 @@ NRSE_DEV void fast_epilogue(const nrse_gemm_params& p, const f32x4 (&acc)[8][4],
 // BMT: tile rows, 256 or 224 (= 7 x 32: e.g. M = 12768 = 57 x 224 frames of 32 utterances fills
 // 228 of the 256 CUs per N-column of tiles instead of 200; nrse_gemm256 picks the one that
 // needs fewer tile waves, see bm_choice)
-template <bool AKC, bool BKC, int BMT>
+// F8: the split-weight mode's fp8 correction segments (ABI 6) follow the bf16 K-tiles
+template <bool AKC, bool BKC, int BMT, bool F8>
 __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params p, int mt, int nt) {
   static_assert(BMT == 256 || BMT == 224, "tile rows");
+  static_assert(!F8 || (AKC && BKC), "fp8 correction segments: k-contiguous operands");
   constexpr int NFI_HI = (BMT / 2 - 64) / 16;  // 16-row blocks in an M-wave's high half: 4 or 3
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
   const int tid = threadIdx.x;
@@ -388,13 +439,29 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
 
   const int tps = (p.K + BK - 1) / BK;
   const int seg0 = split * p.nseg;
-  const int ntiles = p.nseg * tps;
+  const int n16 = p.nseg * tps;               // bf16 K-tiles
+  // fp8 correction K-tiles (128 k each) after them (F8; splits == 1)
+  Ld8 la8, lb8;
+  int tps8 = 1;
+  if constexpr (F8) {
+    ld8_init(la8, p.a8, (const char*)p.a8.ptr + zq * p.a8.z1 + zr * p.a8.z2);
+    ld8_init(lb8, p.b8, (const char*)p.b8.ptr + zq * p.b8.z1 + zr * p.b8.z2);
+    tps8 = p.K / 128;
+  }
+  const int ntiles = n16 + (F8 ? p.nseg8 * tps8 : 0);
 
   // K-tile t -> uniform source offsets of A and B and the K remainder; t >= ntiles -> dead
-  struct TilePos { unsigned sa, sb; int krem; bool live; };
-  auto tile_pos_at = [&](bool live, int sgi, int ki) {
+  struct TilePos { unsigned sa, sb; int krem; bool live; bool f8; };
+  auto tile_pos_at = [&](bool live, int sgi, int ki, bool f8) {
     TilePos q;
     q.live = live;
+    q.f8 = F8 && live && f8;
+    if (q.f8) {
+      q.sa = ld8_soff(la8, sgi, ki);
+      q.sb = ld8_soff(lb8, sgi, ki);
+      q.krem = BK;
+      return q;
+    }
     const int sg = seg0 + (live ? sgi : 0);
     const int k0 = (live ? ki : 0) * BK;
     q.sa = ld_soff<AKC>(la, sg, k0);
@@ -402,10 +469,22 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
     q.krem = p.K - k0;
     return q;
   };
-  auto tile_pos = [&](int t) { return tile_pos_at(t < ntiles, t / tps, t % tps); };
+  auto tile_pos = [&](int t) {
+    if (F8 && t >= n16) return tile_pos_at(t < ntiles, (t - n16) / tps8, (t - n16) % tps8, true);
+    return tile_pos_at(t < ntiles, t / tps, t % tps, false);
+  };
   // half-tile index j of a K-tile in staging (= first-read) order: 0 A-lo, 1 B-lo, 2 B-hi, 3 A-hi
   auto stage = [&](int j, const TilePos& q, int slot) {
     char* dst = smem + slot * HALF;
+    if constexpr (F8) {
+      if (q.f8) {
+        if (j == 0) ld8_issue(la8, la, dst, wave, 0, q.sa);
+        else if (j == 1) ld8_issue(lb8, lb, dst, wave, 0, q.sb);
+        else if (j == 2) ld8_issue(lb8, lb, dst, wave, 1, q.sb);
+        else ld8_issue(la8, la, dst, wave, 1, q.sa);
+        return;
+      }
+    }
     if (j == 0) ld_issue(la, dst, wave, 0, q.sa, q.krem, q.live);
     else if (j == 1) ld_issue(lb, dst, wave, 0, q.sb, q.krem, q.live);
     else if (j == 2) ld_issue(lb, dst, wave, 1, q.sb, q.krem, q.live);
@@ -487,6 +566,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
   // ping-pong start: group 1 falls one barrier behind (schedule and hand-off rules: header)
   if (wm == 1) __builtin_amdgcn_s_barrier();
   int base = 0;  // slot of half-tile sequence number 4t
+  if constexpr (!F8) {
   // K-tile t+2 as (segment, K-tile within the segment), advanced by one per iteration: the
   // division by the segment's K-tile count stays out of the loop (done per iteration by all 8
   // waves on the CU's one scalar unit, it lengthened each K-tile's first phase by ~200 cycles)
@@ -496,7 +576,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
     const int s0 = base, s1 = wrap(base + 1), s2 = wrap(base + 2), s3 = wrap(base + 3);
     // K-tile t+2 is staged over the two phases of K-tile t: A-lo, B-lo in phase 0 (sequence
     // 4t+8, 4t+9), B-hi, A-hi in phase 1 (4t+10, 4t+11)
-    const TilePos q2 = tile_pos_at(t + 2 < ntiles, u_sg, u_k);
+    const TilePos q2 = tile_pos_at(t + 2 < ntiles, u_sg, u_k, false);
     if (++u_k == tps) { u_k = 0; ++u_sg; }
     // phase 0: quadrants (M-half 0, N-half 0) and (0, 1) from A-lo, B-lo, B-hi
     NRSE_READ_A(s0, 4)
@@ -524,6 +604,119 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
     NRSE_BAR();
     NRSE_PSTAMP(3);
     base = wrap(base + 4);
+  }
+  } else {
+  // The same schedule with the fp8 correction K-tiles after the bf16 ones (ABI 6). The fragments
+  // are held as 8-register tuples (both k-substeps of a bf16 K-tile = one fp8 MFMA operand); a
+  // bf16 K-tile runs its 32-deep halves as before, an fp8 K-tile runs one 128-deep MX-scaled MFMA
+  // per (fi, fj) -- twice a bf16 MFMA's cycles for 4x its k: half the time per k. The weight
+  // operand (our B, in the instruction's A slot) carries the scale 2^-b8_exp (E8M0), the
+  // activation operand 1.0.
+  i32x8v fa8[4], fbl8[2], fbh8[2];
+  const int scw = 0x01010101 * (127 - p.b8_exp), sc1 = 0x7f7f7f7f;
+#define NRSE_READ_A8(SLOT, NFI)                                                          \
+  _Pragma("unroll") for (int fi = 0; fi < (NFI); ++fi)                                 \
+    fa8[fi] = frag2(smem + (SLOT) * HALF, wm * 64 + fi * 16, lane);
+#define NRSE_READ_B8(SLOT, FB)                                                           \
+  _Pragma("unroll") for (int fj = 0; fj < 2; ++fj)                                     \
+    FB[fj] = frag2(smem + (SLOT) * HALF, wn * 32 + fj * 16, lane);
+#define NRSE_QUADH(MH, NH, FB)                                                           \
+  __builtin_amdgcn_s_setprio(1);                                                         \
+  _Pragma("unroll") for (int s = 0; s < 2; ++s)                                        \
+  _Pragma("unroll") for (int fi = 0; fi < ((MH) ? NFI_HI : 4); ++fi)                   \
+  _Pragma("unroll") for (int fj = 0; fj < 2; ++fj)                                     \
+    NRSE_MFMA(acc[(MH) * 4 + fi][(NH) * 2 + fj], frag_half(fa8[fi], s), frag_half(FB[fj], s)); \
+  __builtin_amdgcn_s_setprio(0);
+#define NRSE_QUAD8(MH, NH, FB)                                                           \
+  __builtin_amdgcn_s_setprio(1);                                                         \
+  _Pragma("unroll") for (int fi = 0; fi < ((MH) ? NFI_HI : 4); ++fi)                   \
+  _Pragma("unroll") for (int fj = 0; fj < 2; ++fj)                                     \
+    acc[(MH) * 4 + fi][(NH) * 2 + fj] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(  \
+        FB[fj], fa8[fi], acc[(MH) * 4 + fi][(NH) * 2 + fj], 0, 0, 0, scw, 0, sc1);        \
+  __builtin_amdgcn_s_setprio(0);
+// the raw barrier with scheduling fences: without them the compiler moved this loop's MFMAs across
+// the phase barriers (out of their ping-pong segments), and fp8 K-tiles ran at half the bf16 rate
+#define NRSE_BAR8()                          \
+  do {                                       \
+    __builtin_amdgcn_sched_barrier(0);       \
+    NRSE_BAR();                              \
+    __builtin_amdgcn_sched_barrier(0);       \
+  } while (0)
+  // K-tile t+2 as (segment, K-tile, fp8?) advanced per iteration (no divisions in the loop)
+  bool u8 = 2 >= n16;
+  int u_sg = u8 ? (2 - n16) / tps8 : 2 / tps, u_k = u8 ? (2 - n16) % tps8 : 2 % tps;
+  // one K-tile of the schedule; the bf16 tiles and the fp8 tiles run in two loops, so neither
+  // body branches around its MFMAs (a branch there made the compiler copy and spill the
+  // accumulators between the two forms)
+  auto ktile = [&](int t, auto kind) {
+    constexpr bool K8 = decltype(kind)::value;
+    const int s0 = base, s1 = wrap(base + 1), s2 = wrap(base + 2), s3 = wrap(base + 3);
+    // K-tile t+2: in the fp8 loop it is an fp8 tile or dead, staged without a branch (a branch
+    // around the DMA issue let the compiler sink this phase's MFMAs out of their segment)
+    TilePos q2;
+    if constexpr (K8) {
+      q2.live = t + 2 < ntiles;
+      q2.sa = ld8_soff(la8, u_sg, u_k);
+      q2.sb = ld8_soff(lb8, u_sg, u_k);
+      if (++u_k == tps8) { u_k = 0; ++u_sg; }
+    } else {
+      q2 = tile_pos_at(t + 2 < ntiles, u_sg, u_k, u8);
+      if (++u_k == (u8 ? tps8 : tps)) {
+        u_k = 0;
+        if (++u_sg == p.nseg && !u8) { u8 = true; u_sg = 0; }
+      }
+    }
+    auto stg = [&](int j, int slot) {
+      if constexpr (K8) {
+        char* dst = smem + slot * HALF;
+        if (j == 0) ld8_issue(la8, la, dst, wave, 0, q2.sa, q2.live);
+        else if (j == 1) ld8_issue(lb8, lb, dst, wave, 0, q2.sb, q2.live);
+        else if (j == 2) ld8_issue(lb8, lb, dst, wave, 1, q2.sb, q2.live);
+        else ld8_issue(la8, la, dst, wave, 1, q2.sa, q2.live);
+      } else {
+        stage(j, q2, slot);
+      }
+    };
+    NRSE_READ_A8(s0, 4)
+    NRSE_READ_B8(s1, fbl8)
+    NRSE_READ_B8(s2, fbh8)
+    stg(0, wrap(base + 8));
+    stg(1, wrap(base + 9));
+    NRSE_WAIT(12);
+    NRSE_BAR8();
+    if constexpr (K8) {
+      NRSE_QUAD8(0, 0, fbl8)
+      NRSE_QUAD8(0, 1, fbh8)
+    } else {
+      NRSE_QUADH(0, 0, fbl8)
+      NRSE_QUADH(0, 1, fbh8)
+    }
+    NRSE_BAR8();
+    NRSE_READ_A8(s3, NFI_HI)
+    stg(2, base);
+    stg(3, s1);
+    NRSE_WAIT(10);
+    NRSE_BAR8();
+    if constexpr (K8) {
+      NRSE_QUAD8(1, 1, fbh8)
+      NRSE_QUAD8(1, 0, fbl8)
+    } else {
+      NRSE_QUADH(1, 1, fbh8)
+      NRSE_QUADH(1, 0, fbl8)
+    }
+    NRSE_BAR8();
+    base = wrap(base + 4);
+  };
+  int t = 0;
+#pragma unroll 1
+  for (; t < n16; ++t) ktile(t, std::false_type{});
+#pragma unroll 1
+  for (; t < ntiles; ++t) ktile(t, std::true_type{});
+#undef NRSE_READ_A8
+#undef NRSE_READ_B8
+#undef NRSE_QUADH
+#undef NRSE_QUAD8
+#undef NRSE_BAR8
   }
   if (wm == 0) __builtin_amdgcn_s_barrier();
   NRSE_STAMP(2);
@@ -665,15 +858,15 @@ int bm_choice(const nrse_gemm_params* p) {
   return w224 <= w256 ? 224 : 256;
 }
 
-template <bool AKC, bool BKC>
+template <bool AKC, bool BKC, bool F8 = false>
 int launch(const nrse_gemm_params* p, hipStream_t st) {
   const int bm = bm_choice(p);
   const int mt = nrse_cdiv(p->M, bm), nt = nrse_cdiv(p->N, BN);
   const long long total = (long long)mt * nt * p->batch * p->splits;
   if (bm == 224)
-    hipLaunchKernelGGL((gemm256_kernel<AKC, BKC, 224>), dim3((unsigned)total), dim3(NTHR), 0, st, *p, mt, nt);
+    hipLaunchKernelGGL((gemm256_kernel<AKC, BKC, 224, F8>), dim3((unsigned)total), dim3(NTHR), 0, st, *p, mt, nt);
   else
-    hipLaunchKernelGGL((gemm256_kernel<AKC, BKC, 256>), dim3((unsigned)total), dim3(NTHR), 0, st, *p, mt, nt);
+    hipLaunchKernelGGL((gemm256_kernel<AKC, BKC, 256, F8>), dim3((unsigned)total), dim3(NTHR), 0, st, *p, mt, nt);
   return nrse_check_launch("nrse_gemm(256)");
 }
 
@@ -697,7 +890,26 @@ bool nrse_gemm256_ok(const nrse_gemm_params* p) {
 
 int nrse_gemm256_rows(const nrse_gemm_params* p) { return bm_choice(p); }
 
+// the ABI-6 fp8 correction segments' conditions (nrse_gemm checks them before routing here)
+bool nrse_gemm256_f8_ok(const nrse_gemm_params* p) {
+  auto al16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+  auto m16 = [](long long x) { return (x & 15) == 0; };
+  const nrse_gemm_operand* o8[2] = {&p->a8, &p->b8};
+  for (const nrse_gemm_operand* o : o8) {
+    if (!o->ptr || o->dtype != NRSE_FP8 || !o->kcontig || o->chunk_shift != 0 || !al16(o->ptr) ||
+        !m16(o->seg_stride) || !m16(o->z1) || !m16(o->z2) || o->seg_stride < 0)
+      return false;
+  }
+  // the fp8 rows share the bf16 operands' element pitch (the loader derives its offsets from theirs)
+  if (p->a8.ld != p->a.ld || p->b8.ld != p->b.ld || (p->a.ld & 63) || (p->b.ld & 63)) return false;
+  const long long spa = (long long)(p->nseg8 - 1) * p->a8.seg_stride + (long long)p->M * p->a8.ld + p->K;
+  const long long spb = (long long)(p->nseg8 - 1) * p->b8.seg_stride + (long long)p->N * p->b8.ld + p->K;
+  return p->K % 128 == 0 && p->splits == 1 && p->a.kcontig && p->b.kcontig && spa < (1LL << 31) &&
+         spb < (1LL << 31) && p->b8_exp > -127 && p->b8_exp < 127;
+}
+
 int nrse_gemm256(const nrse_gemm_params* p, hipStream_t st) {
+  if (p->nseg8 > 0) return launch<true, true, true>(p, st);
   if (p->a.kcontig && p->b.kcontig) return launch<true, true>(p, st);
   if (p->a.kcontig && !p->b.kcontig) return launch<true, false>(p, st);
   if (!p->a.kcontig && p->b.kcontig) return launch<false, true>(p, st);

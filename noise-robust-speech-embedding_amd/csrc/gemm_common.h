@@ -180,6 +180,12 @@ NRSE_DEV void epi8(const nrse_gemm_params& p, const Epi& e, int m, int n, float*
       for (int i = 0; i < 8; ++i) v[i] += c[i];
     }
     st8(p.c, p.c_dtype, ci, v);
+    if (p.c8 && p.c_dtype == NRSE_BF16) {  // ABI 6: fp8 copy of the stored bf16 values (batch 1)
+      uint2 w;
+      w.x = fp8x4_of_bf(v);
+      w.y = fp8x4_of_bf(v + 4);
+      *reinterpret_cast<uint2*>((unsigned char*)p.c8 + (long long)m * p.ldc8 + n) = w;
+    }
   }
 }
 

@@ -255,6 +255,28 @@ __global__ void split_bf16_kernel(const float* __restrict__ x, bf16_t* __restric
   }
 }
 
+// the fp8 correction plane of the split (nrse_split_lo8), 4 elements (one u32 of fp8) per lane
+__global__ void split_lo8_kernel(const float* __restrict__ x, uint32_t* __restrict__ lo8, float sc, long long n) {
+  const long long n4 = n / 4;
+  for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (long long)gridDim.x * blockDim.x) {
+    const float4 v = reinterpret_cast<const float4*>(x)[q];
+    lo8[q] = fp8x4(lo_resid(v.x) * sc, lo_resid(v.y) * sc, lo_resid(v.z) * sc, lo_resid(v.w) * sc);
+  }
+  for (long long i = n4 * 4 + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    reinterpret_cast<unsigned char*>(lo8)[i] = fp8_1(lo_resid(x[i]) * sc);
+}
+
+__global__ void cast_fp8_kernel(const void* __restrict__ x, int xdt, unsigned char* __restrict__ y, long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    y[i] = fp8_1(load_as_f(x, xdt, i));
+}
+
+__global__ void zero_kernel(float* __restrict__ d, long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    d[i] = 0.f;
+}
+
 __global__ void swap12_kernel(const void* __restrict__ src, int sdt, void* __restrict__ dst, int ddt, int d0, int d1,
                               int d2, int acc) {
   const long long total = (long long)d0 * d1 * d2;
@@ -415,6 +437,30 @@ extern "C" int nrse_split_bf16(const float* x, void* hi, void* lo, long long n, 
   hipLaunchKernelGGL(split_bf16_kernel, dim3(blocks_for(n)), dim3(256), 0, (hipStream_t)stream, x, (bf16_t*)hi,
                      (bf16_t*)lo, n);
   return nrse_check_launch("nrse_split_bf16");
+}
+
+extern "C" int nrse_split_lo8(const float* x, void* lo8, int lo8_exp, long long n, void* stream) {
+  NRSE_REQUIRE(x && lo8 && n >= 0 && lo8_exp > -64 && lo8_exp < 64, "nrse_split_lo8: bad args");
+  NRSE_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)lo8 & 3) == 0, "nrse_split_lo8: x 16-byte, lo8 4-byte aligned");
+  if (n == 0) return NRSE_OK;
+  hipLaunchKernelGGL(split_lo8_kernel, dim3(blocks_for(n / 4 + 1)), dim3(256), 0, (hipStream_t)stream, x,
+                     (uint32_t*)lo8, ldexpf(1.f, lo8_exp), n);
+  return nrse_check_launch("nrse_split_lo8");
+}
+
+extern "C" int nrse_cast_fp8(const void* x, int xdt, void* y8, long long n, void* stream) {
+  NRSE_REQUIRE(x && y8 && n >= 0 && (xdt == NRSE_F32 || xdt == NRSE_BF16), "nrse_cast_fp8: bad args");
+  if (n == 0) return NRSE_OK;
+  hipLaunchKernelGGL(cast_fp8_kernel, dim3(blocks_for(n)), dim3(256), 0, (hipStream_t)stream, x, xdt,
+                     (unsigned char*)y8, n);
+  return nrse_check_launch("nrse_cast_fp8");
+}
+
+extern "C" int nrse_zero(float* dst, long long n, void* stream) {
+  NRSE_REQUIRE(dst && n >= 0, "nrse_zero: bad args");
+  if (n == 0) return NRSE_OK;
+  hipLaunchKernelGGL(zero_kernel, dim3(blocks_for(n)), dim3(256), 0, (hipStream_t)stream, dst, n);
+  return nrse_check_launch("nrse_zero");
 }
 
 extern "C" int nrse_cast(const void* x, int xdt, void* y, int ydt, long long n, void* stream) {

@@ -88,6 +88,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const nrse_ln_fwd_params p)
       for (int e = 0; e < CH; ++e) o[e] = fmaxf(o[e], 0.f);
     }
     store4_out(p.y, p.y_dtype, base + c0, p.rows * C, o);
+    if (p.y8) *reinterpret_cast<uint32_t*>((unsigned char*)p.y8 + base + c0) = fp8x4_of_bf(o);
   }
   if (lane == 0) {
     if (p.mean) p.mean[row] = mean;
@@ -139,6 +140,7 @@ __global__ __launch_bounds__(256) void ln_fwd_f32_kernel(const nrse_ln_fwd_param
       for (int e = 0; e < CH; ++e) o[e] = fmaxf(o[e], 0.f);
     }
     store4_out(p.y, p.y_dtype, base + c0, p.rows * C, o);
+    if (p.y8) *reinterpret_cast<uint32_t*>((unsigned char*)p.y8 + base + c0) = fp8x4_of_bf(o);
   }
   if (lane == 0) {
     if (p.mean) p.mean[row] = mean;
@@ -602,7 +604,9 @@ extern "C" int nrse_layernorm_fwd(const nrse_ln_fwd_params* p, void* stream) {
   if (!c_ok(p->C)) { nrse_set_error("nrse_layernorm_fwd: C=%d not in {256,512,1024}", p->C); return NRSE_ERR_UNSUPPORTED; }
   NRSE_REQUIRE(p->y_dtype == NRSE_F32 || p->y_dtype == NRSE_BF16 || p->y_dtype == NRSE_BF16X3,
                "nrse_layernorm_fwd: bad y_dtype %d", p->y_dtype);
-  if (p->x_dtype == NRSE_BF16 && p->C <= 512 && ((uintptr_t)p->x & 7) == 0) {
+  NRSE_REQUIRE(!p->y8 || (p->y_dtype == NRSE_BF16 && ((uintptr_t)p->y8 & 3) == 0),
+               "nrse_layernorm_fwd: y8 needs a bf16 y and 4-byte alignment");
+  if (p->x_dtype == NRSE_BF16 && p->C <= 512 && ((uintptr_t)p->x & 7) == 0 && !p->y8) {
     constexpr int RPW = 4;
     const dim3 g((unsigned)((p->rows + 4 * RPW - 1) / (4 * RPW)));
     if (p->C == 512) hipLaunchKernelGGL((ln_fwd_bf16_kernel<2, RPW>), g, dim3(256), 0, (hipStream_t)stream, *p);

@@ -62,11 +62,18 @@ __global__ __launch_bounds__(256) void sum_parts_kernel(const double* __restrict
 NRSE_DEV float ema_mix(float t, float o, float decay, float om) { return fmaf(decay, t, om * o); }
 
 // one element of the fused target EMA (nrse_adamw_params.ema_t), as ema_kernel's scalar tail
-NRSE_DEV void ema_one(const nrse_adamw_params& p, long long i, float pn, float eom) {
+NRSE_DEV void ema_one(const nrse_adamw_params& p, long long i, float pn, float eom, float sc8) {
   const float t = ema_mix(p.ema_t[i], pn, p.ema_decay, eom);
   p.ema_t[i] = t;
   if (p.ema_shadow) store_from_f(p.ema_shadow, p.ema_shadow_dtype, i, t);
   if (p.ema_shadow_lo) ((bf16_t*)p.ema_shadow_lo)[i] = bf16_lo(t);
+  if (p.ema_shadow_lo8) ((unsigned char*)p.ema_shadow_lo8)[i] = fp8_1(lo_resid(t) * sc8);
+}
+
+// the fp8 correction plane of 4 consecutive weights at float4 index q (ABI 6)
+NRSE_DEV void store_lo8x4(void* lo8, long long q, const float* x, float sc8) {
+  reinterpret_cast<uint32_t*>(lo8)[q] =
+      fp8x4(lo_resid(x[0]) * sc8, lo_resid(x[1]) * sc8, lo_resid(x[2]) * sc8, lo_resid(x[3]) * sc8);
 }
 
 __global__ __launch_bounds__(256) void adamw_kernel(const nrse_adamw_params p) {
@@ -87,9 +94,12 @@ __global__ __launch_bounds__(256) void adamw_kernel(const nrse_adamw_params p) {
   const long long n4 = p.n / 4;
   const long long e4 = p.ema_n / 4;  // whole quads of the fused EMA range
   const float eom = 1.f - p.ema_decay;
+  const float sc8 = ldexpf(1.f, p.lo8_exp);
   for (long long q = (long long)blockIdx.x * 256 + threadIdx.x; q < n4; q += (long long)gridDim.x * 256) {
     float4 pv = reinterpret_cast<float4*>(p.p)[q];
     const float4 gv = reinterpret_cast<const float4*>(p.g)[q];
+    // zero_grad: the gradient buffer is cleared for the next step's accumulation by this pass
+    if (p.zero_grad) reinterpret_cast<float4*>(const_cast<float*>(p.g))[q] = make_float4(0.f, 0.f, 0.f, 0.f);
     float4 mv = reinterpret_cast<float4*>(p.m)[q];
     float4 vv = reinterpret_cast<float4*>(p.v)[q];
     float* pa = &pv.x; const float* ga = &gv.x; float* ma = &mv.x; float* va = &vv.x;
@@ -112,6 +122,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(const nrse_adamw_params p) {
         reinterpret_cast<float4*>(p.p_shadow)[q] = pv;
       }
     }
+    if (p.p_shadow_lo8) store_lo8x4(p.p_shadow_lo8, q, pa, sc8);
     if (p.ema_t) {
       if (q < e4) {
         float4 tv = reinterpret_cast<float4*>(p.ema_t)[q];
@@ -122,17 +133,19 @@ __global__ __launch_bounds__(256) void adamw_kernel(const nrse_adamw_params p) {
           if (p.ema_shadow_dtype == NRSE_BF16) store_bf16x4(p.ema_shadow, p.ema_shadow_lo, q, &tv.x);
           else reinterpret_cast<float4*>(p.ema_shadow)[q] = tv;
         }
+        if (p.ema_shadow_lo8) store_lo8x4(p.ema_shadow_lo8, q, &tv.x, sc8);
       } else if (q == e4) {
         // the quad holding the EMA range's end: its first ema_n - 4 q elements, from this thread's
         // updated registers
 #pragma unroll
         for (int e = 0; e < 3; ++e)
-          if (4 * q + e < p.ema_n) ema_one(p, 4 * q + e, pa[e], eom);
+          if (4 * q + e < p.ema_n) ema_one(p, 4 * q + e, pa[e], eom, sc8);
       }
     }
   }
   for (long long i = n4 * 4 + (long long)blockIdx.x * 256 + threadIdx.x; i < p.n; i += (long long)gridDim.x * 256) {
     const float g = p.g[i] * coef;
+    if (p.zero_grad) const_cast<float*>(p.g)[i] = 0.f;
     const float w = p.p[i] * decay;
     p.m[i] = p.beta1 * p.m[i] + (1.f - p.beta1) * g;
     p.v[i] = p.beta2 * p.v[i] + (1.f - p.beta2) * g * g;
@@ -140,7 +153,8 @@ __global__ __launch_bounds__(256) void adamw_kernel(const nrse_adamw_params p) {
     p.p[i] = w - step_size * p.m[i] / denom;
     if (p.p_shadow) store_from_f(p.p_shadow, p.shadow_dtype, i, p.p[i]);
     if (p.p_shadow_lo) ((bf16_t*)p.p_shadow_lo)[i] = bf16_lo(p.p[i]);
-    if (p.ema_t && i < p.ema_n) ema_one(p, i, p.p[i], eom);
+    if (p.p_shadow_lo8) ((unsigned char*)p.p_shadow_lo8)[i] = fp8_1(lo_resid(p.p[i]) * sc8);
+    if (p.ema_t && i < p.ema_n) ema_one(p, i, p.p[i], eom, sc8);
   }
 }
 
@@ -227,6 +241,19 @@ extern "C" int nrse_adamw(const nrse_adamw_params* p, void* stream) {
   NRSE_REQUIRE(!p->ema_shadow_lo ||
                    (p->ema_shadow && p->ema_shadow_dtype == NRSE_BF16 && ((uintptr_t)p->ema_shadow_lo & 7) == 0),
                "nrse_adamw: ema_shadow_lo needs a bf16 ema_shadow and 8-byte alignment");
+  // the shadows are written as 4-element vectors: uint2 (bf16) or float4 (f32) per quad
+  auto shadow_ok = [](const void* sh, int dt) {
+    return !sh || (dt == NRSE_BF16 && ((uintptr_t)sh & 7) == 0) || (dt == NRSE_F32 && ((uintptr_t)sh & 15) == 0);
+  };
+  NRSE_REQUIRE(shadow_ok(p->p_shadow, p->shadow_dtype),
+               "nrse_adamw: p_shadow must be bf16 (8-byte aligned) or f32 (16-byte aligned)");
+  NRSE_REQUIRE(!p->ema_shadow || (p->ema_t && shadow_ok(p->ema_shadow, p->ema_shadow_dtype)),
+               "nrse_adamw: ema_shadow needs ema_t and must be bf16 (8-byte aligned) or f32 (16-byte aligned)");
+  NRSE_REQUIRE((!p->p_shadow_lo8 && !p->ema_shadow_lo8) || (p->lo8_exp > -64 && p->lo8_exp < 64),
+               "nrse_adamw: lo8_exp out of range");
+  NRSE_REQUIRE(((uintptr_t)p->p_shadow_lo8 & 3) == 0 && ((uintptr_t)p->ema_shadow_lo8 & 3) == 0 &&
+                   (!p->ema_shadow_lo8 || p->ema_t),
+               "nrse_adamw: fp8 planes need 4-byte alignment (and ema_t for ema_shadow_lo8)");
   if (p->n == 0) return NRSE_OK;
   hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(p->n)), dim3(256), 0, (hipStream_t)stream, *p);
   return nrse_check_launch("nrse_adamw");

@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("NRSE_LIB_PATH") or os.path.join(_HERE, "libnrse_hip.s
 F32 = 0
 BF16 = 1
 BF16X3 = 2   # output-only split-bf16 planes [hi | lo | hi] (include/nrse_hip.h)
+FP8 = 3      # OCP fp8 e4m3fn, the split-weight mode's correction operands (ABI 6)
 
 EPI_BIAS = 1 << 0
 EPI_GELU = 1 << 1
@@ -60,12 +61,15 @@ class GemmParams(ctypes.Structure):
                 ("aux", c_vp), ("aux_dtype", c_int), ("ldaux", c_ll), ("aux_z1", c_ll),
                 ("aux_z2", c_ll), ("resid", c_vp), ("resid_dtype", c_int), ("ldr", c_ll), ("r_z1", c_ll),
                 ("r_z2", c_ll), ("dropout_p", c_f), ("seed", c_u32), ("colsum", c_vp),
-                ("colsum_part", c_vp)]
+                ("colsum_part", c_vp),
+                ("a8", GemmOperand), ("b8", GemmOperand), ("nseg8", c_int), ("b8_exp", c_int),
+                ("c8", c_vp), ("ldc8", c_ll)]
 
 
 class LnFwdParams(ctypes.Structure):
     _fields_ = [("x", c_vp), ("x_dtype", c_int), ("gamma", c_vp), ("beta", c_vp), ("y", c_vp), ("y_dtype", c_int),
-                ("mean", c_vp), ("rstd", c_vp), ("rows", c_ll), ("C", c_int), ("eps", c_f), ("flags", c_int)]
+                ("mean", c_vp), ("rstd", c_vp), ("rows", c_ll), ("C", c_int), ("eps", c_f), ("flags", c_int),
+                ("y8", c_vp)]
 
 
 class LnBwdParams(ctypes.Structure):
@@ -90,7 +94,7 @@ class AttnBwdParams(ctypes.Structure):
     _fields_ = [("qkv", c_vp), ("dtype", c_int), ("gate", c_vp), ("bias", c_vp), ("ctx", c_vp), ("dctx", c_vp),
                 ("lse", c_vp), ("delta", c_vp), ("dqkv", c_vp), ("dgate", c_vp), ("diag", c_vp),
                 ("batch", c_int), ("T", c_int), ("H", c_int), ("head_dim", c_int), ("scale", c_f),
-                ("dropout_p", c_f), ("seed", c_u32), ("bias_vec", c_vp), ("drop_mask", c_vp), ("diag_part", c_vp)]
+                ("dropout_p", c_f), ("seed", c_u32), ("bias_vec", c_vp), ("diag_part", c_vp), ("drop_mask", c_vp)]
 
 
 class Conv0Params(ctypes.Structure):
@@ -107,7 +111,8 @@ class AdamWParams(ctypes.Structure):
                 ("n", c_ll), ("lr", c_f), ("beta1", c_f), ("beta2", c_f), ("eps", c_f), ("weight_decay", c_f),
                 ("step", c_int), ("max_norm", c_f), ("sumsq", c_vp), ("grad_scale", c_f),
                 ("p_shadow_lo", c_vp), ("ema_t", c_vp), ("ema_shadow", c_vp), ("ema_shadow_lo", c_vp),
-                ("ema_shadow_dtype", c_int), ("ema_decay", c_f), ("ema_n", c_ll)]
+                ("ema_shadow_dtype", c_int), ("ema_decay", c_f), ("ema_n", c_ll),
+                ("p_shadow_lo8", c_vp), ("ema_shadow_lo8", c_vp), ("lo8_exp", c_int), ("zero_grad", c_int)]
 
 
 _P = ctypes.POINTER
@@ -154,6 +159,9 @@ _SIGNATURES = {
     "nrse_colsum_workspace": ([c_ll, c_int], c_ll),
     "nrse_cast": ([c_vp, c_int, c_vp, c_int, c_ll, c_vp], c_int),
     "nrse_split_bf16": ([c_vp, c_vp, c_vp, c_ll, c_vp], c_int),
+    "nrse_split_lo8": ([c_vp, c_vp, c_int, c_ll, c_vp], c_int),
+    "nrse_cast_fp8": ([c_vp, c_int, c_vp, c_ll, c_vp], c_int),
+    "nrse_zero": ([c_vp, c_ll, c_vp], c_int),
     "nrse_splitk_reduce": ([c_vp, c_vp, c_int, c_ll, c_int, c_vp], c_int),
     "nrse_rows_reduce": ([c_vp, c_ll, c_vp, c_ll, c_vp, c_ll, c_vp, c_int, c_int, c_int, c_vp], c_int),
     "nrse_swap12": ([c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),

@@ -310,26 +310,46 @@ def seed_host_rng(seed: int, rank: int) -> None:
 
 
 def create_raw_dataloaders(config: dict, *, synthetic_items: int | None = None, rank: int = 0, world: int = 1):
-    """(train_loader, val_loader, base dataset) of RAW batches, split 85/15 with the seeded
-    generator as in create_dataloaders (noisy_speech_dataset.py:163-175)."""
+    """(train_loader, val_loader, base dataset) of RAW batches, split with the seeded generator as
+    in create_dataloaders (noisy_speech_dataset.py:163-175).
+
+    Data: the WAV files under `data.clean_data_path` / `data.noise_data_path`; a directory that is
+    missing or holds no audio file raises (a mistyped path must not train on anything else).
+    Synthetic pairs only when asked for explicitly: `synthetic_items=N` or `data.synthetic: N`.
+
+    Batching follows the reference's DataLoaders (noisy_speech_dataset.py:178-192): no drop_last,
+    so len(loader) = ceil(items / batch_size) and the validation tail is kept. One guard: a final
+    TRAINING batch of exactly one pair is dropped -- the heads' BatchNorm1d in train mode cannot
+    normalise a single row (the reference raises "Expected more than 1 value per channel" there,
+    SURVEY.md §4)."""
     d, t = config["data"], config["training"]
     sr, secs = int(d["sample_rate"]), float(d["max_audio_length"])
-    clean_dir, noise_dir = d.get("clean_data_path", ""), d.get("noise_data_path", "")
-    if os.path.isdir(clean_dir) and os.path.isdir(noise_dir):
-        ds = WavPairs(get_audio_files(clean_dir), get_audio_files(noise_dir), sr, secs, d["snr_range"])
+    synthetic = synthetic_items or int(d.get("synthetic", 0) or 0)
+    if synthetic:
+        ds = SyntheticPairs(int(synthetic), int(sr * secs), d["snr_range"], seed=t.get("seed", 42))
     else:
-        n = synthetic_items or 64 * int(t["batch_size"])
-        ds = SyntheticPairs(n, int(sr * secs), d["snr_range"], seed=t.get("seed", 42))
+        files = {}
+        for key in ("clean_data_path", "noise_data_path"):
+            path = d.get(key, "")
+            if not path or not os.path.isdir(path):
+                raise FileNotFoundError(f"data.{key} = {path!r} is not a directory (set data.synthetic: N for "
+                                        f"synthetic pairs)")
+            files[key] = get_audio_files(path)
+            if not files[key]:
+                raise FileNotFoundError(f"data.{key} = {path!r} holds no .wav/.flac/.mp3 file")
+        ds = WavPairs(files["clean_data_path"], files["noise_data_path"], sr, secs, d["snr_range"])
     val_size = int(len(ds) * d.get("validation_ratio", 0.1))
     train_ds, val_ds = torch.utils.data.random_split(
         ds, [len(ds) - val_size, val_size], generator=torch.Generator().manual_seed(t.get("seed", 42)))
     train_ds, val_ds = _rank_share(train_ds, rank, world), _rank_share(val_ds, rank, world)
-    kw = dict(batch_size=int(t["batch_size"]), num_workers=min(int(t.get("num_workers", 4)), 8), pin_memory=True,
-              drop_last=True)
+    bs = int(t["batch_size"])
+    kw = dict(batch_size=bs, num_workers=min(int(t.get("num_workers", 4)), 8), pin_memory=True)
     seed = int(t.get("seed", 42))
-    train = torch.utils.data.DataLoader(train_ds, shuffle=True, generator=rank_generator(seed, rank), **kw)
-    val = (torch.utils.data.DataLoader(val_ds, shuffle=False, generator=rank_generator(seed + 1, rank), **kw)
-           if len(val_ds) >= int(t["batch_size"]) else None)
+    train = torch.utils.data.DataLoader(train_ds, shuffle=True, generator=rank_generator(seed, rank),
+                                        drop_last=bs > 1 and len(train_ds) % bs == 1, **kw)
+    val = (torch.utils.data.DataLoader(val_ds, shuffle=False, generator=rank_generator(seed + 1, rank),
+                                       drop_last=False, **kw)
+           if len(val_ds) > 0 else None)
     return train, val, ds
 
 
@@ -348,9 +368,10 @@ def create_dataloaders(config: dict, feature_extractor=None, *, device=None, syn
         tr, va = torch.utils.data.random_split(ds, [len(ds) - val_size, val_size],
                                                generator=torch.Generator().manual_seed(t.get("seed", 42)))
         tr, va = _rank_share(tr, rank, world), _rank_share(va, rank, world)
-        kw = dict(batch_size=int(t["batch_size"]), num_workers=0, drop_last=True)
-        return (torch.utils.data.DataLoader(tr, shuffle=True, **kw),
-                torch.utils.data.DataLoader(va, shuffle=False, **kw) if len(va) >= int(t["batch_size"]) else None)
+        bs = int(t["batch_size"])
+        return (torch.utils.data.DataLoader(tr, shuffle=True, batch_size=bs, num_workers=0,
+                                            drop_last=bs > 1 and len(tr) % bs == 1),
+                torch.utils.data.DataLoader(va, shuffle=False, batch_size=bs, num_workers=0) if len(va) > 0 else None)
     if feature_extractor is not None and hasattr(feature_extractor, "do_normalize"):
         d = {**d, "do_normalize": bool(feature_extractor.do_normalize)}
     device = device or torch.device("cuda", torch.cuda.current_device())

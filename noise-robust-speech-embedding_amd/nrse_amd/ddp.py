@@ -68,6 +68,24 @@ class GradAllReduce:
         self._works = []
         self.issued_elems = 0
 
+    def _to_wire(self, dst: torch.Tensor) -> torch.Tensor:
+        """The bucket in the wire dtype: nrse_cast on the GPU (no ATen kernel in the step); CPU
+        tensors (the gloo tests) through torch."""
+        if not dst.is_cuda:
+            return dst.to(self.wire_dtype)
+        from . import kernels as K
+        buf = torch.empty(dst.shape, device=dst.device, dtype=self.wire_dtype)
+        K.cast(dst, buf)
+        return buf
+
+    @staticmethod
+    def _from_wire(buf: torch.Tensor, dst: torch.Tensor) -> None:
+        if not dst.is_cuda:
+            dst.copy_(buf)
+            return
+        from . import kernels as K
+        K.cast(buf, dst)
+
     def issue(self, view: torch.Tensor) -> None:
         """Asynchronously all-reduce one contiguous gradient range (split into buckets)."""
         if not self.active() or view.numel() == 0:
@@ -79,7 +97,7 @@ class GradAllReduce:
         while end > 0:
             start = max(0, end - step)
             dst = view[start:end]
-            buf = dst if self.wire_dtype is None else dst.to(self.wire_dtype)
+            buf = dst if self.wire_dtype is None else self._to_wire(dst)
             work = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
             self._works.append((work, buf, dst))
             end = start
@@ -89,7 +107,7 @@ class GradAllReduce:
         for work, buf, dst in self._works:
             work.wait()
             if buf is not dst:
-                dst.copy_(buf)
+                self._from_wire(buf, dst)
                 if buf.is_cuda:  # the wire copy is freed after this; keep it until the cast-back ran
                     buf.record_stream(torch.cuda.current_stream(buf.device))
         self._works = []

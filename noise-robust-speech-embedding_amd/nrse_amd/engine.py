@@ -64,6 +64,11 @@ _MASK_AHEAD = os.environ.get("NRSE_MASK_AHEAD", "0") == "1"
 # the target EMA in the AdamW pass (nrse_adamw_params.ema_t) instead of a second pass re-reading
 # the updated weights (nrse_ema); NRSE_FUSED_EMA=0 restores the two launches (A/B)
 _FUSED_EMA = os.environ.get("NRSE_FUSED_EMA", "1") != "0"
+# split-weight mode: the layer GEMMs' correction segment x (w - w_hi) on the fp8 MFMA (fp8 x times the
+# fp8 correction plane of the weights, 2x the bf16 rate) instead of a second bf16 segment;
+# NRSE_SPLIT_LO8=0 restores the bf16 lo plane everywhere (A/B)
+_SPLIT_LO8 = os.environ.get("NRSE_SPLIT_LO8", "1") != "0"
+FP8 = K.FP8
 
 
 @dataclass
@@ -78,6 +83,10 @@ class StepConfig:
     # wait per layer (see ByolEngine.optimizer_step). Same kernels, same per-element arithmetic:
     # parameters are bit-identical to the serial order (tests/test_engine_gpu.py).
     overlap_optimizer: bool = False
+    # The AdamW pass zeroes the gradient buffer after reading it (nrse_adamw_params.zero_grad), so
+    # the next step accumulates without a separate 1.3 GB fill on the critical path. self.grad
+    # then no longer holds the last step's gradient after train_step (tests that read it keep False).
+    fused_zero_grad: bool = False
 
 
 @dataclass
@@ -107,10 +116,16 @@ class EncoderWeights:
     and the per-step derived layouts (conv weights in implicit-GEMM order, weight-normed
     pos-conv in forward and flipped-dgrad order)."""
 
-    def __init__(self, eng: "ByolEngine", master: torch.Tensor, shadow: torch.Tensor | None, lo_stride: int = 0):
+    def __init__(self, eng: "ByolEngine", master: torch.Tensor, shadow: torch.Tensor | None, lo_stride: int = 0,
+                 lo8: torch.Tensor | None = None):
         self.eng = eng
         self.m = eng.group_views(master, "encoder")
         self.s = eng.group_views(shadow, "encoder") if shadow is not None else self.m
+        # split-weight mode, fp8 form: the fp8 correction plane of the weights (views, and the flat
+        # buffer for the fused QKV view); None: the bf16 lo plane serves every correction
+        self.s8 = eng.group_views(lo8, "encoder") if lo8 is not None else None
+        self.s8_flat = lo8
+        self.lo8_exp = eng.lo8_exp
         # split-weight mode: every bf16 weight view of the forward GEMMs has its lo plane
         # lo_stride elements further on (shadows: the [2, n] plane buffers; the derived conv /
         # pos-conv layouts below: [2, ...] tensors, plane 0 = hi)
@@ -129,7 +144,7 @@ class EncoderWeights:
                 K.swap12(w, r32, co, ci, k)
                 r3 = torch.empty(3, co, k * ci, device=eng.dev, dtype=cdt)
                 K.split_bf16(r32, r3[0], r3[2])
-                r3[1].copy_(r3[0])
+                K.cast(r3[0], r3[1])
                 self.conv_r.append(r3[0])
                 self.conv_lo.append(r32.numel())
             else:
@@ -163,7 +178,7 @@ class EncoderWeights:
 class ByolEngine:
     def __init__(self, arch: WavLMArch, proj_dim: int, pred_dim: int, *, device="cuda", compute_dtype=torch.bfloat16,
                  seed: int = 1234, step_cfg: StepConfig | None = None, init_flat: torch.Tensor | None = None,
-                 do_normalize: bool = True, weight_split: bool = False):
+                 do_normalize: bool = True, weight_split: bool = False, split_lo8: bool | None = None):
         if arch.head_dim != 64:
             raise _lib.NrseError(f"head_dim {arch.head_dim} unsupported (attention kernels are head_dim 64)")
         if weight_split and compute_dtype != torch.bfloat16:
@@ -188,6 +203,9 @@ class ByolEngine:
         self.m = torch.zeros(n, device=self.dev, dtype=F32)
         self.v = torch.zeros(n, device=self.dev, dtype=F32)
         self.online_lo = self.target_lo = None
+        # fp8 correction planes of the split-weight mode: fp8((w - bf16(w)) 2^lo8_exp)
+        self.online_lo8 = self.target_lo8 = None
+        self.lo8_exp = 0
         if self.cdt == F32:
             self.online_sh = None
             self.target_sh = None
@@ -199,6 +217,9 @@ class ByolEngine:
             self.target_sh, self.target_lo = tg2[0], tg2[1]
             K.split_bf16(self.online, self.online_sh, self.online_lo)
             K.split_bf16(self.target, self.target_sh, self.target_lo)
+            if _SPLIT_LO8 if split_lo8 is None else split_lo8:
+                self.online_lo8 = torch.empty(n, device=self.dev, dtype=FP8)
+                self.target_lo8 = torch.empty(ne, device=self.dev, dtype=FP8)
         else:
             self.online_sh = torch.empty(n, device=self.dev, dtype=self.cdt)
             self.target_sh = torch.empty(ne, device=self.dev, dtype=self.cdt)
@@ -211,6 +232,8 @@ class ByolEngine:
             off, cnt, shp = self.layout.offsets[PR.GROUP_PREFIX[gname] + s.name]
             self._offsets.setdefault(gname, {})[s.name] = (off, cnt, shp)
         self._check_fused_views()
+        if self.online_lo8 is not None:
+            self._set_lo8_planes()
         # BatchNorm running statistics (buffers, not EMA'd: src/models/byol.py:62-73)
         self.bn = {}
         for net, dims in (("online_projector", (proj_dim, proj_dim)), ("target_projector", (proj_dim, proj_dim)),
@@ -218,6 +241,8 @@ class ByolEngine:
             for li, c in zip((1, 4), dims):
                 self.bn[f"{net}.layers.{li}"] = (torch.zeros(c, device=self.dev), torch.ones(c, device=self.dev),
                                                  torch.zeros((), dtype=torch.long, device=self.dev))
+        self._bn_count = {k: 0 for k in self.bn}   # num_batches_tracked, kept on the host (no step kernel)
+        self._grad_zeroed = True                    # self.grad holds zeros (fresh, or a zero_grad AdamW ran)
         self._buckets = {}
         self.sumsq_buf = torch.zeros(1, device=self.dev, dtype=torch.float64)
         self.loss_buf = torch.zeros(1, device=self.dev, dtype=F32)
@@ -248,6 +273,44 @@ class ByolEngine:
                 K.split_bf16(src, sh, lo)
             else:
                 K.cast(src, sh)
+        if self.online_lo8 is not None:
+            self._set_lo8_planes()   # the exponent follows the (possibly loaded) weights' range
+
+    def _lo8_weights(self, flat: torch.Tensor) -> list:
+        """The weight matrices whose forward GEMM takes the fp8 correction segment (the layers'
+        QKV, FFN-up, FFN-down; encoder_forward)."""
+        out = []
+        for li in range(self.arch.layers):
+            p = f"encoder.layers.{li}."
+            out.append(self.fused(flat, li, "qkv_w"))
+            for n in ("feed_forward.intermediate_dense.weight", "feed_forward.output_dense.weight"):
+                off, cnt, shp = self._offsets["encoder"][p + n]
+                out.append(flat[off:off + cnt])
+        return out
+
+    def _set_lo8_planes(self) -> None:
+        """Choose lo8_exp from the range of the fp8-corrected weights and write both networks' fp8
+        correction planes (nrse_split_lo8). |w - bf16(w)| <= 2^-8 |w|, so with W = max |w| the plane's
+        values stay below 448 / 2 (2x headroom for weights that grow in training; beyond it the
+        conversion saturates) at lo8_exp = floor(log2(224 / (2^-8 W))); the smallest weights fall to
+        fp8 subnormals, whose absolute error (2^-9 2^-lo8_exp) is far below the bf16 residual itself."""
+        W = max(float(t.abs().max()) for f in (self.online, self.target) for t in self._lo8_weights(f))
+        self.lo8_exp = int(math.floor(math.log2(224.0 * 256.0 / max(W, 1e-30)))) if W > 0 else 0
+        self.lo8_exp = max(-60, min(60, self.lo8_exp))
+        K.split_lo8(self.online, self.online_lo8, self.lo8_exp)
+        K.split_lo8(self.target, self.target_lo8, self.lo8_exp)
+
+    def bn_state(self, key: str) -> tuple:
+        """(running_mean, running_var, num_batches_tracked) of a head BatchNorm; the counter is kept
+        on the host during training and written into its buffer here."""
+        rm, rv, nbt = self.bn[key]
+        nbt.fill_(self._bn_count[key])
+        return rm, rv, nbt
+
+    def bn_counts_from_buffers(self) -> None:
+        """Adopt num_batches_tracked values written into the buffers (a loaded checkpoint)."""
+        for k, (_, _, nbt) in self.bn.items():
+            self._bn_count[k] = int(nbt)
 
     # ------------------------------------------------------------------ overlapped optimizer
     def _param_segments(self) -> list:
@@ -275,19 +338,21 @@ class ByolEngine:
             torch.cuda.current_stream(self.dev).wait_event(self._opt_done)
 
     # ------------------------------------------------------------------ views
-    def group_views(self, flat: torch.Tensor, group: str) -> dict:
+    def group_views(self, flat: torch.Tensor, group: str, cached: bool = True) -> dict:
         """name -> view of `flat` for every parameter of `group`. Cached per (buffer object,
         group): building the encoder's ~400 views costs ~1.5 ms of host time, and the step asks
         for them five times (both views' master and shadow weights, the gradient), which delayed
         the enqueue of each step's first kernels. The cache holds the buffer itself and is keyed
         on its identity, so a replaced buffer (load_state_dict) gets fresh views."""
         key = (id(flat), group)
-        hit = self._view_cache.get(key)
+        hit = self._view_cache.get(key) if cached else None
         if hit is not None and hit[0] is flat:
             return hit[1]
         out = {}
         for name, (off, cnt, shp) in self._offsets[group].items():
             out[name] = flat[off:off + cnt].view(shp)
+        if not cached:   # a caller that hands the views out (WavLMEncoder.model): its own objects
+            return out
         if len(self._view_cache) >= 32:   # callers passing transient buffers: stay bounded
             self._view_cache.clear()
         self._view_cache[key] = (flat, out)
@@ -437,6 +502,11 @@ class ByolEngine:
         # -------- transformer layers ([TF]modeling_wavlm.py:488-513, 355-373)
         F_ = a.ffn
         hcur = h0
+        lo8 = W.s8 is not None
+
+        def corr(x8, w8):
+            # the weight correction of a layer GEMM: the fp8 segment (x8, w8) or the bf16 lo plane
+            return dict(x8=x8, w8=w8, lo8_exp=W.lo8_exp) if lo8 else dict(w_lo=W.lo)
         pat = a.attention_dropout if train else 0.0
         pact = a.activation_dropout if train else 0.0
         executed = 0
@@ -467,10 +537,13 @@ class ByolEngine:
             x1 = torch.empty(BT, H, device=dev, dtype=cdt)
             m1 = torch.empty(BT, device=dev, dtype=F32)
             r1 = torch.empty(BT, device=dev, dtype=F32)
-            K.ln_fwd(hcur, Pm[p + "layer_norm.weight"], Pm[p + "layer_norm.bias"], x1, m1, r1, a.eps)
+            # split-weight mode, fp8 form: the LN outputs' fp8 copies feed the correction segments
+            x1_8 = torch.empty(BT, H, device=dev, dtype=FP8) if lo8 else None
+            K.ln_fwd(hcur, Pm[p + "layer_norm.weight"], Pm[p + "layer_norm.bias"], x1, m1, r1, a.eps, y8=x1_8)
             qkv = torch.empty(BT, 3 * H, device=dev, dtype=cdt)
             K.linear_fwd(x1, self.fused(W.s_flat, li, "qkv_w"), qkv, bias=self.fused(W.m_flat, li, "qkv_b"),
-                         w_lo=W.lo)
+                         **corr(x1_8, self.fused(W.s8_flat, li, "qkv_w") if lo8 else None))
+            del x1_8
             gate = torch.empty(B, nh, T, device=dev, dtype=F32)
             at = p + "attention."
             K.gate_fwd(x1, Pm[at + "gru_rel_pos_linear.weight"], Pm[at + "gru_rel_pos_linear.bias"],
@@ -488,16 +561,25 @@ class ByolEngine:
             x2 = torch.empty(BT, H, device=dev, dtype=cdt)
             m2 = torch.empty(BT, device=dev, dtype=F32)
             r2 = torch.empty(BT, device=dev, dtype=F32)
-            K.ln_fwd(hmid, Pm[p + "final_layer_norm.weight"], Pm[p + "final_layer_norm.bias"], x2, m2, r2, a.eps)
+            x2_8 = torch.empty(BT, H, device=dev, dtype=FP8) if lo8 else None
+            K.ln_fwd(hmid, Pm[p + "final_layer_norm.weight"], Pm[p + "final_layer_norm.bias"], x2, m2, r2, a.eps,
+                     y8=x2_8)
             f1pre = torch.empty(BT, F_, device=dev, dtype=cdt) if need_grad else None
             g1 = torch.empty(BT, F_, device=dev, dtype=cdt)
+            # (fp8 form: the FFN-up epilogue also writes fp8(g1), FFN-down's correction operand; the
+            # activation dropout, 0 in the step, would come before that copy is taken)
+            g1_8 = torch.empty(BT, F_, device=dev, dtype=FP8) if lo8 else None
             K.linear_fwd(x2, Ps[p + "feed_forward.intermediate_dense.weight"], g1,
                          bias=Pm[p + "feed_forward.intermediate_dense.bias"], flags=_lib.EPI_GELU, aux=f1pre,
-                         ldaux=F_, dropout_p=pact, seed=R.site_seed(fseed, R.site_act(li)), w_lo=W.lo)
+                         ldaux=F_, dropout_p=pact, seed=R.site_seed(fseed, R.site_act(li)), out8=g1_8,
+                         **corr(x2_8, W.s8[p + "feed_forward.intermediate_dense.weight"] if lo8 else None))
+            del x2_8
             hout = torch.empty(BT, H, device=dev, dtype=F32)
             K.linear_fwd(g1, Ps[p + "feed_forward.output_dense.weight"], hout,
                          bias=Pm[p + "feed_forward.output_dense.bias"], resid=hmid, ldr=H, dropout_p=php,
-                         seed=R.site_seed(fseed, R.site_ffn_out(li)), w_lo=W.lo)
+                         seed=R.site_seed(fseed, R.site_ffn_out(li)),
+                         **corr(g1_8, W.s8[p + "feed_forward.output_dense.weight"] if lo8 else None))
+            del g1_8
             if need_grad:
                 tape.layers.append(dict(li=li, h_in=hcur, x1=x1, m1=m1, r1=r1, qkv=qkv, gate=gate, ctx=ctx, lse=lse,
                                         hmid=hmid, x2=x2, m2=m2, r2=r2, f1pre=f1pre, g1=g1, dmask=dmask))
@@ -511,7 +593,8 @@ class ByolEngine:
             K.ln_fwd(hcur, Pm["encoder.layer_norm.weight"], Pm["encoder.layer_norm.bias"], y, mf, rf, a.eps)
             return y.view(B, T, H), None, executed
         # -------- final LN + time-mean shim
-        emb = torch.zeros(B, H, device=dev, dtype=F32)
+        emb = torch.empty(B, H, device=dev, dtype=F32)
+        K.zero(emb)
         mf = torch.empty(BT, device=dev, dtype=F32)
         rf = torch.empty(BT, device=dev, dtype=F32)
         K.ln_mean_fwd(hcur, Pm["encoder.layer_norm.weight"], Pm["encoder.layer_norm.bias"], emb, mf, rf, B, T, H,
@@ -560,7 +643,8 @@ class ByolEngine:
         K.ln_bwd(demb, hfin, Pm["encoder.layer_norm.weight"], mf, rf, dh, dgamma=Gv["encoder.layer_norm.weight"],
                  dbeta=Gv["encoder.layer_norm.bias"], mode=_lib.DY_BCAST, bcast_t=T, dy_scale=1.0 / T, rows=BT, **kw)
         tape.final = None
-        diag = torch.zeros(nh, 2 * T - 1, device=dev, dtype=F32)
+        diag = torch.empty(nh, 2 * T - 1, device=dev, dtype=F32)
+        K.zero(diag)
         delta = torch.empty(B, nh, T, device=dev, dtype=F32)
         # the transformer layers' weight gradients (off the dX critical path) run on a side stream
         main = torch.cuda.current_stream(dev)
@@ -780,12 +864,12 @@ class ByolEngine:
             n = int(round(float(sums[2 * C])))
             K.bn_fwd_global(x, P[name + ".weight"], P[name + ".bias"], y, rm, rv, sm, si, sums[:2 * C], n, relu)
             if train:
-                nbt.add_(1)
+                self._bn_count[bn_key] += 1
             return y, (x, y, sm, si, n)
         else:
             K.bn_fwd(x, P[name + ".weight"], P[name + ".bias"], y, rm, rv, sm, si, train, relu)
         if train:
-            nbt.add_(1)
+            self._bn_count[bn_key] += 1
         return y, (x, y, sm, si)
 
     def projector_forward(self, emb, P, net, train):
@@ -844,10 +928,12 @@ class ByolEngine:
         """Encoder weight views (+ the derived conv / pos-conv GEMM layouts, computed on the
         current stream). Inside forward() the caller has waited for the front-end segment."""
         if which == "online":
-            W = EncoderWeights(self, self.online, self.online_sh, self.online.numel() if self.wsplit else 0)
+            W = EncoderWeights(self, self.online, self.online_sh, self.online.numel() if self.wsplit else 0,
+                               lo8=self.online_lo8)
             W.m_flat, W.s_flat = self.online, (self.online_sh if self.online_sh is not None else self.online)
         else:
-            W = EncoderWeights(self, self.target, self.target_sh, self.target.numel() if self.wsplit else 0)
+            W = EncoderWeights(self, self.target, self.target_sh, self.target.numel() if self.wsplit else 0,
+                               lo8=self.target_lo8)
             W.m_flat, W.s_flat = self.target, (self.target_sh if self.target_sh is not None else self.target)
         return W
 
@@ -1013,19 +1099,25 @@ class ByolEngine:
         c = self.cfg
         self.step_count += 1
         self.sync_optimizer()  # the previous step's update has read sumsq_buf
-        self.sumsq_buf.zero_()
+        K.zero(self.sumsq_buf)
         K.sumsq(self.grad, self.sumsq_buf)
         kw = dict(lr=lr, beta1=c.betas[0], beta2=c.betas[1], eps=c.eps, weight_decay=c.weight_decay,
-                  step=self.step_count, max_norm=c.max_norm, sumsq_buf=self.sumsq_buf, grad_scale=grad_scale)
+                  step=self.step_count, max_norm=c.max_norm, sumsq_buf=self.sumsq_buf, grad_scale=grad_scale,
+                  lo8_exp=self.lo8_exp, zero_grad=c.fused_zero_grad)
+        self._grad_zeroed = c.fused_zero_grad
         ne = self.layout.ema_numel
+        o8, t8 = self.online_lo8, self.target_lo8
         if not c.overlap_optimizer:
             if _FUSED_EMA:
                 K.adamw(self.online, self.grad, self.m, self.v, self.online_sh, shadow_lo=self.online_lo,
                         ema_t=self.target, ema_shadow=self.target_sh, ema_shadow_lo=self.target_lo,
-                        ema_decay=c.ema_decay, **kw)
+                        ema_decay=c.ema_decay, shadow_lo8=o8, ema_shadow_lo8=t8, **kw)
             else:
-                K.adamw(self.online, self.grad, self.m, self.v, self.online_sh, shadow_lo=self.online_lo, **kw)
+                K.adamw(self.online, self.grad, self.m, self.v, self.online_sh, shadow_lo=self.online_lo,
+                        shadow_lo8=o8, **kw)
                 K.ema(self.target, self.online[:ne], self.target_sh, c.ema_decay, shadow_lo=self.target_lo)
+                if t8 is not None:
+                    K.split_lo8(self.target, t8, self.lo8_exp)
             self._opt_events = self._opt_done = None
             return
         main = torch.cuda.current_stream(self.dev)
@@ -1045,10 +1137,13 @@ class ByolEngine:
                             ema_t=self.target[s:te] if fuse else None,
                             ema_shadow=tsh[s:te] if fuse and tsh is not None else None,
                             ema_shadow_lo=tlo[s:te] if fuse and tlo is not None else None,
-                            ema_decay=c.ema_decay, **kw)
+                            ema_decay=c.ema_decay, shadow_lo8=o8[s:e] if o8 is not None else None,
+                            ema_shadow_lo8=t8[s:te] if fuse and t8 is not None else None, **kw)
                     if te > s and not fuse:
                         K.ema(self.target[s:te], self.online[s:te], tsh[s:te] if tsh is not None else None,
                               c.ema_decay, shadow_lo=tlo[s:te] if tlo is not None else None)
+                        if t8 is not None:
+                            K.split_lo8(self.target[s:te], t8[s:te], self.lo8_exp)
                 ev = torch.cuda.Event()
                 ev.record(st)
                 events.append(ev)
@@ -1064,17 +1159,19 @@ class ByolEngine:
         """One iteration of train_one_epoch (train_byol.py:47-77): forward, loss, backward,
         clip, AdamW, EMA. Returns the device-resident loss (no sync)."""
         B = clean.shape[0]
-        self.health_buf.zero_()   # rows: clean, noisy, online_pred, target_proj (nrse_amd/health.py)
+        K.zero(self.health_buf)   # rows: clean, noisy, online_pred, target_proj (nrse_amd/health.py)
         K.health(clean, self.health_buf[0])
         K.health(noisy, self.health_buf[1])
         pred, tproj, ctx = self.forward(clean, noisy, train=True, step_seed=step_seed, rank=rank, need_grad=True)
         K.health(pred, self.health_buf[2])
         K.health(tproj, self.health_buf[3])
-        self.loss_buf.zero_()
+        K.zero(self.loss_buf)
         dpred = torch.empty_like(pred)
         K.byol_loss(pred, tproj, self.loss_buf, dpred, self.loss_stats)
-        self.sync_optimizer()  # the last update has read the gradient buffer
-        self.grad.zero_()
+        self.sync_optimizer()  # the last update has read (and with fused_zero_grad zeroed) the gradient
+        if not self._grad_zeroed:
+            K.zero(self.grad)
+        self._grad_zeroed = False
         self.backward(dpred, ctx, allreduce=allreduce)
         self.optimizer_step(lr, grad_scale=1.0 / world_size)
         return self.loss_buf

@@ -15,7 +15,8 @@ from . import _lib
 from ._lib import (AdamWParams, AttnBwdParams, AttnFwdParams, Conv0Params, GemmOperand, GemmParams, LnBwdParams,
                    LnFwdParams)
 
-_DT = {torch.float32: _lib.F32, torch.bfloat16: _lib.BF16}
+_DT = {torch.float32: _lib.F32, torch.bfloat16: _lib.BF16, torch.float8_e4m3fn: _lib.FP8}
+FP8 = torch.float8_e4m3fn  # NRSE_FP8: OCP e4m3fn, the split-weight mode's correction operands
 
 
 def dtype_code(t: torch.Tensor) -> int:
@@ -100,8 +101,11 @@ def gemm(A: Operand, B: Operand, C: torch.Tensor, M: int, N: int, K: int, *, ldc
          bias_z1: int = 0, bias_z2: int = 0,
          aux: torch.Tensor | None = None, ldaux: int = 0, aux_z1: int = 0, aux_z2: int = 0,
          resid: torch.Tensor | None = None, ldr: int = 0, r_z1: int = 0, r_z2: int = 0,
-         dropout_p: float = 0.0, seed: int = 0, colsum: torch.Tensor | None = None) -> None:
-    """C[m,n] = epilogue(alpha * sum_k A(m,k) B(n,k)); see nrse_gemm."""
+         dropout_p: float = 0.0, seed: int = 0, colsum: torch.Tensor | None = None,
+         a8: Operand | None = None, b8: Operand | None = None, nseg8: int = 0, b8_exp: int = 0,
+         c8: torch.Tensor | None = None, ldc8: int = 0) -> None:
+    """C[m,n] = epilogue(alpha * sum_k A(m,k) B(n,k)); see nrse_gemm. a8 / b8 / nseg8 / b8_exp: the
+    split-weight mode's fp8 correction segments (+ 2^-b8_exp sum a8 b8); c8: an fp8 copy of a bf16 C."""
     if bias is not None:
         assert bias.dtype == torch.float32
         flags |= _lib.EPI_BIAS
@@ -134,6 +138,12 @@ def gemm(A: Operand, B: Operand, C: torch.Tensor, M: int, N: int, K: int, *, ldc
     p.dropout_p = dropout_p
     p.seed = seed & 0xFFFFFFFF
     p.colsum = ptr(colsum)
+    if nseg8:
+        assert a8 is not None and b8 is not None and a8.t.dtype == b8.t.dtype == FP8
+        p.a8, p.b8, p.nseg8, p.b8_exp = a8.c(), b8.c(), nseg8, b8_exp
+    if c8 is not None:
+        assert c8.dtype == FP8
+        p.c8, p.ldc8 = ptr(c8), ldc8
     ws = None
     if colsum is not None and DETERMINISTIC:
         ws = workspace(_lib.lib().nrse_gemm_colsum_workspace(ctypes.byref(p)))
@@ -143,7 +153,7 @@ def gemm(A: Operand, B: Operand, C: torch.Tensor, M: int, N: int, K: int, *, ldc
         # algorithmic HBM bytes: A and B read once, C written once (read too when accumulated),
         # epilogue operands (bias, aux, residual) once
         ea = A.t.element_size()
-        nb = (M * K * nseg * splits + N * K * nseg * splits) * ea * batch
+        nb = (M * K * nseg * splits + N * K * nseg * splits) * ea * batch + (M + N) * K * nseg8 * batch
         cb = M * N * C.element_size() * batch * (splits if flags & _lib.EPI_ATOMIC else 1)
         nb += cb * (2 if flags & (_lib.EPI_ACCUM | _lib.EPI_ATOMIC) else 1)
         if aux is not None:
@@ -157,7 +167,10 @@ def gemm(A: Operand, B: Operand, C: torch.Tensor, M: int, N: int, K: int, *, ldc
     _lib.check(_lib.lib().nrse_gemm(ctypes.byref(p), stream_ptr()), "nrse_gemm")
     if probe is not None:
         e1.record()
-        probe.append((2.0 * M * N * K * nseg * splits * batch, e0, e1, (M, N, K * nseg * splits, batch)))
+        # bf16-equivalent work: an fp8 correction segment runs at twice the bf16 MFMA rate, so its
+        # FLOPs count half against the bf16 dense peak
+        probe.append((2.0 * M * N * K * (nseg * splits + 0.5 * nseg8) * batch, e0, e1,
+                      (M, N, K * nseg * splits, batch) if not nseg8 else (M, N, K * nseg, batch, f"fp8x{nseg8}")))
 
 
 # When set to a list, every nrse_gemm launch appends (algorithmic FLOPs, start event, end event,
@@ -197,15 +210,27 @@ def gemm_probe_bytes():
 
 # ----------------------------------------------------------------------------- linear helpers
 def linear_fwd(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, *, bias=None, flags: int = 0, w_lo: int = 0,
-               **kw) -> None:
+               x8: torch.Tensor | None = None, w8: torch.Tensor | None = None, lo8_exp: int = 0,
+               out8: torch.Tensor | None = None, **kw) -> None:
     """out[M,N] = x[M,K] @ w[N,K]^T (+ epilogue). x, w share the compute dtype. w_lo != 0: the
     split-weight mode, w's lo plane sits w_lo elements after it and the product is
-    x @ (w_hi + w_lo)^T, two K segments of one launch (A read twice, one epilogue)."""
+    x @ (w_hi + w_lo)^T, two K segments of one launch (A read twice, one epilogue). x8, w8 (fp8,
+    the split-weight mode's fp8 form): x @ w_hi^T + 2^-lo8_exp x8 @ w8^T, the
+    correction segment on the MX-scaled fp8 MFMA (x8 = fp8(x), w8 = fp8((w - w_hi) 2^lo8_exp)).
+    out8 (fp8, bf16 out): an fp8 copy of the stored output (the next GEMM's x8)."""
     M, K = x.shape
     N = w.shape[0]
     assert w.shape[1] == K and out.shape[-1] >= N
+    f8 = {}
+    if x8 is not None or w8 is not None:
+        assert not w_lo and x8 is not None and w8 is not None
+        assert x8.shape == x.shape and x8.stride(0) == x.stride(0) and w8.shape == w.shape and w8.stride(0) == w.stride(0)
+        f8 = dict(a8=Operand(x8, True, x8.stride(0)), b8=Operand(w8, True, w8.stride(0)), nseg8=1, b8_exp=lo8_exp)
+    if out8 is not None:
+        assert out8.shape[0] == M and out8.shape[1] >= N
+        f8.update(c8=out8, ldc8=out8.stride(0))
     gemm(Operand(x, True, x.stride(0)), Operand(w, True, w.stride(0), seg_stride=w_lo), out, M, N, K,
-         ldc=out.stride(0), nseg=2 if w_lo else 1, bias=bias, flags=flags, **kw)
+         ldc=out.stride(0), nseg=2 if w_lo else 1, bias=bias, flags=flags, **f8, **kw)
 
 
 def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, dx: torch.Tensor, *, flags: int = 0, **kw) -> None:
@@ -383,10 +408,13 @@ def _out_code(y: torch.Tensor, n: int, split3: bool) -> int:
     return _lib.BF16X3
 
 
-def ln_fwd(x, gamma, beta, y, mean, rstd, eps, gelu=False, relu=False, split3=False):
+def ln_fwd(x, gamma, beta, y, mean, rstd, eps, gelu=False, relu=False, split3=False, y8=None):
+    """y8 (fp8 [rows, C], bf16 y): also y8 = fp8(y), the split-weight mode's next correction operand."""
     rows, C = x.shape[0] if x.dim() == 2 else x.numel() // x.shape[-1], x.shape[-1]
+    if y8 is not None:
+        assert y8.dtype == FP8 and y8.numel() == rows * C and y8.is_contiguous()
     p = LnFwdParams(ptr(x), dtype_code(x), ptr(gamma), ptr(beta), ptr(y), _out_code(y, rows * C, split3), ptr(mean),
-                    ptr(rstd), rows, C, eps, (_lib.LN_GELU if gelu else 0) | (_lib.LN_RELU if relu else 0))
+                    ptr(rstd), rows, C, eps, (_lib.LN_GELU if gelu else 0) | (_lib.LN_RELU if relu else 0), ptr(y8))
     _call("nrse_layernorm_fwd", ctypes.byref(p), stream_ptr())
 
 
@@ -501,7 +529,8 @@ def attn_bwd(qkv, gate, bias, ctx, dctx, lse, delta, dqkv, dgate, diag, batch, T
              bias_vec=None, drop_mask=None):
     p = AttnBwdParams(ptr(qkv), dtype_code(qkv), ptr(gate), ptr(bias), ptr(ctx), ptr(dctx), ptr(lse), ptr(delta),
                       ptr(dqkv), ptr(dgate), ptr(diag), batch, T, H, 64, 0.125, dropout_p, seed & 0xFFFFFFFF,
-                      ptr(bias_vec), ptr(drop_mask))
+                      ptr(bias_vec))
+    p.drop_mask = ptr(drop_mask)
     ws = None
     if DETERMINISTIC and diag is not None:
         ws = workspace(_lib.lib().nrse_attn_bwd_workspace(ctypes.byref(p)))
@@ -667,18 +696,24 @@ def sumsq(x, out):
 
 
 def adamw(p, g, m, v, shadow, *, lr, beta1, beta2, eps, weight_decay, step, max_norm, sumsq_buf, grad_scale=1.0,
-          shadow_lo=None, ema_t=None, ema_shadow=None, ema_shadow_lo=None, ema_decay=0.0):
+          shadow_lo=None, ema_t=None, ema_shadow=None, ema_shadow_lo=None, ema_decay=0.0, shadow_lo8=None,
+          ema_shadow_lo8=None, lo8_exp=0, zero_grad=False):
     """clip + AdamW; shadow (bf16/f32) gets the updated weights, shadow_lo (bf16, with a bf16
     shadow) the split-weight mode's lo plane bf16(p - shadow). ema_t (f32, numel <= p's): the
-    target EMA of the first ema_t.numel() updated weights in the same pass (as ema() after)."""
+    target EMA of the first ema_t.numel() updated weights in the same pass (as ema() after).
+    shadow_lo8 / ema_shadow_lo8 (fp8): the fp8 correction planes fp8((w - bf16(w)) 2^lo8_exp);
+    zero_grad: g is zeroed by the pass after it is read."""
     if ema_t is not None:
         assert ema_t.dtype == torch.float32 and ema_t.numel() <= p.numel()
+    for t, n in ((shadow_lo8, p.numel()), (ema_shadow_lo8, ema_t.numel() if ema_t is not None else 0)):
+        assert t is None or (t.dtype == FP8 and t.numel() == n)
     prm = AdamWParams(ptr(p), ptr(g), ptr(m), ptr(v), ptr(shadow),
                       dtype_code(shadow) if shadow is not None else 0, p.numel(), lr, beta1, beta2, eps,
                       weight_decay, step, max_norm, ptr(sumsq_buf), grad_scale, ptr(shadow_lo),
                       ptr(ema_t), ptr(ema_shadow), ptr(ema_shadow_lo),
                       dtype_code(ema_shadow) if ema_shadow is not None else 0, ema_decay,
-                      ema_t.numel() if ema_t is not None else 0)
+                      ema_t.numel() if ema_t is not None else 0, ptr(shadow_lo8), ptr(ema_shadow_lo8), lo8_exp,
+                      1 if zero_grad else 0)
     _call("nrse_adamw", ctypes.byref(prm), stream_ptr())
 
 
@@ -692,6 +727,24 @@ def split_bf16(x, hi, lo):
     assert x.dtype == torch.float32 and hi.dtype == lo.dtype == torch.bfloat16
     assert hi.numel() == lo.numel() == x.numel()
     _call("nrse_split_bf16", ptr(x), ptr(hi), ptr(lo), x.numel(), stream_ptr())
+
+
+def split_lo8(x, lo8, lo8_exp):
+    """lo8 = fp8((x - bf16(x)) 2^lo8_exp) (nrse_split_lo8): the fp8 correction plane of x."""
+    assert x.dtype == torch.float32 and lo8.dtype == FP8 and lo8.numel() == x.numel()
+    _call("nrse_split_lo8", ptr(x), ptr(lo8), int(lo8_exp), x.numel(), stream_ptr())
+
+
+def cast_fp8(x, y8):
+    """y8 = fp8(x) (nrse_cast_fp8; x f32 or bf16)."""
+    assert y8.dtype == FP8 and y8.numel() == x.numel()
+    _call("nrse_cast_fp8", ptr(x), dtype_code(x), ptr(y8), x.numel(), stream_ptr())
+
+
+def zero(t):
+    """t[:] = 0 for an f32 tensor (nrse_zero; the step's small accumulators, no torch fill)."""
+    assert t.dtype in (torch.float32, torch.float64) and t.is_contiguous()
+    _call("nrse_zero", ptr(t), t.numel() * t.element_size() // 4, stream_ptr())
 
 
 def health(x, stats):

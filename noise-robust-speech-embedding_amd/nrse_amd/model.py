@@ -115,7 +115,8 @@ class WavLMEncoder(nn.Module):
         self.which = which
         self.output_dim = engine.arch.hidden
         flat = engine.online if which == "online" else engine.target
-        self.model = _ParamNamespace(engine.group_views(flat, "encoder"))
+        # uncached views: user code may edit these objects without touching the engine's own views
+        self.model = _ParamNamespace(engine.group_views(flat, "encoder", cached=False))
 
     def forward(self, input_values: torch.Tensor, attention_mask=None) -> torch.Tensor:
         # [B, 1, L] -> [B, L] (encoder.py:20-21); the attention mask is ignored (encoder.py:23-25)
@@ -205,7 +206,7 @@ class BYOLSpeechModel(nn.Module):
             for k, v in views.items():
                 yield k, v
                 if k.endswith(".bias") and k[:-5] in e.bn:
-                    rm, rv, nbt = e.bn[k[:-5]]
+                    rm, rv, nbt = e.bn_state(k[:-5])
                     yield k[:-5] + ".running_mean", rm
                     yield k[:-5] + ".running_var", rv
                     yield k[:-5] + ".num_batches_tracked", nbt
@@ -236,6 +237,7 @@ class BYOLSpeechModel(nn.Module):
             for k, v in own.items():
                 if k in sd:
                     v.copy_(sd[k].to(v.device, v.dtype))
+        self.engine.bn_counts_from_buffers()
         self.refresh_shadows()
         return _IncompatibleKeys(missing, unexpected)
 

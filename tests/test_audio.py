@@ -159,3 +159,56 @@ def test_varlen_substitute_keeps_bucket_length(tmp_path, monkeypatch):
     it = vl[0]                       # a.wav invalid -> b.wav (3 s) stands in, cut to a.wav's 1 s
     assert it["clean"].shape[0] == 16000
     assert int(it["index"]) == 0 and int(it["attempts"]) == 2
+
+
+def _corpus(tmp_path, n_clean, n_noise=3):
+    clean = tmp_path / "clean10"
+    noise = tmp_path / "noise10"
+    clean.mkdir()
+    noise.mkdir()
+    rng = np.random.default_rng(5)
+    for i in range(n_clean):
+        _write_wav(clean / f"{i:02d}.wav", 0.1 * rng.standard_normal(1600), 16000)
+    for i in range(n_noise):
+        _write_wav(noise / f"{i:02d}.wav", rng.standard_normal(1600), 16000)
+    return clean, noise
+
+
+def _cfg(clean, noise, bs, ratio):
+    return {"data": {"clean_data_path": str(clean), "noise_data_path": str(noise), "sample_rate": 16000,
+                     "max_audio_length": 0.1, "snr_range": [5, 10], "validation_ratio": ratio},
+            "training": {"batch_size": bs, "num_workers": 0, "seed": 42}}
+
+
+def test_missing_or_empty_data_directory_raises(tmp_path):
+    """a configured data directory that does not exist, or holds no audio file,
+    fails loudly (the build used to fall back to synthetic pairs silently); synthetic pairs only
+    when asked for (`data.synthetic` / synthetic_items)."""
+    clean, noise = _corpus(tmp_path, 4)
+    cfg = _cfg(clean, tmp_path / "no_such_dir", 2, 0.0)
+    with pytest.raises(FileNotFoundError, match="noise_data_path"):
+        D.create_raw_dataloaders(cfg)
+    empty = tmp_path / "empty"
+    empty.mkdir()
+    with pytest.raises(FileNotFoundError, match="holds no"):
+        D.create_raw_dataloaders(_cfg(empty, noise, 2, 0.0))
+    cfg["data"]["synthetic"] = 8                    # explicit opt-in
+    train, _, ds = D.create_raw_dataloaders(cfg)
+    assert isinstance(ds, D.SyntheticPairs) and len(ds) == 8
+
+
+def test_loader_lengths_match_reference_ragged_split(tmp_path):
+    """The reference's DataLoaders have no drop_last (noisy_speech_dataset.py:178-192): 10 items,
+    validation_ratio 0.3, batch 4 -> val_size = int(10 * 0.3) = 3, train 7 -> ceil(7/4) = 2 train
+    batches (4 + 3) and 1 validation batch of 3 -- the CosineAnnealingLR T_max = len(loader) *
+    epochs (train_byol.py:149-150) follows. The one deviation: a final training batch of exactly
+    one pair is dropped (BatchNorm1d in train mode cannot normalise one row; the reference raises)."""
+    clean, noise = _corpus(tmp_path, 10)
+    train, val, _ = D.create_raw_dataloaders(_cfg(clean, noise, 4, 0.3))
+    assert len(train) == math.ceil(7 / 4) == 2 and len(val) == 1
+    assert sorted(len(b["snr"]) for b in train) == [3, 4]
+    assert [len(b["snr"]) for b in val] == [3]
+    # 10 items, ratio 0.1: train 9 = 4 + 4 + 1 -> the single-pair tail is dropped, val keeps its 1
+    train, val, _ = D.create_raw_dataloaders(_cfg(clean, noise, 4, 0.1))
+    assert len(train) == 2 and [len(b["snr"]) for b in train] == [4, 4]
+    assert len(val) == 1 and [len(b["snr"]) for b in val] == [1]

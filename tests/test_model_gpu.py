@@ -92,7 +92,8 @@ def test_train_cli_synthetic(nrse_device, tmp_path):
                       "weight_decay": 1e-5, "checkpoint_dir": str(tmp_path / "ck"), "log_dir": str(tmp_path / "lg"),
                       "seed": 42, "early_stopping_metric": "val_loss", "early_stopping_patience": 4},
          "data": {"clean_data_path": "/nonexistent", "noise_data_path": "/nonexistent", "sample_rate": 16000,
-                  "max_audio_length": 1.0, "snr_range": [0, 5, 10, 15, 20], "validation_ratio": 0.15},
+                  "max_audio_length": 1.0, "snr_range": [0, 5, 10, 15, 20], "validation_ratio": 0.15,
+                  "synthetic": 256},
          "logging": {"level": "WARNING"}}
     p = tmp_path / "c.yaml"
     p.write_text(yaml.safe_dump(c))
@@ -238,7 +239,8 @@ def test_cli_early_stop_precedes_checkpoints(nrse_device, tmp_path):
                       "seed": 42, "early_stopping_metric": "val_loss", "early_stopping_patience": 1,
                       "early_stopping_min_delta": 1e9},
          "data": {"clean_data_path": "/nonexistent", "noise_data_path": "/nonexistent", "sample_rate": 16000,
-                  "max_audio_length": 0.5, "snr_range": [0, 5, 10, 15, 20], "validation_ratio": 0.15},
+                  "max_audio_length": 0.5, "snr_range": [0, 5, 10, 15, 20], "validation_ratio": 0.15,
+                  "synthetic": 256},
          "logging": {"level": "WARNING"}}
     p = tmp_path / "c.yaml"
     p.write_text(yaml.safe_dump(c))
