@@ -273,6 +273,9 @@ typedef struct {
   int drop_mask_in;               /* nonzero (bf16 MFMA path): drop_mask already holds the keep bits
                                      (nrse_attn_dropout_mask, the same function of seed and position)
                                      and the forward reads them instead of hashing */
+  void* ctx8;                     /* ABI 6, optional (bf16 MFMA path): [B*T, Hd] NRSE_FP8 copy of ctx,
+                                     fp8(bf16 ctx) (the out-projection's fp8 correction operand);
+                                     4-byte aligned. NULL: none */
 } nrse_attn_fwd_params;
 
 typedef struct {

@@ -613,6 +613,8 @@ extern "C" int nrse_attn_fwd(const nrse_attn_fwd_params* p, void* stream) {
                "nrse_attn_fwd: bad args");
   if (p->head_dim != HD) { nrse_set_error("nrse_attn_fwd: head_dim %d != 64", p->head_dim); return NRSE_ERR_UNSUPPORTED; }
   hipStream_t st = (hipStream_t)stream;
+  NRSE_REQUIRE(!p->ctx8 || (nrse_attn_use_mfma(p->dtype, p->head_dim) && ((uintptr_t)p->ctx8 & 3) == 0),
+               "nrse_attn_fwd: ctx8 needs the bf16 MFMA path and 4-byte alignment");
   if (nrse_attn_use_mfma(p->dtype, p->head_dim)) return nrse_attn_fwd_mfma(p, st);
   NRSE_REQUIRE(p->bias, "nrse_attn_fwd: the f32 path needs the [H, T, Tb] bias table");
   dim3 grid((p->T + 63) / 64, p->H, p->batch);

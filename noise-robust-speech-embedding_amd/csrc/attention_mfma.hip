@@ -357,6 +357,12 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
       u.x = (uint32_t)f2bf(o[dt][0] * inv) | ((uint32_t)f2bf(o[dt][1] * inv) << 16);
       u.y = (uint32_t)f2bf(o[dt][2] * inv) | ((uint32_t)f2bf(o[dt][3] * inv) << 16);
       *reinterpret_cast<uint2*>(crow + 16 * dt) = u;
+      if (p.ctx8) {  // ABI 6: fp8(bf16 ctx), the split-weight mode's out-projection operand
+        float b4[4] = {bf2f(f2bf(o[dt][0] * inv)), bf2f(f2bf(o[dt][1] * inv)), bf2f(f2bf(o[dt][2] * inv)),
+                       bf2f(f2bf(o[dt][3] * inv))};
+        *reinterpret_cast<uint32_t*>((unsigned char*)p.ctx8 + ((long long)b * T + qi) * Hd + h * D + 4 * g + 16 * dt) =
+            fp8x4(b4[0], b4[1], b4[2], b4[3]);
+      }
     }
   }
   if (g == 0 && qv) p.lse[bh * T + qi] = (m + __builtin_amdgcn_logf(l)) * LN2;

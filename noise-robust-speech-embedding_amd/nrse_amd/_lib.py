@@ -87,7 +87,7 @@ class AttnFwdParams(ctypes.Structure):
     _fields_ = [("qkv", c_vp), ("dtype", c_int), ("gate", c_vp), ("bias", c_vp), ("ctx", c_vp), ("lse", c_vp),
                 ("batch", c_int), ("T", c_int), ("H", c_int), ("head_dim", c_int), ("scale", c_f),
                 ("dropout_p", c_f), ("seed", c_u32), ("bias_vec", c_vp), ("drop_mask", c_vp),
-                ("drop_mask_in", c_int)]
+                ("drop_mask_in", c_int), ("ctx8", c_vp)]
 
 
 class AttnBwdParams(ctypes.Structure):

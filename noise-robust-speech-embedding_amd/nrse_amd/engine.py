@@ -226,6 +226,8 @@ class ByolEngine:
             K.cast(self.online, self.online_sh)
             K.cast(self.target, self.target_sh)
         self.step_count = 0
+        # the attention dropout keep bits computed ahead on a mask stream (NRSE_MASK_AHEAD, opt-in)
+        self.mask_ahead = _MASK_AHEAD
         self._offsets = {}
         self._view_cache = {}
         for gname, s in self.layout.specs:
@@ -278,12 +280,13 @@ class ByolEngine:
 
     def _lo8_weights(self, flat: torch.Tensor) -> list:
         """The weight matrices whose forward GEMM takes the fp8 correction segment (the layers'
-        QKV, FFN-up, FFN-down; encoder_forward)."""
+        QKV, out-projection, FFN-up, FFN-down; encoder_forward)."""
         out = []
         for li in range(self.arch.layers):
             p = f"encoder.layers.{li}."
             out.append(self.fused(flat, li, "qkv_w"))
-            for n in ("feed_forward.intermediate_dense.weight", "feed_forward.output_dense.weight"):
+            for n in ("attention.out_proj.weight", "feed_forward.intermediate_dense.weight",
+                      "feed_forward.output_dense.weight"):
                 off, cnt, shp = self._offsets["encoder"][p + n]
                 out.append(flat[off:off + cnt])
         return out
@@ -524,7 +527,7 @@ class ByolEngine:
             dmask, mask_ev = None, None
             if pat > 0 and bias_vec is not None:
                 dmask = torch.empty(K.attn_mask_elems(B, T, nh), device=dev, dtype=torch.int16)
-                if _MASK_AHEAD:
+                if self.mask_ahead:
                     cur = torch.cuda.current_stream(dev)
                     ms = self._mask_stream(cur)
                     ms.wait_stream(cur)
@@ -549,15 +552,18 @@ class ByolEngine:
             K.gate_fwd(x1, Pm[at + "gru_rel_pos_linear.weight"], Pm[at + "gru_rel_pos_linear.bias"],
                        Pm[at + "gru_rel_pos_const"], gate, B, T, nh)
             ctx = torch.empty(BT, H, device=dev, dtype=cdt)
+            ctx8 = torch.empty(BT, H, device=dev, dtype=FP8) if lo8 else None
             lse = torch.empty(B, nh, T, device=dev, dtype=F32)
             if mask_ev is not None:
                 torch.cuda.current_stream(dev).wait_event(mask_ev)
             # (without the mask stream the forward hashes and, for the online view, records the bits)
             K.attn_fwd(qkv, gate, bias_tab, ctx, lse, B, T, nh, pat, R.site_seed(fseed, R.site_attn_probs(li)),
-                       bias_vec=bias_vec, drop_mask=dmask, mask_in=mask_ev is not None)
+                       bias_vec=bias_vec, drop_mask=dmask, mask_in=mask_ev is not None, ctx8=ctx8)
             hmid = torch.empty(BT, H, device=dev, dtype=F32)
             K.linear_fwd(ctx, Ps[at + "out_proj.weight"], hmid, bias=Pm[at + "out_proj.bias"], resid=hcur, ldr=H,
-                         dropout_p=php, seed=R.site_seed(fseed, R.site_attn_out(li)), w_lo=W.lo)
+                         dropout_p=php, seed=R.site_seed(fseed, R.site_attn_out(li)),
+                         **corr(ctx8, W.s8[at + "out_proj.weight"] if lo8 else None))
+            del ctx8
             x2 = torch.empty(BT, H, device=dev, dtype=cdt)
             m2 = torch.empty(BT, device=dev, dtype=F32)
             r2 = torch.empty(BT, device=dev, dtype=F32)

@@ -513,15 +513,18 @@ def attn_dropout_mask(mask, batch, T, H, dropout_p, seed):
 
 
 def attn_fwd(qkv, gate, bias, ctx, lse, batch, T, H, dropout_p=0.0, seed=0, bias_vec=None, drop_mask=None,
-             mask_in=False):
+             mask_in=False, ctx8=None):
     """bias: [H, T, Tb] table (f32 parity path), bias_vec: [H, 2T-1] Toeplitz vector (bf16 path);
     drop_mask (optional, int16 [attn_mask_elems]): the keep bits for the backward, recorded by the
-    forward, or (mask_in) read by it (attn_dropout_mask wrote them)."""
+    forward, or (mask_in) read by it (attn_dropout_mask wrote them); ctx8 (fp8, bf16 path): an fp8
+    copy of ctx (the split-weight mode's out-projection correction operand)."""
     if drop_mask is not None:
         assert drop_mask.dtype == torch.int16 and drop_mask.numel() >= attn_mask_elems(batch, T, H)
+    if ctx8 is not None:
+        assert ctx8.dtype == FP8 and ctx8.numel() == ctx.numel() and qkv.dtype == torch.bfloat16
     p = AttnFwdParams(ptr(qkv), dtype_code(qkv), ptr(gate), ptr(bias), ptr(ctx), ptr(lse), batch, T, H, 64,
                       0.125, dropout_p, seed & 0xFFFFFFFF, ptr(bias_vec), ptr(drop_mask),
-                      1 if (mask_in and drop_mask is not None) else 0)
+                      1 if (mask_in and drop_mask is not None) else 0, ptr(ctx8))
     _call("nrse_attn_fwd", ctypes.byref(p), stream_ptr())
 
 

@@ -97,8 +97,13 @@ SITES = ("conv", "proj", "posconv", "qkv", "attn", "oproj", "ffn_up", "ffn_down"
 # weights' hi + lo bf16 pair), the conv stack's activations exact too (split bf16 planes and f32
 # pre-activations), every other activation operand rounded
 SPLIT_WEIGHT_SITES = tuple(f"{s}:a" for s in SITES if s not in ("attn", "conv")) + ("attn",)
+# the split-weight mode's fp8 form (the engine's default bf16sw, ABI 6): at these GEMM sites the
+# weight correction x (w - w_hi) runs as fp8(x) times the fp8 plane fp8((w - w_hi) 2^e), scaled
+# by 2^-e (nrse_gemm's a8 / b8 segment); set_split8(sites, e) switches it on
+SPLIT8_SITES = ("qkv", "oproj", "ffn_up", "ffn_down")
 _OPERAND_DTYPE = None
 _SITES = None
+_SPLIT8 = None   # (frozenset of sites, exponent e) or None
 
 
 def set_operand_dtype(dtype, sites=None) -> None:
@@ -123,6 +128,25 @@ def _site_on(site, kind=None) -> bool:
 
 def operand_dtype():
     return _OPERAND_DTYPE
+
+
+def set_split8(sites=None, exponent: int = 0) -> None:
+    """The fp8 correction form of the split-weight mode at `sites` (None: off), lo8_exp = exponent
+    (engine: ByolEngine._set_lo8_planes)."""
+    global _SPLIT8
+    _SPLIT8 = None if sites is None else (frozenset(sites), int(exponent))
+
+
+def fp8_e4m3(x: torch.Tensor) -> torch.Tensor:
+    """OCP e4m3fn rounding (nearest even) of x saturated at +-448, as nrse_cast_fp8 / the kernels'
+    fp8x4 (torch's own cast gives NaN beyond the range), back in x's dtype."""
+    return x.clamp(-448.0, 448.0).to(torch.float8_e4m3fn).to(x.dtype)
+
+
+def lo8_exponent(weights) -> int:
+    """The engine's lo8_exp: floor(log2(224 / (2^-8 max|w|))) over the fp8-corrected weights."""
+    W = max(float(w.detach().abs().max()) for w in weights)
+    return max(-60, min(60, int(math.floor(math.log2(224.0 * 256.0 / W))))) if W > 0 else 0
 
 
 class _RoundFwd(torch.autograd.Function):
@@ -157,9 +181,24 @@ def _rg(x: torch.Tensor, site=None) -> torch.Tensor:
 def _lin(x, w, b=None, *, store=False, site=None):
     """Linear on the GEMM path: rounded operands, f32 accumulate + bias epilogue, the output's
     gradient rounded (it is the dY operand of this GEMM's dgrad / wgrad); store=True when the
-    engine also stores the output itself in bf16 (QKV, FFN-up pre-activation)."""
-    y = _rg(F.linear(_rf(x, site), _rf(w, site, "w"), b), site)
+    engine also stores the output itself in bf16 (QKV, FFN-up pre-activation). Under set_split8,
+    at its sites: x_b w_hi + 2^-e fp8(x_b) fp8((w - w_hi) 2^e), the correction outside autograd
+    (the engine's backward uses w_hi alone, as the straight-through w_hi here does)."""
+    y = _rg(_linear_core(_rf(x, site), w, b, site), site)
     return _rf(y, site) if store else y
+
+
+def _linear_core(xr, w, b, site):
+    """xr (rounded operand) @ w^T + b at `site`: the weight rounded as the mode says, or under
+    set_split8 the fp8 correction form x_b w_hi + 2^-e fp8(x_b) fp8((w - w_hi) 2^e)."""
+    if _SPLIT8 is not None and site in _SPLIT8[0]:
+        e = _SPLIT8[1]
+        with torch.no_grad():
+            w_hi = w.to(torch.bfloat16).to(w.dtype)
+            lo8 = fp8_e4m3((w - w_hi) * 2.0 ** e)
+            corr = F.linear(fp8_e4m3(xr.detach()), lo8) * 2.0 ** -e
+        return F.linear(xr, _RoundFwd.apply(w, torch.bfloat16), b) + corr
+    return F.linear(xr, _rf(w, site, "w"), b)
 
 
 # ------------------------------------------------------------------------- pieces
@@ -296,8 +335,8 @@ def encoder_forward(P: dict, a, wav: torch.Tensor, *, train: bool = False, fseed
         h = h + att
         x2 = _rf(F.layer_norm(h, (h.shape[-1],), P[pre + "final_layer_norm.weight"],
                               P[pre + "final_layer_norm.bias"], a.eps), "ffn_up")
-        f = _rf(F.gelu(_rg(F.linear(x2, _rf(P[pre + "feed_forward.intermediate_dense.weight"], "ffn_up", "w"),
-                                    P[pre + "feed_forward.intermediate_dense.bias"]), "ffn_up")), "ffn_up")
+        f = _rf(F.gelu(_rg(_linear_core(x2, P[pre + "feed_forward.intermediate_dense.weight"],
+                                        P[pre + "feed_forward.intermediate_dense.bias"], "ffn_up"), "ffn_up")), "ffn_up")
         if train:
             f = _drop(f, a.activation_dropout, rng.site_seed(fseed, rng.site_act(li)))
         f = _lin(f, P[pre + "feed_forward.output_dense.weight"], P[pre + "feed_forward.output_dense.bias"], site="ffn_down")

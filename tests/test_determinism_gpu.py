@@ -17,11 +17,11 @@ pytestmark = pytest.mark.gpu
 PROJ, PRED = 256, 512
 
 
-def _pair(arch, proj, pred, dtype, seed=77):
+def _pair(arch, proj, pred, dtype, seed=77, **kw):
     from nrse_amd.engine import ByolEngine
     layout = PR.byol_layout(arch, proj, pred)
     flat = PR.init_byol_flat(layout, seed)
-    return [ByolEngine(arch, proj, pred, compute_dtype=dtype, init_flat=flat) for _ in range(2)]
+    return [ByolEngine(arch, proj, pred, compute_dtype=dtype, init_flat=flat, **kw) for _ in range(2)]
 
 
 def _batch(B, L, seed=5):
@@ -31,11 +31,13 @@ def _batch(B, L, seed=5):
     return clean.cuda(), noisy.cuda()
 
 
-def _steps_equal(engines, clean, noisy, steps):
+def _steps_equal(engines, clean, noisy, steps, grads=True):
     for i in range(steps):
         losses = [e.train_step(clean, noisy, lr=1e-4, step_seed=100 + i) for e in engines]
         torch.cuda.synchronize()
         assert torch.equal(losses[0], losses[1]), (i, float(losses[0]), float(losses[1]))
+        if not grads:
+            continue
         a, b = engines[0].grad, engines[1].grad
         diff = int((a != b).sum())
         assert diff == 0, f"step {i}: {diff} of {a.numel()} gradient entries differ"
@@ -60,4 +62,37 @@ def test_tiny_stochastic_steps_are_bitwise_repeatable(nrse_device, dtype):
 def test_large_bf16_steps_are_bitwise_repeatable(nrse_device):
     engines = _pair(A.LARGE, 1024, 2048, torch.bfloat16)
     clean, noisy = _batch(8, 128000)
+    _steps_equal(engines, clean, noisy, steps=2)
+
+
+def test_mask_ahead_steps_match_hashed_forward(nrse_device):
+    """NRSE_MASK_AHEAD's engine path (the per-view mask stream, the event wait, the
+    forward and both backward kernels reading the precomputed keep bits, DM 2) against the default
+    hash-and-record forward: identical losses, gradients and parameters over 3 steps of the tiny
+    architecture with every dropout site live (bf16: the MFMA attention kernels)."""
+    engines = _pair(A.TINY, PROJ, PRED, torch.bfloat16)
+    engines[1].mask_ahead = True
+    assert engines[0].arch.attention_dropout > 0
+    clean, noisy = _batch(4, 16000)
+    _steps_equal(engines, clean, noisy, steps=3)
+
+
+def test_fused_zero_grad_steps_match(nrse_device):
+    """StepConfig.fused_zero_grad (the AdamW pass clears the gradient, no fill kernel between
+    steps): identical losses, parameters, moments and EMA target to the separate fill, with the
+    overlapped optimizer as bench.py runs it."""
+    engines = _pair(A.TINY, PROJ, PRED, torch.bfloat16)
+    for e in engines:
+        e.cfg.overlap_optimizer = True
+    engines[1].cfg.fused_zero_grad = True
+    clean, noisy = _batch(4, 16000)
+    _steps_equal(engines, clean, noisy, steps=3, grads=False)
+    assert float(engines[1].grad.abs().max()) == 0.0
+
+
+def test_split_weight_fp8_steps_are_bitwise_repeatable(nrse_device):
+    """The north-star mode (bf16sw, fp8 correction segments and planes) repeats bit for bit."""
+    engines = _pair(A.TINY, PROJ, PRED, torch.bfloat16, weight_split=True, split_lo8=True)
+    assert engines[0].online_lo8 is not None
+    clean, noisy = _batch(4, 16000)
     _steps_equal(engines, clean, noisy, steps=2)

@@ -209,3 +209,23 @@ def test_adamw_fp8_planes_and_zero_grad(nrse_device, n, ne):
     assert torch.equal(a[1], g0) and float(b[1].abs().max()) == 0.0   # zero_grad
     assert torch.equal(bits(b[9]), bits(lo_ref(b[0], e)))
     assert torch.equal(bits(b[10]), bits(lo_ref(b[4], e)))
+
+
+def test_attention_fp8_context_copy(nrse_device):
+    """The attention forward's ctx8 (ABI 6): fp8 of the stored bf16 context, bit-exact, and the
+    context itself unchanged by it."""
+    from nrse_amd import kernels as K
+    B, T, H = 2, 150, 4
+    qkv = (torch.randn(B * T, 3 * H * 64, device="cuda")).to(torch.bfloat16)
+    gate = torch.rand(B, H, T, device="cuda") + 0.5
+    vec = torch.randn(H, 2 * T - 1, device="cuda") * 0.1
+    outs = []
+    for with8 in (False, True):
+        ctx = torch.empty(B * T, H * 64, device="cuda", dtype=torch.bfloat16)
+        lse = torch.empty(B, H, T, device="cuda")
+        c8 = torch.empty(B * T, H * 64, device="cuda", dtype=E4M3) if with8 else None
+        K.attn_fwd(qkv, gate, None, ctx, lse, B, T, H, 0.1, 42, bias_vec=vec, ctx8=c8)
+        torch.cuda.synchronize()
+        outs.append((ctx, c8))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(bits(outs[1][1]), bits(fp8_ref(outs[1][0].float())))

@@ -199,13 +199,22 @@ def test_oracle_split_weight_mode_meets_north_star():
     clean = torch.randn(int(z["B"]), 1, int(z["L"]), generator=g).squeeze(1)[:2]
     P = O.split_flat(layout, flat)["encoder"]
     ref = z["eval_emb"][:2]
+    # the fp8 form's exponent as the engine picks it (ByolEngine._set_lo8_planes)
+    e8 = O.lo8_exponent([P[f"encoder.layers.{li}.{n}"] for li in range(arch.layers)
+                         for n in ("attention.q_proj.weight", "attention.k_proj.weight", "attention.v_proj.weight",
+                                   "attention.out_proj.weight", "feed_forward.intermediate_dense.weight",
+                                   "feed_forward.output_dense.weight")])
     out = {}
-    for name, sites in (("split", O.SPLIT_WEIGHT_SITES), ("bf16", None)):
+    for name, sites, s8 in (("split", O.SPLIT_WEIGHT_SITES, None), ("split_fp8", O.SPLIT_WEIGHT_SITES, O.SPLIT8_SITES),
+                            ("bf16", None, None)):
         O.set_operand_dtype(torch.bfloat16, sites)
+        O.set_split8(s8, e8)
         try:
             with torch.no_grad():
                 out[name] = rel(O.encoder_forward(P, arch, clean, train=False).mean(1).numpy(), ref)
         finally:
             O.set_operand_dtype(None)
+            O.set_split8(None)
     assert out["split"] < 1e-3, out
+    assert out["split_fp8"] < 1e-3, out     # the engine's default bf16sw (fp8 correction segments)
     assert out["bf16"] > 3e-3, out

@@ -24,6 +24,7 @@ def timeit(fn, iters=20):
 
 M = int(os.environ.get("M", 12768))
 rows = [int(r) for r in os.environ.get("ROWS", "256,224").split(",")]
+rows_default = K.gemm_tile_rows(256)   # the process's setting, restored after each shape
 for name, N, Kd in (("qkv", 3072, 1024), ("out", 1024, 1024), ("ffn1", 4096, 1024), ("ffn2", 1024, 4096)):
     x = torch.randn(M, Kd, device=dev).to(torch.bfloat16)
     w = (torch.randn(N, Kd, device=dev) * 0.05).to(torch.bfloat16)
@@ -40,6 +41,6 @@ for name, N, Kd in (("qkv", 3072, 1024), ("out", 1024, 1024), ("ffn1", 4096, 102
             K.gemm_tile_rows(r)
             res.setdefault(f"bm{r}_fwd", []).append(timeit(lambda: K.linear_fwd(x, w, y, bias=b)))
             res.setdefault(f"bm{r}_dgrad", []).append(timeit(lambda: K.linear_dgrad(dy, w, dx)))
-        K.gemm_tile_rows(0)
+        K.gemm_tile_rows(rows_default)
     print(f"{name} {M}x{N}x{Kd}: " + " ".join(f"{k} {fl / statistics.median(v) / 1e9:.0f}TF"
                                               for k, v in res.items()), flush=True)
