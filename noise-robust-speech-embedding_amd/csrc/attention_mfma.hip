@@ -182,6 +182,9 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
   const int q0 = bp.blk * 64;
   const int qi = q0 + w * 16 + i16;
   const bool qv = qi < T;
+  // a wave whose 16 queries all lie past T (the last query block's tail: 3 of its 4 waves at
+  // T = 399) keeps its share of the K/V staging and the barriers but skips the tile math
+  const bool wlive = q0 + w * 16 < T;
   const bf16_t* qkv = (const bf16_t*)p.qkv + (long long)b * T * ld3;
   const KvDma kd = kv_dma_init(qkv, T, ld3, (Hd + h * D) * 2, w, lane);
   const KvDma vd = kv_dma_init(qkv, T, ld3, (2 * Hd + h * D) * 2, w, lane);
@@ -253,6 +256,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
       kv_dma_issue(vd, Kn + TILE_B, kb + 64, w);
       if (DM == 2) mnext = mrow[(long long)(it + 1) * 4 * (ntiles * 64)];
     }
+    if (!wlive) continue;
     // the MFMAs run on every sub-tile (a conditional MFMA makes the compiler stage its result
     // through AGPRs)
     f32x4 s[4];
@@ -387,6 +391,7 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
   const int q0 = bp.blk * 64;
   const int qi = q0 + w * 16 + i16;
   const bool qv = qi < T;
+  const bool wlive = q0 + w * 16 < T;  // as the forward: a wave of queries past T skips the math
   const bf16_t* qkv = (const bf16_t*)p.qkv + (long long)b * T * ld3;
   const bf16_t* dctx = (const bf16_t*)p.dctx + (long long)b * T * Hd;
   const KvDma kd = kv_dma_init(qkv, T, ld3, (Hd + h * D) * 2, w, lane);
@@ -458,6 +463,7 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
       kv_dma_issue(vd, Kn + TILE_B, kb + 64, w);
       if (use_mask) mnext = mrow[(long long)(it + 1) * 4 * Tp];
     }
+    if (!wlive) continue;
     const int nt16 = min(4, (T - kb + 15) >> 4);
     f32x4 s[4], dp[4];
 #pragma unroll
@@ -570,6 +576,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   const int kb0 = bp.blk * 64;
   const int kj = kb0 + w * 16 + i16;
   const bool kv = kj < T;
+  // a wave whose 16 keys all lie past T (the last key block's tail) keeps its staging, barriers
+  // and (zero) diagonal slots but skips the tile math
+  const bool wlive = kb0 + w * 16 < T;
   const float kvf = kv ? 1.f : 0.f;
   const bf16_t* qkv = (const bf16_t*)p.qkv + (long long)b * T * ld3;
   const bf16_t* dctx = (const bf16_t*)p.dctx + (long long)b * T * Hd;
@@ -659,6 +668,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     }
   };
   float dacc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  if (!wlive) {  // this wave's staging row stays zero for every fold (slots i16 + 16 j, j < 4)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) tw[i16 + 16 * j] = 0.f;
+  }
   // rotation by r wraps for lanes i16 >= 16 - r
   const float whi[3] = {i16 >= 15 ? 1.f : 0.f, i16 >= 14 ? 1.f : 0.f, i16 >= 13 ? 1.f : 0.f};
   const float wlo[3] = {1.f - whi[0], 1.f - whi[1], 1.f - whi[2]};
@@ -698,6 +711,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
       kv_dma_issue(od, Qn + TILE_B, qb + 64, w);
       mask_issue(mtile0 + ((it + 1) & 1) * 512, qb + 64);
     }
+    float pd[4][4], ds[4][4], gv[4][4];
+    if (wlive) {
     f32x4 s[4], dp[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -714,7 +729,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     // invalid queries contribute zero by construction (zero Q, dO, lse, delta, gate rows);
     // lanes of invalid keys produce dK/dV rows that are never stored, and kvf keeps them out of
     // the diagonal sums.
-    float pd[4][4], ds[4][4], gv[4][4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int ql = qb + 16 * t + 4 * g;
@@ -788,8 +802,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
       for (int j = 0; j < 4; ++j) tw[i16 - 16 * j + 48] = dacc[j];
       dacc[0] = dacc[4];
       dacc[1] = dacc[2] = dacc[3] = dacc[4] = 0.f;
-      fold(kb0 - qb - dbase);
     }
+    }  // wlive
+    if (p.diag) fold(kb0 - qb - dbase);  // every wave: the fold's barriers
+    if (!wlive) continue;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       const bf16x8 pa = pack8(pd[2 * c], pd[2 * c + 1]);
