@@ -177,6 +177,10 @@ typedef struct {
   /* ABI 6, optional (bf16 y): y8 [rows, C] NRSE_FP8 = fp8(bf16 y), the next GEMM's a8 operand
    * (split-weight mode); 16-byte aligned */
   void* y8;
+  /* ABI 7: y8_split = 1 makes y8 the two fp8 correction planes of the exact output o (the conv
+   * stack's split-weight form): y8 [2, rows, C] = [fp8((o - bf16(o)) 2^y8_exp) |
+   * fp8(bf16(o))], y = bf16(o); the next conv GEMM's a8 segments against [fp8(w_hi) | fp8(w_lo 2^e)] */
+  int y8_split; int y8_exp;
 } nrse_ln_fwd_params;
 
 typedef struct {
@@ -329,6 +333,10 @@ typedef struct {
   float* part;                    /* bwd, optional: f32 workspace of nrse_conv0_bwd_workspace(p)
                                      floats; dw / dgamma / dbeta are then added in a fixed order
                                      (deterministic) instead of by f32 atomics */
+  /* fwd, ABI 7, optional (bf16 out, k = 10, C = 256 | 512): the fp8 correction planes of the exact
+   * output o, y8 [2, B*T0, C] NRSE_FP8 = [fp8((o - bf16(o)) 2^y8_exp) | fp8(bf16(o))] (as
+   * nrse_ln_fwd_params.y8_split); out = bf16(o). 16-byte aligned */
+  void* y8; int y8_exp;
 } nrse_conv0_params;
 int nrse_conv0_fwd(const nrse_conv0_params* p, void* stream);
 int nrse_conv0_bwd(const nrse_conv0_params* p, void* stream);

@@ -74,6 +74,18 @@ NRSE_DEV float lo_resid(float x) { return x - __uint_as_float((uint32_t)f2bf(x) 
 NRSE_DEV uint32_t fp8x4_of_bf(const float* o) {
   return fp8x4(bf2f(f2bf(o[0])), bf2f(f2bf(o[1])), bf2f(f2bf(o[2])), bf2f(f2bf(o[3])));
 }
+// the two fp8 correction planes of 4 exact values o (ABI 7, y8_split): lo8 = fp8((o - bf16(o)) sc)
+// (sc = 2^y8_exp), hi8 = fp8(bf16(o)) -- the conv stack's a8 segments of the split-weight mode
+NRSE_DEV void fp8x4_split(const float* o, float sc, uint32_t& lo8, uint32_t& hi8) {
+  float h[4], l[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    h[e] = bf2f(f2bf(o[e]));
+    l[e] = (o[e] - h[e]) * sc;
+  }
+  lo8 = fp8x4(l[0], l[1], l[2], l[3]);
+  hi8 = fp8x4(h[0], h[1], h[2], h[3]);
+}
 // 8 packed bf16 (a 16-B row chunk) -> 8 fp8 bytes
 NRSE_DEV uint2 fp8x8_from_bf16x8(uint4 u) {
   uint2 r;

@@ -119,8 +119,10 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(const nrse_conv0_params 
 // are lane-local over 4 C / 16 values plus two lane swaps (the VALU kernel above paid two wave
 // reductions per row), and each lane stores 8 consecutive channels (16 B) per block pair. The
 // weight fragments live in LDS in fragment order (one conflict-free ds_read_b128 per block).
+// S8 (ABI 7, y8): the split-planes contraction, stored as bf16 hi + the two fp8 correction planes
+// [fp8((o - hi) 2^y8_exp) | fp8(hi)] (4 instead of 6 bytes per element).
 // Exact f32 outputs (the parity mode) keep conv0_fwd_kernel.
-template <int NB, bool X3>
+template <int NB, bool X3, bool S8>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void conv0_fwd_mfma_kernel(
     const nrse_conv0_params p) {
   constexpr int C = NB * 16, NF = X3 ? 2 : 1;
@@ -170,6 +172,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   UDiv31 dT0;
   dT0.init((unsigned)p.T0);
   const float invC = 1.f / C;
+  const float sc8 = __builtin_ldexpf(1.f, p.y8_exp);
   auto load_x = [&](long long blk, float (&xs)[8]) {
     long long row = blk * 16 + l;
     row = row < rows ? row : rows - 1;
@@ -236,7 +239,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
       bf16_t* dst = (bf16_t*)p.out + row * C + c0;
       if (ok) {
         *reinterpret_cast<uint4*>(dst) = u;
-        if constexpr (X3) {
+        if constexpr (S8) {
+          uint2 l8, h8;
+          fp8x4_split(o, sc8, l8.x, h8.x);
+          fp8x4_split(o + 4, sc8, l8.y, h8.y);
+          unsigned char* d8 = (unsigned char*)p.y8 + row * C + c0;
+          *reinterpret_cast<uint2*>(d8) = l8;
+          *reinterpret_cast<uint2*>(d8 + rows * C) = h8;
+        } else if constexpr (X3) {
           const unsigned uw[4] = {u.x, u.y, u.z, u.w};
           unsigned lw[4];
 #pragma unroll
@@ -703,19 +713,29 @@ extern "C" int nrse_conv0_fwd(const nrse_conv0_params* p, void* stream) {
   if (blocks > 4096) blocks = 4096;
   hipStream_t st = (hipStream_t)stream;
   const bool k10 = p->k == KMAX;
+  if (p->y8) {
+    // ABI 7 fp8 correction planes: the matrix-core kernel's split-planes form only
+    NRSE_REQUIRE(k10 && p->out_dtype == NRSE_BF16 && (p->C == 512 || p->C == 256) && conv0_mfma_on() &&
+                     ((uintptr_t)p->y8 & 15) == 0 && p->y8_exp >= -60 && p->y8_exp <= 60,
+                 "nrse_conv0_fwd: y8 needs k = 10, a bf16 out, C = 256 | 512, the MFMA form (NRSE_CONV0_MFMA), "
+                 "16-byte alignment and |y8_exp| <= 60");
+  }
   if (k10 && p->out_dtype != NRSE_F32 && (p->C == 512 || p->C == 256) && conv0_mfma_on()) {
     // matrix-core form (bf16 / split-bf16 outputs): 2 workgroups per CU, waves loop over 16-row blocks
     const long long nblk = (rows + 15) / 16;
     long long wg = (nblk + 3) / 4;
     if (wg > 1024) wg = 1024;
-    const bool x3 = p->out_dtype == NRSE_BF16X3;
+    const bool x3 = p->out_dtype == NRSE_BF16X3, s8 = p->y8 != nullptr;
+#define NRSE_C0F(NB)                                                                                   \
+  if (s8) hipLaunchKernelGGL((conv0_fwd_mfma_kernel<NB, true, true>), dim3(wg), dim3(256), 0, st, *p); \
+  else if (x3) hipLaunchKernelGGL((conv0_fwd_mfma_kernel<NB, true, false>), dim3(wg), dim3(256), 0, st, *p); \
+  else hipLaunchKernelGGL((conv0_fwd_mfma_kernel<NB, false, false>), dim3(wg), dim3(256), 0, st, *p)
     if (p->C == 512) {
-      if (x3) hipLaunchKernelGGL((conv0_fwd_mfma_kernel<32, true>), dim3(wg), dim3(256), 0, st, *p);
-      else hipLaunchKernelGGL((conv0_fwd_mfma_kernel<32, false>), dim3(wg), dim3(256), 0, st, *p);
+      NRSE_C0F(32);
     } else {
-      if (x3) hipLaunchKernelGGL((conv0_fwd_mfma_kernel<16, true>), dim3(wg), dim3(256), 0, st, *p);
-      else hipLaunchKernelGGL((conv0_fwd_mfma_kernel<16, false>), dim3(wg), dim3(256), 0, st, *p);
+      NRSE_C0F(16);
     }
+#undef NRSE_C0F
     return nrse_check_launch("nrse_conv0_fwd");
   }
   switch (p->C) {

@@ -50,6 +50,19 @@ NRSE_DEV void unpack_bf4(uint2 v, float* o) {
   o[2] = __uint_as_float(v.y << 16); o[3] = __uint_as_float(v.y & 0xffff0000u);
 }
 
+// the fp8 copies of 4 outputs at element i: fp8(bf16 o) (ABI 6), or the split planes (ABI 7)
+NRSE_DEV void store_y8(const nrse_ln_fwd_params& p, long long i, const float* o) {
+  unsigned char* y8 = (unsigned char*)p.y8 + i;
+  if (p.y8_split) {
+    uint32_t lo, hi;
+    fp8x4_split(o, __builtin_ldexpf(1.f, p.y8_exp), lo, hi);
+    *reinterpret_cast<uint32_t*>(y8) = lo;
+    *reinterpret_cast<uint32_t*>(y8 + p.rows * p.C) = hi;
+  } else {
+    *reinterpret_cast<uint32_t*>(y8) = fp8x4_of_bf(o);
+  }
+}
+
 // element c of a row held by this lane: c = (k*64 + lane)*4 + e, k < NK = C/256
 template <int NK>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const nrse_ln_fwd_params p) {
@@ -88,7 +101,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const nrse_ln_fwd_params p)
       for (int e = 0; e < CH; ++e) o[e] = fmaxf(o[e], 0.f);
     }
     store4_out(p.y, p.y_dtype, base + c0, p.rows * C, o);
-    if (p.y8) *reinterpret_cast<uint32_t*>((unsigned char*)p.y8 + base + c0) = fp8x4_of_bf(o);
+    if (p.y8) store_y8(p, base + c0, o);
   }
   if (lane == 0) {
     if (p.mean) p.mean[row] = mean;
@@ -140,7 +153,7 @@ __global__ __launch_bounds__(256) void ln_fwd_f32_kernel(const nrse_ln_fwd_param
       for (int e = 0; e < CH; ++e) o[e] = fmaxf(o[e], 0.f);
     }
     store4_out(p.y, p.y_dtype, base + c0, p.rows * C, o);
-    if (p.y8) *reinterpret_cast<uint32_t*>((unsigned char*)p.y8 + base + c0) = fp8x4_of_bf(o);
+    if (p.y8) store_y8(p, base + c0, o);
   }
   if (lane == 0) {
     if (p.mean) p.mean[row] = mean;
@@ -606,6 +619,8 @@ extern "C" int nrse_layernorm_fwd(const nrse_ln_fwd_params* p, void* stream) {
                "nrse_layernorm_fwd: bad y_dtype %d", p->y_dtype);
   NRSE_REQUIRE(!p->y8 || (p->y_dtype == NRSE_BF16 && ((uintptr_t)p->y8 & 3) == 0),
                "nrse_layernorm_fwd: y8 needs a bf16 y and 4-byte alignment");
+  NRSE_REQUIRE((p->y8_split == 0 || p->y8_split == 1) && p->y8_exp >= -60 && p->y8_exp <= 60,
+               "nrse_layernorm_fwd: y8_split %d / y8_exp %d out of range", p->y8_split, p->y8_exp);
   if (p->x_dtype == NRSE_BF16 && p->C <= 512 && ((uintptr_t)p->x & 7) == 0 && !p->y8) {
     constexpr int RPW = 4;
     const dim3 g((unsigned)((p->rows + 4 * RPW - 1) / (4 * RPW)));

@@ -69,7 +69,7 @@ class GemmParams(ctypes.Structure):
 class LnFwdParams(ctypes.Structure):
     _fields_ = [("x", c_vp), ("x_dtype", c_int), ("gamma", c_vp), ("beta", c_vp), ("y", c_vp), ("y_dtype", c_int),
                 ("mean", c_vp), ("rstd", c_vp), ("rows", c_ll), ("C", c_int), ("eps", c_f), ("flags", c_int),
-                ("y8", c_vp)]
+                ("y8", c_vp), ("y8_split", c_int), ("y8_exp", c_int)]
 
 
 class LnBwdParams(ctypes.Structure):
@@ -103,7 +103,7 @@ class Conv0Params(ctypes.Structure):
                 ("dy", c_vp), ("dy_dtype", c_int), ("dy_mode", c_int), ("col_k", c_int), ("col_s", c_int),
                 ("col_tout", c_int), ("dw", c_vp), ("dgamma", c_vp), ("dbeta", c_vp),
                 ("batch", c_int), ("T0", c_int), ("C", c_int), ("k", c_int), ("s", c_int), ("eps", c_f),
-                ("part", c_vp)]
+                ("part", c_vp), ("y8", c_vp), ("y8_exp", c_int)]
 
 
 class AdamWParams(ctypes.Structure):

@@ -68,6 +68,14 @@ _FUSED_EMA = os.environ.get("NRSE_FUSED_EMA", "1") != "0"
 # fp8 correction plane of the weights, 2x the bf16 rate) instead of a second bf16 segment;
 # NRSE_SPLIT_LO8=0 restores the bf16 lo plane everywhere (A/B)
 _SPLIT_LO8 = os.environ.get("NRSE_SPLIT_LO8", "1") != "0"
+# ... and the conv stack's two correction segments (x_lo w_hi + x_hi w_lo) as fp8 segments against
+# the activations' fp8 planes [fp8(x_lo 2^e) | fp8(x_hi)] (ABI 7) instead of two more bf16 segments;
+# NRSE_CONV_SPLIT8=0 restores the three bf16 planes. The exponent is fixed: 2^11 keeps both
+# (w - w_hi) 2^e and (x - x_hi) 2^e (each <= 2^-8 |.|) inside fp8's +-448 for |w|, |x| < 56 -- the
+# conv activations are GELU(LayerNorm) outputs, |x| <= sqrt(C) max|gamma| + max|beta| (23 at
+# gamma = 1, beta = 0); beyond that the conversion saturates (bounded error, never inf / NaN)
+_CONV_SPLIT8 = os.environ.get("NRSE_CONV_SPLIT8", "1") != "0"
+CONV_LO8_EXP = int(os.environ.get("NRSE_CONV_LO8_EXP", "11"))
 FP8 = K.FP8
 
 
@@ -134,10 +142,26 @@ class EncoderWeights:
         cdt = eng.cdt
         # conv 1..6 weights [co][ci][k] -> [co][k][ci] in the compute dtype
         self.conv_r, self.conv_lo = [], []   # conv_lo[i]: lo-plane offset of conv_r[i] (0: none)
+        # fp8 form: conv_w8[i] = [fp8(w_hi) | fp8((w - w_hi) 2^conv_lo8_exp)] against the activations'
+        # [fp8((x - x_hi) 2^e) | fp8(x_hi)]: x_hi w_hi (bf16) + 2^-e (x_lo8 w_hi8 + x_hi8 w_lo8)
+        self.conv_split8 = bool(self.lo) and lo8 is not None and eng.conv_split8
+        self.conv_lo8_exp = CONV_LO8_EXP
+        self.conv_w8 = []
         for i in range(1, len(a.conv_dim)):
             w = self.m[f"feature_extractor.conv_layers.{i}.conv.weight"]
             co, ci, k = w.shape
-            if self.lo:
+            if self.conv_split8:
+                r32 = torch.empty(co, k * ci, device=eng.dev, dtype=F32)
+                K.swap12(w, r32, co, ci, k)
+                r = torch.empty(co, k * ci, device=eng.dev, dtype=cdt)
+                K.cast(r32, r)
+                w8 = torch.empty(2, co, k * ci, device=eng.dev, dtype=FP8)
+                K.cast_fp8(r, w8[0])
+                K.split_lo8(r32, w8[1], self.conv_lo8_exp)
+                self.conv_r.append(r)
+                self.conv_lo.append(0)
+                self.conv_w8.append(w8)
+            elif self.lo:
                 # planes [hi | hi | lo] against the split activations' [hi | lo | hi] (NRSE_BF16X3):
                 # three K segments of one GEMM, x_hi w_hi + x_lo w_hi + x_hi w_lo
                 r32 = torch.empty(co, k * ci, device=eng.dev, dtype=F32)
@@ -228,6 +252,10 @@ class ByolEngine:
         self.step_count = 0
         # the attention dropout keep bits computed ahead on a mask stream (NRSE_MASK_AHEAD, opt-in)
         self.mask_ahead = _MASK_AHEAD
+        # split-weight fp8 form: the conv stack's correction segments in fp8 too (NRSE_CONV_SPLIT8);
+        # conv_split8_used: whether the last forward ran them (frames >= 128, see encoder_forward)
+        self.conv_split8 = _CONV_SPLIT8
+        self.conv_split8_used = False
         self._offsets = {}
         self._view_cache = {}
         for gname, s in self.layout.specs:
@@ -414,38 +442,59 @@ class ByolEngine:
         # (NRSE_BF16X3 [hi | lo | hi], read by 3-segment GEMMs) and its pre-activations in f32 --
         # the activation roundings that remain in this mode are otherwise dominated by the conv
         # stack (tools/ablate_bf16_sites.py: 6e-4 of 7e-4 at 8 s, more at 3 s)
+        # fp8 form (W.conv_split8, ABI 7): a bf16 hi plane + the fp8 planes [fp8(x_lo 2^e) | fp8(x_hi)],
+        # read by one bf16 and two fp8 K segments
         split = self.wsplit
+        # (the fp8 segments run on the 256x256 kernel only, which needs M = frames >= 128 per
+        # utterance at every conv layer: audio shorter than ~2.6 s keeps the three bf16 planes)
+        t_last = T0
+        for k_, s_ in zip(a.conv_kernel[1:], a.conv_stride[1:]):
+            t_last = (t_last - k_) // s_ + 1
+        s8 = split and W.conv_split8 and t_last >= 128
+        self.conv_split8_used = s8
+        split3 = split and not s8
+        e8 = W.conv_lo8_exp
         nconv = len(a.conv_dim)
-        y = torch.empty((3, B * T0, C0) if split else (B * T0, C0), device=dev, dtype=cdt)
+        y = torch.empty((3, B * T0, C0) if split3 else (B * T0, C0), device=dev, dtype=cdt)
+        x8 = torch.empty(2, B * T0, C0, device=dev, dtype=FP8) if s8 else None
         mean = torch.empty(B * T0, device=dev, dtype=F32)
         rstd = torch.empty(B * T0, device=dev, dtype=F32)
         pre0 = "feature_extractor.conv_layers.0."
         K.conv0_fwd(wav, Pm[pre0 + "conv.weight"], Pm[pre0 + "layer_norm.weight"], Pm[pre0 + "layer_norm.bias"], y,
-                    mean, rstd, T0, k0, s0, a.eps, split3=split)
+                    mean, rstd, T0, k0, s0, a.eps, split3=split3, y8=x8, y8_exp=e8)
         if need_grad:
             tape.conv.append(dict(mean=mean, rstd=rstd, T=T0))
-        x, Tin, Cin = (y[0] if split else y), T0, C0
+        x, Tin, Cin = (y[0] if split3 else y), T0, C0
         for i in range(1, nconv):
             k, s, C = a.conv_kernel[i], a.conv_stride[i], a.conv_dim[i]
             Tout = (Tin - k) // s + 1
             pre_out = torch.empty(B * Tout, C, device=dev, dtype=F32 if split else cdt)
-            K.gemm(K.Operand(x, True, s * Cin, z1=Tin * Cin, seg_stride=B * Tin * Cin if split else 0),
+            f8 = {}
+            if s8:
+                f8 = dict(a8=K.Operand(x8, True, s * Cin, z1=Tin * Cin, seg_stride=B * Tin * Cin),
+                          b8=K.Operand(W.conv_w8[i - 1], True, k * Cin, seg_stride=C * k * Cin), nseg8=2, b8_exp=e8)
+            K.gemm(K.Operand(x, True, s * Cin, z1=Tin * Cin, seg_stride=B * Tin * Cin if split3 else 0),
                    K.Operand(W.conv_r[i - 1], True, k * Cin, seg_stride=W.conv_lo[i - 1]), pre_out,
-                   Tout, C, k * Cin, ldc=C, batch=B, c_z1=Tout * C, nseg=3 if split else 1)
+                   Tout, C, k * Cin, ldc=C, batch=B, c_z1=Tout * C, nseg=3 if split3 else 1, **f8)
             # the last layer's output feeds only the feature-projection LN: f32 in the split mode
             last = i == nconv - 1
-            if split:
-                yo3 = torch.empty((B * Tout, C) if last else (3, B * Tout, C), device=dev, dtype=F32 if last else cdt)
+            yo8 = None
+            if split and last:
+                yo3 = torch.empty(B * Tout, C, device=dev, dtype=F32)
+            elif split3:
+                yo3 = torch.empty(3, B * Tout, C, device=dev, dtype=cdt)
             else:
                 yo3 = torch.empty(B * Tout, C, device=dev, dtype=cdt)
+                if s8:
+                    yo8 = torch.empty(2, B * Tout, C, device=dev, dtype=FP8)
             mo = torch.empty(B * Tout, device=dev, dtype=F32)
             ro = torch.empty(B * Tout, device=dev, dtype=F32)
             p = f"feature_extractor.conv_layers.{i}."
             K.ln_fwd(pre_out, Pm[p + "layer_norm.weight"], Pm[p + "layer_norm.bias"], yo3, mo, ro, a.eps, gelu=True,
-                     split3=split and not last)
+                     split3=split3 and not last, y8=yo8, y8_exp=e8 if yo8 is not None else None)
             if need_grad:
                 tape.conv.append(dict(x=x, pre=pre_out, mean=mo, rstd=ro, Tin=Tin, T=Tout, k=k, s=s))
-            x, Tin, Cin = (yo3[0] if split and not last else yo3), Tout, C
+            x, x8, Tin, Cin = (yo3[0] if split3 and not last else yo3), yo8, Tout, C
         T = Tin
         C = Cin
         H = a.hidden

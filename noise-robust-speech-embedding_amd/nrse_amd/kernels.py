@@ -408,13 +408,17 @@ def _out_code(y: torch.Tensor, n: int, split3: bool) -> int:
     return _lib.BF16X3
 
 
-def ln_fwd(x, gamma, beta, y, mean, rstd, eps, gelu=False, relu=False, split3=False, y8=None):
-    """y8 (fp8 [rows, C], bf16 y): also y8 = fp8(y), the split-weight mode's next correction operand."""
+def ln_fwd(x, gamma, beta, y, mean, rstd, eps, gelu=False, relu=False, split3=False, y8=None, y8_exp=None):
+    """y8 (fp8 [rows, C], bf16 y): also y8 = fp8(y), the split-weight mode's next correction operand;
+    with y8_exp (fp8 [2, rows, C]): the two correction planes [fp8((o - bf16 o) 2^y8_exp) | fp8(bf16 o)]
+    of the exact output o (the conv stack's form, ABI 7)."""
     rows, C = x.shape[0] if x.dim() == 2 else x.numel() // x.shape[-1], x.shape[-1]
     if y8 is not None:
-        assert y8.dtype == FP8 and y8.numel() == rows * C and y8.is_contiguous()
+        n8 = rows * C * (1 if y8_exp is None else 2)
+        assert y8.dtype == FP8 and y8.numel() == n8 and y8.is_contiguous()
     p = LnFwdParams(ptr(x), dtype_code(x), ptr(gamma), ptr(beta), ptr(y), _out_code(y, rows * C, split3), ptr(mean),
-                    ptr(rstd), rows, C, eps, (_lib.LN_GELU if gelu else 0) | (_lib.LN_RELU if relu else 0), ptr(y8))
+                    ptr(rstd), rows, C, eps, (_lib.LN_GELU if gelu else 0) | (_lib.LN_RELU if relu else 0), ptr(y8),
+                    0 if y8_exp is None else 1, 0 if y8_exp is None else int(y8_exp))
     _call("nrse_layernorm_fwd", ctypes.byref(p), stream_ptr())
 
 
@@ -542,10 +546,14 @@ def attn_bwd(qkv, gate, bias, ctx, dctx, lse, delta, dqkv, dgate, diag, batch, T
 
 
 # ----------------------------------------------------------------------------- conv front end
-def conv0_fwd(wav, w, gamma, beta, out, mean, rstd, T0, k, s, eps, split3=False):
+def conv0_fwd(wav, w, gamma, beta, out, mean, rstd, T0, k, s, eps, split3=False, y8=None, y8_exp=0):
+    """y8 (fp8 [2, B*T0, C], bf16 out): the exact output's fp8 correction planes (ABI 7)."""
     B, L = wav.shape
     C = w.shape[0]
     p = Conv0Params()
+    if y8 is not None:
+        assert y8.dtype == FP8 and y8.numel() == 2 * B * T0 * C and y8.is_contiguous() and not split3
+        p.y8, p.y8_exp = ptr(y8), int(y8_exp)
     p.wav, p.L, p.w, p.gamma, p.beta = ptr(wav), L, ptr(w), ptr(gamma), ptr(beta)
     p.out, p.out_dtype, p.mean, p.rstd = ptr(out), _out_code(out, B * T0 * C, split3), ptr(mean), ptr(rstd)
     p.batch, p.T0, p.C, p.k, p.s, p.eps = B, T0, C, k, s, eps

@@ -99,11 +99,14 @@ SITES = ("conv", "proj", "posconv", "qkv", "attn", "oproj", "ffn_up", "ffn_down"
 SPLIT_WEIGHT_SITES = tuple(f"{s}:a" for s in SITES if s not in ("attn", "conv")) + ("attn",)
 # the split-weight mode's fp8 form (the engine's default bf16sw, ABI 6): at these GEMM sites the
 # weight correction x (w - w_hi) runs as fp8(x) times the fp8 plane fp8((w - w_hi) 2^e), scaled
-# by 2^-e (nrse_gemm's a8 / b8 segment); set_split8(sites, e) switches it on
-SPLIT8_SITES = ("qkv", "oproj", "ffn_up", "ffn_down")
+# by 2^-e (nrse_gemm's a8 / b8 segment); at "conv" (ABI 7, conv1-6 over exact activations) both
+# corrections: x_hi w_hi + 2^-c (fp8((x - x_hi) 2^c) fp8(w_hi) + fp8(x_hi) fp8((w - w_hi) 2^c)), c
+# the engine's fixed CONV_LO8_EXP; set_split8(sites, e, c) switches it on
+SPLIT8_SITES = ("qkv", "oproj", "ffn_up", "ffn_down", "conv")
+CONV_LO8_EXP = 11   # nrse_amd/engine.py CONV_LO8_EXP
 _OPERAND_DTYPE = None
 _SITES = None
-_SPLIT8 = None   # (frozenset of sites, exponent e) or None
+_SPLIT8 = None   # (frozenset of sites, exponent e, conv exponent c) or None
 
 
 def set_operand_dtype(dtype, sites=None) -> None:
@@ -130,11 +133,22 @@ def operand_dtype():
     return _OPERAND_DTYPE
 
 
-def set_split8(sites=None, exponent: int = 0) -> None:
+def set_split8(sites=None, exponent: int = 0, conv_exponent: int = CONV_LO8_EXP) -> None:
     """The fp8 correction form of the split-weight mode at `sites` (None: off), lo8_exp = exponent
-    (engine: ByolEngine._set_lo8_planes)."""
+    (engine: ByolEngine._set_lo8_planes), the conv stack's exponent conv_exponent."""
     global _SPLIT8
-    _SPLIT8 = None if sites is None else (frozenset(sites), int(exponent))
+    _SPLIT8 = None if sites is None else (frozenset(sites), int(exponent), int(conv_exponent))
+
+
+def _conv_split8(x: torch.Tensor, w: torch.Tensor, stride: int, c: int) -> torch.Tensor:
+    """The engine's conv1-6 GEMM in the fp8 split form (one bf16 K segment + two fp8 segments over
+    the activations' planes [fp8((x - x_hi) 2^c) | fp8(x_hi)] and the weights' [fp8(w_hi) |
+    fp8((w - w_hi) 2^c)], scaled by 2^-c)."""
+    bf = torch.bfloat16
+    x_hi, w_hi = x.to(bf).to(x.dtype), w.to(bf).to(w.dtype)
+    corr = (F.conv1d(fp8_e4m3((x - x_hi) * 2.0 ** c), fp8_e4m3(w_hi), stride=stride) +
+            F.conv1d(fp8_e4m3(x_hi), fp8_e4m3((w - w_hi) * 2.0 ** c), stride=stride))
+    return F.conv1d(x_hi, w_hi, stride=stride) + corr * 2.0 ** -c
 
 
 def fp8_e4m3(x: torch.Tensor) -> torch.Tensor:
@@ -217,8 +231,13 @@ def conv_stack(P: dict, a, wav: torch.Tensor) -> torch.Tensor:
         if i == 0:   # direct conv from the f32 waveform (engine: conv0 kernel, f32 weights)
             x = F.conv1d(x, P[pre + "conv.weight"], stride=s)
         else:        # implicit GEMM, bf16 operands, pre-LN output stored in the compute dtype
-            x = _rf(_rg(F.conv1d(_rf(x, "conv"), _rf(P[pre + "conv.weight"], "conv", "w"), stride=s), "conv"), "conv",
-                    "p")
+            xin, w = _rf(x, "conv"), _rf(P[pre + "conv.weight"], "conv", "w")
+            y = F.conv1d(xin, w, stride=s)
+            if _SPLIT8 is not None and "conv" in _SPLIT8[0]:   # forward value only (gradient as before)
+                with torch.no_grad():
+                    d = _conv_split8(xin, w, s, _SPLIT8[2]) - y
+                y = y + d
+            x = _rf(_rg(y, "conv"), "conv", "p")
         x = F.layer_norm(x.transpose(1, 2), (x.shape[1],), P[pre + "layer_norm.weight"], P[pre + "layer_norm.bias"],
                          a.eps).transpose(1, 2)
         x = _rg(_rf(F.gelu(x), "conv"), "conv")

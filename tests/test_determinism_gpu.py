@@ -96,3 +96,24 @@ def test_split_weight_fp8_steps_are_bitwise_repeatable(nrse_device):
     assert engines[0].online_lo8 is not None
     clean, noisy = _batch(4, 16000)
     _steps_equal(engines, clean, noisy, steps=2)
+
+
+def test_split_weight_fp8_conv_stack(nrse_device):
+    """The conv stack's fp8 correction segments (ABI 7; they need >= 128 frames, so 3 s here):
+    bitwise repeatable, and the same training losses as the three bf16 planes to the fp8 form's
+    precision (the 1 s steps above keep the bf16 planes: conv_split8_used False there)."""
+    engines = _pair(A.TINY, PROJ, PRED, torch.bfloat16, weight_split=True, split_lo8=True)
+    clean, noisy = _batch(4, 48000)
+    _steps_equal(engines, clean, noisy, steps=2)
+    assert engines[0].conv_split8_used
+    planes = _pair(A.TINY, PROJ, PRED, torch.bfloat16, weight_split=True, split_lo8=True)[0]
+    planes.conv_split8 = False
+    ref = _pair(A.TINY, PROJ, PRED, torch.bfloat16, weight_split=True, split_lo8=True)[0]
+    l8 = [float(ref.train_step(clean, noisy, lr=1e-4, step_seed=100 + i)) for i in range(2)]
+    l3 = [float(planes.train_step(clean, noisy, lr=1e-4, step_seed=100 + i)) for i in range(2)]
+    assert ref.conv_split8_used and not planes.conv_split8_used
+    for a, b in zip(l8, l3):
+        assert abs(a - b) <= 1e-3 * max(abs(b), 1.0), (l8, l3)
+    c1, n1 = _batch(4, 16000)
+    ref.train_step(c1, n1, lr=1e-4, step_seed=7)
+    assert not ref.conv_split8_used

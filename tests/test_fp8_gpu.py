@@ -229,3 +229,122 @@ def test_attention_fp8_context_copy(nrse_device):
         outs.append((ctx, c8))
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(bits(outs[1][1]), bits(fp8_ref(outs[1][0].float())))
+
+
+# ---------------------------------------------------------------- the conv stack's fp8 form (ABI 7)
+def _split_check(hi, lo8, e, ref):
+    """hi + 2^-e lo8 restores the exact ref to ~2^-13 (hi alone: ~2^-9)."""
+    got = d(hi) + 2.0 ** -e * d(lo8)
+    r_hi = rel(hi, ref)
+    assert rel(got, ref) < 1e-4 and rel(got, ref) < r_hi / 8, (rel(got, ref), r_hi)
+
+
+@pytest.mark.parametrize("C", [512, 256])
+def test_conv0_fp8_planes(nrse_device, C):
+    """conv0 (matrix-core form) with y8 (ABI 7): out = bf16(o) as the split-planes form stores it,
+    y8 = [fp8((o - hi) 2^e) | fp8(hi)]: the hi plane bit-exact, hi + lo restoring the float64 conv."""
+    from nrse_amd import kernels as K
+    dev = nrse_device
+    B, L, k, s, e = 3, 8001, 10, 5, 11
+    T0 = (L - k) // s + 1
+    rows = B * T0
+    wav = torch.randn(B, L, device=dev) * 0.2
+    w = torch.randn(C, 1, k, device=dev) * 0.3
+    g = torch.randn(C, device=dev) * 0.1 + 1; b = torch.randn(C, device=dev) * 0.1
+    out3 = torch.empty(3, rows, C, device=dev, dtype=torch.bfloat16)
+    mean, rstd = torch.empty(rows, device=dev), torch.empty(rows, device=dev)
+    K.conv0_fwd(wav, w.view(C, k), g, b, out3, mean, rstd, T0, k, s, 1e-5, split3=True)
+    out = torch.empty(rows, C, device=dev, dtype=torch.bfloat16)
+    y8 = torch.empty(2, rows, C, device=dev, dtype=E4M3)
+    mean2, rstd2 = torch.empty_like(mean), torch.empty_like(rstd)
+    K.conv0_fwd(wav, w.view(C, k), g, b, out, mean2, rstd2, T0, k, s, 1e-5, y8=y8, y8_exp=e)
+    torch.cuda.synchronize()
+    assert torch.equal(out, out3[0]) and torch.equal(mean, mean2) and torch.equal(rstd, rstd2)
+    assert torch.equal(bits(y8[1]), bits(fp8_ref(out.float())))
+    y = F.conv1d(wav.double()[:, None], w.double(), stride=s).transpose(1, 2).reshape(rows, C)
+    mu = y.mean(1); var = y.var(1, unbiased=False)
+    ref = F.gelu((y - mu[:, None]) / torch.sqrt(var[:, None] + 1e-5) * g.double() + b.double())
+    _split_check(out, y8[0], e, ref)
+
+
+def test_layernorm_fp8_split_planes(nrse_device):
+    """LN + GELU with y8_split (the conv stack's form): y = bf16(o), y8 = [fp8((o - y) 2^e) | fp8(y)]."""
+    from nrse_amd import kernels as K
+    rows, C, e = 2053, 512, 11
+    x = torch.randn(rows, C, device="cuda") * 3
+    g, b = torch.randn(C, device="cuda") * 0.2 + 1, torch.randn(C, device="cuda") * 0.1
+    y = torch.empty(rows, C, device="cuda", dtype=torch.bfloat16)
+    y8 = torch.empty(2, rows, C, device="cuda", dtype=E4M3)
+    mean, rstd = torch.empty(rows, device="cuda"), torch.empty(rows, device="cuda")
+    K.ln_fwd(x, g, b, y, mean, rstd, 1e-5, gelu=True, y8=y8, y8_exp=e)
+    torch.cuda.synchronize()
+    ref = F.gelu(F.layer_norm(x.double(), (C,), g.double(), b.double(), 1e-5))
+    assert torch.equal(bits(y8[1]), bits(fp8_ref(y.float())))
+    _split_check(y, y8[0], e, ref)
+    # the plain copy form is unchanged by the new fields
+    y8c = torch.empty(rows, C, device="cuda", dtype=E4M3)
+    K.ln_fwd(x, g, b, y, mean, rstd, 1e-5, gelu=True, y8=y8c)
+    torch.cuda.synchronize()
+    assert torch.equal(bits(y8c), bits(y8[1]))
+
+
+@pytest.mark.parametrize("k,s,Tin", [(3, 2, 301), (2, 2, 300)])
+def test_gemm_fp8_conv_segments(gen3, nrse_device, k, s, Tin):
+    """The conv stack's GEMM in the fp8 split form, as encoder_forward issues it: overlapping rows
+    (ld = s Cin), batch z1 strides, one bf16 segment + two fp8 segments [x_lo8 | x_hi8] x [w_hi8 |
+    w_lo8] scaled by 2^-e, f32 output; against float64 of the same operands, and the exact conv."""
+    K = gen3
+    B, Cin, C, e = 3, 512, 512, 11
+    Tout = (Tin - k) // s + 1
+    x = F.gelu(torch.randn(B, Tin, Cin, device="cuda"))
+    w = torch.randn(C, Cin, k, device="cuda") * 0.03
+    x_hi = x.to(torch.bfloat16)
+    x8 = torch.stack([fp8_ref((x - x_hi.float()) * 2.0 ** e), fp8_ref(x_hi.float())]).cuda()
+    r = w.permute(0, 2, 1).reshape(C, k * Cin).contiguous()   # [co][k][ci]
+    r_hi = r.to(torch.bfloat16)
+    w8 = torch.stack([fp8_ref(r_hi.float()), lo_ref(r, e)]).cuda()
+    out = torch.empty(B * Tout, C, device="cuda")
+    K.gemm(K.Operand(x_hi, True, s * Cin, z1=Tin * Cin), K.Operand(r_hi, True, k * Cin), out, Tout, C, k * Cin,
+           ldc=C, batch=B, c_z1=Tout * C,
+           a8=K.Operand(x8, True, s * Cin, z1=Tin * Cin, seg_stride=B * Tin * Cin),
+           b8=K.Operand(w8, True, k * Cin, seg_stride=C * k * Cin), nseg8=2, b8_exp=e)
+    torch.cuda.synchronize()
+
+    def conv(a, ww):   # a [B, Tin, Cin], ww [C, k*Cin] (tap-major) -> [B*Tout, C]
+        wk = d(ww).view(C, k, Cin).permute(0, 2, 1)
+        return F.conv1d(d(a).permute(0, 2, 1), wk, stride=s).permute(0, 2, 1).reshape(B * Tout, C)
+
+    ref = conv(x_hi, r_hi) + 2.0 ** -e * (conv(x8[0], w8[0]) + conv(x8[1], w8[1]))
+    assert rel(out, ref) < 2e-6, rel(out, ref)
+    exact = conv(x, r)
+    assert rel(out, exact) < rel(conv(x_hi, r_hi), exact) / 8, (rel(out, exact), rel(conv(x_hi, r_hi), exact))
+
+
+def test_conv0_and_ln_fp8_planes_refused(nrse_device):
+    from nrse_amd import kernels as K, _lib
+    dev = nrse_device
+    B, L, k, s, C = 1, 2001, 10, 5, 512
+    T0 = (L - k) // s + 1
+    wav = torch.randn(B, L, device=dev)
+    w = torch.randn(C, k, device=dev); g = torch.ones(C, device=dev); b = torch.zeros(C, device=dev)
+    mean, rstd = torch.empty(T0, device=dev), torch.empty(T0, device=dev)
+    y8 = torch.empty(2, T0, C, device=dev, dtype=E4M3)
+    out32 = torch.empty(T0, C, device=dev)
+    with pytest.raises(_lib.NrseError):   # f32 out: the VALU kernel has no fp8 planes
+        K.conv0_fwd(wav, w, g, b, out32, mean, rstd, T0, k, s, 1e-5, y8=y8, y8_exp=11)
+    x = torch.randn(T0, C, device=dev)
+    y = torch.empty(T0, C, device=dev, dtype=torch.bfloat16)
+    with pytest.raises(_lib.NrseError):   # exponent out of range
+        K.ln_fwd(x, g, b, y, mean, rstd, 1e-5, y8=y8, y8_exp=99)
+    # fp8 segments at M < 128 (a short utterance's last conv layers): refused, never dropped --
+    # the engine keeps the three bf16 planes there
+    Tin, Cin, kk, ss = 160, 512, 2, 2
+    xa = torch.randn(2, Tin, Cin, device=dev).to(torch.bfloat16)
+    x8 = torch.zeros(2, 2, Tin, Cin, device=dev, dtype=E4M3)
+    r = torch.randn(C, kk * Cin, device=dev).to(torch.bfloat16)
+    w8 = torch.zeros(2, C, kk * Cin, device=dev, dtype=E4M3)
+    o = torch.empty(2 * 80, C, device=dev)
+    with pytest.raises(_lib.NrseError):
+        K.gemm(K.Operand(xa, True, ss * Cin, z1=Tin * Cin), K.Operand(r, True, kk * Cin), o, 80, C, kk * Cin, ldc=C,
+               batch=2, c_z1=80 * C, a8=K.Operand(x8, True, ss * Cin, z1=Tin * Cin, seg_stride=2 * Tin * Cin),
+               b8=K.Operand(w8, True, kk * Cin, seg_stride=C * kk * Cin), nseg8=2, b8_exp=11)

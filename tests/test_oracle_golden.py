@@ -215,6 +215,7 @@ def test_oracle_split_weight_mode_meets_north_star():
         finally:
             O.set_operand_dtype(None)
             O.set_split8(None)
+    print("split-weight oracle rel-L2 vs reference:", out)
     assert out["split"] < 1e-3, out
     assert out["split_fp8"] < 1e-3, out     # the engine's default bf16sw (fp8 correction segments)
     assert out["bf16"] > 3e-3, out
