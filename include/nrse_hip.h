@@ -34,7 +34,14 @@ typedef enum {
   NRSE_ERR_UNSUPPORTED = -5 /* configuration outside what the kernels implement */
 } nrse_status;
 
-typedef enum { NRSE_F32 = 0, NRSE_BF16 = 1, NRSE_BF16X3 = 2, NRSE_FP8 = 3 } nrse_dtype;
+typedef enum { NRSE_F32 = 0, NRSE_BF16 = 1, NRSE_BF16X3 = 2, NRSE_FP8 = 3, NRSE_MX6 = 4 } nrse_dtype;
+/* NRSE_MX6 (ABI 8): OCP MXFP6 e2m3 in blocks of 32 consecutive elements along a row, each block
+ * with its own E8M0 scale, stored in NRSE_FP8's footprint (one byte per element): block b of a row
+ * is the 32 bytes at element offset 32b = [24 bytes: value j at bits 6j..6j+5 (little-endian) |
+ * 1 byte scale s, the block's values times 2^(s-127) | 7 zero bytes]. The scale is the smallest
+ * power of two with max|x| <= 7.5 * 2^(s-127); values round to nearest even. The block-scaled MFMA
+ * runs e2m3 at twice the e4m3 rate (4x bf16): the split-weight mode's correction operands
+ * (nrse_gemm_params.a8 / b8 with dtype NRSE_MX6). Rows must hold whole blocks. */
 /* NRSE_FP8 (ABI 6): OCP fp8 e4m3fn (gfx950's native fp8), one byte per element, saturated at +-448;
  * the split-weight mode's correction operands (nrse_gemm_params.a8 / b8). */
 /* NRSE_BF16X3 (an OUTPUT format of nrse_layernorm_fwd and nrse_conv0_fwd only): the split-bf16
@@ -141,6 +148,10 @@ typedef struct {
    * GELU output feeding FFN-down's correction segment). ldc8 % 16 == 0, 16-byte aligned. */
   void* c8;
   long long ldc8;
+  /* ABI 8: a8 / b8 may both be NRSE_MX6 (then b8_exp must be 0: the scales are in the blocks);
+   * c8_dtype NRSE_MX6 writes c8 as MXFP6 blocks of the stored bf16 values (the register epilogue
+   * forms only); 0 or NRSE_FP8: fp8 */
+  int c8_dtype;
 } nrse_gemm_params;
 
 int nrse_gemm(const nrse_gemm_params* p, void* stream);
@@ -181,6 +192,9 @@ typedef struct {
    * stack's split-weight form): y8 [2, rows, C] = [fp8((o - bf16(o)) 2^y8_exp) |
    * fp8(bf16(o))], y = bf16(o); the next conv GEMM's a8 segments against [fp8(w_hi) | fp8(w_lo 2^e)] */
   int y8_split; int y8_exp;
+  /* ABI 8: y8_dtype NRSE_MX6 writes y8 (either form) as MXFP6 blocks instead of fp8 (y8_exp is
+   * then unused: the blocks carry their scales); 0 or NRSE_FP8: fp8 */
+  int y8_dtype;
 } nrse_ln_fwd_params;
 
 typedef struct {
@@ -280,6 +294,8 @@ typedef struct {
   void* ctx8;                     /* ABI 6, optional (bf16 MFMA path): [B*T, Hd] NRSE_FP8 copy of ctx,
                                      fp8(bf16 ctx) (the out-projection's fp8 correction operand);
                                      4-byte aligned. NULL: none */
+  int ctx8_dtype;                 /* ABI 8: NRSE_MX6 = ctx8 as MXFP6 blocks (head_dim 64, 32-byte
+                                     aligned); 0 or NRSE_FP8: fp8 */
 } nrse_attn_fwd_params;
 
 typedef struct {
@@ -337,6 +353,8 @@ typedef struct {
    * output o, y8 [2, B*T0, C] NRSE_FP8 = [fp8((o - bf16(o)) 2^y8_exp) | fp8(bf16(o))] (as
    * nrse_ln_fwd_params.y8_split); out = bf16(o). 16-byte aligned */
   void* y8; int y8_exp;
+  int y8_dtype;                   /* fwd, ABI 8: NRSE_MX6 = the two planes as MXFP6 blocks (no y8_exp);
+                                     0 or NRSE_FP8: fp8 */
 } nrse_conv0_params;
 int nrse_conv0_fwd(const nrse_conv0_params* p, void* stream);
 int nrse_conv0_bwd(const nrse_conv0_params* p, void* stream);
@@ -394,6 +412,10 @@ int nrse_split_bf16(const float* x, void* hi, void* lo, long long n, void* strea
 int nrse_split_lo8(const float* x, void* lo8, int lo8_exp, long long n, void* stream);
 /* ABI 6: y8[i] = fp8(x[i]) of a bf16 / f32 tensor (NRSE_FP8, saturated at +-448), n elements */
 int nrse_cast_fp8(const void* x, int x_dtype, void* y8, long long n, void* stream);
+/* ABI 8: the MXFP6 forms (NRSE_MX6 blocks, n a multiple of 32, 32-byte aligned y):
+ * lo6 = MXFP6(x - bf16(x)) of an f32 tensor, y6 = MXFP6(x) of a bf16 / f32 tensor */
+int nrse_split_lo_mx6(const float* x, void* lo6, long long n, void* stream);
+int nrse_cast_mx6(const void* x, int x_dtype, void* y6, long long n, void* stream);
 /* ABI 6: dst[i] = 0 for i < n floats (the step's small accumulators: no torch fill kernel) */
 int nrse_zero(float* dst, long long n, void* stream);
 /* Split-K reduction of a weight gradient (the Linear wgrads of the backward, train_byol.py:65):
@@ -498,6 +520,10 @@ typedef struct {
   /* ABI 6, optional: nonzero stores 0 to every g[i] after reading it, so the gradient buffer is
    * zeroed for the next step's accumulation inside this pass (no separate fill over g) */
   int zero_grad;
+  /* ABI 8: lo8_dtype NRSE_MX6 writes p_shadow_lo8 / ema_shadow_lo8 as MXFP6 blocks of
+   * p_new - bf16(p_new) (no lo8_exp; n, ema_n multiples of 32, 32-byte aligned planes); 0 or
+   * NRSE_FP8: fp8 */
+  int lo8_dtype;
 } nrse_adamw_params;
 int nrse_adamw(const nrse_adamw_params* p, void* stream);
 /* t_shadow_lo: optional, as nrse_adamw_params.p_shadow_lo */

@@ -207,6 +207,17 @@ NRSE_DEV bf16x8 frag_half(i32x8v v, int s) {
   return s == 0 ? __builtin_bit_cast(bf16x8, __builtin_shufflevector(v, v, 0, 1, 2, 3))
                 : __builtin_bit_cast(bf16x8, __builtin_shufflevector(v, v, 4, 5, 6, 7));
 }
+// MXFP6 operand (ABI 8): lane (g, i) reads its row's block g whole -- the 32 contiguous bytes
+// (chunks 2g, 2g+1 of the 128-byte K-tile row: conflict-free under the row swizzle like frag's
+// chunk pairs): dwords 0..5 the 32 e2m3 values of k = 32g..32g+31, dword 6 the block's scale
+// byte (the MFMA's opsel 0 byte)
+NRSE_DEV i32x8v frag_mx(const char* lds, int base, int lane) {
+  const int g = lane >> 4, row = base + (lane & 15), sw = (row >> 1) & 7;
+  const char* r = lds + row * 128;
+  const i32x4v a = *reinterpret_cast<const i32x4v*>(r + (((2 * g) ^ sw) << 4));
+  const i32x4v b = *reinterpret_cast<const i32x4v*>(r + (((2 * g + 1) ^ sw) << 4));
+  return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+}
 
 // ------------------------------------------------------------------ register epilogue
 // The common epilogues of the step run with their flags fixed at compile time: the lane's
@@ -376,7 +387,19 @@ NRSE_DEV void fast_epilogue(const nrse_gemm_params& p, const f32x4 (&acc)[8][4],
       *reinterpret_cast<uint4*>((char*)p.c + (epi.cbase + (long long)m * p.ldc + n) * ES) = u;
       if constexpr (OBF) {
         // the fp8 copy of the stored bf16 values (ABI 6 c8: the next GEMM's correction operand)
-        if (p.c8) *reinterpret_cast<uint2*>((unsigned char*)p.c8 + (long long)m * p.ldc8 + n) = fp8x8_from_bf16x8(u);
+        if (p.c8) {
+          uint2 w;
+          if (p.c8_dtype == NRSE_MX6) {  // ABI 8: MXFP6 blocks; the block's 4 chunks are lanes tid ^ 0..3
+            const float f[8] = {__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                                __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u),
+                                __uint_as_float(u.z << 16), __uint_as_float(u.z & 0xffff0000u),
+                                __uint_as_float(u.w << 16), __uint_as_float(u.w & 0xffff0000u)};
+            w = mx6_g4(f, lane, ch & 3, 1);
+          } else {
+            w = fp8x8_from_bf16x8(u);
+          }
+          *reinterpret_cast<uint2*>((unsigned char*)p.c8 + (long long)m * p.ldc8 + n) = w;
+        }
       }
       if constexpr (GAUX) {
         const uint4 w = *reinterpret_cast<const uint4*>(aimg + prow * APITCH + ch * 16);
@@ -401,8 +424,9 @@ NRSE_DEV void fast_epilogue(const nrse_gemm_params& p, const f32x4 (&acc)[8][4],
 // BMT: tile rows, 256 or 224 (= 7 x 32: e.g. M = 12768 = 57 x 224 frames of 32 utterances fills
 // 228 of the 256 CUs per N-column of tiles instead of 200; nrse_gemm256 picks the one that
 // needs fewer tile waves, see bm_choice)
-// F8: the split-weight mode's fp8 correction segments (ABI 6) follow the bf16 K-tiles
-template <bool AKC, bool BKC, int BMT, bool F8>
+// F8: the split-weight mode's correction segments follow the bf16 K-tiles: 1 fp8 (ABI 6), 2 MXFP6
+// (ABI 8)
+template <bool AKC, bool BKC, int BMT, int F8>
 __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params p, int mt, int nt) {
   static_assert(BMT == 256 || BMT == 224, "tile rows");
   static_assert(!F8 || (AKC && BKC), "fp8 correction segments: k-contiguous operands");
@@ -443,7 +467,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
   // fp8 correction K-tiles (128 k each) after them (F8; splits == 1)
   Ld8 la8, lb8;
   int tps8 = 1;
-  if constexpr (F8) {
+  if constexpr (F8 != 0) {
     ld8_init(la8, p.a8, (const char*)p.a8.ptr + zq * p.a8.z1 + zr * p.a8.z2);
     ld8_init(lb8, p.b8, (const char*)p.b8.ptr + zq * p.b8.z1 + zr * p.b8.z2);
     tps8 = p.K / 128;
@@ -476,7 +500,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
   // half-tile index j of a K-tile in staging (= first-read) order: 0 A-lo, 1 B-lo, 2 B-hi, 3 A-hi
   auto stage = [&](int j, const TilePos& q, int slot) {
     char* dst = smem + slot * HALF;
-    if constexpr (F8) {
+    if constexpr (F8 != 0) {
       if (q.f8) {
         if (j == 0) ld8_issue(la8, la, dst, wave, 0, q.sa);
         else if (j == 1) ld8_issue(lb8, lb, dst, wave, 0, q.sb);
@@ -566,7 +590,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
   // ping-pong start: group 1 falls one barrier behind (schedule and hand-off rules: header)
   if (wm == 1) __builtin_amdgcn_s_barrier();
   int base = 0;  // slot of half-tile sequence number 4t
-  if constexpr (!F8) {
+  if constexpr (F8 == 0) {
   // K-tile t+2 as (segment, K-tile within the segment), advanced by one per iteration: the
   // division by the segment's K-tile count stays out of the loop (done per iteration by all 8
   // waves on the CU's one scalar unit, it lengthened each K-tile's first phase by ~200 cycles)
@@ -620,6 +644,12 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
 #define NRSE_READ_B8(SLOT, FB)                                                           \
   _Pragma("unroll") for (int fj = 0; fj < 2; ++fj)                                     \
     FB[fj] = frag2(smem + (SLOT) * HALF, wn * 32 + fj * 16, lane);
+#define NRSE_READ_AM(SLOT, NFI)                                                          \
+  _Pragma("unroll") for (int fi = 0; fi < (NFI); ++fi)                                 \
+    fa8[fi] = frag_mx(smem + (SLOT) * HALF, wm * 64 + fi * 16, lane);
+#define NRSE_READ_BM(SLOT, FB)                                                           \
+  _Pragma("unroll") for (int fj = 0; fj < 2; ++fj)                                     \
+    FB[fj] = frag_mx(smem + (SLOT) * HALF, wn * 32 + fj * 16, lane);
 #define NRSE_QUADH(MH, NH, FB)                                                           \
   __builtin_amdgcn_s_setprio(1);                                                         \
   _Pragma("unroll") for (int s = 0; s < 2; ++s)                                        \
@@ -627,12 +657,18 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
   _Pragma("unroll") for (int fj = 0; fj < 2; ++fj)                                     \
     NRSE_MFMA(acc[(MH) * 4 + fi][(NH) * 2 + fj], frag_half(fa8[fi], s), frag_half(FB[fj], s)); \
   __builtin_amdgcn_s_setprio(0);
+// MXFP6 (F8 == 2): format 2 (e2m3) for both operands, each lane's scale the block's own byte
+// (dword 6 of its fragment); e2m3 runs at twice the e4m3 rate
 #define NRSE_QUAD8(MH, NH, FB)                                                           \
   __builtin_amdgcn_s_setprio(1);                                                         \
   _Pragma("unroll") for (int fi = 0; fi < ((MH) ? NFI_HI : 4); ++fi)                   \
   _Pragma("unroll") for (int fj = 0; fj < 2; ++fj)                                     \
-    acc[(MH) * 4 + fi][(NH) * 2 + fj] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(  \
-        FB[fj], fa8[fi], acc[(MH) * 4 + fi][(NH) * 2 + fj], 0, 0, 0, scw, 0, sc1);        \
+    if constexpr (F8 == 2)                                                               \
+      acc[(MH) * 4 + fi][(NH) * 2 + fj] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4( \
+          FB[fj], fa8[fi], acc[(MH) * 4 + fi][(NH) * 2 + fj], 2, 2, 0, FB[fj][6], 0, fa8[fi][6]); \
+    else                                                                                 \
+      acc[(MH) * 4 + fi][(NH) * 2 + fj] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4( \
+          FB[fj], fa8[fi], acc[(MH) * 4 + fi][(NH) * 2 + fj], 0, 0, 0, scw, 0, sc1);      \
   __builtin_amdgcn_s_setprio(0);
 // the raw barrier with scheduling fences: without them the compiler moved this loop's MFMAs across
 // the phase barriers (out of their ping-pong segments), and fp8 K-tiles ran at half the bf16 rate
@@ -677,9 +713,15 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
         stage(j, q2, slot);
       }
     };
-    NRSE_READ_A8(s0, 4)
-    NRSE_READ_B8(s1, fbl8)
-    NRSE_READ_B8(s2, fbh8)
+    if constexpr (K8 && F8 == 2) {
+      NRSE_READ_AM(s0, 4)
+      NRSE_READ_BM(s1, fbl8)
+      NRSE_READ_BM(s2, fbh8)
+    } else {
+      NRSE_READ_A8(s0, 4)
+      NRSE_READ_B8(s1, fbl8)
+      NRSE_READ_B8(s2, fbh8)
+    }
     stg(0, wrap(base + 8));
     stg(1, wrap(base + 9));
     NRSE_WAIT(12);
@@ -692,7 +734,11 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
       NRSE_QUADH(0, 1, fbh8)
     }
     NRSE_BAR8();
-    NRSE_READ_A8(s3, NFI_HI)
+    if constexpr (K8 && F8 == 2) {
+      NRSE_READ_AM(s3, NFI_HI)
+    } else {
+      NRSE_READ_A8(s3, NFI_HI)
+    }
     stg(2, base);
     stg(3, s1);
     NRSE_WAIT(10);
@@ -714,6 +760,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
   for (; t < ntiles; ++t) ktile(t, std::true_type{});
 #undef NRSE_READ_A8
 #undef NRSE_READ_B8
+#undef NRSE_READ_AM
+#undef NRSE_READ_BM
 #undef NRSE_QUADH
 #undef NRSE_QUAD8
 #undef NRSE_BAR8
@@ -858,7 +906,7 @@ int bm_choice(const nrse_gemm_params* p) {
   return w224 <= w256 ? 224 : 256;
 }
 
-template <bool AKC, bool BKC, bool F8 = false>
+template <bool AKC, bool BKC, int F8 = 0>
 int launch(const nrse_gemm_params* p, hipStream_t st) {
   const int bm = bm_choice(p);
   const int mt = nrse_cdiv(p->M, bm), nt = nrse_cdiv(p->N, BN);
@@ -896,7 +944,7 @@ bool nrse_gemm256_f8_ok(const nrse_gemm_params* p) {
   auto m16 = [](long long x) { return (x & 15) == 0; };
   const nrse_gemm_operand* o8[2] = {&p->a8, &p->b8};
   for (const nrse_gemm_operand* o : o8) {
-    if (!o->ptr || o->dtype != NRSE_FP8 || !o->kcontig || o->chunk_shift != 0 || !al16(o->ptr) ||
+    if (!o->ptr || o->dtype != p->a8.dtype || !o->kcontig || o->chunk_shift != 0 || !al16(o->ptr) ||
         !m16(o->seg_stride) || !m16(o->z1) || !m16(o->z2) || o->seg_stride < 0)
       return false;
   }
@@ -904,12 +952,16 @@ bool nrse_gemm256_f8_ok(const nrse_gemm_params* p) {
   if (p->a8.ld != p->a.ld || p->b8.ld != p->b.ld || (p->a.ld & 63) || (p->b.ld & 63)) return false;
   const long long spa = (long long)(p->nseg8 - 1) * p->a8.seg_stride + (long long)p->M * p->a8.ld + p->K;
   const long long spb = (long long)(p->nseg8 - 1) * p->b8.seg_stride + (long long)p->N * p->b8.ld + p->K;
+  // MXFP6 (ABI 8): the scales travel in the blocks, so no b8_exp; blocks start at 32-byte offsets
+  const bool mx = p->a8.dtype == NRSE_MX6;
+  if (p->a8.dtype != NRSE_FP8 && !mx) return false;
+  if (mx && (p->b8_exp != 0 || ((uintptr_t)p->a8.ptr & 31) || ((uintptr_t)p->b8.ptr & 31))) return false;
   return p->K % 128 == 0 && p->splits == 1 && p->a.kcontig && p->b.kcontig && spa < (1LL << 31) &&
          spb < (1LL << 31) && p->b8_exp > -127 && p->b8_exp < 127;
 }
 
 int nrse_gemm256(const nrse_gemm_params* p, hipStream_t st) {
-  if (p->nseg8 > 0) return launch<true, true, true>(p, st);
+  if (p->nseg8 > 0) return p->a8.dtype == NRSE_MX6 ? launch<true, true, 2>(p, st) : launch<true, true, 1>(p, st);
   if (p->a.kcontig && p->b.kcontig) return launch<true, true>(p, st);
   if (p->a.kcontig && !p->b.kcontig) return launch<true, false>(p, st);
   if (!p->a.kcontig && p->b.kcontig) return launch<false, true>(p, st);

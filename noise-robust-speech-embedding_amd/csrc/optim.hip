@@ -70,8 +70,14 @@ NRSE_DEV void ema_one(const nrse_adamw_params& p, long long i, float pn, float e
   if (p.ema_shadow_lo8) ((unsigned char*)p.ema_shadow_lo8)[i] = fp8_1(lo_resid(t) * sc8);
 }
 
-// the fp8 correction plane of 4 consecutive weights at float4 index q (ABI 6)
-NRSE_DEV void store_lo8x4(void* lo8, long long q, const float* x, float sc8) {
+// the fp8 correction plane of 4 consecutive weights at float4 index q (ABI 6); mx: the MXFP6 form
+// (ABI 8), a block = the 8 lanes q & ~7 .. (all live together: the host requires n % 32 == 0)
+NRSE_DEV void store_lo8x4(void* lo8, long long q, const float* x, float sc8, bool mx) {
+  if (mx) {
+    const float l[4] = {lo_resid(x[0]), lo_resid(x[1]), lo_resid(x[2]), lo_resid(x[3])};
+    reinterpret_cast<uint32_t*>(lo8)[q] = mx6_g8(l, threadIdx.x & 63);
+    return;
+  }
   reinterpret_cast<uint32_t*>(lo8)[q] =
       fp8x4(lo_resid(x[0]) * sc8, lo_resid(x[1]) * sc8, lo_resid(x[2]) * sc8, lo_resid(x[3]) * sc8);
 }
@@ -95,6 +101,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(const nrse_adamw_params p) {
   const long long e4 = p.ema_n / 4;  // whole quads of the fused EMA range
   const float eom = 1.f - p.ema_decay;
   const float sc8 = ldexpf(1.f, p.lo8_exp);
+  const bool mx = p.lo8_dtype == NRSE_MX6;
   for (long long q = (long long)blockIdx.x * 256 + threadIdx.x; q < n4; q += (long long)gridDim.x * 256) {
     float4 pv = reinterpret_cast<float4*>(p.p)[q];
     const float4 gv = reinterpret_cast<const float4*>(p.g)[q];
@@ -122,7 +129,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(const nrse_adamw_params p) {
         reinterpret_cast<float4*>(p.p_shadow)[q] = pv;
       }
     }
-    if (p.p_shadow_lo8) store_lo8x4(p.p_shadow_lo8, q, pa, sc8);
+    if (p.p_shadow_lo8) store_lo8x4(p.p_shadow_lo8, q, pa, sc8, mx);
     if (p.ema_t) {
       if (q < e4) {
         float4 tv = reinterpret_cast<float4*>(p.ema_t)[q];
@@ -133,7 +140,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(const nrse_adamw_params p) {
           if (p.ema_shadow_dtype == NRSE_BF16) store_bf16x4(p.ema_shadow, p.ema_shadow_lo, q, &tv.x);
           else reinterpret_cast<float4*>(p.ema_shadow)[q] = tv;
         }
-        if (p.ema_shadow_lo8) store_lo8x4(p.ema_shadow_lo8, q, &tv.x, sc8);
+        if (p.ema_shadow_lo8) store_lo8x4(p.ema_shadow_lo8, q, &tv.x, sc8, mx);
       } else if (q == e4) {
         // the quad holding the EMA range's end: its first ema_n - 4 q elements, from this thread's
         // updated registers
@@ -254,6 +261,10 @@ extern "C" int nrse_adamw(const nrse_adamw_params* p, void* stream) {
   NRSE_REQUIRE(((uintptr_t)p->p_shadow_lo8 & 3) == 0 && ((uintptr_t)p->ema_shadow_lo8 & 3) == 0 &&
                    (!p->ema_shadow_lo8 || p->ema_t),
                "nrse_adamw: fp8 planes need 4-byte alignment (and ema_t for ema_shadow_lo8)");
+  NRSE_REQUIRE(p->lo8_dtype == 0 || p->lo8_dtype == NRSE_FP8 ||
+                   (p->lo8_dtype == NRSE_MX6 && p->n % 32 == 0 && (!p->ema_t || p->ema_n % 32 == 0) &&
+                    ((uintptr_t)p->p_shadow_lo8 & 31) == 0 && ((uintptr_t)p->ema_shadow_lo8 & 31) == 0),
+               "nrse_adamw: lo8_dtype %d (MXFP6: n, ema_n multiples of 32, 32-byte aligned planes)", p->lo8_dtype);
   if (p->n == 0) return NRSE_OK;
   hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(p->n)), dim3(256), 0, (hipStream_t)stream, *p);
   return nrse_check_launch("nrse_adamw");

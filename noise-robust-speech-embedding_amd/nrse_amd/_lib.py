@@ -16,6 +16,7 @@ F32 = 0
 BF16 = 1
 BF16X3 = 2   # output-only split-bf16 planes [hi | lo | hi] (include/nrse_hip.h)
 FP8 = 3      # OCP fp8 e4m3fn, the split-weight mode's correction operands (ABI 6)
+MX6 = 4      # OCP MXFP6 e2m3 in 32-element blocks with E8M0 scales, fp8's byte footprint (ABI 8)
 
 EPI_BIAS = 1 << 0
 EPI_GELU = 1 << 1
@@ -63,13 +64,13 @@ class GemmParams(ctypes.Structure):
                 ("r_z2", c_ll), ("dropout_p", c_f), ("seed", c_u32), ("colsum", c_vp),
                 ("colsum_part", c_vp),
                 ("a8", GemmOperand), ("b8", GemmOperand), ("nseg8", c_int), ("b8_exp", c_int),
-                ("c8", c_vp), ("ldc8", c_ll)]
+                ("c8", c_vp), ("ldc8", c_ll), ("c8_dtype", c_int)]
 
 
 class LnFwdParams(ctypes.Structure):
     _fields_ = [("x", c_vp), ("x_dtype", c_int), ("gamma", c_vp), ("beta", c_vp), ("y", c_vp), ("y_dtype", c_int),
                 ("mean", c_vp), ("rstd", c_vp), ("rows", c_ll), ("C", c_int), ("eps", c_f), ("flags", c_int),
-                ("y8", c_vp), ("y8_split", c_int), ("y8_exp", c_int)]
+                ("y8", c_vp), ("y8_split", c_int), ("y8_exp", c_int), ("y8_dtype", c_int)]
 
 
 class LnBwdParams(ctypes.Structure):
@@ -87,7 +88,7 @@ class AttnFwdParams(ctypes.Structure):
     _fields_ = [("qkv", c_vp), ("dtype", c_int), ("gate", c_vp), ("bias", c_vp), ("ctx", c_vp), ("lse", c_vp),
                 ("batch", c_int), ("T", c_int), ("H", c_int), ("head_dim", c_int), ("scale", c_f),
                 ("dropout_p", c_f), ("seed", c_u32), ("bias_vec", c_vp), ("drop_mask", c_vp),
-                ("drop_mask_in", c_int), ("ctx8", c_vp)]
+                ("drop_mask_in", c_int), ("ctx8", c_vp), ("ctx8_dtype", c_int)]
 
 
 class AttnBwdParams(ctypes.Structure):
@@ -103,7 +104,7 @@ class Conv0Params(ctypes.Structure):
                 ("dy", c_vp), ("dy_dtype", c_int), ("dy_mode", c_int), ("col_k", c_int), ("col_s", c_int),
                 ("col_tout", c_int), ("dw", c_vp), ("dgamma", c_vp), ("dbeta", c_vp),
                 ("batch", c_int), ("T0", c_int), ("C", c_int), ("k", c_int), ("s", c_int), ("eps", c_f),
-                ("part", c_vp), ("y8", c_vp), ("y8_exp", c_int)]
+                ("part", c_vp), ("y8", c_vp), ("y8_exp", c_int), ("y8_dtype", c_int)]
 
 
 class AdamWParams(ctypes.Structure):
@@ -112,7 +113,8 @@ class AdamWParams(ctypes.Structure):
                 ("step", c_int), ("max_norm", c_f), ("sumsq", c_vp), ("grad_scale", c_f),
                 ("p_shadow_lo", c_vp), ("ema_t", c_vp), ("ema_shadow", c_vp), ("ema_shadow_lo", c_vp),
                 ("ema_shadow_dtype", c_int), ("ema_decay", c_f), ("ema_n", c_ll),
-                ("p_shadow_lo8", c_vp), ("ema_shadow_lo8", c_vp), ("lo8_exp", c_int), ("zero_grad", c_int)]
+                ("p_shadow_lo8", c_vp), ("ema_shadow_lo8", c_vp), ("lo8_exp", c_int), ("zero_grad", c_int),
+                ("lo8_dtype", c_int)]
 
 
 _P = ctypes.POINTER
@@ -161,6 +163,8 @@ _SIGNATURES = {
     "nrse_split_bf16": ([c_vp, c_vp, c_vp, c_ll, c_vp], c_int),
     "nrse_split_lo8": ([c_vp, c_vp, c_int, c_ll, c_vp], c_int),
     "nrse_cast_fp8": ([c_vp, c_int, c_vp, c_ll, c_vp], c_int),
+    "nrse_split_lo_mx6": ([c_vp, c_vp, c_ll, c_vp], c_int),
+    "nrse_cast_mx6": ([c_vp, c_int, c_vp, c_ll, c_vp], c_int),
     "nrse_zero": ([c_vp, c_ll, c_vp], c_int),
     "nrse_splitk_reduce": ([c_vp, c_vp, c_int, c_ll, c_int, c_vp], c_int),
     "nrse_rows_reduce": ([c_vp, c_ll, c_vp, c_ll, c_vp, c_ll, c_vp, c_int, c_int, c_int, c_vp], c_int),

@@ -76,6 +76,13 @@ _SPLIT_LO8 = os.environ.get("NRSE_SPLIT_LO8", "1") != "0"
 # gamma = 1, beta = 0); beyond that the conversion saturates (bounded error, never inf / NaN)
 _CONV_SPLIT8 = os.environ.get("NRSE_CONV_SPLIT8", "1") != "0"
 CONV_LO8_EXP = int(os.environ.get("NRSE_CONV_LO8_EXP", "11"))
+# the correction operands as MXFP6 blocks (ABI 8: e2m3 with a scale per 32 elements, no exponents)
+# instead of fp8 e4m3: opt-in (NRSE_SPLIT_MX6=1). Measured slower (bf16sw 455 vs 466-468 pairs/s,
+# profiles/r05_mx6_ab.txt): on this part the 16x16x128 block-scaled MFMA the 256x256 GEMM's
+# 16x16 accumulators need runs e2m3 at the e4m3 rate (tools/probe_mx_rate.hip: fp8 / fp6 / fp4
+# 3.9 / 4.0 / 4.2 PF); only the 32x32x64 shape doubles it (4.2 -> 7.1 PF), which would take a
+# 32x32 accumulator layout in the correction segments
+_SPLIT_MX6 = os.environ.get("NRSE_SPLIT_MX6", "0") == "1"
 FP8 = K.FP8
 
 
@@ -155,7 +162,7 @@ class EncoderWeights:
                 K.swap12(w, r32, co, ci, k)
                 r = torch.empty(co, k * ci, device=eng.dev, dtype=cdt)
                 K.cast(r32, r)
-                w8 = torch.empty(2, co, k * ci, device=eng.dev, dtype=FP8)
+                w8 = torch.empty(2, co, k * ci, device=eng.dev, dtype=eng.corr_dt)
                 K.cast_fp8(r, w8[0])
                 K.split_lo8(r32, w8[1], self.conv_lo8_exp)
                 self.conv_r.append(r)
@@ -202,7 +209,8 @@ class EncoderWeights:
 class ByolEngine:
     def __init__(self, arch: WavLMArch, proj_dim: int, pred_dim: int, *, device="cuda", compute_dtype=torch.bfloat16,
                  seed: int = 1234, step_cfg: StepConfig | None = None, init_flat: torch.Tensor | None = None,
-                 do_normalize: bool = True, weight_split: bool = False, split_lo8: bool | None = None):
+                 do_normalize: bool = True, weight_split: bool = False, split_lo8: bool | None = None,
+                 split_mx6: bool | None = None):
         if arch.head_dim != 64:
             raise _lib.NrseError(f"head_dim {arch.head_dim} unsupported (attention kernels are head_dim 64)")
         if weight_split and compute_dtype != torch.bfloat16:
@@ -230,6 +238,8 @@ class ByolEngine:
         # fp8 correction planes of the split-weight mode: fp8((w - bf16(w)) 2^lo8_exp)
         self.online_lo8 = self.target_lo8 = None
         self.lo8_exp = 0
+        # the correction planes' dtype: fp8 e4m3 (K.FP8, default) or MXFP6 blocks (K.MX6, opt-in)
+        self.corr_dt = K.MX6 if (_SPLIT_MX6 if split_mx6 is None else split_mx6) else FP8
         if self.cdt == F32:
             self.online_sh = None
             self.target_sh = None
@@ -242,8 +252,8 @@ class ByolEngine:
             K.split_bf16(self.online, self.online_sh, self.online_lo)
             K.split_bf16(self.target, self.target_sh, self.target_lo)
             if _SPLIT_LO8 if split_lo8 is None else split_lo8:
-                self.online_lo8 = torch.empty(n, device=self.dev, dtype=FP8)
-                self.target_lo8 = torch.empty(ne, device=self.dev, dtype=FP8)
+                self.online_lo8 = torch.empty(n, device=self.dev, dtype=self.corr_dt)
+                self.target_lo8 = torch.empty(ne, device=self.dev, dtype=self.corr_dt)
         else:
             self.online_sh = torch.empty(n, device=self.dev, dtype=self.cdt)
             self.target_sh = torch.empty(ne, device=self.dev, dtype=self.cdt)
@@ -324,7 +334,13 @@ class ByolEngine:
         correction planes (nrse_split_lo8). |w - bf16(w)| <= 2^-8 |w|, so with W = max |w| the plane's
         values stay below 448 / 2 (2x headroom for weights that grow in training; beyond it the
         conversion saturates) at lo8_exp = floor(log2(224 / (2^-8 W))); the smallest weights fall to
-        fp8 subnormals, whose absolute error (2^-9 2^-lo8_exp) is far below the bf16 residual itself."""
+        fp8 subnormals, whose absolute error (2^-9 2^-lo8_exp) is far below the bf16 residual itself.
+        MXFP6 planes (corr_dt K.MX6) carry a scale per 32 weights and need no exponent."""
+        if self.corr_dt == K.MX6:
+            self.lo8_exp = 0
+            K.split_lo8(self.online, self.online_lo8)
+            K.split_lo8(self.target, self.target_lo8)
+            return
         W = max(float(t.abs().max()) for f in (self.online, self.target) for t in self._lo8_weights(f))
         self.lo8_exp = int(math.floor(math.log2(224.0 * 256.0 / max(W, 1e-30)))) if W > 0 else 0
         self.lo8_exp = max(-60, min(60, self.lo8_exp))
@@ -456,7 +472,7 @@ class ByolEngine:
         e8 = W.conv_lo8_exp
         nconv = len(a.conv_dim)
         y = torch.empty((3, B * T0, C0) if split3 else (B * T0, C0), device=dev, dtype=cdt)
-        x8 = torch.empty(2, B * T0, C0, device=dev, dtype=FP8) if s8 else None
+        x8 = torch.empty(2, B * T0, C0, device=dev, dtype=self.corr_dt) if s8 else None
         mean = torch.empty(B * T0, device=dev, dtype=F32)
         rstd = torch.empty(B * T0, device=dev, dtype=F32)
         pre0 = "feature_extractor.conv_layers.0."
@@ -486,7 +502,7 @@ class ByolEngine:
             else:
                 yo3 = torch.empty(B * Tout, C, device=dev, dtype=cdt)
                 if s8:
-                    yo8 = torch.empty(2, B * Tout, C, device=dev, dtype=FP8)
+                    yo8 = torch.empty(2, B * Tout, C, device=dev, dtype=self.corr_dt)
             mo = torch.empty(B * Tout, device=dev, dtype=F32)
             ro = torch.empty(B * Tout, device=dev, dtype=F32)
             p = f"feature_extractor.conv_layers.{i}."
@@ -590,7 +606,7 @@ class ByolEngine:
             m1 = torch.empty(BT, device=dev, dtype=F32)
             r1 = torch.empty(BT, device=dev, dtype=F32)
             # split-weight mode, fp8 form: the LN outputs' fp8 copies feed the correction segments
-            x1_8 = torch.empty(BT, H, device=dev, dtype=FP8) if lo8 else None
+            x1_8 = torch.empty(BT, H, device=dev, dtype=self.corr_dt) if lo8 else None
             K.ln_fwd(hcur, Pm[p + "layer_norm.weight"], Pm[p + "layer_norm.bias"], x1, m1, r1, a.eps, y8=x1_8)
             qkv = torch.empty(BT, 3 * H, device=dev, dtype=cdt)
             K.linear_fwd(x1, self.fused(W.s_flat, li, "qkv_w"), qkv, bias=self.fused(W.m_flat, li, "qkv_b"),
@@ -601,7 +617,7 @@ class ByolEngine:
             K.gate_fwd(x1, Pm[at + "gru_rel_pos_linear.weight"], Pm[at + "gru_rel_pos_linear.bias"],
                        Pm[at + "gru_rel_pos_const"], gate, B, T, nh)
             ctx = torch.empty(BT, H, device=dev, dtype=cdt)
-            ctx8 = torch.empty(BT, H, device=dev, dtype=FP8) if lo8 else None
+            ctx8 = torch.empty(BT, H, device=dev, dtype=self.corr_dt) if lo8 else None
             lse = torch.empty(B, nh, T, device=dev, dtype=F32)
             if mask_ev is not None:
                 torch.cuda.current_stream(dev).wait_event(mask_ev)
@@ -616,14 +632,14 @@ class ByolEngine:
             x2 = torch.empty(BT, H, device=dev, dtype=cdt)
             m2 = torch.empty(BT, device=dev, dtype=F32)
             r2 = torch.empty(BT, device=dev, dtype=F32)
-            x2_8 = torch.empty(BT, H, device=dev, dtype=FP8) if lo8 else None
+            x2_8 = torch.empty(BT, H, device=dev, dtype=self.corr_dt) if lo8 else None
             K.ln_fwd(hmid, Pm[p + "final_layer_norm.weight"], Pm[p + "final_layer_norm.bias"], x2, m2, r2, a.eps,
                      y8=x2_8)
             f1pre = torch.empty(BT, F_, device=dev, dtype=cdt) if need_grad else None
             g1 = torch.empty(BT, F_, device=dev, dtype=cdt)
             # (fp8 form: the FFN-up epilogue also writes fp8(g1), FFN-down's correction operand; the
             # activation dropout, 0 in the step, would come before that copy is taken)
-            g1_8 = torch.empty(BT, F_, device=dev, dtype=FP8) if lo8 else None
+            g1_8 = torch.empty(BT, F_, device=dev, dtype=self.corr_dt) if lo8 else None
             K.linear_fwd(x2, Ps[p + "feed_forward.intermediate_dense.weight"], g1,
                          bias=Pm[p + "feed_forward.intermediate_dense.bias"], flags=_lib.EPI_GELU, aux=f1pre,
                          ldaux=F_, dropout_p=pact, seed=R.site_seed(fseed, R.site_act(li)), out8=g1_8,

@@ -15,8 +15,10 @@ from . import _lib
 from ._lib import (AdamWParams, AttnBwdParams, AttnFwdParams, Conv0Params, GemmOperand, GemmParams, LnBwdParams,
                    LnFwdParams)
 
-_DT = {torch.float32: _lib.F32, torch.bfloat16: _lib.BF16, torch.float8_e4m3fn: _lib.FP8}
+_DT = {torch.float32: _lib.F32, torch.bfloat16: _lib.BF16, torch.float8_e4m3fn: _lib.FP8, torch.uint8: _lib.MX6}
 FP8 = torch.float8_e4m3fn  # NRSE_FP8: OCP e4m3fn, the split-weight mode's correction operands
+MX6 = torch.uint8          # NRSE_MX6 (ABI 8): MXFP6 blocks in fp8's byte footprint, held as raw bytes
+CORR = (FP8, MX6)          # the correction-plane dtypes
 
 
 def dtype_code(t: torch.Tensor) -> int:
@@ -139,11 +141,12 @@ def gemm(A: Operand, B: Operand, C: torch.Tensor, M: int, N: int, K: int, *, ldc
     p.seed = seed & 0xFFFFFFFF
     p.colsum = ptr(colsum)
     if nseg8:
-        assert a8 is not None and b8 is not None and a8.t.dtype == b8.t.dtype == FP8
-        p.a8, p.b8, p.nseg8, p.b8_exp = a8.c(), b8.c(), nseg8, b8_exp
+        assert a8 is not None and b8 is not None and a8.t.dtype == b8.t.dtype and a8.t.dtype in CORR
+        p.a8, p.b8, p.nseg8 = a8.c(), b8.c(), nseg8
+        p.b8_exp = 0 if a8.t.dtype == MX6 else b8_exp   # MXFP6: the scales are in the blocks
     if c8 is not None:
-        assert c8.dtype == FP8
-        p.c8, p.ldc8 = ptr(c8), ldc8
+        assert c8.dtype in CORR
+        p.c8, p.ldc8, p.c8_dtype = ptr(c8), ldc8, dtype_code(c8)
     ws = None
     if colsum is not None and DETERMINISTIC:
         ws = workspace(_lib.lib().nrse_gemm_colsum_workspace(ctypes.byref(p)))
@@ -167,10 +170,12 @@ def gemm(A: Operand, B: Operand, C: torch.Tensor, M: int, N: int, K: int, *, ldc
     _lib.check(_lib.lib().nrse_gemm(ctypes.byref(p), stream_ptr()), "nrse_gemm")
     if probe is not None:
         e1.record()
-        # bf16-equivalent work: an fp8 correction segment runs at twice the bf16 MFMA rate, so its
-        # FLOPs count half against the bf16 dense peak
-        probe.append((2.0 * M * N * K * (nseg * splits + 0.5 * nseg8) * batch, e0, e1,
-                      (M, N, K * nseg * splits, batch) if not nseg8 else (M, N, K * nseg, batch, f"fp8x{nseg8}")))
+        # bf16-equivalent work: an fp8 correction segment runs at twice the bf16 MFMA rate, an
+        # MXFP6 one at four times, so their FLOPs count 1/2 or 1/4 against the bf16 dense peak
+        w8 = (0.25 if a8.t.dtype == MX6 else 0.5) if nseg8 else 0.0
+        tag = ("mx6" if a8.t.dtype == MX6 else "fp8") if nseg8 else ""
+        probe.append((2.0 * M * N * K * (nseg * splits + w8 * nseg8) * batch, e0, e1,
+                      (M, N, K * nseg * splits, batch) if not nseg8 else (M, N, K * nseg, batch, f"{tag}x{nseg8}")))
 
 
 # When set to a list, every nrse_gemm launch appends (algorithmic FLOPs, start event, end event,
@@ -415,10 +420,11 @@ def ln_fwd(x, gamma, beta, y, mean, rstd, eps, gelu=False, relu=False, split3=Fa
     rows, C = x.shape[0] if x.dim() == 2 else x.numel() // x.shape[-1], x.shape[-1]
     if y8 is not None:
         n8 = rows * C * (1 if y8_exp is None else 2)
-        assert y8.dtype == FP8 and y8.numel() == n8 and y8.is_contiguous()
+        assert y8.dtype in CORR and y8.numel() == n8 and y8.is_contiguous()
     p = LnFwdParams(ptr(x), dtype_code(x), ptr(gamma), ptr(beta), ptr(y), _out_code(y, rows * C, split3), ptr(mean),
                     ptr(rstd), rows, C, eps, (_lib.LN_GELU if gelu else 0) | (_lib.LN_RELU if relu else 0), ptr(y8),
-                    0 if y8_exp is None else 1, 0 if y8_exp is None else int(y8_exp))
+                    0 if y8_exp is None else 1, 0 if y8_exp is None else int(y8_exp),
+                    dtype_code(y8) if y8 is not None else 0)
     _call("nrse_layernorm_fwd", ctypes.byref(p), stream_ptr())
 
 
@@ -525,10 +531,11 @@ def attn_fwd(qkv, gate, bias, ctx, lse, batch, T, H, dropout_p=0.0, seed=0, bias
     if drop_mask is not None:
         assert drop_mask.dtype == torch.int16 and drop_mask.numel() >= attn_mask_elems(batch, T, H)
     if ctx8 is not None:
-        assert ctx8.dtype == FP8 and ctx8.numel() == ctx.numel() and qkv.dtype == torch.bfloat16
+        assert ctx8.dtype in CORR and ctx8.numel() == ctx.numel() and qkv.dtype == torch.bfloat16
     p = AttnFwdParams(ptr(qkv), dtype_code(qkv), ptr(gate), ptr(bias), ptr(ctx), ptr(lse), batch, T, H, 64,
                       0.125, dropout_p, seed & 0xFFFFFFFF, ptr(bias_vec), ptr(drop_mask),
-                      1 if (mask_in and drop_mask is not None) else 0, ptr(ctx8))
+                      1 if (mask_in and drop_mask is not None) else 0, ptr(ctx8),
+                      dtype_code(ctx8) if ctx8 is not None else 0)
     _call("nrse_attn_fwd", ctypes.byref(p), stream_ptr())
 
 
@@ -552,8 +559,8 @@ def conv0_fwd(wav, w, gamma, beta, out, mean, rstd, T0, k, s, eps, split3=False,
     C = w.shape[0]
     p = Conv0Params()
     if y8 is not None:
-        assert y8.dtype == FP8 and y8.numel() == 2 * B * T0 * C and y8.is_contiguous() and not split3
-        p.y8, p.y8_exp = ptr(y8), int(y8_exp)
+        assert y8.dtype in CORR and y8.numel() == 2 * B * T0 * C and y8.is_contiguous() and not split3
+        p.y8, p.y8_exp, p.y8_dtype = ptr(y8), int(y8_exp), dtype_code(y8)
     p.wav, p.L, p.w, p.gamma, p.beta = ptr(wav), L, ptr(w), ptr(gamma), ptr(beta)
     p.out, p.out_dtype, p.mean, p.rstd = ptr(out), _out_code(out, B * T0 * C, split3), ptr(mean), ptr(rstd)
     p.batch, p.T0, p.C, p.k, p.s, p.eps = B, T0, C, k, s, eps
@@ -717,14 +724,16 @@ def adamw(p, g, m, v, shadow, *, lr, beta1, beta2, eps, weight_decay, step, max_
     if ema_t is not None:
         assert ema_t.dtype == torch.float32 and ema_t.numel() <= p.numel()
     for t, n in ((shadow_lo8, p.numel()), (ema_shadow_lo8, ema_t.numel() if ema_t is not None else 0)):
-        assert t is None or (t.dtype == FP8 and t.numel() == n)
+        assert t is None or (t.dtype in CORR and t.numel() == n)
+    lo8_dt = dtype_code(shadow_lo8 if shadow_lo8 is not None else ema_shadow_lo8) \
+        if (shadow_lo8 is not None or ema_shadow_lo8 is not None) else 0
     prm = AdamWParams(ptr(p), ptr(g), ptr(m), ptr(v), ptr(shadow),
                       dtype_code(shadow) if shadow is not None else 0, p.numel(), lr, beta1, beta2, eps,
                       weight_decay, step, max_norm, ptr(sumsq_buf), grad_scale, ptr(shadow_lo),
                       ptr(ema_t), ptr(ema_shadow), ptr(ema_shadow_lo),
                       dtype_code(ema_shadow) if ema_shadow is not None else 0, ema_decay,
                       ema_t.numel() if ema_t is not None else 0, ptr(shadow_lo8), ptr(ema_shadow_lo8), lo8_exp,
-                      1 if zero_grad else 0)
+                      1 if zero_grad else 0, lo8_dt)
     _call("nrse_adamw", ctypes.byref(prm), stream_ptr())
 
 
@@ -740,16 +749,21 @@ def split_bf16(x, hi, lo):
     _call("nrse_split_bf16", ptr(x), ptr(hi), ptr(lo), x.numel(), stream_ptr())
 
 
-def split_lo8(x, lo8, lo8_exp):
-    """lo8 = fp8((x - bf16(x)) 2^lo8_exp) (nrse_split_lo8): the fp8 correction plane of x."""
-    assert x.dtype == torch.float32 and lo8.dtype == FP8 and lo8.numel() == x.numel()
-    _call("nrse_split_lo8", ptr(x), ptr(lo8), int(lo8_exp), x.numel(), stream_ptr())
+def split_lo8(x, lo8, lo8_exp=0):
+    """lo8 = fp8((x - bf16(x)) 2^lo8_exp) (nrse_split_lo8): the fp8 correction plane of x; an MX6
+    (uint8) lo8: the MXFP6 blocks of x - bf16(x) (nrse_split_lo_mx6, no exponent)."""
+    assert x.dtype == torch.float32 and lo8.dtype in CORR and lo8.numel() == x.numel()
+    if lo8.dtype == MX6:
+        _call("nrse_split_lo_mx6", ptr(x), ptr(lo8), x.numel(), stream_ptr())
+    else:
+        _call("nrse_split_lo8", ptr(x), ptr(lo8), int(lo8_exp), x.numel(), stream_ptr())
 
 
 def cast_fp8(x, y8):
-    """y8 = fp8(x) (nrse_cast_fp8; x f32 or bf16)."""
-    assert y8.dtype == FP8 and y8.numel() == x.numel()
-    _call("nrse_cast_fp8", ptr(x), dtype_code(x), ptr(y8), x.numel(), stream_ptr())
+    """y8 = fp8(x) (nrse_cast_fp8; x f32 or bf16); an MX6 (uint8) y8: MXFP6 blocks (nrse_cast_mx6)."""
+    assert y8.dtype in CORR and y8.numel() == x.numel()
+    fn = "nrse_cast_mx6" if y8.dtype == MX6 else "nrse_cast_fp8"
+    _call(fn, ptr(x), dtype_code(x), ptr(y8), x.numel(), stream_ptr())
 
 
 def zero(t):

@@ -90,9 +90,10 @@ def test_fused_zero_grad_steps_match(nrse_device):
     assert float(engines[1].grad.abs().max()) == 0.0
 
 
-def test_split_weight_fp8_steps_are_bitwise_repeatable(nrse_device):
-    """The north-star mode (bf16sw, fp8 correction segments and planes) repeats bit for bit."""
-    engines = _pair(A.TINY, PROJ, PRED, torch.bfloat16, weight_split=True, split_lo8=True)
+@pytest.mark.parametrize("mx6", [True, False], ids=["mx6", "fp8"])
+def test_split_weight_fp8_steps_are_bitwise_repeatable(nrse_device, mx6):
+    """The north-star mode (bf16sw, MXFP6 / fp8 correction segments and planes) repeats bit for bit."""
+    engines = _pair(A.TINY, PROJ, PRED, torch.bfloat16, weight_split=True, split_lo8=True, split_mx6=mx6)
     assert engines[0].online_lo8 is not None
     clean, noisy = _batch(4, 16000)
     _steps_equal(engines, clean, noisy, steps=2)
@@ -112,8 +113,10 @@ def test_split_weight_fp8_conv_stack(nrse_device):
     l8 = [float(ref.train_step(clean, noisy, lr=1e-4, step_seed=100 + i)) for i in range(2)]
     l3 = [float(planes.train_step(clean, noisy, lr=1e-4, step_seed=100 + i)) for i in range(2)]
     assert ref.conv_split8_used and not planes.conv_split8_used
-    for a, b in zip(l8, l3):
-        assert abs(a - b) <= 1e-3 * max(abs(b), 1.0), (l8, l3)
+    # the first step's loss is the forward's numerics; after an update Adam's sign-like first steps
+    # amplify any gradient difference (a loose bound only)
+    assert abs(l8[0] - l3[0]) <= 1e-3 * max(abs(l3[0]), 1.0), (l8, l3)
+    assert abs(l8[1] - l3[1]) <= 1e-2 * max(abs(l3[1]), 1.0), (l8, l3)
     c1, n1 = _batch(4, 16000)
     ref.train_step(c1, n1, lr=1e-4, step_seed=7)
     assert not ref.conv_split8_used
