@@ -22,6 +22,10 @@ NRSE_DEV uint2 ldg(const uint2* p) {  // HIP vector struct: load as an ext vecto
   typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
   return __builtin_bit_cast(uint2, *(const __attribute__((address_space(1))) u32x2v*)p);
 }
+NRSE_DEV uint4 ldg(const uint4* p) {
+  typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+  return __builtin_bit_cast(uint4, *(const __attribute__((address_space(1))) u32x4v*)p);
+}
 
 NRSE_DEV float bf2f(bf16_t x) { return __uint_as_float(((uint32_t)x) << 16); }
 NRSE_DEV bf16_t f2bf(float x) {
@@ -253,6 +257,22 @@ NRSE_DEV f32x2 erf_fast2(f32x2 x) {
   return x * p * f32x2{__builtin_amdgcn_rcpf(q.x), __builtin_amdgcn_rcpf(q.y)};
 }
 NRSE_DEV f32x2 gelu2(f32x2 x) { return splat2(0.5f) * x * (splat2(1.0f) + erf_fast2(x * splat2(0.70710678118654752f))); }
+// gelu_grad_fast of two lanes, op for op (same values): the polynomial and products packed, rcp /
+// exp2 / the sign select per element
+NRSE_DEV f32x2 gelu_grad2(f32x2 x) {
+  const f32x2 ax = f32x2{__builtin_fabsf(x.x), __builtin_fabsf(x.y)};
+  const f32x2 d = pk_fma(ax, splat2(0.3275911f * 0.70710678118654752f), splat2(1.0f));
+  const f32x2 t = f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  f32x2 q = pk_fma(t, splat2(1.061405429f), splat2(-1.453152027f));
+  q = pk_fma(t, q, splat2(1.421413741f));
+  q = pk_fma(t, q, splat2(-0.284496736f));
+  q = pk_fma(t, q, splat2(0.254829592f));
+  const f32x2 ea = (x * splat2(-0.5f * 1.4426950408889634f)) * x;
+  const f32x2 e = f32x2{__builtin_amdgcn_exp2f(ea.x), __builtin_amdgcn_exp2f(ea.y)};
+  const f32x2 h = splat2(0.5f) * (t * q) * e;
+  const f32x2 cdf = f32x2{x.x >= 0.f ? 1.0f - h.x : h.x, x.y >= 0.f ? 1.0f - h.y : h.y};
+  return pk_fma(x * splat2(0.39894228040143268f), e, cdf);
+}
 
 // erf GELU as ACT2FN["gelu"] ([TF] activations.GELUActivation -> F.gelu default), evaluated with
 // erf_fast everywhere (|error| ~5e-7, the order of f32 erff's own; the parity tolerances are

@@ -509,6 +509,298 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
   }
 }
 
+// conv0 backward on the matrix cores (bf16 dy, k = 10, two-tap col2im or direct dy, C = 256 | 512):
+// the VALU kernel above spent ~20 of its ~50 operations per element on the conv recompute and the
+// dW FMAs and exchanged LN sums through a barrier per row. Here a workgroup's 4 waves take a
+// 16-row chunk together, each wave C/4 channels (NBW 16-channel blocks, lane column c owning
+// channels w C/4 + NBW c .. + NBW - 1: one 16-byte dy load per row and tap):
+//  - the conv is recomputed as the forward computes it (one MFMA 16x16x32 bf16 per block, the
+//    split-bf16 packing K = [x_hi w_hi | x_lo w_hi | x_hi w_lo]), not transposed: lane (g, c)
+//    holds rows 4g .. 4g+3 of its channel, so the per-channel sums (dgamma, dbeta) are lane-local
+//    and the LN backward's row sums reduce over 16 lanes, then over the 4 waves through LDS (one
+//    barrier per chunk, double-buffered slots);
+//  - dW[c][j] = sum_rows dc[row][c] x[row][j] is an MFMA 16x16x16 bf16 per block whose A fragment
+//    (channel on the lane column, rows 4g .. 4g+3 along k) is exactly the lane's dc values, in split
+//    bf16 (dc_hi x_hi + dc_lo x_hi + dc_hi x_lo, three MFMAs: ~2^-16, the f32 kernel's accuracy);
+//  - the waves own disjoint channels, so each workgroup stores its partial rows [dW | dgamma |
+//    dbeta] whole (nrse_rows_reduce adds them in workgroup order) without a cross-wave reduction.
+typedef short short4x __attribute__((ext_vector_type(4)));
+NRSE_DEV short4x pk4_hi(const float* v, float* lo) {  // bf16 hi of 4 values; lo[e] = v[e] - hi
+  short4x r;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const bf16_t h = f2bf(v[e]);
+    r[e] = (short)h;
+    lo[e] = v[e] - bf2f(h);
+  }
+  return r;
+}
+NRSE_DEV short4x pk4(const float* v) {
+  short4x r;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) r[e] = (short)f2bf(v[e]);
+  return r;
+}
+
+// one 16-row chunk's operands of a lane (loaded a chunk ahead: two buffers alternate)
+template <int NBW>
+struct C0Chunk {
+  float xa[8];          // X' fragment samples of row R0 + c
+  float xb[4];          // dW B fragment: rows R0 + 4g + r, tap c
+  float mu[4], rs[4];
+  uint32_t d0[4][NBW / 2], d1[4][NBW / 2];  // the two col2im taps of dy, NBW bf16 per row
+  uint32_t vmask;       // bit r: tap 0 valid, bit 4 + r: tap 1 valid
+};
+
+template <int NW, int NBW>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) void conv0_bwd_mfma_kernel(
+    const nrse_conv0_params p) {
+  constexpr int C = NW * NBW * 16, CW = NBW * 16;
+  __shared__ __attribute__((aligned(16))) bf16x8 wimg[NW * NBW * 64];  // [wave][block][lane] W' fragments
+  __shared__ __attribute__((aligned(16))) f32x2 xch[2][16][NW];          // [parity][chunk row][wave]
+  __shared__ __attribute__((aligned(16))) float gbs[2 * C];              // gamma | beta
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, c = lane & 15;
+  const int cbase = w * CW + c * NBW;  // this lane's channels: cbase + n, n < NBW
+  for (int idx = tid; idx < NW * NBW * 64; idx += NW * 64) {
+    const int ww = idx / (NBW * 64), n = (idx / 64) % NBW, ln = idx & 63;
+    const int ch = ww * CW + (ln & 15) * NBW + n;
+    bf16x8 v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = 8 * (ln >> 4) + e;
+      float wv = 0.f;
+      if (k < 30) {
+        const float wf = p.w[ch * KMAX + k % 10];
+        const float hi = bf2f(f2bf(wf));
+        wv = k < 20 ? hi : wf - hi;
+      }
+      v[e] = (__bf16)wv;
+    }
+    wimg[idx] = v;
+  }
+  for (int i = tid; i < C; i += NW * 64) {
+    gbs[i] = p.gamma[i];
+    gbs[C + i] = p.beta[i];
+  }
+  __syncthreads();
+
+  int tap[8], part[8];  // this lane's K positions of the X' fragment (as the forward)
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int k = 8 * g + e;
+    tap[e] = k < 30 ? k % 10 : 0;
+    part[e] = k / 10;
+  }
+  const long long rows = (long long)p.batch * p.T0;
+  const long long nch = (rows + 15) >> 4;
+  UDiv31 dT0, dS;
+  dT0.init((unsigned)p.T0);
+  dS.init(p.col_s > 0 ? (unsigned)p.col_s : 1u);
+  const bool col = p.dy_mode == NRSE_DY_COL2IM;
+  const float invC = 1.f / C;
+  const bf16_t* dyp = (const bf16_t*)p.dy;
+  f32x4 dwa[NBW];
+  f32x2 dga2[NBW / 2], dbe2[NBW / 2];
+#pragma unroll
+  for (int n = 0; n < NBW; ++n) dwa[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int m = 0; m < NBW / 2; ++m) dga2[m] = dbe2[m] = f32x2{0.f, 0.f};
+  auto xrow = [&](long long row) {  // waveform of conv0 row (row < rows)
+    const unsigned b = dT0.div((unsigned)row);
+    const int t = (int)((unsigned)row - b * (unsigned)p.T0);
+    return p.wav + (long long)b * p.L + (long long)t * p.s;
+  };
+  // every load issued from a valid address (clamped rows, tap offsets 0 when invalid + mask bits),
+  // so the wait-count pass sees a fixed number of loads in flight
+  auto load = [&](long long ck, C0Chunk<NBW>& q) {
+    const long long R0 = (ck < nch ? ck : nch - 1) * 16;
+    {
+      const long long ra = R0 + c < rows ? R0 + c : rows - 1;
+      const float* x = xrow(ra);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) q.xa[e] = ldg(x + tap[e]);
+    }
+    uint32_t vm = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const long long row = R0 + 4 * g + r;
+      const bool live = row < rows;
+      const long long rw = live ? row : rows - 1;
+      q.xb[r] = ldg(xrow(rw) + (c < KMAX ? c : 0));
+      q.mu[r] = ldg(p.mean + rw);
+      q.rs[r] = ldg(p.rstd + rw);
+      long long o0 = rw * C, o1 = 0;
+      bool a0 = true, a1 = false;
+      if (col) {
+        const unsigned b = dT0.div((unsigned)rw);
+        const int t = (int)((unsigned)rw - b * (unsigned)p.T0);
+        const int qq = (int)dS.div((unsigned)t);
+        const int j0 = t - qq * p.col_s, j1 = j0 + p.col_s;
+        a0 = j0 < p.col_k && qq < p.col_tout;
+        a1 = j1 < p.col_k && t >= j1 && qq - 1 < p.col_tout;
+        o0 = a0 ? (((long long)b * p.col_tout + qq) * p.col_k + j0) * (long long)C : 0;
+        o1 = a1 ? (((long long)b * p.col_tout + qq - 1) * p.col_k + j1) * (long long)C : 0;
+      }
+      vm |= (a0 && live ? 1u : 0u) << r;
+      vm |= (a1 && live ? 1u : 0u) << (4 + r);
+      if constexpr (NBW == 8) {
+        const uint4 e0 = ldg(reinterpret_cast<const uint4*>(dyp + o0 + cbase));
+        const uint4 e1 = ldg(reinterpret_cast<const uint4*>(dyp + o1 + cbase));
+        q.d0[r][0] = e0.x; q.d0[r][1] = e0.y; q.d0[r][2] = e0.z; q.d0[r][3] = e0.w;
+        q.d1[r][0] = e1.x; q.d1[r][1] = e1.y; q.d1[r][2] = e1.z; q.d1[r][3] = e1.w;
+      } else {
+        const uint2 e0 = ldg(reinterpret_cast<const uint2*>(dyp + o0 + cbase));
+        const uint2 e1 = ldg(reinterpret_cast<const uint2*>(dyp + o1 + cbase));
+        q.d0[r][0] = e0.x; q.d0[r][1] = e0.y;
+        q.d1[r][0] = e1.x; q.d1[r][1] = e1.y;
+      }
+    }
+    q.vmask = vm;
+  };
+
+  auto step = [&](long long ck, int it) {
+    C0Chunk<NBW> q;
+    load(ck, q);  // (a register prefetch of the next chunk pushed the kernel past 256 VGPRs)
+    // ---- the conv, recomputed: D[row 4g + r][channel cbase + n]
+    bf16x8 xf;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float hi = bf2f(f2bf(q.xa[e]));
+      xf[e] = (__bf16)(part[e] == 1 ? q.xa[e] - hi : (part[e] == 3 ? 0.f : hi));
+    }
+    f32x4 acc[NBW];
+#pragma unroll
+    for (int n = 0; n < NBW; ++n)
+      acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf, wimg[(w * NBW + n) * 64 + lane], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    // ---- LN + GELU backward, first half, in channel pairs (n, n + 1) as packed FP32 (the dy word
+    // of a pair holds both): gg, dgamma, dbeta, g = gg gamma and the row sums
+    constexpr int NP = NBW / 2;
+    f32x2 gv[NP][4], xh2[NP][4], s1[4], s2[4];
+    f32x2 ga[NP], be[NP];
+#pragma unroll
+    for (int m = 0; m < NP; ++m) {
+      ga[m] = *reinterpret_cast<const f32x2*>(gbs + cbase + 2 * m);
+      be[m] = *reinterpret_cast<const f32x2*>(gbs + C + cbase + 2 * m);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      s1[r] = s2[r] = f32x2{0.f, 0.f};
+      const bool v0 = (q.vmask >> r) & 1u, v1 = (q.vmask >> (4 + r)) & 1u;
+      const f32x2 rs2 = splat2(q.rs[r]), nm2 = splat2(-q.mu[r] * q.rs[r]);
+#pragma unroll
+      for (int m = 0; m < NP; ++m) {
+        const uint32_t u0 = v0 ? q.d0[r][m] : 0u, u1 = v1 ? q.d1[r][m] : 0u;
+        const f32x2 dyv = f32x2{__uint_as_float(u0 << 16), __uint_as_float(u0 & 0xffff0000u)} +
+                          f32x2{__uint_as_float(u1 << 16), __uint_as_float(u1 & 0xffff0000u)};
+        const f32x2 xh = pk_fma(f32x2{acc[2 * m][r], acc[2 * m + 1][r]}, rs2, nm2);
+        const f32x2 gg = dyv * gelu_grad2(pk_fma(xh, ga[m], be[m]));
+        dga2[m] = pk_fma(gg, xh, dga2[m]);
+        dbe2[m] += gg;
+        const f32x2 gq = gg * ga[m];
+        gv[m][r] = gq;
+        xh2[m][r] = xh;
+        s1[r] += gq;
+        s2[r] = pk_fma(gq, xh, s2[r]);
+      }
+    }
+    float rsc[4], xbc[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      rsc[r] = q.rs[r];
+      xbc[r] = q.xb[r];
+    }
+    // row sums over the wave's channels (16 lane columns), then over the NW waves (fixed order)
+    float t1[4], t2[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      t1[r] = s1[r].x + s1[r].y;
+      t2[r] = s2[r].x + s2[r].y;
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        t1[r] += __shfl_xor(t1[r], o, 16);
+        t2[r] += __shfl_xor(t2[r], o, 16);
+      }
+    }
+    const int par = it & 1;
+    if (c == 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) xch[par][4 * g + r][w] = f32x2{t1[r], t2[r]};
+    }
+    __syncthreads();
+    f32x2 S1[4], S2[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float a = 0.f, b2 = 0.f;
+#pragma unroll
+      for (int qq = 0; qq < NW; ++qq) {
+        const f32x2 v = xch[par][4 * g + r][qq];
+        a += v.x;
+        b2 += v.y;
+      }
+      S1[r] = splat2(a * invC);
+      S2[r] = splat2(b2 * invC);
+    }
+    // ---- second half: dc, and dW += dc^T x on the matrix cores (split bf16)
+    float xv[4], xlo[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) xv[r] = c < KMAX ? xbc[r] : 0.f;
+    const short4x xbh = pk4_hi(xv, xlo);
+    const short4x xbl = pk4(xlo);
+#pragma unroll
+    for (int m = 0; m < NP; ++m) {
+      float dc[2][4], dlo[2][4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const f32x2 v = pk_fma(-xh2[m][r], S2[r], gv[m][r] - S1[r]) * splat2(rsc[r]);
+        dc[0][r] = v.x;
+        dc[1][r] = v.y;
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int n = 2 * m + h;
+        const short4x ah = pk4_hi(dc[h], dlo[h]);
+        const short4x al = pk4(dlo[h]);
+        dwa[n] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ah, xbh, dwa[n], 0, 0, 0);
+        dwa[n] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(al, xbh, dwa[n], 0, 0, 0);
+        dwa[n] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ah, xbl, dwa[n], 0, 0, 0);
+      }
+    }
+  };
+
+  // uniform trip count over the workgroup (the LN-sum exchange is a workgroup barrier)
+  int it = 0;
+#pragma unroll 1
+  for (long long ck = blockIdx.x; ck < nch; ck += gridDim.x) step(ck, it++);
+  // ---- the workgroup's partial rows: dW (lane (g, j): channels w CW + (4g + r) NBW + n, tap j),
+  // dgamma / dbeta (summed over the 4 row groups g)
+  const int kk = KMAX;
+#pragma unroll
+  for (int n = 0; n < NBW; ++n) {
+    const float a = xor32_sum(xor16_sum((n & 1) ? dga2[n >> 1].y : dga2[n >> 1].x));
+    const float b2 = xor32_sum(xor16_sum((n & 1) ? dbe2[n >> 1].y : dbe2[n >> 1].x));
+    if (g == 0) {
+      const int ch = cbase + n;
+      if (p.part) {
+        p.part[((long long)blockIdx.x * (kk + 2) + kk) * C + ch] = a;
+        p.part[((long long)blockIdx.x * (kk + 2) + kk + 1) * C + ch] = b2;
+      } else {
+        atomicAdd(p.dgamma + ch, a);
+        atomicAdd(p.dbeta + ch, b2);
+      }
+    }
+    if (c < KMAX) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ch = w * CW + (4 * g + r) * NBW + n;
+        if (p.part) p.part[((long long)blockIdx.x * (kk + 2) + c) * C + ch] = dwa[n][r];
+        else atomicAdd(p.dw + (long long)c * C + ch, dwa[n][r]);
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------- weight norm (dim = 2)
 // v [H][cpg][K] ; per tap j: norm_j = ||v[:, :, j]||
 __global__ __launch_bounds__(256) void wn_norm_kernel(const float* __restrict__ v, float* __restrict__ norms,
@@ -764,9 +1056,19 @@ extern "C" int nrse_conv0_fwd(const nrse_conv0_params* p, void* stream) {
   return nrse_check_launch("nrse_conv0_fwd");
 }
 
+// the matrix-core backward's conditions (the bf16 step's form); NRSE_CONV0_MFMA=0 keeps the VALU one
+static bool conv0_bwd_mfma(const nrse_conv0_params* p) {
+  return p->dy_dtype == NRSE_BF16 && p->k == KMAX && (p->C == 512 || p->C == 256) && conv0_mfma_on() &&
+         (p->dy_mode == NRSE_DY_DIRECT || (p->dy_mode == NRSE_DY_COL2IM && p->col_k <= 2 * p->col_s));
+}
+
 // each block adds (k + 2) * C partial sums at the end (atomics or its partial row)
 static long long conv0_bwd_blocks(const nrse_conv0_params* p) {
   const long long rows = (long long)p->batch * p->T0;
+  if (conv0_bwd_mfma(p)) {  // 16-row chunks
+    const long long ch = (rows + 15) / 16;
+    return ch > 1024 ? 1024 : ch;
+  }
   const int rpb = p->C == 512 ? 2 : 4;
   const long long blocks = (rows + rpb - 1) / rpb;
   return blocks > 1024 ? 1024 : blocks;
@@ -786,6 +1088,10 @@ extern "C" int nrse_conv0_bwd(const nrse_conv0_params* p, void* stream) {
   // the model's geometry (k = 10, two-tap col2im) specialised; anything else takes the generic form
   const bool k10 = p->k == KMAX && (p->dy_mode != NRSE_DY_COL2IM || p->col_k <= 2 * p->col_s);
 #define NRSE_C0B(W, B, K) hipLaunchKernelGGL((conv0_bwd_kernel<W, B, K>), dim3(blocks), dim3(256), 0, st, *p)
+  if (conv0_bwd_mfma(p)) {
+    if (p->C == 512) hipLaunchKernelGGL((conv0_bwd_mfma_kernel<4, 8>), dim3(blocks), dim3(256), 0, st, *p);
+    else hipLaunchKernelGGL((conv0_bwd_mfma_kernel<4, 4>), dim3(blocks), dim3(256), 0, st, *p);
+  } else
   switch (p->C) {
     case 256:
       if (k10) { if (bf) NRSE_C0B(1, true, true); else NRSE_C0B(1, false, true); }

@@ -572,7 +572,8 @@ def conv0_bwd(wav, w, gamma, beta, mean, rstd, dy, dw, dgamma, dbeta, T0, k, s, 
     tap-major [k, C] copy, transposed into dw here)."""
     B, L = wav.shape
     C = w.shape[0]
-    dwT = torch.zeros(k, C, device=wav.device, dtype=torch.float32)
+    dwT = torch.empty(k, C, device=wav.device, dtype=torch.float32)
+    zero(dwT)   # nrse_zero: no ATen fill kernel in the step
     p = Conv0Params()
     p.wav, p.L, p.w, p.gamma, p.beta = ptr(wav), L, ptr(w), ptr(gamma), ptr(beta)
     p.mean, p.rstd = ptr(mean), ptr(rstd)

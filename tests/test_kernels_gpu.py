@@ -198,6 +198,45 @@ def test_conv0_bwd_col2im(nrse_device, C, ck, cs, dt):
     assert rel(dg, gr.grad) < 1e-5 and rel(db, br.grad) < 1e-5
 
 
+@pytest.mark.parametrize("C,mode", [(512, "col"), (256, "col"), (512, "direct")])
+def test_conv0_bwd_bf16_matrix_core(nrse_device, C, mode):
+    """The bf16 step's conv0 backward (matrix-core kernel: the conv recomputed by MFMA as the
+    forward computes it, dW as split-bf16 MFMAs over 16-row chunks, LN sums across 4 waves) against
+    float64 autograd, with the MFMA forward's mean / rstd as the step has them; a ragged last chunk."""
+    from nrse_amd import kernels as K
+    dev = nrse_device
+    B, L, k, s = 3, 4003, 10, 5
+    T0 = (L - k) // s + 1      # 799 rows per utterance: 2397 rows, the last 16-row chunk partial
+    wav = torch.randn(B, L, device=dev) * 0.3
+    w = torch.randn(C, 1, k, device=dev) * 0.3
+    g = torch.randn(C, device=dev) * 0.1 + 1; b = torch.randn(C, device=dev) * 0.1
+    out = torch.empty(B * T0, C, device=dev, dtype=torch.bfloat16)
+    mean = torch.empty(B * T0, device=dev); rstd = torch.empty_like(mean)
+    K.conv0_fwd(wav, w.view(C, k), g, b, out, mean, rstd, T0, k, s, 1e-5)
+    if mode == "col":
+        ck, cs = 3, 2
+        Tout = (T0 - ck) // cs + 1
+        dy = torch.randn(B * Tout, ck * C, device=dev).to(torch.bfloat16)
+        dyf = torch.zeros(B, T0, C, device=dev, dtype=torch.float64)
+        cv = dy.double().view(B, Tout, ck, C)
+        for j in range(ck):
+            dyf[:, j:j + cs * (Tout - 1) + 1:cs] += cv[:, :, j]
+        colspec = (ck, cs, Tout)
+    else:
+        dy = torch.randn(B * T0, C, device=dev).to(torch.bfloat16)
+        dyf = dy.double().view(B, T0, C)
+        colspec = None
+    wr = w.double().requires_grad_(True); gr = g.double().requires_grad_(True); br = b.double().requires_grad_(True)
+    ref = F.conv1d(wav.double()[:, None], wr, stride=s)
+    ref = F.gelu(F.layer_norm(ref.transpose(1, 2), (C,), gr, br, 1e-5))
+    ref.backward(dyf)
+    dw = torch.zeros(C, k, device=dev); dg = torch.zeros(C, device=dev); db = torch.zeros(C, device=dev)
+    K.conv0_bwd(wav, w.view(C, k), g, b, mean, rstd, dy, dw, dg, db, T0, k, s, colspec)
+    torch.cuda.synchronize()
+    assert rel(dw, wr.grad.view(C, k)) < 1e-4, rel(dw, wr.grad.view(C, k))
+    assert rel(dg, gr.grad) < 2e-5 and rel(db, br.grad) < 2e-5, (rel(dg, gr.grad), rel(db, br.grad))
+
+
 def test_weight_norm_fwd_bwd(nrse_device):
     from nrse_amd import kernels as K
     dev = nrse_device

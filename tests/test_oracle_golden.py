@@ -58,7 +58,15 @@ def _state(tag, arch):
     return z, layout, O.OracleState(layout, flat)
 
 
-@pytest.mark.parametrize("tag", ["tiny", "large", "large_3s", "large_12s"])
+# the WavLM-Large 8 s / 12 s pins take ~5-13 CPU-minutes each (one oracle train step of 317 M
+# weights): opt-in (NRSE_ORACLE_FULL=1) so the default CPU suite stays within minutes; the 3 s
+# pin of the same code path, the tiny ones and the 8 s split-weight check always run
+_FULL = os.environ.get("NRSE_ORACLE_FULL") == "1"
+_LONG = pytest.mark.skipif(not _FULL, reason="WavLM-Large 8 s / 12 s oracle pins: NRSE_ORACLE_FULL=1")
+_TAGS = ["tiny", pytest.param("large", marks=_LONG), "large_3s", pytest.param("large_12s", marks=_LONG)]
+
+
+@pytest.mark.parametrize("tag", _TAGS)
 def test_oracle_eval_forward(tag):
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     arch = (A.TINY if tag == "tiny" else A.LARGE).deterministic()
@@ -77,7 +85,7 @@ def test_oracle_eval_forward(tag):
         assert rel(h, z["eval_hidden"]) < 1e-5
 
 
-@pytest.mark.parametrize("tag", ["tiny", "large", "large_3s", "large_12s"])
+@pytest.mark.parametrize("tag", _TAGS)
 def test_oracle_train_step(tag):
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     arch = (A.TINY if tag == "tiny" else A.LARGE).deterministic()
