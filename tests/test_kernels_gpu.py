@@ -497,9 +497,10 @@ def test_gate_bwd_into_layernorm_bwd(nrse_device, xdt, B, T, H):
         K.ln_bwd(dy, h, g, mean, rstd, dx, resid=resid, dgamma=dg, dbeta=dbe, dv=dv, dv_colsum=dvc, dv_p=0.1,
                  dv_seed=3, **kw)
         outs.append((dx, dv.float(), dg, dbe, dvc, dW, db, dc))
-    # (dv is bf16: a last-bit difference of dx may flip its rounding)
+    # (dv is bf16: a last-bit difference of dx may flip its rounding; the gate parameter gradients
+    # dW / db / dc (5..7) are summed over rows by two different kernels, in different orders)
     for i, (a, b) in enumerate(zip(*outs)):
-        assert rel(a, b) < (1e-4 if i == 1 else 1e-6), (i, rel(a, b))
+        assert rel(a, b) < (1e-4 if i == 1 else (1e-5 if i >= 5 else 1e-6)), (i, rel(a, b))
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
