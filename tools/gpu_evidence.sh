@@ -14,5 +14,5 @@ bash tools/pmc_gemm.sh ${TAG} || exit 1
 timeout -k 10 400 python -u bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || { tail -30 gpurun_out/${TAG}_bench.err; exit 1; }
 python -c "import json; d=json.load(open('gpurun_out/${TAG}_bench.json')); print(d['value'], d['ms_per_step'], d['roofline'], d['cpu_baseline'])"
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-NRSE_SERIAL_TARGET=1 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_serial -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/${TAG}_serial.log 2>&1 || { tail -30 gpurun_out/${TAG}_serial.log; exit 1; }
+NRSE_SERIAL_TARGET=1 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_serial -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-north-star > gpurun_out/${TAG}_serial.log 2>&1 || { tail -30 gpurun_out/${TAG}_serial.log; exit 1; }
 python tools/prof_summary.py gpurun_out/${TAG}_serial/run_kernel_stats.csv 9 12
