@@ -1197,9 +1197,15 @@ class ByolEngine:
         st = self._opt_stream
         st.wait_stream(main)
         events = []
-        sh, tsh, slo, tlo = self.online_sh, self.target_sh, self.online_lo, self.target_lo
+        sh, tsh = self.online_sh, self.target_sh
         with torch.cuda.stream(st):
-            for s, e in self._segments:
+            for si, (s, e) in enumerate(self._segments):
+                # fp8 form: the encoder layers' GEMMs read the fp8 correction planes, never the bf16
+                # lo plane, so the pure layer segments (1 .. L-1) skip its writes (2 B per weight
+                # for each network)
+                layer_only = o8 is not None and 1 <= si < len(self._segments) - 1
+                slo = None if layer_only else self.online_lo
+                tlo = None if layer_only else self.target_lo
                 if e > s:
                     te = min(e, ne)
                     fuse = _FUSED_EMA and te > s
