@@ -285,7 +285,7 @@ def main():
         # fused_zero_grad: the AdamW pass clears the gradient for the next step (no fill kernel)
         eng = ByolEngine(arch, 1024, 2048, device=dev, compute_dtype=cdt, seed=1234, weight_split=wsplit,
                          step_cfg=StepConfig(ema_decay=0.997, overlap_optimizer=not args.serial_optimizer,
-                                             fused_zero_grad=True))
+                                             fused_zero_grad=os.environ.get("NRSE_FUSED_ZERO_GRAD", "1") != "0"))
         return eng, cdt
 
     def make_step(eng):
