@@ -897,8 +897,20 @@ int tile_rows_setting() {
   return g_tile_rows;
 }
 
+// per-orientation overrides for step-level tuning: NRSE_GEMM_BM_FWD (A and B k-contiguous: the
+// forward linears and convs), NRSE_GEMM_BM_DGRAD, NRSE_GEMM_BM_WGRAD (256, 224 or 0 = automatic);
+// unset: the process setting above
+int orient_rows(const nrse_gemm_params* p) {
+  static int v[3] = {-2, -2, -2};
+  static const char* names[3] = {"NRSE_GEMM_BM_FWD", "NRSE_GEMM_BM_DGRAD", "NRSE_GEMM_BM_WGRAD"};
+  const int o = (p->a.kcontig && p->b.kcontig) ? 0 : (p->a.kcontig ? 1 : 2);
+  if (v[o] == -2) v[o] = getenv(names[o]) ? atoi(getenv(names[o])) : -1;
+  return v[o];
+}
+
 int bm_choice(const nrse_gemm_params* p) {
-  const int pinned = tile_rows_setting();
+  const int ov = orient_rows(p);
+  const int pinned = ov >= 0 ? ov : tile_rows_setting();
   if (pinned == 256 || pinned == 224) return pinned;
   const long long per = (long long)nrse_cdiv(p->N, BN) * p->batch * p->splits;
   const long long w256 = (nrse_cdiv(p->M, 256) * per + 255) / 256;
