@@ -219,6 +219,18 @@ NRSE_DEV i32x8v frag_mx(const char* lds, int base, int lane) {
   return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
+// MXFP6 operand of the 32x32x64 shape (F8 == 3): lane (h, r) = (lane >> 5, lane & 31) reads row
+// base + r's block 2s + h of the 128-k K-tile (k = 64s + 32h .. +31): chunks 2(2s+h), 2(2s+h)+1,
+// the same 32-byte block reads as frag_mx, 32 rows deep instead of 16
+NRSE_DEV i32x8v frag_mx32(const char* lds, int base, int s, int lane) {
+  const int h = lane >> 5, row = base + (lane & 31), sw = (row >> 1) & 7, c = 2 * (2 * s + h);
+  const char* r = lds + row * 128;
+  const i32x4v a = *reinterpret_cast<const i32x4v*>(r + ((c ^ sw) << 4));
+  const i32x4v b = *reinterpret_cast<const i32x4v*>(r + (((c + 1) ^ sw) << 4));
+  return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
 // ------------------------------------------------------------------ register epilogue
 // The common epilogues of the step run with their flags fixed at compile time: the lane's
 // accumulator values are finished in registers -- bias, GELU (+ bf16 pre-activation to aux),
@@ -425,11 +437,12 @@ NRSE_DEV void fast_epilogue(const nrse_gemm_params& p, const f32x4 (&acc)[8][4],
 // 228 of the 256 CUs per N-column of tiles instead of 200; nrse_gemm256 picks the one that
 // needs fewer tile waves, see bm_choice)
 // F8: the split-weight mode's correction segments follow the bf16 K-tiles: 1 fp8 (ABI 6), 2 MXFP6
-// (ABI 8)
+// (ABI 8); 3 MXFP6 on the 32x32x64 MFMA shape, the correction K-tiles first (BMT 256 only)
 template <bool AKC, bool BKC, int BMT, int F8>
 __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params p, int mt, int nt) {
   static_assert(BMT == 256 || BMT == 224, "tile rows");
   static_assert(!F8 || (AKC && BKC), "fp8 correction segments: k-contiguous operands");
+  static_assert(F8 != 3 || BMT == 256, "the 32x32 correction blocks tile 256-row tiles");
   constexpr int NFI_HI = (BMT / 2 - 64) / 16;  // 16-row blocks in an M-wave's high half: 4 or 3
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
   const int tid = threadIdx.x;
@@ -494,6 +507,11 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
     return q;
   };
   auto tile_pos = [&](int t) {
+    if constexpr (F8 == 3) {  // correction K-tiles first
+      const int n8 = ntiles - n16;
+      if (t < n8) return tile_pos_at(true, t / tps8, t % tps8, true);
+      return tile_pos_at(t < ntiles, (t - n8) / tps, (t - n8) % tps, false);
+    }
     if (F8 && t >= n16) return tile_pos_at(t < ntiles, (t - n16) / tps8, (t - n16) % tps8, true);
     return tile_pos_at(t < ntiles, t / tps, t % tps, false);
   };
@@ -534,11 +552,13 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
     }
   }
 
-  f32x4 acc[8][4];
+  f32x4 acc[8][4];  // F8 == 3: assigned from the 32x32 accumulators after the correction tiles
+  if constexpr (F8 != 3) {
 #pragma unroll
-  for (int a = 0; a < 8; ++a)
+    for (int a = 0; a < 8; ++a)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
 
   // prologue: K-tiles 0 and 1 (half-tile sequence numbers 0..7, slot = seq % 10), then wait for
   // the three read in phase 0 (A-lo, B-lo, B-hi; 5 younger half-tiles = 10 DMAs may stay in flight)
@@ -629,6 +649,145 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
     NRSE_PSTAMP(3);
     base = wrap(base + 4);
   }
+  } else if constexpr (F8 == 3) {
+  // MXFP6 correction on the 32x32x64 shape (e2m3 there runs at ~1.8x its 16x16x128 rate,
+  // tools/probe_mx_rate.hip). The correction K-tiles run FIRST, into one 32x32 accumulator per
+  // 32-row x 32-column block of the wave's 128 x 64 output (c32[MH*4 + NH*2 + bi]: M-half MH,
+  // N-half NH, 32-row block bi), which are then permuted in registers into the 16x16 layout that
+  // the bf16 K-tiles and the epilogue use. Same ring, phases, waits and hand-off rules as above;
+  // per phase 8 MFMAs of 32x32x64 (two k-steps of 64 per 128-k K-tile) instead of 16 of 16x16x128.
+  f32x16 c32[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) c32[i][e] = 0.f;
+  i32x8v fa32[2][2], fl32[2], fh32[2];
+#define NRSE_READ_A32(SLOT)                                                              \
+  _Pragma("unroll") for (int bi = 0; bi < 2; ++bi)                                     \
+  _Pragma("unroll") for (int s = 0; s < 2; ++s)                                        \
+    fa32[bi][s] = frag_mx32(smem + (SLOT) * HALF, wm * 64 + 32 * bi, s, lane);
+#define NRSE_READ_B32(SLOT, FB)                                                          \
+  _Pragma("unroll") for (int s = 0; s < 2; ++s)                                        \
+    FB[s] = frag_mx32(smem + (SLOT) * HALF, wn * 32, s, lane);
+#define NRSE_QUAD32(MH, NH, FB)                                                          \
+  __builtin_amdgcn_s_setprio(1);                                                         \
+  _Pragma("unroll") for (int s = 0; s < 2; ++s)                                        \
+  _Pragma("unroll") for (int bi = 0; bi < 2; ++bi)                                     \
+    c32[(MH) * 4 + (NH) * 2 + bi] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(     \
+        FB[s], fa32[bi][s], c32[(MH) * 4 + (NH) * 2 + bi], 2, 2, 0, FB[s][6], 0, fa32[bi][s][6]); \
+  __builtin_amdgcn_s_setprio(0);
+#define NRSE_BAR8()                          \
+  do {                                       \
+    __builtin_amdgcn_sched_barrier(0);       \
+    NRSE_BAR();                              \
+    __builtin_amdgcn_sched_barrier(0);       \
+  } while (0)
+  const int n8 = ntiles - n16;
+  // staging cursors: correction tile t+2 while t+2 < n8, then bf16 tiles from index max(0, 2 - n8)
+  int v_sg = 2 / tps8, v_k = 2 % tps8;
+  const int b0 = n8 >= 2 ? 0 : 2 - n8;
+  int u_sg = b0 / tps, u_k = b0 % tps;
+  auto ktile32 = [&](int t, auto stage8) {
+    constexpr bool S8 = decltype(stage8)::value;
+    const int s0 = base, s1 = wrap(base + 1), s2 = wrap(base + 2), s3 = wrap(base + 3);
+    TilePos q2;
+    if constexpr (S8) {
+      q2.live = true;
+      q2.sa = ld8_soff(la8, v_sg, v_k);
+      q2.sb = ld8_soff(lb8, v_sg, v_k);
+      if (++v_k == tps8) { v_k = 0; ++v_sg; }
+    } else {
+      q2 = tile_pos_at(t + 2 < ntiles, u_sg, u_k, false);
+      if (++u_k == tps) { u_k = 0; ++u_sg; }
+    }
+    auto stg = [&](int j, int slot) {
+      if constexpr (S8) {
+        char* dst = smem + slot * HALF;
+        if (j == 0) ld8_issue(la8, la, dst, wave, 0, q2.sa);
+        else if (j == 1) ld8_issue(lb8, lb, dst, wave, 0, q2.sb);
+        else if (j == 2) ld8_issue(lb8, lb, dst, wave, 1, q2.sb);
+        else ld8_issue(la8, la, dst, wave, 1, q2.sa);
+      } else {
+        stage(j, q2, slot);
+      }
+    };
+    NRSE_READ_A32(s0)
+    NRSE_READ_B32(s1, fl32)
+    NRSE_READ_B32(s2, fh32)
+    stg(0, wrap(base + 8));
+    stg(1, wrap(base + 9));
+    NRSE_WAIT(12);
+    NRSE_BAR8();
+    NRSE_QUAD32(0, 0, fl32)
+    NRSE_QUAD32(0, 1, fh32)
+    NRSE_BAR8();
+    NRSE_READ_A32(s3)
+    stg(2, base);
+    stg(3, s1);
+    NRSE_WAIT(10);
+    NRSE_BAR8();
+    NRSE_QUAD32(1, 1, fh32)
+    NRSE_QUAD32(1, 0, fl32)
+    NRSE_BAR8();
+    base = wrap(base + 4);
+  };
+  int t = 0;
+  const int n8a = n8 >= 2 ? n8 - 2 : 0;
+#pragma unroll 1
+  for (; t < n8a; ++t) ktile32(t, std::true_type{});
+#pragma unroll 1
+  for (; t < n8; ++t) ktile32(t, std::false_type{});
+  // 32x32 -> 16x16: lane l of block (MH, NH, bi) holds row l % 32, columns 8j + 4(l / 32) + r in
+  // register 4j + r; the 16x16 blocks [2bi + a][2NH + fj] want row 16a + (l % 16), columns 16fj +
+  // 4(l / 16) + r. For each (fj, r) the register pair X0 = c[8fj + r], X1 = c[8fj + 4 + r] (16-lane
+  // rows q0..q3) must become [X0.q0, X0.q2, X1.q0, X1.q2] (a = 0) and [X0.q1, X0.q3, X1.q1, X1.q3]
+  // (a = 1): a permlane32 swap (X0's upper half <-> X1's lower) then a permlane16 swap (odd rows
+  // of the first <-> even rows of the second), in place.
+#pragma unroll
+  for (int blk = 0; blk < 8; ++blk) {
+    const int mh = blk >> 2, nh = (blk >> 1) & 1, bi = blk & 1;
+#pragma unroll
+    for (int fj = 0; fj < 2; ++fj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const auto w = __builtin_amdgcn_permlane32_swap(__float_as_uint(c32[blk][8 * fj + r]),
+                                                        __float_as_uint(c32[blk][8 * fj + 4 + r]), false, false);
+        const auto v = __builtin_amdgcn_permlane16_swap(w[0], w[1], false, false);
+        acc[mh * 4 + 2 * bi][nh * 2 + fj][r] = __uint_as_float(v[0]);
+        acc[mh * 4 + 2 * bi + 1][nh * 2 + fj][r] = __uint_as_float(v[1]);
+      }
+  }
+  // the bf16 K-tiles (t + 2 staged as bf16 or dead)
+  auto ktileb = [&](int t) {
+    const int s0 = base, s1 = wrap(base + 1), s2 = wrap(base + 2), s3 = wrap(base + 3);
+    const TilePos q2 = tile_pos_at(t + 2 < ntiles, u_sg, u_k, false);
+    if (++u_k == tps) { u_k = 0; ++u_sg; }
+    NRSE_READ_A(s0, 4)
+    NRSE_READ_B(s1, fbl)
+    NRSE_READ_B(s2, fbh)
+    stage(0, q2, wrap(base + 8));
+    stage(1, q2, wrap(base + 9));
+    NRSE_WAIT(12);
+    NRSE_BAR8();
+    NRSE_QUAD(0, 0, fbl)
+    NRSE_QUAD(0, 1, fbh)
+    NRSE_BAR8();
+    NRSE_READ_A(s3, 4)
+    stage(2, q2, base);
+    stage(3, q2, s1);
+    NRSE_WAIT(10);
+    NRSE_BAR8();
+    NRSE_QUAD(1, 1, fbh)
+    NRSE_QUAD(1, 0, fbl)
+    NRSE_BAR8();
+    base = wrap(base + 4);
+  };
+#pragma unroll 1
+  for (; t < ntiles; ++t) ktileb(t);
+#undef NRSE_READ_A32
+#undef NRSE_READ_B32
+#undef NRSE_QUAD32
+#undef NRSE_BAR8
   } else {
   // The same schedule with the fp8 correction K-tiles after the bf16 ones (ABI 6). The fragments
   // are held as 8-register tuples (both k-substeps of a bf16 K-tile = one fp8 MFMA operand); a
@@ -920,13 +1079,21 @@ int bm_choice(const nrse_gemm_params* p) {
 
 template <bool AKC, bool BKC, int F8 = 0>
 int launch(const nrse_gemm_params* p, hipStream_t st) {
+  if constexpr (F8 == 3) {
+    const int mt = nrse_cdiv(p->M, 256), nt = nrse_cdiv(p->N, BN);
+    const long long total = (long long)mt * nt * p->batch * p->splits;
+    hipLaunchKernelGGL((gemm256_kernel<AKC, BKC, 256, 3>), dim3((unsigned)total), dim3(NTHR), 0, st, *p, mt, nt);
+    return nrse_check_launch("nrse_gemm(256)");
+  }
   const int bm = bm_choice(p);
   const int mt = nrse_cdiv(p->M, bm), nt = nrse_cdiv(p->N, BN);
   const long long total = (long long)mt * nt * p->batch * p->splits;
-  if (bm == 224)
-    hipLaunchKernelGGL((gemm256_kernel<AKC, BKC, 224, F8>), dim3((unsigned)total), dim3(NTHR), 0, st, *p, mt, nt);
-  else
-    hipLaunchKernelGGL((gemm256_kernel<AKC, BKC, 256, F8>), dim3((unsigned)total), dim3(NTHR), 0, st, *p, mt, nt);
+  if constexpr (F8 != 3) {
+    if (bm == 224)
+      hipLaunchKernelGGL((gemm256_kernel<AKC, BKC, 224, F8>), dim3((unsigned)total), dim3(NTHR), 0, st, *p, mt, nt);
+    else
+      hipLaunchKernelGGL((gemm256_kernel<AKC, BKC, 256, F8>), dim3((unsigned)total), dim3(NTHR), 0, st, *p, mt, nt);
+  }
   return nrse_check_launch("nrse_gemm(256)");
 }
 
@@ -972,8 +1139,18 @@ bool nrse_gemm256_f8_ok(const nrse_gemm_params* p) {
          spb < (1LL << 31) && p->b8_exp > -127 && p->b8_exp < 127;
 }
 
+// MXFP6 segments on the 32x32x64 shape unless NRSE_MX6_SHAPE=16 (the 16x16x128 form, F8 = 2)
+static bool mx6_wide() {
+  static int v = -1;
+  if (v < 0) v = (getenv("NRSE_MX6_SHAPE") && atoi(getenv("NRSE_MX6_SHAPE")) == 16) ? 0 : 1;
+  return v == 1;
+}
+
 int nrse_gemm256(const nrse_gemm_params* p, hipStream_t st) {
-  if (p->nseg8 > 0) return p->a8.dtype == NRSE_MX6 ? launch<true, true, 2>(p, st) : launch<true, true, 1>(p, st);
+  if (p->nseg8 > 0) {
+    if (p->a8.dtype != NRSE_MX6) return launch<true, true, 1>(p, st);
+    return mx6_wide() ? launch<true, true, 3>(p, st) : launch<true, true, 2>(p, st);
+  }
   if (p->a.kcontig && p->b.kcontig) return launch<true, true>(p, st);
   if (p->a.kcontig && !p->b.kcontig) return launch<true, false>(p, st);
   if (!p->a.kcontig && p->b.kcontig) return launch<false, true>(p, st);
