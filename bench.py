@@ -327,7 +327,7 @@ def main():
         E._SERIAL_TARGET, eng.cfg.overlap_optimizer = serial_prev, overlap_prev
         s_gflops = sum(f for f, _, _, _ in sprobe)
         s_ms = sum(e0.elapsed_time(e1) for _, e0, e1, _ in sprobe)
-        return dict(gflops=s_gflops, ms=s_ms, bytes=sum(sbytes), launches=len(sprobe), step_ms=sdt_ms)
+        return dict(gflops=s_gflops, ms=s_ms, bytes=sum(sbytes), launches=len(sprobe), step_ms=sdt_ms, probe=sprobe)
 
     def timed(eng, step):
         """W untimed warm-up steps, then EXACTLY K steps bracketed by a barrier + device sync on both
@@ -400,14 +400,18 @@ def main():
     n_launch = len(probe)
     achieved_tfs = gflops / (gms * 1e-3) / 1e12 if gms > 0 else 0.0
     if args.detail and rank == 0:
-        per = {}
-        for f, e0, e1, shp in probe:
-            k = str(shp)
-            d = per.setdefault(k, [0.0, 0.0, 0])
-            d[0] += f; d[1] += e0.elapsed_time(e1); d[2] += 1
+        # per GEMM shape: the in-step (overlapped) and the serial-probe durations
+        out = {}
+        for tag, pr in (("in_step", probe), ("serial", sp["probe"])):
+            per = {}
+            for f, e0, e1, shp in pr:
+                k = str(shp)
+                d = per.setdefault(k, [0.0, 0.0, 0])
+                d[0] += f; d[1] += e0.elapsed_time(e1); d[2] += 1
+            out[tag] = {k: {"tflops": v[0] / (v[1] * 1e-3) / 1e12, "ms_total": v[1], "launches": v[2]}
+                        for k, v in sorted(per.items(), key=lambda kv: -kv[1][1])}
         with open(args.detail, "w") as fh:
-            json.dump({k: {"tflops": v[0] / (v[1] * 1e-3) / 1e12, "ms_total": v[1], "launches": v[2]}
-                       for k, v in sorted(per.items(), key=lambda kv: -kv[1][1])}, fh, indent=1)
+            json.dump(out, fh, indent=1)
     avg_exec = (executed[0] / args.steps, executed[1] / args.steps)
     if varlen_batches is None:
         fpp, _ = flops_per_pair(arch, L, avg_exec)

@@ -299,8 +299,44 @@ NRSE_DEV void fast_epilogue(const nrse_gemm_params& p, const f32x4 (&acc)[8][4],
   for (int fn = 0; fn < 4; ++fn) {
     bias4[fn][0] = bpre[fn].x; bias4[fn][1] = bpre[fn].y; bias4[fn][2] = bpre[fn].z; bias4[fn][3] = bpre[fn].w;
   }
+  // The residual (RESID) and pre-activation (GELUB) operands of a pass are loaded as one batch of
+  // branch-free buffer loads before its math (elements past M / N read zeros): loaded per element
+  // group behind an `if (ok)`, each load sat in its own basic block and the pass waited for the
+  // memory latency 16 times (s_waitcnt vmcnt(0) after every load; the out-projection's epilogue
+  // was then longer than its main loop)
+  __amdgpu_buffer_rsrc_t rrs, ars;
+  if constexpr (RESID)
+    rrs = make_rsrc(reinterpret_cast<const char*>((const float*)p.resid + epi.rbase + (long long)m0 * p.ldr + n0));
+  if constexpr (GELUB)
+    ars = make_rsrc(reinterpret_cast<const char*>((const bf16_t*)p.aux + epi.abase + (long long)m0 * p.ldaux + n0));
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
+    float4 rpre[4][4];
+    uint2 apre[4][4];
+    if constexpr (RESID || GELUB) {
+#pragma unroll
+      for (int fi = 0; fi < 4; ++fi) {
+        if (pass == 1 && fi >= NFI_HI) continue;
+        const int trow = wm * (BMT / 2) + pass * 64 + fi * 16 + li;
+        const bool mok = m0 + trow < p.M;
+#pragma unroll
+        for (int fn = 0; fn < 4; ++fn) {
+          const int tcol = wn * 64 + fn * 16 + 4 * g;
+          const bool ok = mok && n0 + tcol < p.N;
+          if constexpr (RESID) {
+            const unsigned off = ok ? (unsigned)((trow * p.ldr + tcol) * 4) : OOB;
+            const auto r = __builtin_amdgcn_raw_buffer_load_b128(rrs, off, 0, 0);
+            rpre[fi][fn] = make_float4(__uint_as_float(r[0]), __uint_as_float(r[1]), __uint_as_float(r[2]),
+                                       __uint_as_float(r[3]));
+          }
+          if constexpr (GELUB) {
+            const unsigned off = ok ? (unsigned)((trow * p.ldaux + tcol) * 2) : OOB;
+            const auto r = __builtin_amdgcn_raw_buffer_load_b64(ars, off, 0, 0);
+            apre[fi][fn] = make_uint2(r[0], r[1]);
+          }
+        }
+      }
+    }
 #pragma unroll
     for (int fi = 0; fi < 4; ++fi) {
       if (pass == 1 && fi >= NFI_HI) continue;
@@ -330,8 +366,7 @@ NRSE_DEV void fast_epilogue(const nrse_gemm_params& p, const f32x4 (&acc)[8][4],
           }
         }
         if constexpr (GELUB) {
-          uint2 u = make_uint2(0, 0);
-          if (ok) u = *reinterpret_cast<const uint2*>((const bf16_t*)p.aux + epi.abase + (long long)m * p.ldaux + n);
+          const uint2 u = apre[fi][fn];
           v[0] *= gelu_grad_fast(__uint_as_float(u.x << 16));
           v[1] *= gelu_grad_fast(__uint_as_float(u.x & 0xffff0000u));
           v[2] *= gelu_grad_fast(__uint_as_float(u.y << 16));
@@ -344,8 +379,7 @@ NRSE_DEV void fast_epilogue(const nrse_gemm_params& p, const f32x4 (&acc)[8][4],
           }
         }
         if constexpr (RESID) {
-          float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (ok) r = *reinterpret_cast<const float4*>((const float*)p.resid + epi.rbase + (long long)m * p.ldr + n);
+          const float4 r = rpre[fi][fn];
           v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
         }
         if constexpr (DROP) {

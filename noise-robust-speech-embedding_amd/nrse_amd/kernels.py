@@ -174,8 +174,12 @@ def gemm(A: Operand, B: Operand, C: torch.Tensor, M: int, N: int, K: int, *, ldc
         # MXFP6 one at four times, so their FLOPs count 1/2 or 1/4 against the bf16 dense peak
         w8 = (0.25 if a8.t.dtype == MX6 else 0.5) if nseg8 else 0.0
         tag = ("mx6" if a8.t.dtype == MX6 else "fp8") if nseg8 else ""
+        # shape key: M, N, K, batch (+ the correction form), the operand orientation (T: k-contiguous)
+        # and the epilogue flags and split count (bench.py --detail)
+        orient = ("T" if A.kcontig else "N") + ("T" if B.kcontig else "N") + f"/f{flags}/s{splits}"
         probe.append((2.0 * M * N * K * (nseg * splits + w8 * nseg8) * batch, e0, e1,
-                      (M, N, K * nseg * splits, batch) if not nseg8 else (M, N, K * nseg, batch, f"{tag}x{nseg8}")))
+                      (M, N, K * nseg * splits, batch, orient) if not nseg8
+                      else (M, N, K * nseg, batch, f"{tag}x{nseg8}", orient)))
 
 
 # When set to a list, every nrse_gemm launch appends (algorithmic FLOPs, start event, end event,
