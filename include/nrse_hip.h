@@ -428,6 +428,18 @@ int nrse_splitk_reduce(float* dst, const float* slabs, int splits, long long n, 
  * b < batch (16-byte vectors when every n_j % 4 == 0 and the pointers are aligned). */
 int nrse_rows_reduce(float* d0, long long n0, float* d1, long long n1, float* d2, long long n2, const float* slab, int S,
                      int batch, int accumulate, void* stream);
+/* ABI 9: deferred reductions. nrse_reduce_defer(1) makes every later nrse_rows_reduce -- including
+ * the ones the LayerNorm / attention / gate backward, GEMM column-sum and colsum entry points end
+ * with -- queue its reduction (up to 256) instead of launching it; nrse_reduce_flush(stream) runs
+ * the queue on `stream` (batched, up to 12 reductions per launch, bitwise the sums of the
+ * immediate form) and empties it. The caller keeps each queued slab and destination alive and
+ * unchanged until the flush's work has run on that stream (the step's backward queues a layer's
+ * reductions on the dX chain's stream and flushes them on the weight-gradient stream:
+ * engine.py encoder_backward). Returns the previous setting; process-wide, not thread-safe
+ * (one engine per process). Replaces nothing in the reference (its reductions are ATen's). */
+int nrse_reduce_defer(int on);
+int nrse_reduce_pending(void);
+int nrse_reduce_flush(void* stream);
 /* dst[a][c][b] (+)= src[a][b][c]  (conv weight [co][ci][k] <-> implicit-GEMM layout [co][k][ci]) */
 int nrse_swap12(const void* src, int src_dtype, void* dst, int dst_dtype, int d0, int d1, int d2, int accumulate,
                 void* stream);

@@ -5,6 +5,7 @@
 //   bias gradients         column sums of the output gradients of every nn.Linear
 #include <algorithm>
 
+#include <cstdlib>
 #include "common.h"
 
 namespace {
@@ -611,15 +612,16 @@ struct RowsDst { float* d[3]; long long n[3]; };
 
 // RG row groups x (1024 / RG) column quads per workgroup: RG = 16 (256 columns) by default; RG =
 // 64 (64 columns) when that grid would leave most CUs idle (r04: the encoder LayerNorm's 512
-// partial rows x 3072 columns ran on 12 workgroups at ~1 TB/s)
+// partial rows x 3072 columns ran on 12 workgroups at ~1 TB/s). The bodies are device functions
+// of the workgroup's (column block bx, row group by) so that the batched form below runs them
+// unchanged (bitwise the same sums).
 template <int RG>
-__global__ __launch_bounds__(1024) void rows_reduce_kernel(RowsDst dst, const float* __restrict__ slab, int S,
-                                                           long long n, int acc) {
+NRSE_DEV void rows_reduce_body(float4 (*red)[1024 / RG], const RowsDst& dst, const float* __restrict__ slab, int S,
+                               long long n, int acc, long long bx, int by) {
   constexpr int NQ = 1024 / RG;
-  __shared__ float4 red[RG][NQ];
   const int q = threadIdx.x % NQ, r = threadIdx.x / NQ;
-  const long long col = (long long)blockIdx.x * (4 * NQ) + 4 * q;
-  const float* sl = slab + (long long)blockIdx.y * S * n;
+  const long long col = bx * (4 * NQ) + 4 * q;
+  const float* sl = slab + (long long)by * S * n;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   if (col < n) {
     int k = r;
@@ -644,7 +646,7 @@ __global__ __launch_bounds__(1024) void rows_reduce_kernel(RowsDst dst, const fl
     int j = 0;
     long long c = col;
     while (j < 2 && c >= dst.n[j]) { c -= dst.n[j]; ++j; }
-    float* d = dst.d[j] + (long long)blockIdx.y * dst.n[j] + c;
+    float* d = dst.d[j] + (long long)by * dst.n[j] + c;
     if (acc) {
       const float4 o = *reinterpret_cast<const float4*>(d);
       t.x += o.x; t.y += o.y; t.z += o.z; t.w += o.w;
@@ -654,12 +656,11 @@ __global__ __launch_bounds__(1024) void rows_reduce_kernel(RowsDst dst, const fl
 }
 
 // the same with one column per thread (lengths that are not multiples of 4, unaligned vectors)
-__global__ __launch_bounds__(1024) void rows_reduce1_kernel(RowsDst dst, const float* __restrict__ slab, int S,
-                                                            long long n, int acc) {
-  __shared__ float red[16][64];
+NRSE_DEV void rows_reduce1_body(float (*red)[64], const RowsDst& dst, const float* __restrict__ slab, int S,
+                                long long n, int acc, long long bx, int by) {
   const int q = threadIdx.x & 63, r = threadIdx.x >> 6;
-  const long long col = (long long)blockIdx.x * 64 + q;
-  const float* sl = slab + (long long)blockIdx.y * S * n;
+  const long long col = bx * 64 + q;
+  const float* sl = slab + (long long)by * S * n;
   float s = 0.f;
   if (col < n) {
     int k = r;
@@ -681,30 +682,136 @@ __global__ __launch_bounds__(1024) void rows_reduce1_kernel(RowsDst dst, const f
     int j = 0;
     long long c = col;
     while (j < 2 && c >= dst.n[j]) { c -= dst.n[j]; ++j; }
-    float* d = dst.d[j] + (long long)blockIdx.y * dst.n[j] + c;
+    float* d = dst.d[j] + (long long)by * dst.n[j] + c;
     *d = acc ? *d + t : t;
   }
+}
+
+template <int RG>
+__global__ __launch_bounds__(1024) void rows_reduce_kernel(RowsDst dst, const float* __restrict__ slab, int S,
+                                                           long long n, int acc) {
+  __shared__ float4 red[RG][1024 / RG];
+  rows_reduce_body<RG>(red, dst, slab, S, n, acc, blockIdx.x, blockIdx.y);
+}
+
+__global__ __launch_bounds__(1024) void rows_reduce1_kernel(RowsDst dst, const float* __restrict__ slab, int S,
+                                                            long long n, int acc) {
+  __shared__ float red[16][64];
+  rows_reduce1_body(red, dst, slab, S, n, acc, blockIdx.x, blockIdx.y);
+}
+
+// One reduction as nrse_rows_reduce launches it: the form (0: RG 16, 1: RG 64, 2: one column per
+// thread) and its grid (gx column blocks x batch row groups).
+struct RowsJob {
+  RowsDst dst;
+  const float* slab;
+  long long n;
+  int S, batch, acc, form, gx;
+};
+
+static RowsJob rows_job(float* d0, long long n0, float* d1, long long n1, float* d2, long long n2, const float* slab, int S,
+                 int batch, int accumulate) {
+  auto al16 = [](const void* x) { return ((uintptr_t)x & 15) == 0; };
+  RowsJob j;
+  j.dst.d[0] = d0; j.dst.d[1] = d1; j.dst.d[2] = d2;
+  j.dst.n[0] = n0; j.dst.n[1] = d1 ? n1 : 0; j.dst.n[2] = d2 ? n2 : 0;
+  j.n = j.dst.n[0] + j.dst.n[1] + j.dst.n[2];
+  j.slab = slab; j.S = S; j.batch = batch; j.acc = accumulate;
+  const bool vec = n0 % 4 == 0 && j.dst.n[1] % 4 == 0 && j.dst.n[2] % 4 == 0 && al16(d0) && (!d1 || al16(d1)) &&
+                   (!d2 || al16(d2)) && al16(slab);
+  if (vec && S >= 128 && ((j.n + 255) / 256) * batch < 128) { j.form = 1; j.gx = (int)((j.n + 63) / 64); }
+  else if (vec) { j.form = 0; j.gx = (int)((j.n + 255) / 256); }
+  else { j.form = 2; j.gx = (int)((j.n + 63) / 64); }
+  return j;
+}
+
+// ABI 9: deferred reductions. While deferral is on, every nrse_rows_reduce (the gradient
+// reductions the LayerNorm, attention, gate, GEMM column-sum and colsum entry points end with) is
+// queued instead of launched; nrse_reduce_flush then runs the queue as batched launches of up to
+// RJ_MAX jobs each, on the stream it is given. The step's backward queues one transformer layer's
+// reductions on the dX chain's stream and flushes them on the weight-gradient stream, so the
+// ~6 small launches per layer leave the critical stream (each job's arithmetic is the
+// single-launch form's: the sums are bitwise the same).
+constexpr int RJ_MAX = 12;
+struct RowsJobs {
+  RowsJob j[RJ_MAX];
+  int begin[RJ_MAX + 1];  // first flat workgroup of job i
+  int count;
+};
+
+__global__ __launch_bounds__(1024) void rows_reduce_multi_kernel(const RowsJobs jobs) {
+  __shared__ __attribute__((aligned(16))) float4 red[1024];
+  int i = 0;
+  while (i + 1 < jobs.count && (int)blockIdx.x >= jobs.begin[i + 1]) ++i;
+  const RowsJob& j = jobs.j[i];
+  const int local = (int)blockIdx.x - jobs.begin[i];
+  const int bx = local % j.gx, by = local / j.gx;
+  if (j.form == 0) rows_reduce_body<16>(reinterpret_cast<float4(*)[64]>(red), j.dst, j.slab, j.S, j.n, j.acc, bx, by);
+  else if (j.form == 1) rows_reduce_body<64>(reinterpret_cast<float4(*)[16]>(red), j.dst, j.slab, j.S, j.n, j.acc, bx, by);
+  else rows_reduce1_body(reinterpret_cast<float(*)[64]>(red), j.dst, j.slab, j.S, j.n, j.acc, bx, by);
+}
+
+struct DeferQueue {
+  bool on = false;
+  int count = 0;
+  RowsJob q[256];
+};
+static DeferQueue g_defer;
+
+static int launch_job(const RowsJob& j, hipStream_t st) {
+  const dim3 grid((unsigned)j.gx, (unsigned)j.batch);
+  if (j.form == 1) hipLaunchKernelGGL(rows_reduce_kernel<64>, grid, dim3(1024), 0, st, j.dst, j.slab, j.S, j.n, j.acc);
+  else if (j.form == 0) hipLaunchKernelGGL(rows_reduce_kernel<16>, grid, dim3(1024), 0, st, j.dst, j.slab, j.S, j.n, j.acc);
+  else hipLaunchKernelGGL(rows_reduce1_kernel, grid, dim3(1024), 0, st, j.dst, j.slab, j.S, j.n, j.acc);
+  return nrse_check_launch("nrse_rows_reduce");
 }
 
 extern "C" int nrse_rows_reduce(float* d0, long long n0, float* d1, long long n1, float* d2, long long n2,
                                 const float* slab, int S, int batch, int accumulate, void* stream) {
   NRSE_REQUIRE(d0 && n0 > 0 && slab && S >= 1 && batch >= 1, "nrse_rows_reduce: bad args");
   NRSE_REQUIRE((!d1 || n1 > 0) && (!d2 || (d1 && n2 > 0)), "nrse_rows_reduce: destinations d0[, d1[, d2]] in order");
-  auto al16 = [](const void* x) { return ((uintptr_t)x & 15) == 0; };
-  RowsDst dst;
-  dst.d[0] = d0; dst.d[1] = d1; dst.d[2] = d2;
-  dst.n[0] = n0; dst.n[1] = d1 ? n1 : 0; dst.n[2] = d2 ? n2 : 0;
-  const long long n = dst.n[0] + dst.n[1] + dst.n[2];
-  const bool vec = n0 % 4 == 0 && dst.n[1] % 4 == 0 && dst.n[2] % 4 == 0 && al16(d0) && (!d1 || al16(d1)) &&
-                   (!d2 || al16(d2)) && al16(slab);
-  if (vec && S >= 128 && ((n + 255) / 256) * batch < 128)
-    hipLaunchKernelGGL(rows_reduce_kernel<64>, dim3((unsigned)((n + 63) / 64), (unsigned)batch), dim3(1024), 0,
-                       (hipStream_t)stream, dst, slab, S, n, accumulate);
-  else if (vec)
-    hipLaunchKernelGGL(rows_reduce_kernel<16>, dim3((unsigned)((n + 255) / 256), (unsigned)batch), dim3(1024), 0,
-                       (hipStream_t)stream, dst, slab, S, n, accumulate);
-  else
-    hipLaunchKernelGGL(rows_reduce1_kernel, dim3((unsigned)((n + 63) / 64), (unsigned)batch), dim3(1024), 0,
-                       (hipStream_t)stream, dst, slab, S, n, accumulate);
-  return nrse_check_launch("nrse_rows_reduce");
+  const RowsJob job = rows_job(d0, n0, d1, n1, d2, n2, slab, S, batch, accumulate);
+  if (g_defer.on) {
+    NRSE_REQUIRE(g_defer.count < 256, "nrse_rows_reduce: more than 256 deferred reductions (flush first)");
+    g_defer.q[g_defer.count++] = job;
+    return 0;
+  }
+  return launch_job(job, (hipStream_t)stream);
+}
+
+extern "C" int nrse_reduce_defer(int on) {
+  const int prev = g_defer.on ? 1 : 0;
+  g_defer.on = on != 0;
+  return prev;
+}
+
+extern "C" int nrse_reduce_pending(void) { return g_defer.count; }
+
+extern "C" int nrse_reduce_flush(void* stream) {
+  const hipStream_t st = (hipStream_t)stream;
+  int k = 0;
+  while (k < g_defer.count) {
+    const int m = g_defer.count - k < RJ_MAX ? g_defer.count - k : RJ_MAX;
+    if (m == 1) {
+      const int rc = launch_job(g_defer.q[k], st);
+      if (rc) { g_defer.count = 0; return rc; }
+      ++k;
+      continue;
+    }
+    RowsJobs jobs;
+    jobs.count = m;
+    long long total = 0;
+    for (int i = 0; i < m; ++i) {
+      jobs.j[i] = g_defer.q[k + i];
+      jobs.begin[i] = (int)total;
+      total += (long long)jobs.j[i].gx * jobs.j[i].batch;
+    }
+    jobs.begin[m] = (int)total;
+    hipLaunchKernelGGL(rows_reduce_multi_kernel, dim3((unsigned)total), dim3(1024), 0, st, jobs);
+    const int rc = nrse_check_launch("nrse_reduce_flush");
+    if (rc) { g_defer.count = 0; return rc; }
+    k += m;
+  }
+  g_defer.count = 0;
+  return 0;
 }

@@ -168,6 +168,9 @@ _SIGNATURES = {
     "nrse_zero": ([c_vp, c_ll, c_vp], c_int),
     "nrse_splitk_reduce": ([c_vp, c_vp, c_int, c_ll, c_int, c_vp], c_int),
     "nrse_rows_reduce": ([c_vp, c_ll, c_vp, c_ll, c_vp, c_ll, c_vp, c_int, c_int, c_int, c_vp], c_int),
+    "nrse_reduce_defer": ([c_int], c_int),
+    "nrse_reduce_pending": ([], c_int),
+    "nrse_reduce_flush": ([c_vp], c_int),
     "nrse_swap12": ([c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
     "nrse_gelu_bwd_pad": ([c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
     "nrse_bn_fwd": ([c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_f, c_f, c_int, c_int, c_vp], c_int),

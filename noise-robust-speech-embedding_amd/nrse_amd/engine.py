@@ -74,6 +74,9 @@ _SPLIT_LO8 = os.environ.get("NRSE_SPLIT_LO8", "1") != "0"
 # (w - w_hi) 2^e and (x - x_hi) 2^e (each <= 2^-8 |.|) inside fp8's +-448 for |w|, |x| < 56 -- the
 # conv activations are GELU(LayerNorm) outputs, |x| <= sqrt(C) max|gamma| + max|beta| (23 at
 # gamma = 1, beta = 0); beyond that the conversion saturates (bounded error, never inf / NaN)
+# ABI 9: the backward's per-layer gradient reductions batched on the side stream (0: on the dX
+# chain's stream, one launch each, as before)
+_DEFER_REDUCE = os.environ.get("NRSE_DEFER_REDUCE", "1") != "0"
 _CONV_SPLIT8 = os.environ.get("NRSE_CONV_SPLIT8", "1") != "0"
 CONV_LO8_EXP = int(os.environ.get("NRSE_CONV_LO8_EXP", "11"))
 # the correction operands as MXFP6 blocks (ABI 8: e2m3 with a scale per 32 elements, no exponents)
@@ -719,10 +722,18 @@ class ByolEngine:
         delta = torch.empty(B, nh, T, device=dev, dtype=F32)
         # the transformer layers' weight gradients (off the dX critical path) run on a side stream
         main = torch.cuda.current_stream(dev)
+        # each layer's ordered gradient reductions (LayerNorm gamma / beta and fused bias column
+        # sums, the FFN-up bias column sums, the rel-pos diagonals, the gate parameters: ~6 small
+        # launches) are queued and run batched on the side stream after the layer (ABI 9), off
+        # the dX chain; their destinations are read only by the all-reduce units (enqueued on the
+        # side stream after them), the rel-pos bias backward and the optimizer (after the joins)
+        defer = _DEFER_REDUCE and not _SERIAL_TARGET
         for j, L_ in enumerate(order):
             li = L_["li"]
             p = f"encoder.layers.{li}."
             at = p + "attention."
+            if defer:
+                K.reduce_defer(True)
             # FFN branch (its output-dropout backward was fused into the LN backward that made dh)
             dv2 = dv2_next
             df1 = torch.empty(BT, F_, device=dev, dtype=cdt)
@@ -781,6 +792,11 @@ class ByolEngine:
             del dx1, dhmid, gdp
             L_.clear()
             dh = dhin
+            if defer:
+                K.reduce_defer(False)
+                side = self._bwd_side_stream()
+                side.wait_stream(main)
+                K.reduce_flush(side)
             if on_layer is not None:
                 on_layer(li)
         tape.layers = []

@@ -58,9 +58,40 @@ def _call(name, *args):
 DETERMINISTIC = os.environ.get("NRSE_ATOMIC_REDUCTIONS", "0") != "1"
 
 
+# ABI 9 deferred reductions (nrse_reduce_defer / nrse_reduce_flush): while on, the workspaces the
+# queued reductions read are kept here until reduce_flush hands them to the flushing stream
+_DEFER_KEEP = None
+
+
 def workspace(nfloats: int) -> torch.Tensor:
     """f32 scratch on the current device and stream (the caching allocator keeps it stream-ordered)."""
-    return torch.empty(max(int(nfloats), 4), device="cuda", dtype=torch.float32)
+    t = torch.empty(max(int(nfloats), 4), device="cuda", dtype=torch.float32)
+    if _DEFER_KEEP is not None:
+        _DEFER_KEEP.append(t)
+    return t
+
+
+def reduce_defer(on: bool) -> None:
+    """Queue (on) the ordered gradient reductions that the following calls end with, instead of
+    launching them on the current stream (nrse_reduce_defer, ABI 9); reduce_flush runs the queue.
+    Their workspaces are held until then."""
+    global _DEFER_KEEP
+    _lib.lib().nrse_reduce_defer(1 if on else 0)
+    if on and _DEFER_KEEP is None:
+        _DEFER_KEEP = []
+
+
+def reduce_flush(stream: torch.cuda.Stream | None = None) -> None:
+    """Run the queued reductions on `stream` (default: the current one), batched; the queued
+    workspaces are recorded on that stream, so the allocator reuses them only after its work."""
+    global _DEFER_KEEP
+    st = stream if stream is not None else torch.cuda.current_stream()
+    for t in _DEFER_KEEP or ():
+        t.record_stream(st)
+    _call("nrse_reduce_flush", ctypes.c_void_p(st.cuda_stream))
+    on = _lib.lib().nrse_reduce_defer(0)
+    _lib.lib().nrse_reduce_defer(on)
+    _DEFER_KEEP = [] if on else None
 
 
 def splitk_reduce(out: torch.Tensor, slab: torch.Tensor, S: int, accumulate: bool) -> None:

@@ -35,7 +35,7 @@ def test_library_exports_every_declared_symbol(lib):
     L = lib.lib()
     for name in declared():
         assert hasattr(L, name), name
-    assert L.nrse_abi_version() == 8
+    assert L.nrse_abi_version() == 9
 
 
 def test_nm_dynamic_symbols(lib):
