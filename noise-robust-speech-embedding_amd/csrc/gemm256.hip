@@ -476,7 +476,8 @@ template <bool AKC, bool BKC, int BMT, int F8>
 __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params p, int mt, int nt) {
   static_assert(BMT == 256 || BMT == 224, "tile rows");
   static_assert(!F8 || (AKC && BKC), "fp8 correction segments: k-contiguous operands");
-  static_assert(F8 != 3 || BMT == 256, "the 32x32 correction blocks tile 256-row tiles");
+  static_assert(F8 < 3 || BMT == 256, "the 32x32 correction blocks tile 256-row tiles");
+  constexpr bool W32 = F8 >= 3;  // the correction on the 32x32x64 shape (3 MXFP6, 4 fp8)
   constexpr int NFI_HI = (BMT / 2 - 64) / 16;  // 16-row blocks in an M-wave's high half: 4 or 3
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
   const int tid = threadIdx.x;
@@ -541,7 +542,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
     return q;
   };
   auto tile_pos = [&](int t) {
-    if constexpr (F8 == 3) {  // correction K-tiles first
+    if constexpr (W32) {  // correction K-tiles first
       const int n8 = ntiles - n16;
       if (t < n8) return tile_pos_at(true, t / tps8, t % tps8, true);
       return tile_pos_at(t < ntiles, (t - n8) / tps, (t - n8) % tps, false);
@@ -586,8 +587,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
     }
   }
 
-  f32x4 acc[8][4];  // F8 == 3: assigned from the 32x32 accumulators after the correction tiles
-  if constexpr (F8 != 3) {
+  f32x4 acc[8][4];  // W32: assigned from the 32x32 accumulators after the correction tiles
+  if constexpr (!W32) {
 #pragma unroll
     for (int a = 0; a < 8; ++a)
 #pragma unroll
@@ -683,13 +684,16 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
     NRSE_PSTAMP(3);
     base = wrap(base + 4);
   }
-  } else if constexpr (F8 == 3) {
-  // MXFP6 correction on the 32x32x64 shape (e2m3 there runs at ~1.8x its 16x16x128 rate,
+  } else if constexpr (W32) {
+  // MXFP6 (F8 3) or fp8 (F8 4) correction on the 32x32x64 shape (e2m3 there runs at ~1.8x its 16x16x128 rate,
   // tools/probe_mx_rate.hip). The correction K-tiles run FIRST, into one 32x32 accumulator per
   // 32-row x 32-column block of the wave's 128 x 64 output (c32[MH*4 + NH*2 + bi]: M-half MH,
   // N-half NH, 32-row block bi), which are then permuted in registers into the 16x16 layout that
   // the bf16 K-tiles and the epilogue use. Same ring, phases, waits and hand-off rules as above;
   // per phase 8 MFMAs of 32x32x64 (two k-steps of 64 per 128-k K-tile) instead of 16 of 16x16x128.
+  // fp8 (F8 4): every operand byte pair meets its partner whatever k the hardware assigns a lane's
+  // 32 bytes (A and B lanes read the same positions); the weight operand carries 2^-b8_exp
+  const int scw32 = 0x01010101 * (127 - p.b8_exp);
   f32x16 c32[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
@@ -707,8 +711,12 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
   __builtin_amdgcn_s_setprio(1);                                                         \
   _Pragma("unroll") for (int s = 0; s < 2; ++s)                                        \
   _Pragma("unroll") for (int bi = 0; bi < 2; ++bi)                                     \
-    c32[(MH) * 4 + (NH) * 2 + bi] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(     \
-        FB[s], fa32[bi][s], c32[(MH) * 4 + (NH) * 2 + bi], 2, 2, 0, FB[s][6], 0, fa32[bi][s][6]); \
+    if constexpr (F8 == 3)                                                               \
+      c32[(MH) * 4 + (NH) * 2 + bi] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(   \
+          FB[s], fa32[bi][s], c32[(MH) * 4 + (NH) * 2 + bi], 2, 2, 0, FB[s][6], 0, fa32[bi][s][6]); \
+    else                                                                                 \
+      c32[(MH) * 4 + (NH) * 2 + bi] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(   \
+          FB[s], fa32[bi][s], c32[(MH) * 4 + (NH) * 2 + bi], 0, 0, 0, scw32, 0, 0x7f7f7f7f); \
   __builtin_amdgcn_s_setprio(0);
 #define NRSE_BAR8()                          \
   do {                                       \
@@ -1113,16 +1121,16 @@ int bm_choice(const nrse_gemm_params* p) {
 
 template <bool AKC, bool BKC, int F8 = 0>
 int launch(const nrse_gemm_params* p, hipStream_t st) {
-  if constexpr (F8 == 3) {
+  if constexpr (F8 >= 3) {
     const int mt = nrse_cdiv(p->M, 256), nt = nrse_cdiv(p->N, BN);
     const long long total = (long long)mt * nt * p->batch * p->splits;
-    hipLaunchKernelGGL((gemm256_kernel<AKC, BKC, 256, 3>), dim3((unsigned)total), dim3(NTHR), 0, st, *p, mt, nt);
+    hipLaunchKernelGGL((gemm256_kernel<AKC, BKC, 256, F8>), dim3((unsigned)total), dim3(NTHR), 0, st, *p, mt, nt);
     return nrse_check_launch("nrse_gemm(256)");
   }
   const int bm = bm_choice(p);
   const int mt = nrse_cdiv(p->M, bm), nt = nrse_cdiv(p->N, BN);
   const long long total = (long long)mt * nt * p->batch * p->splits;
-  if constexpr (F8 != 3) {
+  if constexpr (F8 < 3) {
     if (bm == 224)
       hipLaunchKernelGGL((gemm256_kernel<AKC, BKC, 224, F8>), dim3((unsigned)total), dim3(NTHR), 0, st, *p, mt, nt);
     else
@@ -1173,6 +1181,15 @@ bool nrse_gemm256_f8_ok(const nrse_gemm_params* p) {
          spb < (1LL << 31) && p->b8_exp > -127 && p->b8_exp < 127;
 }
 
+// fp8 segments on the 32x32x64 shape (F8 = 4: e4m3 there runs at ~1.08x its 16x16x128 rate,
+// tools/probe_mx_rate.hip; bf16sw step +1.4 %, profiles/r05_step_ab.txt) unless NRSE_FP8_SHAPE=16
+// (the 16x16x128 form, F8 = 1)
+static bool fp8_wide() {
+  static int v = -1;
+  if (v < 0) v = (getenv("NRSE_FP8_SHAPE") && atoi(getenv("NRSE_FP8_SHAPE")) == 16) ? 0 : 1;
+  return v == 1;
+}
+
 // MXFP6 segments on the 32x32x64 shape unless NRSE_MX6_SHAPE=16 (the 16x16x128 form, F8 = 2)
 static bool mx6_wide() {
   static int v = -1;
@@ -1182,7 +1199,7 @@ static bool mx6_wide() {
 
 int nrse_gemm256(const nrse_gemm_params* p, hipStream_t st) {
   if (p->nseg8 > 0) {
-    if (p->a8.dtype != NRSE_MX6) return launch<true, true, 1>(p, st);
+    if (p->a8.dtype != NRSE_MX6) return fp8_wide() ? launch<true, true, 4>(p, st) : launch<true, true, 1>(p, st);
     return mx6_wide() ? launch<true, true, 3>(p, st) : launch<true, true, 2>(p, st);
   }
   if (p->a.kcontig && p->b.kcontig) return launch<true, true>(p, st);
