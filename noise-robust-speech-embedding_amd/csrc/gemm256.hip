@@ -230,6 +230,12 @@ NRSE_DEV i32x8v frag_mx32(const char* lds, int base, int s, int lane) {
   return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+// bf16 operand of the 32x32x16 shape (F8 == 5): lane (h, r) reads row base + r, k = 16j + 8h .. +7
+// of the 64-k K-tile, i.e. its 16-B chunk 2j + h under the row swizzle
+NRSE_DEV bf16x8 frag_b32(const char* lds, int base, int j, int lane) {
+  const int h = lane >> 5, row = base + (lane & 31), sw = (row >> 1) & 7;
+  return *reinterpret_cast<const bf16x8*>(lds + row * 128 + (((2 * j + h) ^ sw) << 4));
+}
 
 // ------------------------------------------------------------------ register epilogue
 // The common epilogues of the step run with their flags fixed at compile time: the lane's
@@ -478,6 +484,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
   static_assert(!F8 || (AKC && BKC), "fp8 correction segments: k-contiguous operands");
   static_assert(F8 < 3 || BMT == 256, "the 32x32 correction blocks tile 256-row tiles");
   constexpr bool W32 = F8 >= 3;  // the correction on the 32x32x64 shape (3 MXFP6, 4 fp8)
+  constexpr bool B32 = F8 == 5;  // the bf16 K-tiles on 32x32x16 (no correction segments)
   constexpr int NFI_HI = (BMT / 2 - 64) / 16;  // 16-row blocks in an M-wave's high half: 4 or 3
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
   const int tid = threadIdx.x;
@@ -785,25 +792,67 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
   // rows q0..q3) must become [X0.q0, X0.q2, X1.q0, X1.q2] (a = 0) and [X0.q1, X0.q3, X1.q1, X1.q3]
   // (a = 1): a permlane32 swap (X0's upper half <-> X1's lower) then a permlane16 swap (odd rows
   // of the first <-> even rows of the second), in place.
+  auto convert = [&]() {
 #pragma unroll
-  for (int blk = 0; blk < 8; ++blk) {
-    const int mh = blk >> 2, nh = (blk >> 1) & 1, bi = blk & 1;
+    for (int blk = 0; blk < 8; ++blk) {
+      const int mh = blk >> 2, nh = (blk >> 1) & 1, bi = blk & 1;
 #pragma unroll
-    for (int fj = 0; fj < 2; ++fj)
+      for (int fj = 0; fj < 2; ++fj)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const auto w = __builtin_amdgcn_permlane32_swap(__float_as_uint(c32[blk][8 * fj + r]),
-                                                        __float_as_uint(c32[blk][8 * fj + 4 + r]), false, false);
-        const auto v = __builtin_amdgcn_permlane16_swap(w[0], w[1], false, false);
-        acc[mh * 4 + 2 * bi][nh * 2 + fj][r] = __uint_as_float(v[0]);
-        acc[mh * 4 + 2 * bi + 1][nh * 2 + fj][r] = __uint_as_float(v[1]);
-      }
-  }
+        for (int r = 0; r < 4; ++r) {
+          const auto w = __builtin_amdgcn_permlane32_swap(__float_as_uint(c32[blk][8 * fj + r]),
+                                                          __float_as_uint(c32[blk][8 * fj + 4 + r]), false, false);
+          const auto v = __builtin_amdgcn_permlane16_swap(w[0], w[1], false, false);
+          acc[mh * 4 + 2 * bi][nh * 2 + fj][r] = __uint_as_float(v[0]);
+          acc[mh * 4 + 2 * bi + 1][nh * 2 + fj][r] = __uint_as_float(v[1]);
+        }
+    }
+  };
+  if constexpr (!B32) convert();
+  // B32: the bf16 K-tiles on v_mfma_f32_32x32x16_bf16 into the same 32x32 accumulators (4 k-steps
+  // of 16 per 64-k K-tile, 8 MFMAs per quadrant pair as the 16x16 form's 16), converted after
+  bf16x8 fa3[2][4], fl3[4], fh3[4];
+#define NRSE_READ_A3(SLOT)                                                               \
+  _Pragma("unroll") for (int bi = 0; bi < 2; ++bi)                                     \
+  _Pragma("unroll") for (int j = 0; j < 4; ++j)                                        \
+    fa3[bi][j] = frag_b32(smem + (SLOT) * HALF, wm * 64 + 32 * bi, j, lane);
+#define NRSE_READ_B3(SLOT, FB)                                                           \
+  _Pragma("unroll") for (int j = 0; j < 4; ++j)                                        \
+    FB[j] = frag_b32(smem + (SLOT) * HALF, wn * 32, j, lane);
+#define NRSE_QUAD3(MH, NH, FB)                                                           \
+  __builtin_amdgcn_s_setprio(1);                                                         \
+  _Pragma("unroll") for (int j = 0; j < 4; ++j)                                        \
+  _Pragma("unroll") for (int bi = 0; bi < 2; ++bi)                                     \
+    c32[(MH) * 4 + (NH) * 2 + bi] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(             \
+        FB[j], fa3[bi][j], c32[(MH) * 4 + (NH) * 2 + bi], 0, 0, 0);                      \
+  __builtin_amdgcn_s_setprio(0);
   // the bf16 K-tiles (t + 2 staged as bf16 or dead)
   auto ktileb = [&](int t) {
     const int s0 = base, s1 = wrap(base + 1), s2 = wrap(base + 2), s3 = wrap(base + 3);
     const TilePos q2 = tile_pos_at(t + 2 < ntiles, u_sg, u_k, false);
     if (++u_k == tps) { u_k = 0; ++u_sg; }
+    if constexpr (B32) {
+      NRSE_READ_A3(s0)
+      NRSE_READ_B3(s1, fl3)
+      NRSE_READ_B3(s2, fh3)
+      stage(0, q2, wrap(base + 8));
+      stage(1, q2, wrap(base + 9));
+      NRSE_WAIT(12);
+      NRSE_BAR8();
+      NRSE_QUAD3(0, 0, fl3)
+      NRSE_QUAD3(0, 1, fh3)
+      NRSE_BAR8();
+      NRSE_READ_A3(s3)
+      stage(2, q2, base);
+      stage(3, q2, s1);
+      NRSE_WAIT(10);
+      NRSE_BAR8();
+      NRSE_QUAD3(1, 1, fh3)
+      NRSE_QUAD3(1, 0, fl3)
+      NRSE_BAR8();
+      base = wrap(base + 4);
+      return;
+    }
     NRSE_READ_A(s0, 4)
     NRSE_READ_B(s1, fbl)
     NRSE_READ_B(s2, fbh)
@@ -826,6 +875,10 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
   };
 #pragma unroll 1
   for (; t < ntiles; ++t) ktileb(t);
+  if constexpr (B32) convert();
+#undef NRSE_READ_A3
+#undef NRSE_READ_B3
+#undef NRSE_QUAD3
 #undef NRSE_READ_A32
 #undef NRSE_READ_B32
 #undef NRSE_QUAD32
@@ -1190,6 +1243,13 @@ static bool fp8_wide() {
   return v == 1;
 }
 
+// the forward GEMMs' bf16 K-tiles on the 32x32x16 shape (F8 = 5) with NRSE_GEMM_W32=1
+static bool bf16_wide() {
+  static int v = -1;
+  if (v < 0) v = (getenv("NRSE_GEMM_W32") && atoi(getenv("NRSE_GEMM_W32")) == 1) ? 1 : 0;
+  return v == 1;
+}
+
 // MXFP6 segments on the 32x32x64 shape unless NRSE_MX6_SHAPE=16 (the 16x16x128 form, F8 = 2)
 static bool mx6_wide() {
   static int v = -1;
@@ -1199,10 +1259,14 @@ static bool mx6_wide() {
 
 int nrse_gemm256(const nrse_gemm_params* p, hipStream_t st) {
   if (p->nseg8 > 0) {
-    if (p->a8.dtype != NRSE_MX6) return fp8_wide() ? launch<true, true, 4>(p, st) : launch<true, true, 1>(p, st);
-    return mx6_wide() ? launch<true, true, 3>(p, st) : launch<true, true, 2>(p, st);
+    const bool r256 = bm_choice(p) == 256;
+    if (p->a8.dtype != NRSE_MX6) return fp8_wide() && r256 ? launch<true, true, 4>(p, st) : launch<true, true, 1>(p, st);
+    return mx6_wide() && r256 ? launch<true, true, 3>(p, st) : launch<true, true, 2>(p, st);
   }
-  if (p->a.kcontig && p->b.kcontig) return launch<true, true>(p, st);
+  // (the 32x32 forms tile 256 rows: a problem pinned to 224-row tiles keeps the 16x16 form, whose
+  // row count the column-sum workspace was sized for)
+  if (p->a.kcontig && p->b.kcontig)
+    return (bf16_wide() && bm_choice(p) == 256) ? launch<true, true, 5>(p, st) : launch<true, true>(p, st);
   if (p->a.kcontig && !p->b.kcontig) return launch<true, false>(p, st);
   if (!p->a.kcontig && p->b.kcontig) return launch<false, true>(p, st);
   return launch<false, false>(p, st);
