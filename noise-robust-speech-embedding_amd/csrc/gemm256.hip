@@ -420,9 +420,24 @@ NRSE_DEV void fast_epilogue(const nrse_gemm_params& p, const f32x4 (&acc)[8][4],
       const int nr = vrows < mlim ? vrows : (mlim > 0 ? mlim : 0);
       float sum = 0.f;
       const char* col = oimg + (h * 64) * PITCH + c * ES;
-      for (int r = 0; r < nr; ++r) {
-        if constexpr (OBF) sum += bf2f(*reinterpret_cast<const bf16_t*>(col + r * PITCH));
-        else sum += *reinterpret_cast<const float*>(col + r * PITCH);
+      auto at = [&](int r) {
+        if constexpr (OBF) return bf2f(*reinterpret_cast<const bf16_t*>(col + r * PITCH));
+        else return *reinterpret_cast<const float*>(col + r * PITCH);
+      };
+      if (nr == 64) {
+        // full pass: 16 LDS reads in flight per batch, added in the same row order (the runtime
+        // trip count had kept each read's latency in front of its add: +15 us on the FFN-down
+        // dgrad, tools/bench_dgrad_gelu.py)
+#pragma unroll
+        for (int r0 = 0; r0 < 64; r0 += 16) {
+          float t[16];
+#pragma unroll
+          for (int i = 0; i < 16; ++i) t[i] = at(r0 + i);
+#pragma unroll
+          for (int i = 0; i < 16; ++i) sum += t[i];
+        }
+      } else {
+        for (int r = 0; r < nr; ++r) sum += at(r);
       }
       colacc[tid] = pass == 0 ? sum : colacc[tid] + sum;
     }
