@@ -145,14 +145,29 @@ __host__ __device__ inline int bv_len(int T) { return ((T + 63) & ~63) + 64; }
 // dK/dV; time unchanged, the kernels are VALU-bound). An aligned float4 never straddles a block,
 // and bv_pos(j + 64 m, s) = bv_pos(j, s) + 64 m: a lane keeps one offset per 16-key sub-tile.
 __host__ __device__ inline int bv_pos(int j, int s) { return (j & ~63) | ((j + 16 * s) & 63); }
+// The loads are unconditional (an index outside [0, 2T-1) reads a clamped one and is zeroed after)
+// and issued two strides at a time before their LDS stores: behind a conditional each load had
+// waited for its own round trip, in every workgroup's prologue.
+NRSE_DEV float clamped_ld(const float* v, int e, int n) { return v[e < 0 ? 0 : (e >= n ? n - 1 : e)]; }
 NRSE_DEV void bv_stage(float* bv, const float* vec, int T, int q0, int tid) {
   const int len = bv_len(T), nd = 2 * T - 1;
   const int e_lo = T - 1 - q0 - 63;
-  for (int j = tid; j < len; j += 256) {
+  for (int j0 = tid; j0 < len; j0 += 512) {
+    float v[2][4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int e = e_lo + j + s;
-      bv[s * len + bv_pos(j, s)] = (e >= 0 && e < nd) ? vec[e] : 0.f;
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) v[u][s] = clamped_ld(vec, e_lo + j0 + 256 * u + s, nd);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int j = j0 + 256 * u;
+      if (j < len) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int e = e_lo + j + s;
+          bv[s * len + bv_pos(j, s)] = (e >= 0 && e < nd) ? v[u][s] : 0.f;
+        }
+      }
     }
   }
 }
@@ -194,14 +209,16 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
   bv_stage(bv, p.bias_vec + (long long)h * (2 * T - 1), T, q0, tid);
   // Q fragments (B operand of S^T = K Q^T): Q[qi][8g + 32s .. +8]
   bf16x8 qf[2];
+  const int qc = qv ? qi : T - 1;  // loads from a clamped row, zeroed after (no branch around them)
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    uint4 u = make_uint4(0, 0, 0, 0);
-    if (qv) u = *reinterpret_cast<const uint4*>(qkv + (long long)qi * ld3 + h * D + 8 * g + 32 * s);
+    uint4 u = *reinterpret_cast<const uint4*>(qkv + (long long)qc * ld3 + h * D + 8 * g + 32 * s);
+    if (!qv) u = make_uint4(0, 0, 0, 0);
     qf[s] = __builtin_bit_cast(bf16x8, u);
   }
   const long long bh = (long long)b * H + h;
-  const float gi = qv ? p.gate[bh * T + qi] : 0.f;
+  const float gi0 = p.gate[bh * T + qc];
+  const float gi = qv ? gi0 : 0.f;
   const float c1 = p.scale * LOG2E, gl = gi * LOG2E;
   // bias copy and base for this lane: segment index u0 = kb + 4g + 63 - (qi - q0)
   const int bvl = bv_len(T);
@@ -419,14 +436,13 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
   bf16x8 qf[2], dof[2];
   const bf16_t* octx = (const bf16_t*)p.ctx + (long long)b * T * Hd;
   float dsum = 0.f;  // delta = rowsum(dO * O) for this lane's 16 of the 64 dims
+  const int qc = qv ? qi : T - 1;  // loads from a clamped row, zeroed after (no branch around them)
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    uint4 u = make_uint4(0, 0, 0, 0), d = make_uint4(0, 0, 0, 0), o = make_uint4(0, 0, 0, 0);
-    if (qv) {
-      u = *reinterpret_cast<const uint4*>(qkv + (long long)qi * ld3 + h * D + 8 * g + 32 * s);
-      d = *reinterpret_cast<const uint4*>(dctx + (long long)qi * Hd + h * D + 8 * g + 32 * s);
-      o = *reinterpret_cast<const uint4*>(octx + (long long)qi * Hd + h * D + 8 * g + 32 * s);
-    }
+    uint4 u = *reinterpret_cast<const uint4*>(qkv + (long long)qc * ld3 + h * D + 8 * g + 32 * s);
+    uint4 d = *reinterpret_cast<const uint4*>(dctx + (long long)qc * Hd + h * D + 8 * g + 32 * s);
+    uint4 o = *reinterpret_cast<const uint4*>(octx + (long long)qc * Hd + h * D + 8 * g + 32 * s);
+    if (!qv) u = d = o = make_uint4(0, 0, 0, 0);
     qf[s] = __builtin_bit_cast(bf16x8, u);
     dof[s] = __builtin_bit_cast(bf16x8, d);
     const unsigned dw[4] = {d.x, d.y, d.z, d.w}, ow[4] = {o.x, o.y, o.z, o.w};
@@ -437,9 +453,10 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
   }
   dsum = xor32_sum(xor16_sum(dsum));
   const long long bh = (long long)b * H + h;
-  const float gi = qv ? p.gate[bh * T + qi] : 0.f;
+  const float gi0 = p.gate[bh * T + qc], lse0 = p.lse[bh * T + qc];
+  const float gi = qv ? gi0 : 0.f;
   const float c1 = p.scale * LOG2E, gl = gi * LOG2E;
-  const float lse = qv ? p.lse[bh * T + qi] : 0.f;
+  const float lse = qv ? lse0 : 0.f;
   const float lse2 = lse * LOG2E;
   const float delta = dsum;
   if (g == 0 && qv) p.delta[bh * T + qi] = delta;  // consumed by attn_bwd_kv_kernel (launched after)
@@ -615,11 +632,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   kv_dma_issue(qd, qo0, 0, w);
   kv_dma_issue(od, qo0 + TILE_B, 0, w);
   mask_issue(mtile0, 0);
-  for (int q = tid; q < Tp; q += 256) {
-    const bool ok = q < T;
-    rowall[q] = ok ? p.lse[bh * T + q] * LOG2E : 0.f;
-    rowall[Tp + q] = ok ? p.delta[bh * T + q] : 0.f;
-    rowall[2 * Tp + q] = ok ? p.gate[bh * T + q] : 0.f;
+  // (loads unconditional from clamped rows, two strides in flight, zeroed past T)
+  for (int q0r = tid; q0r < Tp; q0r += 512) {
+    float l[2], dl[2], gt[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int qq = q0r + 256 * u, qc = qq < T ? qq : T - 1;
+      l[u] = p.lse[bh * T + qc];
+      dl[u] = p.delta[bh * T + qc];
+      gt[u] = p.gate[bh * T + qc];
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int qq = q0r + 256 * u;
+      if (qq < Tp) {
+        const bool ok = qq < T;
+        rowall[qq] = ok ? l[u] * LOG2E : 0.f;
+        rowall[Tp + qq] = ok ? dl[u] : 0.f;
+        rowall[2 * Tp + qq] = ok ? gt[u] : 0.f;
+      }
+    }
   }
   // bias of (query q, key kj) = vec[kj - q + T - 1]: reversed copies, copy s index j holds
   // log2e * vec[e_hi - j - s], e_hi = kb0 + 63 + T - 1; element (q, kj) sits at segment index
@@ -628,22 +660,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   {
     const float* vec = p.bias_vec + (long long)h * (2 * T - 1);
     const int nd = 2 * T - 1, e_hi = kb0 + 63 + T - 1;
-    for (int j = tid; j < bvl; j += 256) {
+    for (int j0 = tid; j0 < bvl; j0 += 512) {   // as bv_stage: loads first, clamped
+      float v[2][4];
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) {
-        const int e = e_hi - j - s4;
-        rbv[s4 * bvl + bv_pos(j, s4)] = (e >= 0 && e < nd) ? vec[e] * LOG2E : 0.f;
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) v[u][s4] = clamped_ld(vec, e_hi - (j0 + 256 * u) - s4, nd);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int j = j0 + 256 * u;
+        if (j < bvl) {
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) {
+            const int e = e_hi - j - s4;
+            rbv[s4 * bvl + bv_pos(j, s4)] = (e >= 0 && e < nd) ? v[u][s4] * LOG2E : 0.f;
+          }
+        }
       }
     }
   }
   bf16x8 kf[2], vf[2];
+  const int kc = kv ? kj : T - 1;  // clamped row, zeroed after
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    uint4 a = make_uint4(0, 0, 0, 0), c = make_uint4(0, 0, 0, 0);
-    if (kv) {
-      a = *reinterpret_cast<const uint4*>(qkv + (long long)kj * ld3 + Hd + h * D + 8 * g + 32 * s);
-      c = *reinterpret_cast<const uint4*>(qkv + (long long)kj * ld3 + 2 * Hd + h * D + 8 * g + 32 * s);
-    }
+    uint4 a = *reinterpret_cast<const uint4*>(qkv + (long long)kc * ld3 + Hd + h * D + 8 * g + 32 * s);
+    uint4 c = *reinterpret_cast<const uint4*>(qkv + (long long)kc * ld3 + 2 * Hd + h * D + 8 * g + 32 * s);
+    if (!kv) a = c = make_uint4(0, 0, 0, 0);
     kf[s] = __builtin_bit_cast(bf16x8, a);
     vf[s] = __builtin_bit_cast(bf16x8, c);
   }
