@@ -136,18 +136,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     const int n = rem >> 6, gg = (rem >> 4) & 3, ll = rem & 15;
     const int ch = 32 * (n >> 1) + 8 * (ll >> 2) + 4 * (n & 1) + (ll & 3);
     bf16x8 v;
+    // the 8 weight loads unconditional (tap k % 10 is always in range), the selection after: behind
+    // the conditions each load had waited for its own round trip, 8 per fragment
+    float wl[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) wl[e] = p.w[ch * KMAX + (8 * gg + e) % 10];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const int k = 8 * gg + e;
+      const float w = wl[e];
+      const float hi = bf2f(f2bf(w));
       float wv = 0.f;
-      if (m == 0 && k < 30) {
-        const float w = p.w[ch * KMAX + k % 10];
-        const float hi = bf2f(f2bf(w));
-        wv = k < 20 ? hi : w - hi;  // [w_hi | w_hi | w_lo]; w_lo rounds to bf16 below
-      } else if (m == 1 && k < 10) {
-        const float w = p.w[ch * KMAX + k];
-        wv = w - bf2f(f2bf(w));
-      }
+      if (m == 0 && k < 30) wv = k < 20 ? hi : w - hi;  // [w_hi | w_hi | w_lo]; w_lo rounds to bf16 below
+      else if (m == 1 && k < 10) wv = w - hi;
       v[e] = (__bf16)wv;
     }
     wimg[idx] = v;
