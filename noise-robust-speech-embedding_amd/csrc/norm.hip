@@ -6,6 +6,7 @@
 // instruction covers 512 B - 1 KiB of a row; gamma/beta grads are accumulated per lane across
 // the rows a wave visits (grid-stride), reduced across the block in LDS, then one f32 atomic
 // per column per block.
+#include <cstdlib>
 #include "common.h"
 
 namespace {
@@ -280,10 +281,12 @@ NRSE_DEV float load_dy(const nrse_ln_bwd_params& p, long long row, int c, float*
 // words and compute() unpacks them, so no unpack (and no wait for the load) sits between the
 // prefetch of the next row and its use; converting at load time put an s_waitcnt vmcnt(0)
 // after every dy / x load and serialised the prefetch away.
-template <int NK, bool RES, bool COL, bool BF>
+// XF (with BF): x is f32 (the split-weight step's f32 conv pre-activations), kept as raw 16-B words
+template <int NK, bool RES, bool COL, bool BF, bool XF = false>
 struct LnRow {
   float x[BF ? 1 : NK][CH], dy[BF ? 1 : NK][CH], r[RES ? NK : 1][CH], dy2[COL && !BF ? NK : 1][CH];
-  uint2 xr[BF ? NK : 1], dyr[BF ? NK : 1], dy2r[COL && BF ? NK : 1];
+  uint2 xr[BF && !XF ? NK : 1], dyr[BF ? NK : 1], dy2r[COL && BF ? NK : 1];
+  uint4 xw[XF ? NK : 1];
   float gd[RES ? NK : 1][2];  // GT: the row's gate-path (dpa, dpb) of this lane's head per k
   float mean, rstd;
   bool v0, v1;  // BF: col2im taps present (their loads are issued regardless, from a valid address)
@@ -312,9 +315,9 @@ NRSE_DEV void col_taps(const nrse_ln_bwd_params& p, const ColDiv& cd, long long 
 
 // FD (encoder form, RES): x, dy and the residual all f32, dy direct: three unconditional 16-B
 // loads per word, no dtype / mode branches (each of which had made the compiler wait for the load)
-template <int NK, bool RES, bool COL, bool BF, bool FD, bool GT>
+template <int NK, bool RES, bool COL, bool BF, bool FD, bool GT, bool XF = false>
 NRSE_DEV void ln_bwd_load(const nrse_ln_bwd_params& p, const ColDiv& cd, long long row, int lane,
-                          LnRow<NK, RES, COL, BF>& b) {
+                          LnRow<NK, RES, COL, BF, XF>& b) {
   b.mean = p.mean[row];
   b.rstd = p.rstd[row];
   if constexpr (GT) {
@@ -359,7 +362,8 @@ NRSE_DEV void ln_bwd_load(const nrse_ln_bwd_params& p, const ColDiv& cd, long lo
     const int c0 = (k * 64 + lane) * CH;
     if constexpr (BF) {
       const bf16_t* dyp = (const bf16_t*)p.dy;
-      b.xr[k] = ldg(reinterpret_cast<const uint2*>((const bf16_t*)p.x + row * p.C + c0));
+      if constexpr (XF) b.xw[k] = ldg(reinterpret_cast<const uint4*>((const float*)p.x + row * p.C + c0));
+      else b.xr[k] = ldg(reinterpret_cast<const uint2*>((const bf16_t*)p.x + row * p.C + c0));
       b.dyr[k] = ldg(reinterpret_cast<const uint2*>(dyp + o0 + c0));
       if constexpr (COL) b.dy2r[k] = ldg(reinterpret_cast<const uint2*>(dyp + o1 + c0));
     } else {
@@ -382,8 +386,9 @@ NRSE_DEV void ln_bwd_load(const nrse_ln_bwd_params& p, const ColDiv& cd, long lo
 // RES: the encoder-layer form (residual input, fused dropout-cast consumer); !RES (conv / feature
 // projection LNs) drops their registers: 137 -> fewer VGPRs, more waves for the long row sweeps
 // GT (with FD): dy += the gate path's gradient, nrse_ln_bwd_params.gate_dp
-template <int NK, bool RES, bool COL, bool BF, bool FD = false, bool GT = false>
+template <int NK, bool RES, bool COL, bool BF, bool FD = false, bool GT = false, bool XF = false>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const nrse_ln_bwd_params p) {
+  static_assert(!XF || BF, "XF: f32 x beside the bf16 dy words");
   static_assert(!GT || FD, "the gate term rides on the encoder form");
   constexpr bool GBL = RES && !FD;  // gamma / beta read from global memory per row
   __shared__ float red[4][NK * 64 * CH];
@@ -427,7 +432,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const nrse_ln_bwd_params p)
 #pragma unroll
     for (int e = 0; e < CH; ++e) dc[k][e] = 0.f;
 
-  auto compute = [&](const LnRow<NK, RES, COL, BF>& b, long long row) {
+  auto compute = [&](const LnRow<NK, RES, COL, BF, XF>& b, long long row) {
     float xh[NK][CH], g[NK][CH];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -450,7 +455,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const nrse_ln_bwd_params p)
       float xv[CH], dv0[CH], dv1[CH] = {0.f, 0.f, 0.f, 0.f};
       if constexpr (BF) {
         const uint2 z2 = make_uint2(0u, 0u);
-        unpack_bf4(b.xr[k], xv);
+        if constexpr (XF) {
+          xv[0] = __uint_as_float(b.xw[k].x); xv[1] = __uint_as_float(b.xw[k].y);
+          xv[2] = __uint_as_float(b.xw[k].z); xv[3] = __uint_as_float(b.xw[k].w);
+        } else {
+          unpack_bf4(b.xr[k], xv);
+        }
         unpack_bf4(b.v0 ? b.dyr[k] : z2, dv0);
         if constexpr (COL) unpack_bf4(b.v1 ? b.dy2r[k] : z2, dv1);
       } else {
@@ -509,26 +519,26 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const nrse_ln_bwd_params p)
     cd.tin.init((unsigned)p.col_tin);
     cd.s.init((unsigned)p.col_s);
   }
-  LnRow<NK, RES, COL, BF> ba, bb;
+  LnRow<NK, RES, COL, BF, XF> ba, bb;
   const long long last = p.rows - 1;
-  if (row < p.rows) ln_bwd_load<NK, RES, COL, BF, FD, GT>(p, cd, row, lane, ba);
+  if (row < p.rows) ln_bwd_load<NK, RES, COL, BF, FD, GT, XF>(p, cd, row, lane, ba);
   for (; row < p.rows; row += 2 * nw) {
     const long long rb = row + nw;
     // BF: unconditional (clamped) prefetch, fenced from the scheduler, which otherwise sinks the
     // loads below part of the current row's math to save registers (and then waits for them)
     if (BF || FD) {
-      ln_bwd_load<NK, RES, COL, BF, FD, GT>(p, cd, rb < last ? rb : last, lane, bb);
+      ln_bwd_load<NK, RES, COL, BF, FD, GT, XF>(p, cd, rb < last ? rb : last, lane, bb);
       __builtin_amdgcn_sched_barrier(0);
     } else if (rb < p.rows) {
-      ln_bwd_load<NK, RES, COL, BF, FD, GT>(p, cd, rb, lane, bb);
+      ln_bwd_load<NK, RES, COL, BF, FD, GT, XF>(p, cd, rb, lane, bb);
     }
     compute(ba, row);
     if (rb >= p.rows) break;
     if (BF || FD) {
-      ln_bwd_load<NK, RES, COL, BF, FD, GT>(p, cd, rb + nw < last ? rb + nw : last, lane, ba);
+      ln_bwd_load<NK, RES, COL, BF, FD, GT, XF>(p, cd, rb + nw < last ? rb + nw : last, lane, ba);
       __builtin_amdgcn_sched_barrier(0);
     } else if (rb + nw < p.rows) {
-      ln_bwd_load<NK, RES, COL, BF, FD, GT>(p, cd, rb + nw, lane, ba);
+      ln_bwd_load<NK, RES, COL, BF, FD, GT, XF>(p, cd, rb + nw, lane, ba);
     }
     compute(bb, rb);
   }
@@ -673,6 +683,13 @@ static long long ln_bwd_blocks(const nrse_ln_bwd_params* p) {
 // column-sum vectors per workgroup: dgamma, dbeta, the fused dropout consumer's colsum
 static int ln_bwd_nd(const nrse_ln_bwd_params* p) { return (p->dgamma ? 2 : 0) + ((p->dv && p->dv_colsum) ? 1 : 0); }
 
+// NRSE_LN_XF=0 keeps the generic form for f32 x with bf16 col2im dy (A/B)
+static bool xf_enabled() {
+  static int v = -1;
+  if (v < 0) v = (getenv("NRSE_LN_XF") && atoi(getenv("NRSE_LN_XF")) == 0) ? 0 : 1;
+  return v == 1;
+}
+
 extern "C" int nrse_layernorm_bwd(const nrse_ln_bwd_params* p, void* stream) {
   NRSE_REQUIRE(p && p->dy && p->x && p->gamma && p->mean && p->rstd && p->dx && p->rows > 0,
                "nrse_layernorm_bwd: bad args");
@@ -696,6 +713,10 @@ extern "C" int nrse_layernorm_bwd(const nrse_ln_bwd_params* p, void* stream) {
   const bool bf = !res && p->x_dtype == NRSE_BF16 && p->dy_dtype == NRSE_BF16 &&
                   (col2 || p->dy_mode == NRSE_DY_DIRECT);
   // encoder form with every operand f32 and dy direct: the branch-free loads
+  // f32 x (the split-weight step's conv pre-activations), bf16 two-tap col2im dy: the bf16 form's
+  // raw-word loads with x as 16-B f32 words
+  const bool xf = !res && p->x_dtype == NRSE_F32 && p->dy_dtype == NRSE_BF16 && col2 &&
+                  (((uintptr_t)p->x) & 15) == 0 && xf_enabled();
   const bool fd = res && p->resid && p->x_dtype == NRSE_F32 && p->dy_dtype == NRSE_F32 &&
                   p->dy_mode == NRSE_DY_DIRECT &&
                   ((((uintptr_t)p->x) | ((uintptr_t)p->dy) | ((uintptr_t)p->resid)) & 15) == 0;
@@ -706,6 +727,7 @@ extern "C" int nrse_layernorm_bwd(const nrse_ln_bwd_params* p, void* stream) {
   else if (fd) hipLaunchKernelGGL((ln_bwd_kernel<NK, true, false, false, true>), grid, dim3(256), 0, st, *p); \
   else if (res) hipLaunchKernelGGL((ln_bwd_kernel<NK, true, false, false>), grid, dim3(256), 0, st, *p);    \
   else if (bf && col2) hipLaunchKernelGGL((ln_bwd_kernel<NK, false, true, true>), grid, dim3(256), 0, st, *p); \
+  else if (xf) hipLaunchKernelGGL((ln_bwd_kernel<NK, false, true, true, false, false, true>), grid, dim3(256), 0, st, *p); \
   else if (bf) hipLaunchKernelGGL((ln_bwd_kernel<NK, false, false, true>), grid, dim3(256), 0, st, *p); \
   else if (col2) hipLaunchKernelGGL((ln_bwd_kernel<NK, false, true, false>), grid, dim3(256), 0, st, *p); \
   else hipLaunchKernelGGL((ln_bwd_kernel<NK, false, false, false>), grid, dim3(256), 0, st, *p);

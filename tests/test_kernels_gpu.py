@@ -111,6 +111,34 @@ def test_layernorm_bwd_col2im_and_bcast(nrse_device, C, k, s):
     assert rel(dx, xr.grad) < 1e-6
 
 
+@pytest.mark.parametrize("C,k,s", [(512, 3, 2), (512, 2, 2), (256, 3, 2)])
+def test_layernorm_bwd_col2im_f32x_bf16dy(nrse_device, C, k, s):
+    """The split-weight conv stack's LN + GELU backward: f32 pre-activation x, bf16 two-tap col2im
+    dy (the XF form, raw-word loads), against float64 autograd of the same bf16 dy values."""
+    from nrse_amd import kernels as K, _lib
+    dev = nrse_device
+    B, Tin = 3, 52
+    Tout = (Tin - k) // s + 1
+    x = torch.randn(B * Tin, C, device=dev)
+    g = 1 + 0.1 * torch.randn(C, device=dev); b = 0.1 * torch.randn(C, device=dev)
+    y = torch.empty_like(x); mean = torch.empty(B * Tin, device=dev); rstd = torch.empty_like(mean)
+    K.ln_fwd(x, g, b, y, mean, rstd, 1e-5)
+    G = torch.randn(B * Tout, k * C, device=dev).to(torch.bfloat16)
+    dy = torch.zeros(B, Tin, C, device=dev, dtype=torch.float64)
+    Gv = G.double().view(B, Tout, k, C)
+    for j in range(k):
+        dy[:, j:j + s * (Tout - 1) + 1:s] += Gv[:, :, j]
+    dx = torch.empty(B * Tin, C, device=dev, dtype=torch.bfloat16)
+    dg = torch.zeros(C, device=dev); db = torch.zeros(C, device=dev)
+    K.ln_bwd(G, x, g, mean, rstd, dx, mode=_lib.DY_COL2IM, col=(k, s, Tout, Tin), rows=B * Tin,
+             dgamma=dg, dbeta=db, gelu=True, beta=b)
+    xr = x.double().requires_grad_(True)
+    gr, br = g.double().requires_grad_(True), b.double().requires_grad_(True)
+    F.gelu(F.layer_norm(xr, (C,), gr, br, 1e-5)).backward(dy.view(B * Tin, C))
+    assert rel(dx, xr.grad) < 1e-2   # bf16 output
+    assert rel(dg, gr.grad) < 1e-5 and rel(db, br.grad) < 1e-5
+
+
 @pytest.mark.parametrize("C,k", [(256, 10), (512, 10), (512, 8)])
 def test_conv0_fwd_bwd(nrse_device, C, k):
     """conv0 + LN + GELU forward / backward against float64 autograd: the model's k = 10 (the
