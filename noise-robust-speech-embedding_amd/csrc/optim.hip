@@ -102,13 +102,19 @@ __global__ __launch_bounds__(256) void adamw_kernel(const nrse_adamw_params p) {
   const float eom = 1.f - p.ema_decay;
   const float sc8 = ldexpf(1.f, p.lo8_exp);
   const bool mx = p.lo8_dtype == NRSE_MX6;
+  const bool ema4 = p.ema_t && e4 > 0;  // uniform: a whole EMA quad exists to load
   for (long long q = (long long)blockIdx.x * 256 + threadIdx.x; q < n4; q += (long long)gridDim.x * 256) {
+    // the five operand quads issued together: the target's quad (from a clamped index past the
+    // EMA range) before the stores below, which may alias it and would otherwise order its load
+    // after them as a second memory round trip per iteration
     float4 pv = reinterpret_cast<float4*>(p.p)[q];
     const float4 gv = reinterpret_cast<const float4*>(p.g)[q];
-    // zero_grad: the gradient buffer is cleared for the next step's accumulation by this pass
-    if (p.zero_grad) reinterpret_cast<float4*>(const_cast<float*>(p.g))[q] = make_float4(0.f, 0.f, 0.f, 0.f);
     float4 mv = reinterpret_cast<float4*>(p.m)[q];
     float4 vv = reinterpret_cast<float4*>(p.v)[q];
+    float4 tv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (ema4) tv = reinterpret_cast<const float4*>(p.ema_t)[q < e4 ? q : 0];
+    // zero_grad: the gradient buffer is cleared for the next step's accumulation by this pass
+    if (p.zero_grad) reinterpret_cast<float4*>(const_cast<float*>(p.g))[q] = make_float4(0.f, 0.f, 0.f, 0.f);
     float* pa = &pv.x; const float* ga = &gv.x; float* ma = &mv.x; float* va = &vv.x;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -132,7 +138,6 @@ __global__ __launch_bounds__(256) void adamw_kernel(const nrse_adamw_params p) {
     if (p.p_shadow_lo8) store_lo8x4(p.p_shadow_lo8, q, pa, sc8, mx);
     if (p.ema_t) {
       if (q < e4) {
-        float4 tv = reinterpret_cast<float4*>(p.ema_t)[q];
         tv.x = ema_mix(tv.x, pv.x, p.ema_decay, eom); tv.y = ema_mix(tv.y, pv.y, p.ema_decay, eom);
         tv.z = ema_mix(tv.z, pv.z, p.ema_decay, eom); tv.w = ema_mix(tv.w, pv.w, p.ema_decay, eom);
         reinterpret_cast<float4*>(p.ema_t)[q] = tv;

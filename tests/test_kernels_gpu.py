@@ -360,7 +360,7 @@ def test_adamw_clip_ema(nrse_device):
 def test_adamw_fused_ema_matches_two_passes(nrse_device):
     """The target EMA fused into the AdamW pass (nrse_adamw_params.ema_t) equals nrse_adamw followed
     by nrse_ema on the updated weights, bit for bit, with the EMA range ending inside a float4 quad,
-    on a quad boundary, and in the scalar tail; shadows (bf16 and split-plane) included."""
+    on a quad boundary, in the scalar tail and shorter than one quad; shadows (bf16 and split-plane) included."""
     from nrse_amd import kernels as K
     dev = nrse_device
     n = 100_003
@@ -371,7 +371,8 @@ def test_adamw_fused_ema_matches_two_passes(nrse_device):
     base = torch.randn(n, device=dev)
     m0, v0 = torch.randn(n, device=dev) * 0.1, torch.rand(n, device=dev) * 0.01
     t0 = torch.randn(n, device=dev)
-    for ne, split in ((n, False), (n - 1, True), (4 * 11111, False), (4 * 11111 + 3, True), (4 * 25000 + 2, False)):
+    for ne, split in ((n, False), (n - 1, True), (4 * 11111, False), (4 * 11111 + 3, True), (4 * 25000 + 2, False),
+                      (3, False), (4, True)):
         outs = []
         for fused in (False, True):
             p, m, v, t = base.clone(), m0.clone(), v0.clone(), t0[:ne].clone()
