@@ -10,7 +10,13 @@
  *   - return 0 on success, a negative nrse_status otherwise; nrse_last_error() returns a
  *     thread-local message for the last failure on the calling thread;
  *   - per-sample data validity (the reference's `None` returns) is reported through int32
- *     status arrays, never through the return code.
+ *     status arrays, never through the return code;
+ *   - ABI handshake (ABI 10): every params struct starts with `uint32_t struct_size`, which the
+ *     caller sets to sizeof(struct) as compiled against THIS header (NRSE_PARAMS_INIT below). An
+ *     entry point (and a *_workspace query) refuses any other value with NRSE_ERR_ARG before it
+ *     reads a further field, so a caller built against an older or newer header -- whose struct is
+ *     shorter or longer -- is refused instead of having its struct read past the end.
+ *     nrse_abi_version() returns NRSE_ABI_VERSION for callers that also want to log it.
  *
  * Reference interface each group replaces is cited per entry point (file:line in the
  * reference, [TF] = transformers 5.15.0 modeling_wavlm.py, see SURVEY.md citation rules).
@@ -20,6 +26,15 @@
 
 #include <stddef.h>
 #include <stdint.h>
+#include <string.h>
+
+#define NRSE_ABI_VERSION 10
+/* zero-initialise a params struct and stamp its size: nrse_gemm_params p; NRSE_PARAMS_INIT(p); */
+#define NRSE_PARAMS_INIT(s)            \
+  do {                                 \
+    memset(&(s), 0, sizeof(s));        \
+    (s).struct_size = sizeof(s);       \
+  } while (0)
 
 #ifdef __cplusplus
 extern "C" {
@@ -110,6 +125,7 @@ typedef struct {
 } nrse_gemm_operand;
 
 typedef struct {
+  uint32_t struct_size;  /* ABI 10: sizeof(nrse_gemm_params), checked by every entry point taking it */
   nrse_gemm_operand a, b;
   int M, N, K, nseg, splits, batch, zdiv;
   float alpha;
@@ -180,6 +196,7 @@ enum { NRSE_LN_GELU = 1, NRSE_LN_RELU = 2 };   /* RELU: emotion heads, src/model
 enum { NRSE_DY_DIRECT = 0, NRSE_DY_COL2IM = 1, NRSE_DY_BCAST = 2 };
 
 typedef struct {
+  uint32_t struct_size;  /* ABI 10: sizeof(nrse_ln_fwd_params), checked by every entry point taking it */
   const void* x; int x_dtype;
   const float* gamma; const float* beta;
   void* y; int y_dtype;
@@ -195,9 +212,15 @@ typedef struct {
   /* ABI 8: y8_dtype NRSE_MX6 writes y8 (either form) as MXFP6 blocks instead of fp8 (y8_exp is
    * then unused: the blocks carry their scales); 0 or NRSE_FP8: fp8 */
   int y8_dtype;
+  /* ABI 10, optional: sat_count[0] += the number of y8 values whose fp8 conversion saturated
+   * (|v| > 448 before rounding; the scaled correction plane and the unscaled hi / fp8(bf16 y) plane
+   * alike). Never touched when nothing saturates; the engine reads it back lagged and re-derives
+   * the split-weight exponents when it moves (nrse_amd/engine.py rederive_split_exponents) */
+  unsigned int* sat_count;
 } nrse_ln_fwd_params;
 
 typedef struct {
+  uint32_t struct_size;  /* ABI 10: sizeof(nrse_ln_bwd_params), checked by every entry point taking it */
   const void* dy; int dy_dtype; int dy_mode;
   int col_k, col_s, col_tout, col_tin;   /* NRSE_DY_COL2IM geometry; rows = batch * col_tin */
   int bcast_t; float dy_scale;           /* NRSE_DY_BCAST: rows per utterance, scale */
@@ -275,6 +298,7 @@ int nrse_gate_bwd_dp(const void* x1, int x_dtype, const float* W, const float* b
 long long nrse_gate_bwd_workspace(int H);
 
 typedef struct {
+  uint32_t struct_size;  /* ABI 10: sizeof(nrse_attn_fwd_params), checked by every entry point taking it */
   const void* qkv; int dtype;     /* q/k/v (bf16 or f32) */
   const float* gate; const float* bias;
   void* ctx;                      /* [B*T, Hd] same dtype as qkv */
@@ -299,6 +323,7 @@ typedef struct {
 } nrse_attn_fwd_params;
 
 typedef struct {
+  uint32_t struct_size;  /* ABI 10: sizeof(nrse_attn_bwd_params), checked by every entry point taking it */
   const void* qkv; int dtype;
   const float* gate; const float* bias;
   const void* ctx; const void* dctx;   /* O and dO */
@@ -338,6 +363,7 @@ int nrse_attn_dropout_mask(uint16_t* drop_mask, int batch, int T, int H, float d
  * nrse_ln_bwd_params).
  * ------------------------------------------------------------------------------------------ */
 typedef struct {
+  uint32_t struct_size;  /* ABI 10: sizeof(nrse_conv0_params), checked by every entry point taking it */
   const float* wav; int L;        /* [B, L] f32 */
   const float* w;                 /* [C, k] */
   const float* gamma; const float* beta;
@@ -355,6 +381,7 @@ typedef struct {
   void* y8; int y8_exp;
   int y8_dtype;                   /* fwd, ABI 8: NRSE_MX6 = the two planes as MXFP6 blocks (no y8_exp);
                                      0 or NRSE_FP8: fp8 */
+  unsigned int* sat_count;        /* fwd, ABI 10, optional: as nrse_ln_fwd_params.sat_count, for y8 */
 } nrse_conv0_params;
 int nrse_conv0_fwd(const nrse_conv0_params* p, void* stream);
 int nrse_conv0_bwd(const nrse_conv0_params* p, void* stream);
@@ -409,7 +436,8 @@ int nrse_cast(const void* x, int x_dtype, void* y, int y_dtype, long long n, voi
 int nrse_split_bf16(const float* x, void* hi, void* lo, long long n, void* stream);
 /* ABI 6: the fp8 correction plane of the same split: lo8[i] = fp8((x[i] - bf16(x[i])) * 2^lo8_exp)
  * (NRSE_FP8, saturated), as nrse_adamw_params.p_shadow_lo8 writes it */
-int nrse_split_lo8(const float* x, void* lo8, int lo8_exp, long long n, void* stream);
+int nrse_split_lo8(const float* x, void* lo8, int lo8_exp, long long n, unsigned int* sat_count, void* stream);
+/* (ABI 10: sat_count optional, += the saturated conversions, as nrse_adamw_params.sat_count) */
 /* ABI 6: y8[i] = fp8(x[i]) of a bf16 / f32 tensor (NRSE_FP8, saturated at +-448), n elements */
 int nrse_cast_fp8(const void* x, int x_dtype, void* y8, long long n, void* stream);
 /* ABI 8: the MXFP6 forms (NRSE_MX6 blocks, n a multiple of 32, 32-byte aligned y):
@@ -440,6 +468,9 @@ int nrse_rows_reduce(float* d0, long long n0, float* d1, long long n1, float* d2
 int nrse_reduce_defer(int on);
 int nrse_reduce_pending(void);
 int nrse_reduce_flush(void* stream);
+/* ABI 10: drop the queued reductions without running them and turn deferral off (error recovery:
+ * a caller whose backward raised mid-layer must not flush jobs whose workspaces it has released) */
+int nrse_reduce_discard(void);
 /* dst[a][c][b] (+)= src[a][b][c]  (conv weight [co][ci][k] <-> implicit-GEMM layout [co][k][ci]) */
 int nrse_swap12(const void* src, int src_dtype, void* dst, int dst_dtype, int d0, int d1, int d2, int accumulate,
                 void* stream);
@@ -506,6 +537,7 @@ int nrse_sumsq(const float* x, long long n, double* out, double* part, void* str
 /* part (optional): f64 workspace of 4096 doubles; the per-workgroup sums are then added in a
  * fixed order (deterministic) instead of by f64 atomics */
 typedef struct {
+  uint32_t struct_size;  /* ABI 10: sizeof(nrse_adamw_params), checked by every entry point taking it */
   float* p; const float* g; float* m; float* v; void* p_shadow; int shadow_dtype;
   long long n;
   float lr, beta1, beta2, eps, weight_decay; int step;
@@ -536,6 +568,10 @@ typedef struct {
    * p_new - bf16(p_new) (no lo8_exp; n, ema_n multiples of 32, 32-byte aligned planes); 0 or
    * NRSE_FP8: fp8 */
   int lo8_dtype;
+  /* ABI 10, optional: sat_count[0] += the number of fp8 correction values (p_shadow_lo8 and
+   * ema_shadow_lo8) that saturated, |(w - bf16 w) 2^lo8_exp| > 448: lo8_exp no longer has headroom
+   * for the weights (they grew in training); the caller re-derives it (see nrse_ln_fwd_params) */
+  unsigned int* sat_count;
 } nrse_adamw_params;
 int nrse_adamw(const nrse_adamw_params* p, void* stream);
 /* t_shadow_lo: optional, as nrse_adamw_params.p_shadow_lo */

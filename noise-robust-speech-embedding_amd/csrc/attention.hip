@@ -609,6 +609,7 @@ int nrse_attn_bwd_mfma(const nrse_attn_bwd_params* p, hipStream_t st);
 int nrse_attn_use_mfma(int dtype, int head_dim);
 
 extern "C" int nrse_attn_fwd(const nrse_attn_fwd_params* p, void* stream) {
+  NRSE_CHECK_PARAMS(p, "nrse_attn_fwd");
   NRSE_REQUIRE(p && p->qkv && p->gate && (p->bias || p->bias_vec) && p->ctx && p->lse && p->batch > 0 && p->T > 0 && p->H > 0,
                "nrse_attn_fwd: bad args");
   if (p->head_dim != HD) { nrse_set_error("nrse_attn_fwd: head_dim %d != 64", p->head_dim); return NRSE_ERR_UNSUPPORTED; }
@@ -628,12 +629,14 @@ extern "C" int nrse_attn_fwd(const nrse_attn_fwd_params* p, void* stream) {
 
 // diag partial rows: one per (h, b, key tile) on both paths
 extern "C" long long nrse_attn_bwd_workspace(const nrse_attn_bwd_params* p) {
+  NRSE_CHECK_PARAMS(p, "nrse_attn_bwd_workspace");
   if (!p || p->T <= 0 || p->batch <= 0 || p->H <= 0) return 0;
   const long long nt = (p->T + 63) / 64;
   return (long long)p->H * p->batch * nt * (2LL * p->T - 1);
 }
 
 extern "C" int nrse_attn_bwd(const nrse_attn_bwd_params* p, void* stream) {
+  NRSE_CHECK_PARAMS(p, "nrse_attn_bwd");
   NRSE_REQUIRE(p && p->qkv && p->gate && (p->bias || p->bias_vec) && p->ctx && p->dctx && p->lse && p->delta && p->dqkv && p->dgate &&
                p->batch > 0 && p->T > 0 && p->H > 0, "nrse_attn_bwd: bad args");
   if (p->head_dim != HD) { nrse_set_error("nrse_attn_bwd: head_dim %d != 64", p->head_dim); return NRSE_ERR_UNSUPPORTED; }

@@ -26,7 +26,7 @@ int nrse_check_launch(const char* what) {
 
 extern "C" const char* nrse_last_error(void) { return g_err; }
 
-extern "C" int nrse_abi_version(void) { return 9; }
+extern "C" int nrse_abi_version(void) { return NRSE_ABI_VERSION; }
 
 extern "C" int nrse_init(int device, nrse_caps* caps) {
   hipDeviceProp_t prop;

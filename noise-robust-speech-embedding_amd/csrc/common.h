@@ -72,6 +72,14 @@ NRSE_DEV uint32_t fp8x4(float a, float b, float c, float d) {
   return (uint32_t)w;
 }
 NRSE_DEV unsigned char fp8_1(float a) { return (unsigned char)(fp8x4(a, 0.f, 0.f, 0.f) & 0xffu); }
+// ABI 10: how many of 4 values fp8x4 saturates (|v| > 448, clamped instead of rounded), and the
+// producers' counter update (an atomic only when something saturated: never in normal operation)
+NRSE_DEV int fp8_nsat4(float a, float b, float c, float d) {
+  return (int)(fabsf(a) > 448.f) + (int)(fabsf(b) > 448.f) + (int)(fabsf(c) > 448.f) + (int)(fabsf(d) > 448.f);
+}
+NRSE_DEV void sat_count_add(unsigned int* cnt, int n) {
+  if (n && cnt) atomicAdd(cnt, (unsigned int)n);
+}
 // the split-weight mode's fp8 correction of x (nrse_split_lo8): (x - bf16(x)) * sc, sc = 2^lo8_exp
 NRSE_DEV float lo_resid(float x) { return x - __uint_as_float((uint32_t)f2bf(x) << 16); }
 // fp8 of 4 values as they are stored in bf16 (the a8 operand is fp8(bf16 y), one rounding path)
@@ -80,7 +88,7 @@ NRSE_DEV uint32_t fp8x4_of_bf(const float* o) {
 }
 // the two fp8 correction planes of 4 exact values o (ABI 7, y8_split): lo8 = fp8((o - bf16(o)) sc)
 // (sc = 2^y8_exp), hi8 = fp8(bf16(o)) -- the conv stack's a8 segments of the split-weight mode
-NRSE_DEV void fp8x4_split(const float* o, float sc, uint32_t& lo8, uint32_t& hi8) {
+NRSE_DEV void fp8x4_split(const float* o, float sc, uint32_t& lo8, uint32_t& hi8, int* nsat = nullptr) {
   float h[4], l[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -89,6 +97,7 @@ NRSE_DEV void fp8x4_split(const float* o, float sc, uint32_t& lo8, uint32_t& hi8
   }
   lo8 = fp8x4(l[0], l[1], l[2], l[3]);
   hi8 = fp8x4(h[0], h[1], h[2], h[3]);
+  if (nsat) *nsat += fp8_nsat4(l[0], l[1], l[2], l[3]) + fp8_nsat4(h[0], h[1], h[2], h[3]);
 }
 // ---- MXFP6 (ABI 8, NRSE_MX6): e2m3 values in blocks of 32 with an E8M0 scale each; block b of a
 // row = 32 bytes at byte 32b: [24 B, value j at bits 6j..6j+5 | scale byte | 7 zero bytes]
@@ -434,6 +443,23 @@ int nrse_check_launch(const char* what);
       nrse_set_error(__VA_ARGS__);           \
       return NRSE_ERR_ARG;                   \
     }                                        \
+  } while (0)
+
+// ABI 10 handshake: a params struct whose struct_size is not this build's sizeof is refused before
+// any other field is read (a caller compiled against another nrse_hip.h passes a shorter or longer
+// struct). RET is the entry point's error value (NRSE_ERR_ARG for both int and long long returns).
+#define NRSE_CHECK_PARAMS(p, fn)                                                                        \
+  do {                                                                                                \
+    if (!(p)) {                                                                                       \
+      nrse_set_error("%s: null params", fn);                                                          \
+      return NRSE_ERR_ARG;                                                                            \
+    }                                                                                                 \
+    if ((p)->struct_size != (uint32_t)sizeof(*(p))) {                                                 \
+      nrse_set_error("%s: struct_size %u, this library's is %u (caller built against another "        \
+                     "nrse_hip.h; library ABI %d)", fn, (unsigned)(p)->struct_size,                   \
+                     (unsigned)sizeof(*(p)), NRSE_ABI_VERSION);                                       \
+      return NRSE_ERR_ARG;                                                                            \
+    }                                                                                                 \
   } while (0)
 
 static inline int nrse_cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }

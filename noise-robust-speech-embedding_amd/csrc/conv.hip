@@ -252,8 +252,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
             l8 = mx6_g4(lo, lane, g, 16);
             h8 = mx6_g4(h, lane, g, 16);
           } else {
-            fp8x4_split(o, sc8, l8.x, h8.x);
-            fp8x4_split(o + 4, sc8, l8.y, h8.y);
+            int ns = 0;
+            fp8x4_split(o, sc8, l8.x, h8.x, &ns);
+            fp8x4_split(o + 4, sc8, l8.y, h8.y, &ns);
+            sat_count_add(p.sat_count, ns);
           }
           unsigned char* d8 = (unsigned char*)p.y8 + row * C + c0;
           *reinterpret_cast<uint2*>(d8) = l8;
@@ -1007,6 +1009,7 @@ __global__ void wn_dg_kernel(const float* __restrict__ sdot, const float* __rest
 }  // namespace
 
 extern "C" int nrse_conv0_fwd(const nrse_conv0_params* p, void* stream) {
+  NRSE_CHECK_PARAMS(p, "nrse_conv0_fwd");
   NRSE_REQUIRE(p && p->wav && p->w && p->gamma && p->beta && p->out && p->mean && p->rstd, "nrse_conv0_fwd: bad args");
   NRSE_REQUIRE(p->k > 0 && p->k <= KMAX && p->T0 == (p->L - p->k) / p->s + 1, "nrse_conv0_fwd: bad geometry");
   NRSE_REQUIRE((long long)p->batch * p->T0 < (1LL << 31), "nrse_conv0_fwd: too many rows");
@@ -1076,6 +1079,7 @@ static long long conv0_bwd_blocks(const nrse_conv0_params* p) {
 }
 
 extern "C" int nrse_conv0_bwd(const nrse_conv0_params* p, void* stream) {
+  NRSE_CHECK_PARAMS(p, "nrse_conv0_bwd");
   NRSE_REQUIRE(p && p->wav && p->w && p->gamma && p->beta && p->mean && p->rstd && p->dy && p->dw && p->dgamma &&
                p->dbeta, "nrse_conv0_bwd: bad args");
   NRSE_REQUIRE(p->k > 0 && p->k <= KMAX, "nrse_conv0_bwd: bad k");
@@ -1112,6 +1116,7 @@ extern "C" int nrse_conv0_bwd(const nrse_conv0_params* p, void* stream) {
 }
 
 extern "C" long long nrse_conv0_bwd_workspace(const nrse_conv0_params* p) {
+  NRSE_CHECK_PARAMS(p, "nrse_conv0_bwd_workspace");
   if (!p || p->batch <= 0 || p->T0 <= 0) return 0;
   return conv0_bwd_blocks(p) * (p->k + 2) * (long long)p->C;
 }

@@ -354,7 +354,7 @@ int launch_dt(const nrse_gemm_params* p, hipStream_t st) {
 }  // namespace
 
 extern "C" int nrse_gemm(const nrse_gemm_params* p, void* stream) {
-  NRSE_REQUIRE(p != nullptr, "nrse_gemm: null params");
+  NRSE_CHECK_PARAMS(p, "nrse_gemm");
   NRSE_REQUIRE(p->a.ptr && p->b.ptr && p->c, "nrse_gemm: null operand");
   NRSE_REQUIRE(p->M > 0 && p->N > 0 && p->K >= 0 && p->nseg >= 1 && p->splits >= 1 && p->batch >= 1 && p->zdiv >= 1,
                "nrse_gemm: bad sizes M=%d N=%d K=%d nseg=%d splits=%d batch=%d zdiv=%d", p->M, p->N, p->K, p->nseg,
@@ -459,6 +459,7 @@ extern "C" int nrse_gemm(const nrse_gemm_params* p, void* stream) {
 
 // floats of colsum_part any kernel generation may write: 2 rows of N per (z, 128-row M-tile)
 extern "C" long long nrse_gemm_colsum_workspace(const nrse_gemm_params* p) {
+  NRSE_CHECK_PARAMS(p, "nrse_gemm_colsum_workspace");
   if (!p || p->M <= 0 || p->N <= 0) return 0;
   return 2LL * nrse_cdiv(p->M, 128) * p->batch * p->splits * p->N;
 }

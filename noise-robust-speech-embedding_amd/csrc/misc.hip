@@ -257,15 +257,23 @@ __global__ void split_bf16_kernel(const float* __restrict__ x, bf16_t* __restric
 }
 
 // the fp8 correction plane of the split (nrse_split_lo8), 4 elements (one u32 of fp8) per lane
-__global__ void split_lo8_kernel(const float* __restrict__ x, uint32_t* __restrict__ lo8, float sc, long long n) {
+__global__ void split_lo8_kernel(const float* __restrict__ x, uint32_t* __restrict__ lo8, float sc, long long n,
+                                 unsigned int* __restrict__ sat) {
   const long long n4 = n / 4;
+  int ns = 0;
   for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (long long)gridDim.x * blockDim.x) {
     const float4 v = reinterpret_cast<const float4*>(x)[q];
-    lo8[q] = fp8x4(lo_resid(v.x) * sc, lo_resid(v.y) * sc, lo_resid(v.z) * sc, lo_resid(v.w) * sc);
+    const float a = lo_resid(v.x) * sc, b = lo_resid(v.y) * sc, c = lo_resid(v.z) * sc, d = lo_resid(v.w) * sc;
+    lo8[q] = fp8x4(a, b, c, d);
+    ns += fp8_nsat4(a, b, c, d);
   }
   for (long long i = n4 * 4 + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (long long)gridDim.x * blockDim.x)
-    reinterpret_cast<unsigned char*>(lo8)[i] = fp8_1(lo_resid(x[i]) * sc);
+       i += (long long)gridDim.x * blockDim.x) {
+    const float a = lo_resid(x[i]) * sc;
+    reinterpret_cast<unsigned char*>(lo8)[i] = fp8_1(a);
+    ns += fp8_nsat4(a, 0.f, 0.f, 0.f);
+  }
+  sat_count_add(sat, ns);
 }
 
 __global__ void cast_fp8_kernel(const void* __restrict__ x, int xdt, unsigned char* __restrict__ y, long long n) {
@@ -460,12 +468,13 @@ extern "C" int nrse_split_bf16(const float* x, void* hi, void* lo, long long n, 
   return nrse_check_launch("nrse_split_bf16");
 }
 
-extern "C" int nrse_split_lo8(const float* x, void* lo8, int lo8_exp, long long n, void* stream) {
+extern "C" int nrse_split_lo8(const float* x, void* lo8, int lo8_exp, long long n, unsigned int* sat_count,
+                              void* stream) {
   NRSE_REQUIRE(x && lo8 && n >= 0 && lo8_exp > -64 && lo8_exp < 64, "nrse_split_lo8: bad args");
   NRSE_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)lo8 & 3) == 0, "nrse_split_lo8: x 16-byte, lo8 4-byte aligned");
   if (n == 0) return NRSE_OK;
   hipLaunchKernelGGL(split_lo8_kernel, dim3(blocks_for(n / 4 + 1)), dim3(256), 0, (hipStream_t)stream, x,
-                     (uint32_t*)lo8, ldexpf(1.f, lo8_exp), n);
+                     (uint32_t*)lo8, ldexpf(1.f, lo8_exp), n, sat_count);
   return nrse_check_launch("nrse_split_lo8");
 }
 
@@ -786,6 +795,12 @@ extern "C" int nrse_reduce_defer(int on) {
 }
 
 extern "C" int nrse_reduce_pending(void) { return g_defer.count; }
+
+extern "C" int nrse_reduce_discard(void) {
+  g_defer.count = 0;
+  g_defer.on = false;
+  return 0;
+}
 
 extern "C" int nrse_reduce_flush(void* stream) {
   const hipStream_t st = (hipStream_t)stream;

@@ -72,11 +72,15 @@ NRSE_DEV void store_y8(const nrse_ln_fwd_params& p, long long i, const float* o)
   }
   if (p.y8_split) {
     uint32_t lo, hi;
-    fp8x4_split(o, __builtin_ldexpf(1.f, p.y8_exp), lo, hi);
+    int ns = 0;
+    fp8x4_split(o, __builtin_ldexpf(1.f, p.y8_exp), lo, hi, &ns);
     *reinterpret_cast<uint32_t*>(y8) = lo;
     *reinterpret_cast<uint32_t*>(y8 + p.rows * p.C) = hi;
+    sat_count_add(p.sat_count, ns);
   } else {
     *reinterpret_cast<uint32_t*>(y8) = fp8x4_of_bf(o);
+    // (|bf16 o| > 448 iff |o| >= 448 + half a bf16 ulp: the stored value decides)
+    sat_count_add(p.sat_count, fp8_nsat4(bf2f(f2bf(o[0])), bf2f(f2bf(o[1])), bf2f(f2bf(o[2])), bf2f(f2bf(o[3]))));
   }
 }
 
@@ -639,6 +643,7 @@ bool c_ok(int C) { return C == 256 || C == 512 || C == 1024; }
 }  // namespace
 
 extern "C" int nrse_layernorm_fwd(const nrse_ln_fwd_params* p, void* stream) {
+  NRSE_CHECK_PARAMS(p, "nrse_layernorm_fwd");
   NRSE_REQUIRE(p && p->x && p->y && p->gamma && p->beta && p->rows > 0, "nrse_layernorm_fwd: bad args");
   if (!c_ok(p->C)) { nrse_set_error("nrse_layernorm_fwd: C=%d not in {256,512,1024}", p->C); return NRSE_ERR_UNSUPPORTED; }
   NRSE_REQUIRE(p->y_dtype == NRSE_F32 || p->y_dtype == NRSE_BF16 || p->y_dtype == NRSE_BF16X3,
@@ -691,6 +696,7 @@ static bool xf_enabled() {
 }
 
 extern "C" int nrse_layernorm_bwd(const nrse_ln_bwd_params* p, void* stream) {
+  NRSE_CHECK_PARAMS(p, "nrse_layernorm_bwd");
   NRSE_REQUIRE(p && p->dy && p->x && p->gamma && p->mean && p->rstd && p->dx && p->rows > 0,
                "nrse_layernorm_bwd: bad args");
   NRSE_REQUIRE(!(p->flags & (NRSE_LN_GELU | NRSE_LN_RELU)) || p->beta, "nrse_layernorm_bwd: GELU/ReLU need beta");
@@ -748,6 +754,7 @@ extern "C" int nrse_layernorm_bwd(const nrse_ln_bwd_params* p, void* stream) {
 }
 
 extern "C" long long nrse_layernorm_bwd_workspace(const nrse_ln_bwd_params* p) {
+  NRSE_CHECK_PARAMS(p, "nrse_layernorm_bwd_workspace");
   if (!p || p->rows <= 0) return 0;
   return ln_bwd_blocks(p) * ln_bwd_nd(p) * (long long)p->C;
 }

@@ -62,24 +62,29 @@ __global__ __launch_bounds__(256) void sum_parts_kernel(const double* __restrict
 NRSE_DEV float ema_mix(float t, float o, float decay, float om) { return fmaf(decay, t, om * o); }
 
 // one element of the fused target EMA (nrse_adamw_params.ema_t), as ema_kernel's scalar tail
-NRSE_DEV void ema_one(const nrse_adamw_params& p, long long i, float pn, float eom, float sc8) {
+NRSE_DEV void ema_one(const nrse_adamw_params& p, long long i, float pn, float eom, float sc8, int& ns) {
   const float t = ema_mix(p.ema_t[i], pn, p.ema_decay, eom);
   p.ema_t[i] = t;
   if (p.ema_shadow) store_from_f(p.ema_shadow, p.ema_shadow_dtype, i, t);
   if (p.ema_shadow_lo) ((bf16_t*)p.ema_shadow_lo)[i] = bf16_lo(t);
-  if (p.ema_shadow_lo8) ((unsigned char*)p.ema_shadow_lo8)[i] = fp8_1(lo_resid(t) * sc8);
+  if (p.ema_shadow_lo8) {
+    const float l = lo_resid(t) * sc8;
+    ((unsigned char*)p.ema_shadow_lo8)[i] = fp8_1(l);
+    ns += fp8_nsat4(l, 0.f, 0.f, 0.f);
+  }
 }
 
 // the fp8 correction plane of 4 consecutive weights at float4 index q (ABI 6); mx: the MXFP6 form
 // (ABI 8), a block = the 8 lanes q & ~7 .. (all live together: the host requires n % 32 == 0)
-NRSE_DEV void store_lo8x4(void* lo8, long long q, const float* x, float sc8, bool mx) {
+NRSE_DEV void store_lo8x4(void* lo8, long long q, const float* x, float sc8, bool mx, int& ns) {
   if (mx) {
     const float l[4] = {lo_resid(x[0]), lo_resid(x[1]), lo_resid(x[2]), lo_resid(x[3])};
     reinterpret_cast<uint32_t*>(lo8)[q] = mx6_g8(l, threadIdx.x & 63);
     return;
   }
-  reinterpret_cast<uint32_t*>(lo8)[q] =
-      fp8x4(lo_resid(x[0]) * sc8, lo_resid(x[1]) * sc8, lo_resid(x[2]) * sc8, lo_resid(x[3]) * sc8);
+  const float a = lo_resid(x[0]) * sc8, b = lo_resid(x[1]) * sc8, c = lo_resid(x[2]) * sc8, d = lo_resid(x[3]) * sc8;
+  reinterpret_cast<uint32_t*>(lo8)[q] = fp8x4(a, b, c, d);
+  ns += fp8_nsat4(a, b, c, d);
 }
 
 __global__ __launch_bounds__(256) void adamw_kernel(const nrse_adamw_params p) {
@@ -103,6 +108,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(const nrse_adamw_params p) {
   const float sc8 = ldexpf(1.f, p.lo8_exp);
   const bool mx = p.lo8_dtype == NRSE_MX6;
   const bool ema4 = p.ema_t && e4 > 0;  // uniform: a whole EMA quad exists to load
+  int ns = 0;                           // saturated fp8 corrections (ABI 10 sat_count)
   for (long long q = (long long)blockIdx.x * 256 + threadIdx.x; q < n4; q += (long long)gridDim.x * 256) {
     // the five operand quads issued together: the target's quad (from a clamped index past the
     // EMA range) before the stores below, which may alias it and would otherwise order its load
@@ -135,7 +141,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(const nrse_adamw_params p) {
         reinterpret_cast<float4*>(p.p_shadow)[q] = pv;
       }
     }
-    if (p.p_shadow_lo8) store_lo8x4(p.p_shadow_lo8, q, pa, sc8, mx);
+    if (p.p_shadow_lo8) store_lo8x4(p.p_shadow_lo8, q, pa, sc8, mx, ns);
     if (p.ema_t) {
       if (q < e4) {
         tv.x = ema_mix(tv.x, pv.x, p.ema_decay, eom); tv.y = ema_mix(tv.y, pv.y, p.ema_decay, eom);
@@ -145,13 +151,13 @@ __global__ __launch_bounds__(256) void adamw_kernel(const nrse_adamw_params p) {
           if (p.ema_shadow_dtype == NRSE_BF16) store_bf16x4(p.ema_shadow, p.ema_shadow_lo, q, &tv.x);
           else reinterpret_cast<float4*>(p.ema_shadow)[q] = tv;
         }
-        if (p.ema_shadow_lo8) store_lo8x4(p.ema_shadow_lo8, q, &tv.x, sc8, mx);
+        if (p.ema_shadow_lo8) store_lo8x4(p.ema_shadow_lo8, q, &tv.x, sc8, mx, ns);
       } else if (q == e4) {
         // the quad holding the EMA range's end: its first ema_n - 4 q elements, from this thread's
         // updated registers
 #pragma unroll
         for (int e = 0; e < 3; ++e)
-          if (4 * q + e < p.ema_n) ema_one(p, 4 * q + e, pa[e], eom, sc8);
+          if (4 * q + e < p.ema_n) ema_one(p, 4 * q + e, pa[e], eom, sc8, ns);
       }
     }
   }
@@ -165,9 +171,14 @@ __global__ __launch_bounds__(256) void adamw_kernel(const nrse_adamw_params p) {
     p.p[i] = w - step_size * p.m[i] / denom;
     if (p.p_shadow) store_from_f(p.p_shadow, p.shadow_dtype, i, p.p[i]);
     if (p.p_shadow_lo) ((bf16_t*)p.p_shadow_lo)[i] = bf16_lo(p.p[i]);
-    if (p.p_shadow_lo8) ((unsigned char*)p.p_shadow_lo8)[i] = fp8_1(lo_resid(p.p[i]) * sc8);
-    if (p.ema_t && i < p.ema_n) ema_one(p, i, p.p[i], eom, sc8);
+    if (p.p_shadow_lo8) {
+      const float l = lo_resid(p.p[i]) * sc8;
+      ((unsigned char*)p.p_shadow_lo8)[i] = fp8_1(l);
+      ns += fp8_nsat4(l, 0.f, 0.f, 0.f);
+    }
+    if (p.ema_t && i < p.ema_n) ema_one(p, i, p.p[i], eom, sc8, ns);
   }
+  sat_count_add(p.sat_count, ns);
 }
 
 __global__ __launch_bounds__(256) void ema_kernel(float* __restrict__ t, const float* __restrict__ o,
@@ -243,6 +254,7 @@ extern "C" int nrse_sumsq(const float* x, long long n, double* out, double* part
 }
 
 extern "C" int nrse_adamw(const nrse_adamw_params* p, void* stream) {
+  NRSE_CHECK_PARAMS(p, "nrse_adamw");
   NRSE_REQUIRE(p && p->p && p->g && p->m && p->v && p->n >= 0 && p->step >= 1, "nrse_adamw: bad args");
   NRSE_REQUIRE((((uintptr_t)p->p | (uintptr_t)p->g | (uintptr_t)p->m | (uintptr_t)p->v) & 15) == 0,
                "nrse_adamw: buffers must be 16-byte aligned");

@@ -46,13 +46,26 @@ class NrseCaps(ctypes.Structure):
                 ("lds_bytes_per_cu", c_int), ("hbm_bytes", c_ll), ("arch", ctypes.c_char * 32)]
 
 
+ABI_VERSION = 10   # NRSE_ABI_VERSION of include/nrse_hip.h this binding is written against
+
+
+class _Sized(ctypes.Structure):
+    """A params struct of the ABI 10 handshake: its first field is `struct_size`, stamped with
+    sizeof(struct) as laid out here; the library refuses any other value (NRSE_ERR_ARG), so a
+    binding out of step with the header fails loudly instead of having its struct over-read.
+    Positional constructor arguments fill the fields after struct_size."""
+
+    def __init__(self, *args, **kw):
+        super().__init__(ctypes.sizeof(type(self)), *args, **kw)
+
+
 class GemmOperand(ctypes.Structure):
     _fields_ = [("ptr", c_vp), ("dtype", c_int), ("kcontig", c_int), ("chunk_shift", c_int),
                 ("ld", c_ll), ("ld_chunk", c_ll), ("seg_stride", c_ll), ("z1", c_ll), ("z2", c_ll)]
 
 
-class GemmParams(ctypes.Structure):
-    _fields_ = [("a", GemmOperand), ("b", GemmOperand),
+class GemmParams(_Sized):
+    _fields_ = [("struct_size", c_u32), ("a", GemmOperand), ("b", GemmOperand),
                 ("M", c_int), ("N", c_int), ("K", c_int), ("nseg", c_int),
                 ("splits", c_int), ("batch", c_int), ("zdiv", c_int),
                 ("alpha", c_f), ("flags", c_int),
@@ -67,14 +80,14 @@ class GemmParams(ctypes.Structure):
                 ("c8", c_vp), ("ldc8", c_ll), ("c8_dtype", c_int)]
 
 
-class LnFwdParams(ctypes.Structure):
-    _fields_ = [("x", c_vp), ("x_dtype", c_int), ("gamma", c_vp), ("beta", c_vp), ("y", c_vp), ("y_dtype", c_int),
+class LnFwdParams(_Sized):
+    _fields_ = [("struct_size", c_u32), ("x", c_vp), ("x_dtype", c_int), ("gamma", c_vp), ("beta", c_vp), ("y", c_vp), ("y_dtype", c_int),
                 ("mean", c_vp), ("rstd", c_vp), ("rows", c_ll), ("C", c_int), ("eps", c_f), ("flags", c_int),
-                ("y8", c_vp), ("y8_split", c_int), ("y8_exp", c_int), ("y8_dtype", c_int)]
+                ("y8", c_vp), ("y8_split", c_int), ("y8_exp", c_int), ("y8_dtype", c_int), ("sat_count", c_vp)]
 
 
-class LnBwdParams(ctypes.Structure):
-    _fields_ = [("dy", c_vp), ("dy_dtype", c_int), ("dy_mode", c_int),
+class LnBwdParams(_Sized):
+    _fields_ = [("struct_size", c_u32), ("dy", c_vp), ("dy_dtype", c_int), ("dy_mode", c_int),
                 ("col_k", c_int), ("col_s", c_int), ("col_tout", c_int), ("col_tin", c_int),
                 ("bcast_t", c_int), ("dy_scale", c_f),
                 ("x", c_vp), ("x_dtype", c_int), ("gamma", c_vp), ("beta", c_vp), ("mean", c_vp), ("rstd", c_vp),
@@ -84,37 +97,37 @@ class LnBwdParams(ctypes.Structure):
                 ("part", c_vp), ("gate_dp", c_vp), ("gate_w", c_vp)]
 
 
-class AttnFwdParams(ctypes.Structure):
-    _fields_ = [("qkv", c_vp), ("dtype", c_int), ("gate", c_vp), ("bias", c_vp), ("ctx", c_vp), ("lse", c_vp),
+class AttnFwdParams(_Sized):
+    _fields_ = [("struct_size", c_u32), ("qkv", c_vp), ("dtype", c_int), ("gate", c_vp), ("bias", c_vp), ("ctx", c_vp), ("lse", c_vp),
                 ("batch", c_int), ("T", c_int), ("H", c_int), ("head_dim", c_int), ("scale", c_f),
                 ("dropout_p", c_f), ("seed", c_u32), ("bias_vec", c_vp), ("drop_mask", c_vp),
                 ("drop_mask_in", c_int), ("ctx8", c_vp), ("ctx8_dtype", c_int)]
 
 
-class AttnBwdParams(ctypes.Structure):
-    _fields_ = [("qkv", c_vp), ("dtype", c_int), ("gate", c_vp), ("bias", c_vp), ("ctx", c_vp), ("dctx", c_vp),
+class AttnBwdParams(_Sized):
+    _fields_ = [("struct_size", c_u32), ("qkv", c_vp), ("dtype", c_int), ("gate", c_vp), ("bias", c_vp), ("ctx", c_vp), ("dctx", c_vp),
                 ("lse", c_vp), ("delta", c_vp), ("dqkv", c_vp), ("dgate", c_vp), ("diag", c_vp),
                 ("batch", c_int), ("T", c_int), ("H", c_int), ("head_dim", c_int), ("scale", c_f),
                 ("dropout_p", c_f), ("seed", c_u32), ("bias_vec", c_vp), ("diag_part", c_vp), ("drop_mask", c_vp)]
 
 
-class Conv0Params(ctypes.Structure):
-    _fields_ = [("wav", c_vp), ("L", c_int), ("w", c_vp), ("gamma", c_vp), ("beta", c_vp), ("out", c_vp),
+class Conv0Params(_Sized):
+    _fields_ = [("struct_size", c_u32), ("wav", c_vp), ("L", c_int), ("w", c_vp), ("gamma", c_vp), ("beta", c_vp), ("out", c_vp),
                 ("out_dtype", c_int), ("mean", c_vp), ("rstd", c_vp),
                 ("dy", c_vp), ("dy_dtype", c_int), ("dy_mode", c_int), ("col_k", c_int), ("col_s", c_int),
                 ("col_tout", c_int), ("dw", c_vp), ("dgamma", c_vp), ("dbeta", c_vp),
                 ("batch", c_int), ("T0", c_int), ("C", c_int), ("k", c_int), ("s", c_int), ("eps", c_f),
-                ("part", c_vp), ("y8", c_vp), ("y8_exp", c_int), ("y8_dtype", c_int)]
+                ("part", c_vp), ("y8", c_vp), ("y8_exp", c_int), ("y8_dtype", c_int), ("sat_count", c_vp)]
 
 
-class AdamWParams(ctypes.Structure):
-    _fields_ = [("p", c_vp), ("g", c_vp), ("m", c_vp), ("v", c_vp), ("p_shadow", c_vp), ("shadow_dtype", c_int),
+class AdamWParams(_Sized):
+    _fields_ = [("struct_size", c_u32), ("p", c_vp), ("g", c_vp), ("m", c_vp), ("v", c_vp), ("p_shadow", c_vp), ("shadow_dtype", c_int),
                 ("n", c_ll), ("lr", c_f), ("beta1", c_f), ("beta2", c_f), ("eps", c_f), ("weight_decay", c_f),
                 ("step", c_int), ("max_norm", c_f), ("sumsq", c_vp), ("grad_scale", c_f),
                 ("p_shadow_lo", c_vp), ("ema_t", c_vp), ("ema_shadow", c_vp), ("ema_shadow_lo", c_vp),
                 ("ema_shadow_dtype", c_int), ("ema_decay", c_f), ("ema_n", c_ll),
                 ("p_shadow_lo8", c_vp), ("ema_shadow_lo8", c_vp), ("lo8_exp", c_int), ("zero_grad", c_int),
-                ("lo8_dtype", c_int)]
+                ("lo8_dtype", c_int), ("sat_count", c_vp)]
 
 
 _P = ctypes.POINTER
@@ -161,7 +174,7 @@ _SIGNATURES = {
     "nrse_colsum_workspace": ([c_ll, c_int], c_ll),
     "nrse_cast": ([c_vp, c_int, c_vp, c_int, c_ll, c_vp], c_int),
     "nrse_split_bf16": ([c_vp, c_vp, c_vp, c_ll, c_vp], c_int),
-    "nrse_split_lo8": ([c_vp, c_vp, c_int, c_ll, c_vp], c_int),
+    "nrse_split_lo8": ([c_vp, c_vp, c_int, c_ll, c_vp, c_vp], c_int),
     "nrse_cast_fp8": ([c_vp, c_int, c_vp, c_ll, c_vp], c_int),
     "nrse_split_lo_mx6": ([c_vp, c_vp, c_ll, c_vp], c_int),
     "nrse_cast_mx6": ([c_vp, c_int, c_vp, c_ll, c_vp], c_int),
@@ -171,6 +184,7 @@ _SIGNATURES = {
     "nrse_reduce_defer": ([c_int], c_int),
     "nrse_reduce_pending": ([], c_int),
     "nrse_reduce_flush": ([c_vp], c_int),
+    "nrse_reduce_discard": ([], c_int),
     "nrse_swap12": ([c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
     "nrse_gelu_bwd_pad": ([c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
     "nrse_bn_fwd": ([c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_f, c_f, c_int, c_int, c_vp], c_int),
@@ -212,6 +226,9 @@ def lib():
             fn = getattr(L, name)
             fn.argtypes = argt
             fn.restype = rest
+        v = int(L.nrse_abi_version())
+        if v != ABI_VERSION:
+            raise NrseError(f"{LIB_PATH} is ABI {v}, this binding is ABI {ABI_VERSION}: rebuild the library")
         _lib = L
     return _lib
 

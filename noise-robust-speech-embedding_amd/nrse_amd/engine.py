@@ -70,15 +70,17 @@ _FUSED_EMA = os.environ.get("NRSE_FUSED_EMA", "1") != "0"
 _SPLIT_LO8 = os.environ.get("NRSE_SPLIT_LO8", "1") != "0"
 # ... and the conv stack's two correction segments (x_lo w_hi + x_hi w_lo) as fp8 segments against
 # the activations' fp8 planes [fp8(x_lo 2^e) | fp8(x_hi)] (ABI 7) instead of two more bf16 segments;
-# NRSE_CONV_SPLIT8=0 restores the three bf16 planes. The exponent is fixed: 2^11 keeps both
-# (w - w_hi) 2^e and (x - x_hi) 2^e (each <= 2^-8 |.|) inside fp8's +-448 for |w|, |x| < 56 -- the
-# conv activations are GELU(LayerNorm) outputs, |x| <= sqrt(C) max|gamma| + max|beta| (23 at
-# gamma = 1, beta = 0); beyond that the conversion saturates (bounded error, never inf / NaN)
+# NRSE_CONV_SPLIT8=0 restores the three bf16 planes. The exponent (ABI 10: derived, no longer fixed)
+# keeps both (w - w_hi) 2^e and (x - x_hi) 2^e (each <= 2^-8 |.|) inside half of fp8's +-448: the
+# conv activations are GELU(LayerNorm) outputs, |x| <= sqrt(C) max|gamma| + max|beta| (23.6 at
+# gamma = 1, beta = 0: e = 11), so ByolEngine._set_lo8_planes takes e from the conv LayerNorms'
+# gamma / beta and the conv weights' range; NRSE_CONV_LO8_EXP pins it (A/B)
 # ABI 9: the backward's per-layer gradient reductions batched on the side stream (0: on the dX
 # chain's stream, one launch each, as before)
 _DEFER_REDUCE = os.environ.get("NRSE_DEFER_REDUCE", "1") != "0"
 _CONV_SPLIT8 = os.environ.get("NRSE_CONV_SPLIT8", "1") != "0"
-CONV_LO8_EXP = int(os.environ.get("NRSE_CONV_LO8_EXP", "11"))
+CONV_LO8_EXP = 11   # the derived value at the seeded init (gamma = 1, beta = 0)
+_CONV_LO8_PIN = os.environ.get("NRSE_CONV_LO8_EXP")
 # the correction operands as MXFP6 blocks (ABI 8: e2m3 with a scale per 32 elements, no exponents)
 # instead of fp8 e4m3: opt-in (NRSE_SPLIT_MX6=1). Measured slower (bf16sw 455 vs 466-468 pairs/s,
 # profiles/r05_mx6_ab.txt): on this part the 16x16x128 block-scaled MFMA the 256x256 GEMM's
@@ -87,6 +89,16 @@ CONV_LO8_EXP = int(os.environ.get("NRSE_CONV_LO8_EXP", "11"))
 # 32x32 accumulator layout in the correction segments
 _SPLIT_MX6 = os.environ.get("NRSE_SPLIT_MX6", "0") == "1"
 FP8 = K.FP8
+
+
+SAT_WEIGHTS, SAT_CONV, SAT_ACT = 0, 1, 2   # rows of ByolEngine.sat_buf
+
+
+def _headroom_exp(W: float) -> int:
+    """The fp8 correction exponent of values bounded by W: |v - bf16(v)| <= 2^-8 W, scaled by 2^e
+    to at most 224 (half of e4m3's 448: 2x headroom), e = floor(log2(224 * 256 / W))."""
+    e = int(math.floor(math.log2(224.0 * 256.0 / W))) if W > 0 else 0
+    return max(-60, min(60, e))
 
 
 @dataclass
@@ -155,7 +167,7 @@ class EncoderWeights:
         # fp8 form: conv_w8[i] = [fp8(w_hi) | fp8((w - w_hi) 2^conv_lo8_exp)] against the activations'
         # [fp8((x - x_hi) 2^e) | fp8(x_hi)]: x_hi w_hi (bf16) + 2^-e (x_lo8 w_hi8 + x_hi8 w_lo8)
         self.conv_split8 = bool(self.lo) and lo8 is not None and eng.conv_split8
-        self.conv_lo8_exp = CONV_LO8_EXP
+        self.conv_lo8_exp = eng.conv_lo8_exp
         self.conv_w8 = []
         for i in range(1, len(a.conv_dim)):
             w = self.m[f"feature_extractor.conv_layers.{i}.conv.weight"]
@@ -167,7 +179,7 @@ class EncoderWeights:
                 K.cast(r32, r)
                 w8 = torch.empty(2, co, k * ci, device=eng.dev, dtype=eng.corr_dt)
                 K.cast_fp8(r, w8[0])
-                K.split_lo8(r32, w8[1], self.conv_lo8_exp)
+                K.split_lo8(r32, w8[1], self.conv_lo8_exp, sat=eng.sat_buf[SAT_CONV:SAT_CONV + 1])
                 self.conv_r.append(r)
                 self.conv_lo.append(0)
                 self.conv_w8.append(w8)
@@ -241,6 +253,18 @@ class ByolEngine:
         # fp8 correction planes of the split-weight mode: fp8((w - bf16(w)) 2^lo8_exp)
         self.online_lo8 = self.target_lo8 = None
         self.lo8_exp = 0
+        self.conv_lo8_exp = CONV_LO8_EXP if _CONV_LO8_PIN is None else int(_CONV_LO8_PIN)
+        # ABI 10 saturation counters of the fp8 correction producers (cumulative since the last
+        # re-derivation of the exponents): [SAT_WEIGHTS] the layer weights' planes (AdamW / EMA,
+        # nrse_split_lo8), [SAT_CONV] the conv stack's weight and activation planes, [SAT_ACT] the
+        # layer LayerNorms' fp8(bf16 y) copies. Read back lagged by health.HealthMonitor, which calls
+        # rederive_split_exponents() when a count moves (no host sync in the step)
+        self.sat_buf = torch.zeros(4, device=self.dev, dtype=torch.int32)
+        self.sat_epoch = 0
+        # the bf16 lo planes of the layer weights are skipped by the overlapped optimizer's layer
+        # segments in the fp8 form (nothing reads them); a forward that falls back to them (fewer
+        # than 128 frames in the batch: no fp8 segments) rebuilds them first (_ensure_lo_planes)
+        self._lo_stale = {"online": False, "target": False}
         # the correction planes' dtype: fp8 e4m3 (K.FP8, default) or MXFP6 blocks (K.MX6, opt-in)
         self.corr_dt = K.MX6 if (_SPLIT_MX6 if split_mx6 is None else split_mx6) else FP8
         if self.cdt == F32:
@@ -304,6 +328,33 @@ class ByolEngine:
         self.ar_timing = False
         self.ar_events = []
 
+    def rederive_split_exponents(self) -> dict:
+        """Re-derive lo8_exp / conv_lo8_exp from the current weights and rewrite the fp8 correction
+        planes (host sync). Called when a saturation counter moved: the weights (or the conv
+        LayerNorms' gamma / beta) grew past the exponents' 2x headroom during training."""
+        self.sync_optimizer()
+        torch.cuda.current_stream(self.dev).synchronize()
+        counts = [int(v) for v in self.sat_buf.cpu()]
+        old = (self.lo8_exp, self.conv_lo8_exp)
+        if self.online_lo8 is not None:
+            self._set_lo8_planes()
+        torch.cuda.current_stream(self.dev).synchronize()
+        self.sat_buf.zero_()
+        self.sat_epoch += 1
+        return dict(counts=counts, old=old, new=(self.lo8_exp, self.conv_lo8_exp))
+
+    def _ensure_lo_planes(self, W: "EncoderWeights") -> None:
+        """Rebuild network W's bf16 lo plane if the overlapped optimizer skipped it (fp8 form) and a
+        forward is about to read it (the fallback for batches under 128 frames)."""
+        net = W.net
+        if not self._lo_stale.get(net):
+            return
+        self.sync_optimizer()
+        master, lo = (self.online, self.online_lo) if net == "online" else (self.target, self.target_lo)
+        scratch = torch.empty_like(lo)   # the hi plane is current: only lo is written
+        K.split_bf16(master, scratch, lo)
+        self._lo_stale[net] = False
+
     def refresh_shadows(self, which=("online", "target")) -> None:
         """Re-derive the bf16 GEMM-operand copies (and the split mode's lo planes) of the f32
         weights after they were changed outside the fused AdamW / EMA kernels."""
@@ -345,10 +396,30 @@ class ByolEngine:
             K.split_lo8(self.target, self.target_lo8)
             return
         W = max(float(t.abs().max()) for f in (self.online, self.target) for t in self._lo8_weights(f))
-        self.lo8_exp = int(math.floor(math.log2(224.0 * 256.0 / max(W, 1e-30)))) if W > 0 else 0
-        self.lo8_exp = max(-60, min(60, self.lo8_exp))
-        K.split_lo8(self.online, self.online_lo8, self.lo8_exp)
-        K.split_lo8(self.target, self.target_lo8, self.lo8_exp)
+        self.lo8_exp = _headroom_exp(W)
+        if _CONV_LO8_PIN is None:
+            self.conv_lo8_exp = _headroom_exp(self._conv_plane_bound())
+        sat = self.sat_buf[SAT_WEIGHTS:SAT_WEIGHTS + 1]
+        K.split_lo8(self.online, self.online_lo8, self.lo8_exp, sat=sat)
+        K.split_lo8(self.target, self.target_lo8, self.lo8_exp, sat=sat)
+
+    def _conv_plane_bound(self) -> float:
+        """The largest value the conv stack's fp8 correction planes carry unscaled (host sync): the
+        conv activations feeding conv 1..n-1 are GELU(LayerNorm_C) outputs, |x| <= sqrt(C) max|gamma|
+        + max|beta| (GELU(z) <= max(z, 0) + 0.17), and the conv weights' |w|; each residual is at
+        most 2^-8 of it (oracle/wavlm_byol.py conv_lo8_exponent restates this)."""
+        a = self.arch
+        B = 0.0
+        for flat in (self.online, self.target):
+            P = self.group_views(flat, "encoder")
+            for i in range(len(a.conv_dim) - 1):
+                pre = f"feature_extractor.conv_layers.{i}."
+                g = float(P[pre + "layer_norm.weight"].abs().max())
+                b = float(P[pre + "layer_norm.bias"].abs().max())
+                B = max(B, math.sqrt(a.conv_dim[i]) * g + b)
+            for i in range(1, len(a.conv_dim)):
+                B = max(B, float(P[f"feature_extractor.conv_layers.{i}.conv.weight"].abs().max()))
+        return B
 
     def bn_state(self, key: str) -> tuple:
         """(running_mean, running_var, num_batches_tracked) of a head BatchNorm; the counter is kept
@@ -480,7 +551,8 @@ class ByolEngine:
         rstd = torch.empty(B * T0, device=dev, dtype=F32)
         pre0 = "feature_extractor.conv_layers.0."
         K.conv0_fwd(wav, Pm[pre0 + "conv.weight"], Pm[pre0 + "layer_norm.weight"], Pm[pre0 + "layer_norm.bias"], y,
-                    mean, rstd, T0, k0, s0, a.eps, split3=split3, y8=x8, y8_exp=e8)
+                    mean, rstd, T0, k0, s0, a.eps, split3=split3, y8=x8, y8_exp=e8,
+                    sat=self.sat_buf[SAT_CONV:SAT_CONV + 1] if s8 else None)
         if need_grad:
             tape.conv.append(dict(mean=mean, rstd=rstd, T=T0))
         x, Tin, Cin = (y[0] if split3 else y), T0, C0
@@ -510,7 +582,8 @@ class ByolEngine:
             ro = torch.empty(B * Tout, device=dev, dtype=F32)
             p = f"feature_extractor.conv_layers.{i}."
             K.ln_fwd(pre_out, Pm[p + "layer_norm.weight"], Pm[p + "layer_norm.bias"], yo3, mo, ro, a.eps, gelu=True,
-                     split3=split3 and not last, y8=yo8, y8_exp=e8 if yo8 is not None else None)
+                     split3=split3 and not last, y8=yo8, y8_exp=e8 if yo8 is not None else None,
+                     sat=self.sat_buf[SAT_CONV:SAT_CONV + 1] if yo8 is not None else None)
             if need_grad:
                 tape.conv.append(dict(x=x, pre=pre_out, mean=mo, rstd=ro, Tin=Tin, T=Tout, k=k, s=s))
             x, x8, Tin, Cin = (yo3[0] if split3 and not last else yo3), yo8, Tout, C
@@ -573,7 +646,13 @@ class ByolEngine:
         # -------- transformer layers ([TF]modeling_wavlm.py:488-513, 355-373)
         F_ = a.ffn
         hcur = h0
-        lo8 = W.s8 is not None
+        # the fp8 correction segments need the 256x256 kernel (M = B*T >= 128 rows); a smaller batch
+        # (one clip under ~2.6 s, a short validation tail) takes the bf16 lo plane instead, rebuilt
+        # first if the overlapped optimizer skipped it
+        lo8 = W.s8 is not None and BT >= 128
+        if W.s8 is not None and not lo8:
+            self._ensure_lo_planes(W)
+        sat_a = self.sat_buf[SAT_ACT:SAT_ACT + 1] if lo8 else None
 
         def corr(x8, w8):
             # the weight correction of a layer GEMM: the fp8 segment (x8, w8) or the bf16 lo plane
@@ -610,7 +689,8 @@ class ByolEngine:
             r1 = torch.empty(BT, device=dev, dtype=F32)
             # split-weight mode, fp8 form: the LN outputs' fp8 copies feed the correction segments
             x1_8 = torch.empty(BT, H, device=dev, dtype=self.corr_dt) if lo8 else None
-            K.ln_fwd(hcur, Pm[p + "layer_norm.weight"], Pm[p + "layer_norm.bias"], x1, m1, r1, a.eps, y8=x1_8)
+            K.ln_fwd(hcur, Pm[p + "layer_norm.weight"], Pm[p + "layer_norm.bias"], x1, m1, r1, a.eps, y8=x1_8,
+                     sat=sat_a)
             qkv = torch.empty(BT, 3 * H, device=dev, dtype=cdt)
             K.linear_fwd(x1, self.fused(W.s_flat, li, "qkv_w"), qkv, bias=self.fused(W.m_flat, li, "qkv_b"),
                          **corr(x1_8, self.fused(W.s8_flat, li, "qkv_w") if lo8 else None))
@@ -637,7 +717,7 @@ class ByolEngine:
             r2 = torch.empty(BT, device=dev, dtype=F32)
             x2_8 = torch.empty(BT, H, device=dev, dtype=self.corr_dt) if lo8 else None
             K.ln_fwd(hmid, Pm[p + "final_layer_norm.weight"], Pm[p + "final_layer_norm.bias"], x2, m2, r2, a.eps,
-                     y8=x2_8)
+                     y8=x2_8, sat=sat_a)
             f1pre = torch.empty(BT, F_, device=dev, dtype=cdt) if need_grad else None
             g1 = torch.empty(BT, F_, device=dev, dtype=cdt)
             # (fp8 form: the FFN-up epilogue also writes fp8(g1), FFN-down's correction operand; the
@@ -703,17 +783,7 @@ class ByolEngine:
         dh = torch.empty(BT, H, device=dev, dtype=F32)
         order = list(reversed(tape.layers))
 
-        def ffn_out_dropout(j):
-            """The fused consumer of a layer-output gradient: layer order[j]'s FFN output-dropout
-            backward + output_dense bias gradient (kwargs of K.ln_bwd), and its bf16/f32 result."""
-            if j >= len(order):
-                return None, {}
-            lj = order[j]["li"]
-            dv = torch.empty(BT, H, device=dev, dtype=cdt)
-            return dv, dict(dv=dv, dv_colsum=Gv[f"encoder.layers.{lj}.feed_forward.output_dense.bias"], dv_p=php,
-                            dv_seed=R.site_seed(fseed, R.site_ffn_out(lj)))
-
-        dv2_next, kw = ffn_out_dropout(0)
+        dv2_next, kw = self._ffn_out_dropout(order, 0, Gv, BT, fseed)
         K.ln_bwd(demb, hfin, Pm["encoder.layer_norm.weight"], mf, rf, dh, dgamma=Gv["encoder.layer_norm.weight"],
                  dbeta=Gv["encoder.layer_norm.bias"], mode=_lib.DY_BCAST, bcast_t=T, dy_scale=1.0 / T, rows=BT, **kw)
         tape.final = None
@@ -728,6 +798,39 @@ class ByolEngine:
         # the dX chain; their destinations are read only by the all-reduce units (enqueued on the
         # side stream after them), the rel-pos bias backward and the optimizer (after the joins)
         defer = _DEFER_REDUCE and not _SERIAL_TARGET
+        if defer and K.reduce_pending():
+            raise _lib.NrseError(f"{K.reduce_pending()} deferred reductions pending before the backward")
+        try:
+            dh = self._layers_backward(order, tape, Gv, W, dh, dv2_next, diag, delta, defer, on_layer)
+        except BaseException:
+            if defer:
+                K.reduce_discard()   # the queued jobs' workspaces are about to be released: never flush them
+            raise
+        self._front_backward(tape, Gv, W, dh, diag, front)
+
+    def _ffn_out_dropout(self, order, j, Gv, BT, fseed):
+        """The fused consumer of a layer-output gradient: layer order[j]'s FFN output-dropout
+        backward + output_dense bias gradient (kwargs of K.ln_bwd), and its bf16/f32 result."""
+        if j >= len(order):
+            return None, {}
+        lj = order[j]["li"]
+        dv = torch.empty(BT, self.arch.hidden, device=self.dev, dtype=self.cdt)
+        return dv, dict(dv=dv, dv_colsum=Gv[f"encoder.layers.{lj}.feed_forward.output_dense.bias"],
+                        dv_p=self.arch.hidden_dropout, dv_seed=R.site_seed(fseed, R.site_ffn_out(lj)))
+
+    def _layers_backward(self, order, tape, Gv, W, dh, dv2_next, diag, delta, defer, on_layer):
+        """The transformer layers' backward, top layer first (encoder_backward); returns the
+        gradient of the first layer's input."""
+        a = self.arch
+        cdt = self.cdt
+        dev = self.dev
+        B, T = tape.B, tape.T
+        H, F_, nh = a.hidden, a.ffn, a.heads
+        BT = B * T
+        Pm, Ps = W.m, W.s
+        fseed = tape.fseed
+        php, pat, pact = a.hidden_dropout, a.attention_dropout, a.activation_dropout
+        main = torch.cuda.current_stream(dev)
         for j, L_ in enumerate(order):
             li = L_["li"]
             p = f"encoder.layers.{li}."
@@ -785,7 +888,7 @@ class ByolEngine:
                            Gv[at + "gru_rel_pos_linear.bias"], Gv[at + "gru_rel_pos_const"], B, T, nh)
             dhin = torch.empty(BT, H, device=dev, dtype=F32)
             # + the next (lower) layer's FFN output-dropout backward, fused
-            dv2_next, kw = ffn_out_dropout(j + 1)
+            dv2_next, kw = self._ffn_out_dropout(order, j + 1, Gv, BT, fseed)
             K.ln_bwd(dx1, L_["h_in"], Pm[p + "layer_norm.weight"], L_["m1"], L_["r1"], dhin, resid=dhmid,
                      dgamma=Gv[p + "layer_norm.weight"], dbeta=Gv[p + "layer_norm.bias"], gate_dp=gdp,
                      gate_w=Pm[at + "gru_rel_pos_linear.weight"] if gdp is not None else None, **kw)
@@ -800,6 +903,22 @@ class ByolEngine:
             if on_layer is not None:
                 on_layer(li)
         tape.layers = []
+        return dh
+
+    def _front_backward(self, tape, Gv, W, dh, diag, front):
+        """The rel-pos bias, positional conv, feature projection and conv stack backward
+        (encoder_backward, after the transformer layers)."""
+        a = self.arch
+        cdt = self.cdt
+        dev = self.dev
+        B, T = tape.B, tape.T
+        H, nh = a.hidden, a.heads
+        BT = B * T
+        Pm = W.m
+        Ps = W.s
+        fseed = tape.fseed
+        php = a.hidden_dropout
+        main = torch.cuda.current_stream(dev)
         main.wait_stream(self._bwd_side_stream())
         K.rel_bias_bwd(diag, *self.bucket_runs(T), Gv["encoder.layers.0.attention.rel_attn_embed.weight"], nh, T)
         front("rel")
@@ -1018,10 +1137,12 @@ class ByolEngine:
             W = EncoderWeights(self, self.online, self.online_sh, self.online.numel() if self.wsplit else 0,
                                lo8=self.online_lo8)
             W.m_flat, W.s_flat = self.online, (self.online_sh if self.online_sh is not None else self.online)
+            W.net = "online"
         else:
             W = EncoderWeights(self, self.target, self.target_sh, self.target.numel() if self.wsplit else 0,
                                lo8=self.target_lo8)
             W.m_flat, W.s_flat = self.target, (self.target_sh if self.target_sh is not None else self.target)
+            W.net = "target"
         return W
 
     def _bwd_side_stream(self) -> torch.cuda.Stream:
@@ -1190,7 +1311,8 @@ class ByolEngine:
         K.sumsq(self.grad, self.sumsq_buf)
         kw = dict(lr=lr, beta1=c.betas[0], beta2=c.betas[1], eps=c.eps, weight_decay=c.weight_decay,
                   step=self.step_count, max_norm=c.max_norm, sumsq_buf=self.sumsq_buf, grad_scale=grad_scale,
-                  lo8_exp=self.lo8_exp, zero_grad=c.fused_zero_grad)
+                  lo8_exp=self.lo8_exp, zero_grad=c.fused_zero_grad,
+                  sat=self.sat_buf[SAT_WEIGHTS:SAT_WEIGHTS + 1] if self.online_lo8 is not None else None)
         self._grad_zeroed = c.fused_zero_grad
         ne = self.layout.ema_numel
         o8, t8 = self.online_lo8, self.target_lo8
@@ -1204,7 +1326,7 @@ class ByolEngine:
                         shadow_lo8=o8, **kw)
                 K.ema(self.target, self.online[:ne], self.target_sh, c.ema_decay, shadow_lo=self.target_lo)
                 if t8 is not None:
-                    K.split_lo8(self.target, t8, self.lo8_exp)
+                    K.split_lo8(self.target, t8, self.lo8_exp, sat=kw["sat"])
             self._opt_events = self._opt_done = None
             return
         main = torch.cuda.current_stream(self.dev)
@@ -1220,6 +1342,8 @@ class ByolEngine:
                 # lo plane, so the pure layer segments (1 .. L-1) skip its writes (2 B per weight
                 # for each network)
                 layer_only = o8 is not None and 1 <= si < len(self._segments) - 1
+                if layer_only:
+                    self._lo_stale = {"online": True, "target": True}
                 slo = None if layer_only else self.online_lo
                 tlo = None if layer_only else self.target_lo
                 if e > s:
@@ -1236,7 +1360,7 @@ class ByolEngine:
                         K.ema(self.target[s:te], self.online[s:te], tsh[s:te] if tsh is not None else None,
                               c.ema_decay, shadow_lo=tlo[s:te] if tlo is not None else None)
                         if t8 is not None:
-                            K.split_lo8(self.target[s:te], t8[s:te], self.lo8_exp)
+                            K.split_lo8(self.target[s:te], t8[s:te], self.lo8_exp, sat=kw["sat"])
                 ev = torch.cuda.Event()
                 ev.record(st)
                 events.append(ev)

@@ -57,32 +57,53 @@ def check_audio_tensor(tensor, name, config, max_threshold=1e6, min_threshold=1e
     return True
 
 
+SAT_NAMES = ("layer-weight fp8 correction planes", "conv-stack fp8 planes", "layer-activation fp8 copies")
+
+
 class HealthMonitor:
-    """Deferred reader of the engine's per-step health rows (engine.health_buf [4, 4])."""
+    """Deferred reader of the engine's per-step health rows (engine.health_buf [4, 4]) and, with
+    an engine, of its fp8 saturation counters (engine.sat_buf, ABI 10): a count that moved since
+    the engine's last re-derivation makes the monitor call engine.rederive_split_exponents() (the
+    split-weight mode's exponents follow weights that grew in training), with the same lag."""
 
     def __init__(self, lag: int = 2, names=HEALTH_NAMES):
         self.lag = lag
         self.names = names
         self._pending = deque()
         self.warnings = []       # (step, message), for tests and logs
+        self.rederived = []      # (step, engine.rederive_split_exponents() result)
 
-    def record(self, step: int, health_buf: torch.Tensor) -> None:
+    def record(self, step: int, health_buf: torch.Tensor, engine=None) -> None:
         host = torch.empty(health_buf.shape, dtype=health_buf.dtype, pin_memory=True)
         host.copy_(health_buf, non_blocking=True)
+        sat = None
+        if engine is not None and getattr(engine, "sat_buf", None) is not None:
+            sat = torch.empty(engine.sat_buf.shape, dtype=engine.sat_buf.dtype, pin_memory=True)
+            sat.copy_(engine.sat_buf, non_blocking=True)
+            sat = (sat, engine, engine.sat_epoch)
         ev = torch.cuda.Event()
         ev.record()
-        self._pending.append((step, host, ev))
+        self._pending.append((step, host, ev, sat))
         while len(self._pending) > self.lag:
             self._drain_one()
 
     def _drain_one(self) -> None:
-        step, host, ev = self._pending.popleft()
+        step, host, ev, sat = self._pending.popleft()
         ev.synchronize()
         for row, name in zip(host, self.names):
             ok, msg = interpret(row, name)
             if not ok:
                 logger.warning(f"step {step}: {msg}")
                 self.warnings.append((step, msg))
+        if sat is not None:
+            counts, engine, epoch = sat
+            # a copy taken before the last re-derivation reports counts that are already handled
+            if epoch == engine.sat_epoch and int(counts.abs().sum()) > 0:
+                what = ", ".join(f"{n}: {int(c)}" for n, c in zip(SAT_NAMES, counts) if int(c))
+                msg = f"fp8 correction conversions saturated ({what}); re-deriving the split-weight exponents"
+                logger.warning(f"step {step}: {msg}")
+                self.warnings.append((step, msg))
+                self.rederived.append((step, engine.rederive_split_exponents()))
 
     def flush(self) -> None:
         while self._pending:

@@ -81,6 +81,26 @@ def reduce_defer(on: bool) -> None:
         _DEFER_KEEP = []
 
 
+def reduce_discard() -> None:
+    """Drop the queued reductions unrun and turn deferral off (nrse_reduce_discard, ABI 10): the
+    error path of a backward that raised mid-layer, whose queued jobs' workspaces are released."""
+    global _DEFER_KEEP
+    _call("nrse_reduce_discard")
+    _DEFER_KEEP = None
+
+
+def reduce_pending() -> int:
+    return int(_lib.lib().nrse_reduce_pending())
+
+
+def _ws_floats(fn: str, p) -> int:
+    """A *_workspace query of a params struct; a negative answer is the ABI 10 refusal."""
+    n = int(getattr(_lib.lib(), fn)(ctypes.byref(p)))
+    if n < 0:
+        _lib.check(n, fn)
+    return n
+
+
 def reduce_flush(stream: torch.cuda.Stream | None = None) -> None:
     """Run the queued reductions on `stream` (default: the current one), batched; the queued
     workspaces are recorded on that stream, so the allocator reuses them only after its work."""
@@ -180,7 +200,7 @@ def gemm(A: Operand, B: Operand, C: torch.Tensor, M: int, N: int, K: int, *, ldc
         p.c8, p.ldc8, p.c8_dtype = ptr(c8), ldc8, dtype_code(c8)
     ws = None
     if colsum is not None and DETERMINISTIC:
-        ws = workspace(_lib.lib().nrse_gemm_colsum_workspace(ctypes.byref(p)))
+        ws = workspace(_ws_floats("nrse_gemm_colsum_workspace", p))
         p.colsum_part = ptr(ws)
     probe = _GEMM_PROBE
     if probe is not None:
@@ -448,10 +468,19 @@ def _out_code(y: torch.Tensor, n: int, split3: bool) -> int:
     return _lib.BF16X3
 
 
-def ln_fwd(x, gamma, beta, y, mean, rstd, eps, gelu=False, relu=False, split3=False, y8=None, y8_exp=None):
+def _sat_ptr(sat):
+    """The ABI 10 saturation counter (int32 device tensor, element 0) or None."""
+    if sat is None:
+        return None
+    assert sat.dtype == torch.int32 and sat.is_cuda
+    return ptr(sat)
+
+
+def ln_fwd(x, gamma, beta, y, mean, rstd, eps, gelu=False, relu=False, split3=False, y8=None, y8_exp=None, sat=None):
     """y8 (fp8 [rows, C], bf16 y): also y8 = fp8(y), the split-weight mode's next correction operand;
     with y8_exp (fp8 [2, rows, C]): the two correction planes [fp8((o - bf16 o) 2^y8_exp) | fp8(bf16 o)]
-    of the exact output o (the conv stack's form, ABI 7)."""
+    of the exact output o (the conv stack's form, ABI 7). sat (int32 device tensor): += the number
+    of y8 conversions that saturated (ABI 10)."""
     rows, C = x.shape[0] if x.dim() == 2 else x.numel() // x.shape[-1], x.shape[-1]
     if y8 is not None:
         n8 = rows * C * (1 if y8_exp is None else 2)
@@ -459,7 +488,7 @@ def ln_fwd(x, gamma, beta, y, mean, rstd, eps, gelu=False, relu=False, split3=Fa
     p = LnFwdParams(ptr(x), dtype_code(x), ptr(gamma), ptr(beta), ptr(y), _out_code(y, rows * C, split3), ptr(mean),
                     ptr(rstd), rows, C, eps, (_lib.LN_GELU if gelu else 0) | (_lib.LN_RELU if relu else 0), ptr(y8),
                     0 if y8_exp is None else 1, 0 if y8_exp is None else int(y8_exp),
-                    dtype_code(y8) if y8 is not None else 0)
+                    dtype_code(y8) if y8 is not None else 0, _sat_ptr(sat))
     _call("nrse_layernorm_fwd", ctypes.byref(p), stream_ptr())
 
 
@@ -490,7 +519,7 @@ def ln_bwd(dy, x, gamma, mean, rstd, dx, *, beta=None, gelu=False, relu=False, r
         p.gate_dp, p.gate_w = ptr(gate_dp), ptr(gate_w)
     ws = None
     if DETERMINISTIC and (dgamma is not None or (dv is not None and dv_colsum is not None)):
-        ws = workspace(_lib.lib().nrse_layernorm_bwd_workspace(ctypes.byref(p)))
+        ws = workspace(_ws_floats("nrse_layernorm_bwd_workspace", p))
         p.part = ptr(ws)
     _call("nrse_layernorm_bwd", ctypes.byref(p), stream_ptr())
 
@@ -582,20 +611,22 @@ def attn_bwd(qkv, gate, bias, ctx, dctx, lse, delta, dqkv, dgate, diag, batch, T
     p.drop_mask = ptr(drop_mask)
     ws = None
     if DETERMINISTIC and diag is not None:
-        ws = workspace(_lib.lib().nrse_attn_bwd_workspace(ctypes.byref(p)))
+        ws = workspace(_ws_floats("nrse_attn_bwd_workspace", p))
         p.diag_part = ptr(ws)
     _call("nrse_attn_bwd", ctypes.byref(p), stream_ptr())
 
 
 # ----------------------------------------------------------------------------- conv front end
-def conv0_fwd(wav, w, gamma, beta, out, mean, rstd, T0, k, s, eps, split3=False, y8=None, y8_exp=0):
-    """y8 (fp8 [2, B*T0, C], bf16 out): the exact output's fp8 correction planes (ABI 7)."""
+def conv0_fwd(wav, w, gamma, beta, out, mean, rstd, T0, k, s, eps, split3=False, y8=None, y8_exp=0, sat=None):
+    """y8 (fp8 [2, B*T0, C], bf16 out): the exact output's fp8 correction planes (ABI 7); sat: the
+    saturation counter of those conversions (ABI 10)."""
     B, L = wav.shape
     C = w.shape[0]
     p = Conv0Params()
     if y8 is not None:
         assert y8.dtype in CORR and y8.numel() == 2 * B * T0 * C and y8.is_contiguous() and not split3
         p.y8, p.y8_exp, p.y8_dtype = ptr(y8), int(y8_exp), dtype_code(y8)
+        p.sat_count = _sat_ptr(sat)
     p.wav, p.L, p.w, p.gamma, p.beta = ptr(wav), L, ptr(w), ptr(gamma), ptr(beta)
     p.out, p.out_dtype, p.mean, p.rstd = ptr(out), _out_code(out, B * T0 * C, split3), ptr(mean), ptr(rstd)
     p.batch, p.T0, p.C, p.k, p.s, p.eps = B, T0, C, k, s, eps
@@ -622,7 +653,7 @@ def conv0_bwd(wav, w, gamma, beta, mean, rstd, dy, dw, dgamma, dbeta, T0, k, s, 
     p.batch, p.T0, p.C, p.k, p.s = B, T0, C, k, s
     ws = None
     if DETERMINISTIC:
-        ws = workspace(_lib.lib().nrse_conv0_bwd_workspace(ctypes.byref(p)))
+        ws = workspace(_ws_floats("nrse_conv0_bwd_workspace", p))
         p.part = ptr(ws)
     _call("nrse_conv0_bwd", ctypes.byref(p), stream_ptr())
     swap12(dwT, dw, 1, k, C, accumulate=True)
@@ -751,12 +782,13 @@ def sumsq(x, out):
 
 def adamw(p, g, m, v, shadow, *, lr, beta1, beta2, eps, weight_decay, step, max_norm, sumsq_buf, grad_scale=1.0,
           shadow_lo=None, ema_t=None, ema_shadow=None, ema_shadow_lo=None, ema_decay=0.0, shadow_lo8=None,
-          ema_shadow_lo8=None, lo8_exp=0, zero_grad=False):
+          ema_shadow_lo8=None, lo8_exp=0, zero_grad=False, sat=None):
     """clip + AdamW; shadow (bf16/f32) gets the updated weights, shadow_lo (bf16, with a bf16
     shadow) the split-weight mode's lo plane bf16(p - shadow). ema_t (f32, numel <= p's): the
     target EMA of the first ema_t.numel() updated weights in the same pass (as ema() after).
     shadow_lo8 / ema_shadow_lo8 (fp8): the fp8 correction planes fp8((w - bf16(w)) 2^lo8_exp);
-    zero_grad: g is zeroed by the pass after it is read."""
+    zero_grad: g is zeroed by the pass after it is read. sat (int32 device tensor): += the number of
+    fp8 corrections that saturated (ABI 10)."""
     if ema_t is not None:
         assert ema_t.dtype == torch.float32 and ema_t.numel() <= p.numel()
     for t, n in ((shadow_lo8, p.numel()), (ema_shadow_lo8, ema_t.numel() if ema_t is not None else 0)):
@@ -769,7 +801,7 @@ def adamw(p, g, m, v, shadow, *, lr, beta1, beta2, eps, weight_decay, step, max_
                       ptr(ema_t), ptr(ema_shadow), ptr(ema_shadow_lo),
                       dtype_code(ema_shadow) if ema_shadow is not None else 0, ema_decay,
                       ema_t.numel() if ema_t is not None else 0, ptr(shadow_lo8), ptr(ema_shadow_lo8), lo8_exp,
-                      1 if zero_grad else 0, lo8_dt)
+                      1 if zero_grad else 0, lo8_dt, _sat_ptr(sat))
     _call("nrse_adamw", ctypes.byref(prm), stream_ptr())
 
 
@@ -785,14 +817,15 @@ def split_bf16(x, hi, lo):
     _call("nrse_split_bf16", ptr(x), ptr(hi), ptr(lo), x.numel(), stream_ptr())
 
 
-def split_lo8(x, lo8, lo8_exp=0):
+def split_lo8(x, lo8, lo8_exp=0, sat=None):
     """lo8 = fp8((x - bf16(x)) 2^lo8_exp) (nrse_split_lo8): the fp8 correction plane of x; an MX6
-    (uint8) lo8: the MXFP6 blocks of x - bf16(x) (nrse_split_lo_mx6, no exponent)."""
+    (uint8) lo8: the MXFP6 blocks of x - bf16(x) (nrse_split_lo_mx6, no exponent). sat: the
+    saturation counter (ABI 10)."""
     assert x.dtype == torch.float32 and lo8.dtype in CORR and lo8.numel() == x.numel()
     if lo8.dtype == MX6:
         _call("nrse_split_lo_mx6", ptr(x), ptr(lo8), x.numel(), stream_ptr())
     else:
-        _call("nrse_split_lo8", ptr(x), ptr(lo8), int(lo8_exp), x.numel(), stream_ptr())
+        _call("nrse_split_lo8", ptr(x), ptr(lo8), int(lo8_exp), x.numel(), _sat_ptr(sat), stream_ptr())
 
 
 def cast_fp8(x, y8):

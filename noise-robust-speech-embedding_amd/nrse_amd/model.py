@@ -135,8 +135,11 @@ class BYOLSpeechModel(nn.Module):
         arch = arch or arch_from_name(m["name"])
         self.ema_decay = float(m["ema_decay"])
         tr = config.get("training", {})
+        # the engine's own loop (train_one_epoch -> engine.train_step) clears the gradient inside the
+        # AdamW pass (no 1.3 GB fill kernel between steps); the autograd path below writes each
+        # backward into a fresh buffer, and FusedAdamW.step copies it in before the update
         cfg = StepConfig(lr=float(tr.get("learning_rate", 1e-5)), weight_decay=float(tr.get("weight_decay", 1e-5)),
-                         ema_decay=self.ema_decay, overlap_optimizer=True)
+                         ema_decay=self.ema_decay, overlap_optimizer=True, fused_zero_grad=True)
         seed = seed if seed is not None else int(tr.get("seed", 42))
         self.engine = ByolEngine(arch, int(m["projection_dim"]), int(m["prediction_dim"]),
                                  device=device or _device_default(), compute_dtype=compute_dtype, seed=seed,
@@ -176,6 +179,10 @@ class BYOLSpeechModel(nn.Module):
         e.sync_optimizer()
         self._sync_shadows()
         K.ema(e.target, e.online[:e.layout.ema_numel], e.target_sh, self.ema_decay, shadow_lo=e.target_lo)
+        if e.target_lo8 is not None:
+            # the split-weight mode's fp8 correction plane of the updated target (the fused AdamW + EMA
+            # pass writes it in the engine's own step; nrse_ema has no fp8 output)
+            K.split_lo8(e.target, e.target_lo8, e.lo8_exp, sat=e.sat_buf[0:1])
 
     def _copy_weights(self, *args) -> None:
         e = self.engine

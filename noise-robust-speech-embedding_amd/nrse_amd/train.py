@@ -147,7 +147,7 @@ def train_one_epoch(model, dataloader, optimizer, scheduler, device, config, all
                               lr=optimizer.lr, step_seed=step0 + steps, rank=rank, allreduce=allreduce,
                               world_size=world)
         if health is not None:
-            health.record(step0 + steps, eng.health_buf)
+            health.record(step0 + steps, eng.health_buf, engine=eng)
         losses.append(loss.clone())
         scheduler.step()
         steps += 1

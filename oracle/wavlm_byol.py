@@ -102,9 +102,9 @@ SPLIT_WEIGHT_SITES = tuple(f"{s}:a" for s in SITES if s not in ("attn", "conv"))
 # weight correction x (w - w_hi) runs as fp8(x) times the fp8 plane fp8((w - w_hi) 2^e), scaled
 # by 2^-e (nrse_gemm's a8 / b8 segment); at "conv" (ABI 7, conv1-6 over exact activations) both
 # corrections: x_hi w_hi + 2^-c (fp8((x - x_hi) 2^c) fp8(w_hi) + fp8(x_hi) fp8((w - w_hi) 2^c)), c
-# the engine's fixed CONV_LO8_EXP; set_split8(sites, e, c) switches it on
+# the engine's conv_lo8_exp (conv_lo8_exponent; 11 at the seeded init); set_split8(sites, e, c) switches it on
 SPLIT8_SITES = ("qkv", "oproj", "ffn_up", "ffn_down", "conv")
-CONV_LO8_EXP = 11   # nrse_amd/engine.py CONV_LO8_EXP
+CONV_LO8_EXP = 11   # nrse_amd/engine.py CONV_LO8_EXP: conv_lo8_exponent at gamma = 1, beta = 0
 _OPERAND_DTYPE = None
 _SITES = None
 _SPLIT8 = None   # (frozenset of sites, exponent e, conv exponent c, format "fp8" | "mx6") or None
@@ -182,6 +182,20 @@ def lo8_exponent(weights) -> int:
     """The engine's lo8_exp: floor(log2(224 / (2^-8 max|w|))) over the fp8-corrected weights."""
     W = max(float(w.detach().abs().max()) for w in weights)
     return max(-60, min(60, int(math.floor(math.log2(224.0 * 256.0 / W))))) if W > 0 else 0
+
+
+def conv_lo8_exponent(P: dict, a) -> int:
+    """The engine's conv-stack exponent (ABI 10, ByolEngine._conv_plane_bound): the conv planes carry
+    residuals of the activations feeding conv 1..n-1 -- GELU(LayerNorm_C) outputs, bounded by
+    sqrt(C) max|gamma| + max|beta| -- and of the conv weights; e = floor(log2(224 / (2^-8 bound)))."""
+    B = 0.0
+    for i in range(len(a.conv_dim) - 1):
+        pre = f"feature_extractor.conv_layers.{i}.layer_norm."
+        B = max(B, math.sqrt(a.conv_dim[i]) * float(P[pre + "weight"].detach().abs().max())
+                + float(P[pre + "bias"].detach().abs().max()))
+    for i in range(1, len(a.conv_dim)):
+        B = max(B, float(P[f"feature_extractor.conv_layers.{i}.conv.weight"].detach().abs().max()))
+    return max(-60, min(60, int(math.floor(math.log2(224.0 * 256.0 / B))))) if B > 0 else 0
 
 
 class _RoundFwd(torch.autograd.Function):

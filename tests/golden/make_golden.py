@@ -13,6 +13,9 @@ What is generated (SURVEY.md §8c recipe):
   * byol_large.npz— WavLM-Large arch, 4 x 8 s, eval forward and one det train step
   * byol_large_3s.npz / byol_large_12s.npz — the same at the ends of configs[4]'s 3-12 s
                     range (T = 149 and 599 frames), 4 utterances each (--varlen)
+  * traj_large_3s.npz — WavLM-Large det-train trajectory, 6 steps of B = 4 x 3 s with the
+                    reference's AdamW + CosineAnnealingLR, per-step loss / pre-clip grad norm, a
+                    held-out batch's embeddings after the last step (--trajectory)
 Weights come from nrse_amd.params (portable seeded init), written to a local HF directory the
 reference loads through AutoModel.from_pretrained(config['model']['name']) (src/models/
 encoder.py:14). The reference's 3-D encoder output is pooled with a time-mean monkeypatch
@@ -182,6 +185,53 @@ def run_byol(arch, B, L, proj_dim, pred_dim, ema, lr, wd, tag, full_hidden, stor
               f"grad norm {res['train_grad_norm']:.4f}")
 
 
+def run_trajectory(arch, B, L, steps, proj_dim, pred_dim, ema, lr, wd, tag):
+    """A det-train TRAJECTORY on the reference: `steps` iterations of the
+    train_byol.py:56-74 loop body (zero_grad, forward, byol_loss, backward, clip_grad_norm_(1.0),
+    AdamW.step, _update_target_network, CosineAnnealingLR.step) on a fresh seeded batch each step;
+    per step the loss, the pre-clip gradient norm and the lr; after the last step a held-out batch's
+    online / target embeddings and eval-mode online_pred / target_proj / loss, and a sample of the
+    final online weights. The tests replay the batches from the seeds (make_inputs)."""
+    from src.models.byol import byol_loss
+    with tempfile.TemporaryDirectory() as td:
+        model, layout, flat0 = build_reference_model(arch, proj_dim, pred_dim, ema, td)
+        opt = torch.optim.AdamW(model.parameters(), lr=lr, weight_decay=wd)
+        sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=steps)
+        res = {"B": B, "L": L, "steps": steps, "proj_dim": proj_dim, "pred_dim": pred_dim, "ema": ema, "lr": lr,
+               "wd": wd, "seed": SEED}
+        losses, norms, lrs = [], [], []
+        model.train()
+        for i in range(steps):
+            clean, noisy = make_inputs(B, L, seed=SEED + 100 + i)
+            lrs.append(opt.param_groups[0]["lr"])
+            opt.zero_grad()
+            pred, tproj = model(clean, noisy)
+            loss = byol_loss(pred, tproj)
+            loss.backward()
+            gn = torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1.0)
+            opt.step()
+            model._update_target_network()
+            sched.step()
+            losses.append(float(loss))
+            norms.append(float(gn))
+            print(f"  {tag} step {i}: loss {losses[-1]:.6f} grad norm {norms[-1]:.5f} lr {lrs[-1]:.3e}", flush=True)
+        held_c, held_n = make_inputs(B, L, seed=SEED + 99)
+        model.eval()
+        with torch.no_grad():
+            emb = model.get_encoder()(held_c)
+            temb = model.target_encoder(held_n)
+            pred, tproj = model(held_c, held_n)
+            hl = byol_loss(pred, tproj)
+        on = flat_from_model(model, layout)
+        idx = sample_idx(layout.numel, seed=2)
+        res.update(losses=np.array(losses), grad_norms=np.array(norms), lrs=np.array(lrs),
+                   held_emb=emb.numpy(), held_temb=temb.numpy(), held_pred=pred.numpy(), held_tproj=tproj.numpy(),
+                   held_loss=float(hl), w_idx=idx, w_delta_sample=(on - flat0)[idx].numpy(),
+                   w_delta_norm=float((on - flat0).norm()))
+        np.savez_compressed(os.path.join(HERE, f"traj_{tag}.npz"), **res)
+        print(f"traj_{tag}: losses {np.round(losses, 6).tolist()} held loss {float(hl):.6f}")
+
+
 def make_snr():
     from src.data.augment import add_noise_to_speech
     from transformers import Wav2Vec2FeatureExtractor
@@ -273,7 +323,13 @@ def main():
     ap.add_argument("--manifest-only", action="store_true")
     ap.add_argument("--varlen", action="store_true",
                     help="only the WavLM-Large 3 s / 12 s fixtures (configs[4]'s length range)")
+    ap.add_argument("--trajectory", action="store_true",
+                    help="only the WavLM-Large det-train trajectory (B = 4 x 3 s, 6 steps)")
     args = ap.parse_args()
+    if args.trajectory:
+        torch.set_num_threads(8)
+        run_trajectory(A.LARGE.deterministic(), 4, 48000, 6, 1024, 2048, 0.997, 1e-5, 1e-5, "large_3s")
+        return
     if args.varlen:
         torch.set_num_threads(8)
         for secs in (3, 12):
