@@ -407,6 +407,15 @@ int nrse_weight_norm_bwd(const float* dWf, const float* g, const float* v, const
  * applied in place to the f32 hidden state ([TF]modeling_wavlm.py:1006-1011). */
 int nrse_specaug_pad(float* h_inout, const unsigned char* mask, const float* embed, void* dst, int dst_dtype,
                      int batch, int T, int C, int pad_front, int pad_back, void* stream);
+/* ABI 10: the SpecAugment time masks of one forward, drawn on the device ([TF]modeling_wavlm.py:834-954
+ * _compute_mask_indices, full-length utterances): mask [batch, T] u8 (1 = masked frame). The span
+ * count n = int(mask_prob T / mask_length + eps) (then >= min_masks, <= T / mask_length, <= the
+ * T - mask_length + 1 candidate starts), eps = 24 random bits of the seed; per utterance the n starts
+ * are a uniform random subset of the candidates (the n smallest counter-hash keys), each masking
+ * mask_length frames. mask_prob <= 0: all zeros. T - mask_length + 1 <= 4096. Replaces the reference's
+ * numpy draw and the per-step host-to-device copy of its mask (oracle/masks.py specaug_mask replays it). */
+int nrse_specaug_mask(unsigned char* mask, int batch, int T, double mask_prob, int mask_length, int min_masks,
+                      uint32_t seed, void* stream);
 /* generic padded copy: dst[b, pad_front + t, :] = src[b, t, :], pad rows zeroed */
 int nrse_pad_rows(const void* src, int src_dtype, void* dst, int dst_dtype, int batch, int T, int C, int pad_front,
                   int pad_back, void* stream);

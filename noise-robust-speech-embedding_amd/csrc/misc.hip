@@ -61,6 +61,46 @@ __global__ void pad_rows_kernel(const void* __restrict__ src, int sdt, void* __r
 }
 
 // one block per row chunk; thread per column
+// ABI 10: the SpecAugment time masks drawn on the device ([TF]modeling_wavlm.py:834-954,
+// _compute_mask_indices without an attention mask: every utterance has the full T). Utterance b
+// masks n spans of L frames whose starts are a uniformly random n-subset of the C = T - L + 1
+// candidates: the n candidates with the smallest 64-bit keys (mix32 of the flat candidate index
+// b*C + k under the step's key, then k itself, so keys never tie). The reference draws the subset
+// with numpy (np.random.choice(..., replace=False)); the distribution is the same, the stream is
+// a counter hash that oracle/masks.py specaug_mask replays bit for bit. One workgroup per
+// utterance: keys in LDS, each candidate ranked by one broadcast sweep, then each frame ORs the
+// selection flags of the L starts that cover it (one coalesced byte store per frame).
+constexpr int SPEC_CMAX = 4096;
+__global__ __launch_bounds__(256) void specaug_mask_kernel(unsigned char* __restrict__ mask, int T, int L, int n,
+                                                           uint32_t key) {
+  __shared__ unsigned long long keys[SPEC_CMAX];
+  __shared__ unsigned char sel[SPEC_CMAX];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int C = T - L + 1;
+  if (n > 0) {
+    for (int k = tid; k < C; k += 256) {
+      const uint32_t h = mix32(((uint32_t)b * (uint32_t)C + (uint32_t)k) ^ key);
+      keys[k] = ((unsigned long long)h << 32) | (unsigned long long)(unsigned)k;
+    }
+    __syncthreads();
+    for (int k = tid; k < C; k += 256) {
+      const unsigned long long mine = keys[k];
+      int rank = 0;
+      for (int j = 0; j < C; ++j) rank += keys[j] < mine ? 1 : 0;
+      sel[k] = rank < n ? 1 : 0;
+    }
+    __syncthreads();
+  }
+  for (int t = tid; t < T; t += 256) {
+    unsigned char m = 0;
+    if (n > 0) {
+      const int lo = t - L + 1 < 0 ? 0 : t - L + 1, hi = t < C - 1 ? t : C - 1;
+      for (int s2 = lo; s2 <= hi; ++s2) m |= sel[s2];
+    }
+    mask[(long long)b * T + t] = m;
+  }
+}
+
 __global__ void specaug_bwd_kernel(const float* __restrict__ dh, const unsigned char* __restrict__ mask,
                                    float* __restrict__ dembed, void* __restrict__ out, int odt, int batch, int T, int C,
                                    float p, uint32_t seed, float* __restrict__ part) {
@@ -363,6 +403,32 @@ extern "C" int nrse_specaug_pad(float* h, const unsigned char* mask, const float
   hipLaunchKernelGGL(specaug_pad_kernel, dim3(blocks_for(total)), dim3(256), 0, (hipStream_t)stream, h, mask, embed,
                      dst, dst_dtype, batch, T, C, pf, pb);
   return nrse_check_launch("nrse_specaug_pad");
+}
+
+// host restatement of common.h's mix32 / site_key (the span count needs eps on the host)
+static uint32_t mix32_host(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+  return x;
+}
+
+extern "C" int nrse_specaug_mask(unsigned char* mask, int batch, int T, double mask_prob, int mask_length,
+                                 int min_masks, uint32_t seed, void* stream) {
+  NRSE_REQUIRE(mask && batch > 0 && T > 0, "nrse_specaug_mask: bad args");
+  int n = 0, L = mask_length < 1 ? 1 : mask_length;
+  if (mask_prob > 0 && mask_length >= 1) {
+    NRSE_REQUIRE(mask_length <= T, "nrse_specaug_mask: mask_length %d > sequence_length %d", mask_length, T);
+    NRSE_REQUIRE(T - mask_length + 1 <= SPEC_CMAX, "nrse_specaug_mask: more than %d span starts", SPEC_CMAX);
+    const uint32_t key = mix32_host(seed * 0x9e3779b9U + 0x632be5abU);
+    // the reference's one eps per call (np.random.rand()), 24 random bits
+    const double eps = (double)(mix32_host(key ^ 0x2545f491U) >> 8) * (1.0 / 16777216.0);
+    n = (int)(mask_prob * T / mask_length + eps);
+    if (n < min_masks) n = min_masks;
+    if (n * mask_length > T) n = T / mask_length;
+    if (T - (mask_length - 1) < n) n = T - (mask_length - 1) > 0 ? T - (mask_length - 1) : 0;
+    seed = mix32_host(key ^ 0x5bd1e995U);
+  }
+  hipLaunchKernelGGL(specaug_mask_kernel, dim3(batch), dim3(256), 0, (hipStream_t)stream, mask, T, L, n, seed);
+  return nrse_check_launch("nrse_specaug_mask");
 }
 
 extern "C" int nrse_pad_rows(const void* src, int sdt, void* dst, int ddt, int batch, int T, int C, int pf, int pb,

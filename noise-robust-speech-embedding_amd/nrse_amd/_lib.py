@@ -166,6 +166,7 @@ _SIGNATURES = {
     "nrse_weight_norm_fwd": ([c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_vp, c_vp], c_int),
     "nrse_weight_norm_bwd": ([c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp], c_int),
     "nrse_specaug_pad": ([c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
+    "nrse_specaug_mask": ([c_vp, c_int, c_int, ctypes.c_double, c_int, c_int, c_u32, c_vp], c_int),
     "nrse_pad_rows": ([c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
     "nrse_specaug_bwd": ([c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_f, c_u32, c_vp, c_vp], c_int),
     "nrse_dropout_cast": ([c_vp, c_vp, c_int, c_ll, c_f, c_u32, c_vp], c_int),

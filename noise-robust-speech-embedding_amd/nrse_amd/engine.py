@@ -28,7 +28,7 @@ from . import kernels as K
 from . import params as PR
 from . import rng as R
 from .arch import WavLMArch
-from .hostside import bucket_runs, bucket_vector, compute_mask_indices, layerdrop_decisions
+from .hostside import bucket_runs, bucket_vector, layerdrop_decisions
 
 F32 = torch.float32
 # NRSE_SERIAL_TARGET=1 runs the target view and the backward weight gradients on the main
@@ -606,10 +606,15 @@ class ByolEngine:
         pk, G = a.pos_kernel, a.pos_groups
         cpg = H // G
         mask = None
-        if train and mask_np is not None and mask_np.any():
-            # pinned staging: a copy from pageable memory blocks the host until the stream
-            # reaches it, which stalled the enqueue of the rest of the step behind the GPU
-            # (the two views' forwards then ran one after the other instead of concurrently)
+        if train and isinstance(mask_np, (int, np.integer)):
+            # the time masks drawn on the device from the forward's mask seed (nrse_specaug_mask,
+            # ABI 10): no host RNG and no host-to-device copy in the step
+            if a.mask_time_prob > 0 and a.mask_time_length >= 1:
+                mask = torch.empty(B, T, device=dev, dtype=torch.uint8)
+                K.specaug_mask(mask, a.mask_time_prob, a.mask_time_length, a.mask_time_min_masks, int(mask_np))
+        elif train and mask_np is not None and mask_np.any():
+            # explicit host masks (tests, replays): pinned staging -- a copy from pageable memory
+            # blocks the host until the stream reaches it
             mask = torch.from_numpy(mask_np.astype(np.uint8)).pin_memory().to(dev, non_blocking=True)
         hpad = torch.empty(B, T + pk, H, device=dev, dtype=cdt)
         K.specaug_pad(h, mask, Pm.get("masked_spec_embed"), hpad, B, T, H, pk // 2, pk - pk // 2)
@@ -1182,17 +1187,27 @@ class ByolEngine:
     def stochastic_inputs(self, step_seed: int, B: int, T: int, train: bool, rank: int = 0):
         """LayerDrop decisions for both branches from a rank-SHARED stream (every replica skips
         the same layers, so skipped layers carry zero gradient everywhere and are not sent), and
-        SpecAugment masks from a rank-DISTINCT stream (each rank masks its own utterances, as
-        dropout does through the rank in forward_seed)."""
+        the SpecAugment mask SEEDS of both views, rank-DISTINCT (each rank masks its own utterances,
+        as dropout does through the rank in forward_seed): the masks themselves are drawn on the
+        device by nrse_specaug_mask inside the forward (spec_masks() reads them back for replays)."""
         a = self.arch
         if not train:
             return (None, None), (None, None)
         g = np.random.default_rng([step_seed, 7])
         skips = (layerdrop_decisions(g, a.layers, a.layerdrop), layerdrop_decisions(g, a.layers, a.layerdrop))
-        gm = np.random.default_rng([step_seed, 11, rank])
-        masks = (compute_mask_indices(gm, B, T, a.mask_time_prob, a.mask_time_length, a.mask_time_min_masks),
-                 compute_mask_indices(gm, B, T, a.mask_time_prob, a.mask_time_length, a.mask_time_min_masks))
+        masks = tuple(R.site_seed(R.forward_seed(step_seed, v, rank), R.SITE_SPEC) for v in (0, 1))
         return skips, masks
+
+    def spec_masks(self, seeds, B: int, T: int):
+        """The [B, T] bool SpecAugment masks the forward draws from `seeds` (host copies, for the
+        oracle replay and tests; a host sync)."""
+        a = self.arch
+        out = []
+        for s in seeds:
+            m = torch.empty(B, T, device=self.dev, dtype=torch.uint8)
+            K.specaug_mask(m, a.mask_time_prob, a.mask_time_length, a.mask_time_min_masks, int(s))
+            out.append(m.cpu().numpy().astype(bool))
+        return tuple(out)
 
     def forward(self, clean: torch.Tensor, noisy: torch.Tensor, *, train: bool, step_seed: int = 0, rank: int = 0,
                 need_grad: bool = False, skips=None, masks=None):

@@ -682,6 +682,14 @@ def specaug_pad(h, mask, embed, dst, batch, T, C, pf, pb):
           stream_ptr())
 
 
+def specaug_mask(mask, mask_prob, mask_length, min_masks, seed):
+    """mask [B, T] u8 <- the SpecAugment time masks drawn on the device (nrse_specaug_mask, ABI 10)."""
+    assert mask.dtype == torch.uint8 and mask.dim() == 2 and mask.is_contiguous()
+    B, T = mask.shape
+    _call("nrse_specaug_mask", ptr(mask), B, T, float(mask_prob), int(mask_length), int(min_masks), seed & 0xFFFFFFFF,
+          stream_ptr())
+
+
 def pad_rows(src, dst, batch, T, C, pf, pb):
     _call("nrse_pad_rows", ptr(src), dtype_code(src), ptr(dst), dtype_code(dst), batch, T, C, pf, pb, stream_ptr())
 

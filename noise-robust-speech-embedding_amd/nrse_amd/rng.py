@@ -13,6 +13,7 @@ M = 0xFFFFFFFF
 
 SITE_FEAT_PROJ = 1
 SITE_POS = 2
+SITE_SPEC = 3     # the SpecAugment time-mask draw of a forward (nrse_specaug_mask)
 
 
 def site_attn_probs(layer: int) -> int:

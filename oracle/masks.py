@@ -73,3 +73,35 @@ def attn_dropout_mask(seed: int, p: float, shape) -> np.ndarray:
     rows = int(np.prod(shape[:-1]))
     k = attn_keep_mask(seed, p, rows, T).reshape(shape)
     return k.astype(np.float32) * np.float32(1.0 / (1.0 - p)) if p < 1 else np.zeros(shape, np.float32)
+
+
+def specaug_mask(seed: int, batch: int, T: int, mask_prob: float, mask_length: int, min_masks: int) -> np.ndarray:
+    """[batch, T] bool SpecAugment time masks as nrse_specaug_mask draws them (csrc/misc.hip
+    specaug_mask_kernel): the reference's span count and span semantics ([TF]modeling_wavlm.py:
+    834-954, _compute_mask_indices over full-length utterances) with a counter-hash stream -- eps =
+    24 bits of the seed's key; per utterance the starts are the n candidates (of C = T - L + 1) with
+    the smallest keys (mix32((b C + k) ^ key2) << 32 | k), a uniformly random n-subset."""
+    mask = np.zeros((batch, T), dtype=bool)
+    if mask_prob <= 0 or mask_length < 1:
+        return mask
+    if mask_length > T:
+        raise ValueError(f"mask_length {mask_length} > sequence_length {T}")
+    key = site_key(seed)
+    eps = float(mix32(key ^ np.uint64(0x2545F491)) >> np.uint64(8)) / 16777216.0
+    n = int(mask_prob * T / mask_length + eps)
+    n = max(n, min_masks)
+    if n * mask_length > T:
+        n = T // mask_length
+    if T - (mask_length - 1) < n:
+        n = max(T - (mask_length - 1), 0)
+    if n == 0:
+        return mask
+    C = T - mask_length + 1
+    key2 = mix32(key ^ np.uint64(0x5BD1E995))
+    k = np.arange(C, dtype=np.uint64)
+    for b in range(batch):
+        h = mix32(((np.uint64(b) * np.uint64(C) + k) & M32) ^ key2)
+        starts = np.argsort((h << np.uint64(32)) | k, kind="stable")[:n]
+        idx = (starts[:, None] + np.arange(mask_length)[None, :]).reshape(-1)
+        mask[b, idx] = True
+    return mask

@@ -116,7 +116,9 @@ def test_stochastic_step_matches_oracle_with_same_masks(nrse_device):
     lr = 1e-4
     eng.cfg.ema_decay = 0.99
     B, T = clean.shape[0], arch.frames(clean.shape[1])
-    skips, masks = eng.stochastic_inputs(11, B, T, True)
+    skips, seeds = eng.stochastic_inputs(11, B, T, True)
+    masks = eng.spec_masks(seeds, B, T)     # drawn on the device (nrse_specaug_mask)
+    assert all(m.any() for m in masks)
     loss = eng.train_step(clean.cuda(), noisy.cuda(), lr=lr, step_seed=11)
     r = O.train_step(st, clean, noisy, lr=lr, weight_decay=eng.cfg.weight_decay, ema_decay=0.99, step_seed=11,
                      layer_skip=skips, mask_time=masks)

@@ -135,3 +135,38 @@ def test_bucket_runs_invert_the_bucket_vector():
         for k in range(320):
             run = order[offsets[k]:offsets[k + 1]]
             assert (b[run] == k).all() and (np.diff(run) > 0).all()
+
+
+def test_device_span_mask_restatement_semantics():
+    """oracle/masks.py specaug_mask (what nrse_specaug_mask draws on the device, ABI 10) keeps the
+    reference's span semantics ([TF]modeling_wavlm.py:834-954): n = int(p T / L + eps) spans clamped
+    to [min_masks, T // L], shared by the batch; each utterance's n starts distinct and uniformly
+    spread over the T - L + 1 candidates; every span L frames; deterministic in the seed."""
+    p, L, mn = 0.075, 10, 2
+    for T in (49, 149, 399, 599):
+        m = MK.specaug_mask(1234, 64, T, p, L, mn)
+        assert (m == MK.specaug_mask(1234, 64, T, p, L, mn)).all()
+        counts = m.sum(1)
+        n_lo = max(int(p * T / L), mn)
+        n_hi = max(int(p * T / L + 1), mn)
+        # frames covered: n spans of L minus overlaps, never more than n L
+        assert (counts <= n_hi * L).all() and (counts >= L).all()
+        for b in range(64):
+            row = m[b]
+            # a masked run's length is a multiple-span union: at least L
+            runs = np.diff(np.flatnonzero(np.diff(np.concatenate([[0], row.astype(int), [0]]))))[::2]
+            assert (runs >= L).all()
+        assert n_lo >= 1
+    # uniform starts: over many utterances every candidate is chosen about n / C of the time
+    T = 149
+    C = T - L + 1
+    big = MK.specaug_mask(7, 20000, T, p, L, mn)
+    first = np.array([np.flatnonzero(r)[0] for r in big])     # the first span's start (its smallest)
+    assert first.min() == 0 and first.max() <= C - 1
+    n = mn                                                   # int(0.075 * 149 / 10 + eps) <= 2
+    cover = big.mean(0)                                      # per-frame mask rate, flat in the middle
+    mid = cover[L:T - L]
+    assert abs(mid.mean() - n * L / C) < 0.05 and mid.std() < 0.02, (mid.mean(), mid.std())
+    assert not MK.specaug_mask(3, 4, 100, 0.0, 10, 2).any()
+    with pytest.raises(ValueError):
+        MK.specaug_mask(3, 4, 5, 0.5, 10, 2)

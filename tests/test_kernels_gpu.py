@@ -629,3 +629,23 @@ def test_rows_reduce(nrse_device, S, n, batch, acc):
     ref = slab.double().sum(1) + torch.cat(base, 1).double()
     assert rel(outs[0], ref) < 1e-6
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("T,B", [(49, 4), (149, 32), (399, 32), (599, 7)])
+def test_specaug_mask_device_matches_oracle(nrse_device, T, B):
+    """ABI 10: the SpecAugment time masks drawn on the device (nrse_specaug_mask) equal the oracle's
+    restatement (oracle/masks.py specaug_mask) bit for bit, for several seeds and the step's lengths;
+    mask_prob 0 gives zeros."""
+    from nrse_amd import kernels as K
+    from oracle import masks as MK
+    for seed in (1, 77, 0xDEADBEEF):
+        m = torch.empty(B, T, device="cuda", dtype=torch.uint8)
+        K.specaug_mask(m, 0.075, 10, 2, seed)
+        torch.cuda.synchronize()
+        ref = MK.specaug_mask(seed, B, T, 0.075, 10, 2)
+        assert np.array_equal(m.cpu().numpy().astype(bool), ref), (T, seed)
+        assert ref.any()
+    m.fill_(7)
+    K.specaug_mask(m, 0.0, 10, 2, 5)
+    torch.cuda.synchronize()
+    assert int(m.sum()) == 0
