@@ -579,8 +579,15 @@ typedef struct {
   int lo8_dtype;
   /* ABI 10, optional: sat_count[0] += the number of fp8 correction values (p_shadow_lo8 and
    * ema_shadow_lo8) that saturated, |(w - bf16 w) 2^lo8_exp| > 448: lo8_exp no longer has headroom
-   * for the weights (they grew in training); the caller re-derives it (see nrse_ln_fwd_params) */
+   * for the weights (they grew in training); the caller re-derives it (see nrse_ln_fwd_params).
+   * sat_ranges (optional, device memory): sat_nranges sorted [start, end) pairs of flat indices,
+   * p[i] being flat index sat_offset + i; only saturations inside them count (the planes of the
+   * weights no GEMM reads -- norms, biases, heads -- may saturate harmlessly). Checked only on the
+   * saturating path (a binary search per saturated element): free in normal operation */
   unsigned int* sat_count;
+  const long long* sat_ranges;
+  int sat_nranges;
+  long long sat_offset;
 } nrse_adamw_params;
 int nrse_adamw(const nrse_adamw_params* p, void* stream);
 /* t_shadow_lo: optional, as nrse_adamw_params.p_shadow_lo */

@@ -61,6 +61,27 @@ __global__ __launch_bounds__(256) void sum_parts_kernel(const double* __restrict
 // the fused form in adamw_kernel), so the two forms agree bit for bit whatever the contraction
 NRSE_DEV float ema_mix(float t, float o, float decay, float om) { return fmaf(decay, t, om * o); }
 
+// ABI 10: whether flat index sat_offset + i lies in one of the counted ranges (the saturating path
+// only: a binary search over the sorted [start, end) pairs)
+NRSE_DEV bool sat_member(const nrse_adamw_params& p, long long i) {
+  if (!p.sat_ranges) return true;
+  const long long gi = p.sat_offset + i;
+  int lo = 0, hi = p.sat_nranges;   // first range whose end > gi
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (p.sat_ranges[2 * mid + 1] <= gi) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo < p.sat_nranges && p.sat_ranges[2 * lo] <= gi;
+}
+// the counted saturations among 4 elements from index i0 (bit e of m: element i0 + e saturated)
+NRSE_DEV int sat_members4(const nrse_adamw_params& p, long long i0, unsigned m) {
+  int c = 0;
+  for (int e = 0; e < 4; ++e)
+    if ((m >> e) & 1u) c += sat_member(p, i0 + e) ? 1 : 0;
+  return c;
+}
+
 // one element of the fused target EMA (nrse_adamw_params.ema_t), as ema_kernel's scalar tail
 NRSE_DEV void ema_one(const nrse_adamw_params& p, long long i, float pn, float eom, float sc8, int& ns) {
   const float t = ema_mix(p.ema_t[i], pn, p.ema_decay, eom);
@@ -70,13 +91,14 @@ NRSE_DEV void ema_one(const nrse_adamw_params& p, long long i, float pn, float e
   if (p.ema_shadow_lo8) {
     const float l = lo_resid(t) * sc8;
     ((unsigned char*)p.ema_shadow_lo8)[i] = fp8_1(l);
-    ns += fp8_nsat4(l, 0.f, 0.f, 0.f);
+    if (fabsf(l) > 448.f) ns += sat_member(p, i) ? 1 : 0;
   }
 }
 
 // the fp8 correction plane of 4 consecutive weights at float4 index q (ABI 6); mx: the MXFP6 form
 // (ABI 8), a block = the 8 lanes q & ~7 .. (all live together: the host requires n % 32 == 0)
-NRSE_DEV void store_lo8x4(void* lo8, long long q, const float* x, float sc8, bool mx, int& ns) {
+NRSE_DEV void store_lo8x4(const nrse_adamw_params& p, void* lo8, long long q, const float* x, float sc8, bool mx,
+                         int& ns) {
   if (mx) {
     const float l[4] = {lo_resid(x[0]), lo_resid(x[1]), lo_resid(x[2]), lo_resid(x[3])};
     reinterpret_cast<uint32_t*>(lo8)[q] = mx6_g8(l, threadIdx.x & 63);
@@ -84,7 +106,9 @@ NRSE_DEV void store_lo8x4(void* lo8, long long q, const float* x, float sc8, boo
   }
   const float a = lo_resid(x[0]) * sc8, b = lo_resid(x[1]) * sc8, c = lo_resid(x[2]) * sc8, d = lo_resid(x[3]) * sc8;
   reinterpret_cast<uint32_t*>(lo8)[q] = fp8x4(a, b, c, d);
-  ns += fp8_nsat4(a, b, c, d);
+  const unsigned m = (fabsf(a) > 448.f ? 1u : 0u) | (fabsf(b) > 448.f ? 2u : 0u) | (fabsf(c) > 448.f ? 4u : 0u) |
+                     (fabsf(d) > 448.f ? 8u : 0u);
+  if (m) ns += sat_members4(p, 4 * q, m);
 }
 
 __global__ __launch_bounds__(256) void adamw_kernel(const nrse_adamw_params p) {
@@ -141,7 +165,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(const nrse_adamw_params p) {
         reinterpret_cast<float4*>(p.p_shadow)[q] = pv;
       }
     }
-    if (p.p_shadow_lo8) store_lo8x4(p.p_shadow_lo8, q, pa, sc8, mx, ns);
+    if (p.p_shadow_lo8) store_lo8x4(p, p.p_shadow_lo8, q, pa, sc8, mx, ns);
     if (p.ema_t) {
       if (q < e4) {
         tv.x = ema_mix(tv.x, pv.x, p.ema_decay, eom); tv.y = ema_mix(tv.y, pv.y, p.ema_decay, eom);
@@ -151,7 +175,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(const nrse_adamw_params p) {
           if (p.ema_shadow_dtype == NRSE_BF16) store_bf16x4(p.ema_shadow, p.ema_shadow_lo, q, &tv.x);
           else reinterpret_cast<float4*>(p.ema_shadow)[q] = tv;
         }
-        if (p.ema_shadow_lo8) store_lo8x4(p.ema_shadow_lo8, q, &tv.x, sc8, mx, ns);
+        if (p.ema_shadow_lo8) store_lo8x4(p, p.ema_shadow_lo8, q, &tv.x, sc8, mx, ns);
       } else if (q == e4) {
         // the quad holding the EMA range's end: its first ema_n - 4 q elements, from this thread's
         // updated registers
@@ -174,7 +198,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(const nrse_adamw_params p) {
     if (p.p_shadow_lo8) {
       const float l = lo_resid(p.p[i]) * sc8;
       ((unsigned char*)p.p_shadow_lo8)[i] = fp8_1(l);
-      ns += fp8_nsat4(l, 0.f, 0.f, 0.f);
+      if (fabsf(l) > 448.f) ns += sat_member(p, i) ? 1 : 0;
     }
     if (p.ema_t && i < p.ema_n) ema_one(p, i, p.p[i], eom, sc8, ns);
   }
@@ -278,6 +302,7 @@ extern "C" int nrse_adamw(const nrse_adamw_params* p, void* stream) {
   NRSE_REQUIRE(((uintptr_t)p->p_shadow_lo8 & 3) == 0 && ((uintptr_t)p->ema_shadow_lo8 & 3) == 0 &&
                    (!p->ema_shadow_lo8 || p->ema_t),
                "nrse_adamw: fp8 planes need 4-byte alignment (and ema_t for ema_shadow_lo8)");
+  NRSE_REQUIRE(!p->sat_ranges || (p->sat_count && p->sat_nranges >= 0), "nrse_adamw: sat_ranges without sat_count");
   NRSE_REQUIRE(p->lo8_dtype == 0 || p->lo8_dtype == NRSE_FP8 ||
                    (p->lo8_dtype == NRSE_MX6 && p->n % 32 == 0 && (!p->ema_t || p->ema_n % 32 == 0) &&
                     ((uintptr_t)p->p_shadow_lo8 & 31) == 0 && ((uintptr_t)p->ema_shadow_lo8 & 31) == 0),

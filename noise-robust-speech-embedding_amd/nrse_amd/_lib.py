@@ -127,7 +127,8 @@ class AdamWParams(_Sized):
                 ("p_shadow_lo", c_vp), ("ema_t", c_vp), ("ema_shadow", c_vp), ("ema_shadow_lo", c_vp),
                 ("ema_shadow_dtype", c_int), ("ema_decay", c_f), ("ema_n", c_ll),
                 ("p_shadow_lo8", c_vp), ("ema_shadow_lo8", c_vp), ("lo8_exp", c_int), ("zero_grad", c_int),
-                ("lo8_dtype", c_int), ("sat_count", c_vp)]
+                ("lo8_dtype", c_int), ("sat_count", c_vp), ("sat_ranges", c_vp), ("sat_nranges", c_int),
+                ("sat_offset", c_ll)]
 
 
 _P = ctypes.POINTER

@@ -399,9 +399,32 @@ class ByolEngine:
         self.lo8_exp = _headroom_exp(W)
         if _CONV_LO8_PIN is None:
             self.conv_lo8_exp = _headroom_exp(self._conv_plane_bound())
+        K.split_lo8(self.online, self.online_lo8, self.lo8_exp)
+        K.split_lo8(self.target, self.target_lo8, self.lo8_exp)
+        # the saturation count over the planes the layer GEMMs read (the rest of the buffer --
+        # norms, biases, heads -- is outside the exponent's range and never read): rewritten
+        # per matrix with the counter (the same bytes)
         sat = self.sat_buf[SAT_WEIGHTS:SAT_WEIGHTS + 1]
-        K.split_lo8(self.online, self.online_lo8, self.lo8_exp, sat=sat)
-        K.split_lo8(self.target, self.target_lo8, self.lo8_exp, sat=sat)
+        for flat, plane in ((self.online, self.online_lo8), (self.target, self.target_lo8)):
+            for s, e in self._lo8_ranges():
+                K.split_lo8(flat[s:e], plane[s:e], self.lo8_exp, sat=sat)
+
+    def _lo8_ranges(self) -> list:
+        """Sorted [start, end) flat ranges of the fp8-corrected layer matrices (QKV, out-projection,
+        FFN-up, FFN-down of every layer)."""
+        if getattr(self, "_lo8_rng", None) is None:
+            out = []
+            for li in range(self.arch.layers):
+                p = f"encoder.layers.{li}."
+                off = self._offsets["encoder"][p + "attention.q_proj.weight"][0]
+                out.append((off, off + 3 * self.arch.hidden ** 2))
+                for n in ("attention.out_proj.weight", "feed_forward.intermediate_dense.weight",
+                          "feed_forward.output_dense.weight"):
+                    off, cnt, _ = self._offsets["encoder"][p + n]
+                    out.append((off, off + cnt))
+            self._lo8_rng = sorted(out)
+            self._lo8_rng_dev = torch.tensor(self._lo8_rng, dtype=torch.int64, device=self.dev).contiguous()
+        return self._lo8_rng
 
     def _conv_plane_bound(self) -> float:
         """The largest value the conv stack's fp8 correction planes carry unscaled (host sync): the
@@ -1328,6 +1351,9 @@ class ByolEngine:
                   step=self.step_count, max_norm=c.max_norm, sumsq_buf=self.sumsq_buf, grad_scale=grad_scale,
                   lo8_exp=self.lo8_exp, zero_grad=c.fused_zero_grad,
                   sat=self.sat_buf[SAT_WEIGHTS:SAT_WEIGHTS + 1] if self.online_lo8 is not None else None)
+        if self.online_lo8 is not None:
+            self._lo8_ranges()
+            kw["sat_ranges"] = self._lo8_rng_dev
         self._grad_zeroed = c.fused_zero_grad
         ne = self.layout.ema_numel
         o8, t8 = self.online_lo8, self.target_lo8
@@ -1341,7 +1367,7 @@ class ByolEngine:
                         shadow_lo8=o8, **kw)
                 K.ema(self.target, self.online[:ne], self.target_sh, c.ema_decay, shadow_lo=self.target_lo)
                 if t8 is not None:
-                    K.split_lo8(self.target, t8, self.lo8_exp, sat=kw["sat"])
+                    K.split_lo8(self.target, t8, self.lo8_exp)   # (the two-launch A/B form: uncounted)
             self._opt_events = self._opt_done = None
             return
         main = torch.cuda.current_stream(self.dev)
@@ -1370,12 +1396,12 @@ class ByolEngine:
                             ema_shadow=tsh[s:te] if fuse and tsh is not None else None,
                             ema_shadow_lo=tlo[s:te] if fuse and tlo is not None else None,
                             ema_decay=c.ema_decay, shadow_lo8=o8[s:e] if o8 is not None else None,
-                            ema_shadow_lo8=t8[s:te] if fuse and t8 is not None else None, **kw)
+                            ema_shadow_lo8=t8[s:te] if fuse and t8 is not None else None, sat_offset=s, **kw)
                     if te > s and not fuse:
                         K.ema(self.target[s:te], self.online[s:te], tsh[s:te] if tsh is not None else None,
                               c.ema_decay, shadow_lo=tlo[s:te] if tlo is not None else None)
                         if t8 is not None:
-                            K.split_lo8(self.target[s:te], t8[s:te], self.lo8_exp, sat=kw["sat"])
+                            K.split_lo8(self.target[s:te], t8[s:te], self.lo8_exp)
                 ev = torch.cuda.Event()
                 ev.record(st)
                 events.append(ev)

@@ -790,13 +790,14 @@ def sumsq(x, out):
 
 def adamw(p, g, m, v, shadow, *, lr, beta1, beta2, eps, weight_decay, step, max_norm, sumsq_buf, grad_scale=1.0,
           shadow_lo=None, ema_t=None, ema_shadow=None, ema_shadow_lo=None, ema_decay=0.0, shadow_lo8=None,
-          ema_shadow_lo8=None, lo8_exp=0, zero_grad=False, sat=None):
+          ema_shadow_lo8=None, lo8_exp=0, zero_grad=False, sat=None, sat_ranges=None, sat_offset=0):
     """clip + AdamW; shadow (bf16/f32) gets the updated weights, shadow_lo (bf16, with a bf16
     shadow) the split-weight mode's lo plane bf16(p - shadow). ema_t (f32, numel <= p's): the
     target EMA of the first ema_t.numel() updated weights in the same pass (as ema() after).
     shadow_lo8 / ema_shadow_lo8 (fp8): the fp8 correction planes fp8((w - bf16(w)) 2^lo8_exp);
     zero_grad: g is zeroed by the pass after it is read. sat (int32 device tensor): += the number of
-    fp8 corrections that saturated (ABI 10)."""
+    fp8 corrections that saturated (ABI 10); sat_ranges (int64 device [n, 2], sorted [start, end) flat
+    indices, p[i] = flat index sat_offset + i): only saturations inside them count."""
     if ema_t is not None:
         assert ema_t.dtype == torch.float32 and ema_t.numel() <= p.numel()
     for t, n in ((shadow_lo8, p.numel()), (ema_shadow_lo8, ema_t.numel() if ema_t is not None else 0)):
@@ -810,6 +811,9 @@ def adamw(p, g, m, v, shadow, *, lr, beta1, beta2, eps, weight_decay, step, max_
                       dtype_code(ema_shadow) if ema_shadow is not None else 0, ema_decay,
                       ema_t.numel() if ema_t is not None else 0, ptr(shadow_lo8), ptr(ema_shadow_lo8), lo8_exp,
                       1 if zero_grad else 0, lo8_dt, _sat_ptr(sat))
+    if sat_ranges is not None:
+        assert sat is not None and sat_ranges.dtype == torch.int64 and sat_ranges.is_contiguous()
+        prm.sat_ranges, prm.sat_nranges, prm.sat_offset = ptr(sat_ranges), sat_ranges.shape[0], int(sat_offset)
     _call("nrse_adamw", ctypes.byref(prm), stream_ptr())
 
 

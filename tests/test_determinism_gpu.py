@@ -101,22 +101,38 @@ def test_split_weight_fp8_steps_are_bitwise_repeatable(nrse_device, mx6):
 
 def test_split_weight_fp8_conv_stack(nrse_device):
     """The conv stack's fp8 correction segments (ABI 7; they need >= 128 frames, so 3 s here):
-    bitwise repeatable, and the same training losses as the three bf16 planes to the fp8 form's
-    precision (the 1 s steps above keep the bf16 planes: conv_split8_used False there)."""
+    bitwise repeatable over two stochastic steps (the 1 s steps above keep the bf16 planes:
+    conv_split8_used False there). VERDICT r05 #3: the SECOND step's forward -- after an AdamW pass
+    has rewritten every fp8 plane -- is pinned against the oracle's split8 restatement
+    (O.SPLIT8_SITES, the engine's exponents) evaluated at the engine's own post-step weights: loss
+    and both views' embeddings, at the first step's bounds. (Comparing two independent trajectories
+    instead measures the heads' ill-conditioning: one Adam step at lr 1e-4 turns a 1e-4 forward
+    difference into ~1e-2 in the next loss, tests/test_trajectory_gpu.py.)"""
+    from oracle import wavlm_byol as O
     engines = _pair(A.TINY, PROJ, PRED, torch.bfloat16, weight_split=True, split_lo8=True)
     clean, noisy = _batch(4, 48000)
     _steps_equal(engines, clean, noisy, steps=2)
     assert engines[0].conv_split8_used
-    planes = _pair(A.TINY, PROJ, PRED, torch.bfloat16, weight_split=True, split_lo8=True)[0]
-    planes.conv_split8 = False
-    ref = _pair(A.TINY, PROJ, PRED, torch.bfloat16, weight_split=True, split_lo8=True)[0]
-    l8 = [float(ref.train_step(clean, noisy, lr=1e-4, step_seed=100 + i)) for i in range(2)]
-    l3 = [float(planes.train_step(clean, noisy, lr=1e-4, step_seed=100 + i)) for i in range(2)]
-    assert ref.conv_split8_used and not planes.conv_split8_used
-    # the first step's loss is the forward's numerics; after an update Adam's sign-like first steps
-    # amplify any gradient difference (a loose bound only)
-    assert abs(l8[0] - l3[0]) <= 1e-3 * max(abs(l3[0]), 1.0), (l8, l3)
-    assert abs(l8[1] - l3[1]) <= 1e-2 * max(abs(l3[1]), 1.0), (l8, l3)
-    c1, n1 = _batch(4, 16000)
-    ref.train_step(c1, n1, lr=1e-4, step_seed=7)
-    assert not ref.conv_split8_used
+    arch = A.TINY.deterministic()
+    layout = PR.byol_layout(arch, PROJ, PRED)
+    eng = _pair(arch, PROJ, PRED, torch.bfloat16, weight_split=True, split_lo8=True)[0]
+    eng.cfg.overlap_optimizer = True
+    O.set_operand_dtype(torch.bfloat16, O.SPLIT_WEIGHT_SITES)
+    try:
+        for i in range(2):
+            eng.sync_optimizer()
+            st = O.OracleState(layout, eng.online.cpu())
+            st.target = eng.target.cpu()
+            O.set_split8(O.SPLIT8_SITES, eng.lo8_exp, eng.conv_lo8_exp)
+            emb = eng.embed(clean)          # (the det arch: the train-mode encoder forward is this)
+            loss = float(eng.train_step(clean, noisy, lr=1e-4, step_seed=100 + i))
+            with torch.no_grad():
+                rp, rt, remb = O.forward(st, clean.cpu(), noisy.cpu(), train=True, step_seed=100 + i)
+                rl = float(O.byol_loss(rp, rt))
+            assert eng.conv_split8_used
+            assert abs(loss - rl) <= 1e-3 * max(abs(rl), 1.0), (i, loss, rl)
+            assert ((emb.cpu() - remb).norm() / remb.norm()) < 5e-3
+            O.set_split8(None)
+    finally:
+        O.set_operand_dtype(None)
+        O.set_split8(None)
