@@ -14,6 +14,8 @@
 // LDS tiles are [64 rows][64 bf16] (128-byte rows) with the 16-byte chunk XOR-swizzled by
 // ((row>>1)&3)<<1 so both ds_read_b128 row reads and ds_read_b64_tr_b16 column reads of one
 // image stay (nearly) conflict-free.
+#include <type_traits>
+
 #include "common.h"
 
 namespace {
@@ -257,7 +259,10 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
   // In the last key tile the keys past T get -inf scores, so probability 0 whatever the dropout
   // hash says; every sub-tile is hashed (a per-sub-tile branch made the compiler copy the
   // probability registers across it on every tile).
-  for (int it = 0; it < ntiles; ++it) {
+  // LAST: the tile that may hold keys past T (their masking compiled only into it: in the loop of
+  // the other tiles it was 16 compares + 16 selects per tile, if-converted by the compiler)
+  auto tile = [&](const int it, auto last_c) {
+    constexpr bool LAST = decltype(last_c)::value;
     const int kb = it * 64;
     char* const Kt = kv0 + (it & 1) * 2 * TILE_B;
     char* const Vt = Kt + TILE_B;
@@ -267,13 +272,13 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
     asm volatile("" ::: "memory");
     // prefetch tile it+1 into the other buffer (its last readers finished before this barrier)
     const uint32_t mcur = mnext;
-    if (it + 1 < ntiles) {
+    if (!LAST || it + 1 < ntiles) {
       char* const Kn = kv0 + ((it + 1) & 1) * 2 * TILE_B;
       kv_dma_issue(kd, Kn, kb + 64, w);
       kv_dma_issue(vd, Kn + TILE_B, kb + 64, w);
       if (DM == 2) mnext = mrow[(long long)(it + 1) * 4 * (ntiles * 64)];
     }
-    if (!wlive) continue;
+    if (!wlive) return;
     // the MFMAs run on every sub-tile (a conditional MFMA makes the compiler stage its result
     // through AGPRs)
     f32x4 s[4];
@@ -292,7 +297,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
       const f32x2 r1 = pk_fma(f32x2{s[t][2], s[t][3]}, c12, pk_fma(gl2, f32x2{bb.z, bb.w}, nm2));
       v[t][0] = r0.x; v[t][1] = r0.y; v[t][2] = r1.x; v[t][3] = r1.y;
     }
-    if (kb + 64 > T) {
+    if (LAST && kb + 64 > T) {
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -342,7 +347,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
       for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int rp = 0; rp < 2; ++rp) {
-          const uint32_t hh = mix32((rowpair + (uint32_t)((kb >> 1) + 8 * t + rp)) ^ key);
+          const uint32_t hh = attn_mix((rowpair + (uint32_t)((kb >> 1) + 8 * t + rp)) ^ key);
           const bool k0 = attn_half_keep(hh, 0, thr), k1 = attn_half_keep(hh, 1, thr);
           pd[t][2 * rp] = k0 ? pd[t][2 * rp] : 0.f;
           pd[t][2 * rp + 1] = k1 ? pd[t][2 * rp + 1] : 0.f;
@@ -363,7 +368,13 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
       for (int dt = 0; dt < 4; ++dt)
         o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rd_tr(Vt, 32 * c, 32 * c + 16, 16 * dt, lane), pa, o[dt], 0, 0, 0);
     }
-  }
+  };
+#if NRSE_ATTN_NOPEEL
+  for (int it = 0; it < ntiles; ++it) tile(it, std::true_type{});
+#else
+  for (int it = 0; it + 1 < ntiles; ++it) tile(it, std::false_type{});
+  tile(ntiles - 1, std::true_type{});
+#endif
   const float lpart = lpart2.x + lpart2.y;
   const float m = mref;
   const float l = xor32_sum(xor16_sum(lpart));
@@ -482,7 +493,10 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
   f32x4 dq[4];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int it = 0; it < ntiles; ++it) {
+  // LAST: the key tile that may reach past T (its sub-tile skips and masking compiled only into it,
+  // as the forward's)
+  auto tile = [&](const int it, auto last_c) {
+    constexpr bool LAST = decltype(last_c)::value;
     const int kb = it * 64;
     char* const Kt = kv0 + (it & 1) * 2 * TILE_B;
     char* const Vt = Kt + TILE_B;
@@ -490,14 +504,14 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     const uint32_t mcur = mnext;
-    if (it + 1 < ntiles) {
+    if (!LAST || it + 1 < ntiles) {
       char* const Kn = kv0 + ((it + 1) & 1) * 2 * TILE_B;
       kv_dma_issue(kd, Kn, kb + 64, w);
       kv_dma_issue(vd, Kn + TILE_B, kb + 64, w);
       if (use_mask) mnext = mrow[(long long)(it + 1) * 4 * Tp];
     }
-    if (!wlive) continue;
-    const int nt16 = min(4, (T - kb + 15) >> 4);
+    if (!wlive) return;
+    const int nt16 = LAST ? min(4, (T - kb + 15) >> 4) : 4;
     f32x4 s[4], dp[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -530,7 +544,7 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
           if (t < nt16) {
 #pragma unroll
             for (int rp = 0; rp < 2; ++rp) {
-              const uint32_t hh = mix32((rowpair + (uint32_t)((kb >> 1) + 8 * t + rp)) ^ key);
+              const uint32_t hh = attn_mix((rowpair + (uint32_t)((kb >> 1) + 8 * t + rp)) ^ key);
               dp[t][2 * rp] = attn_half_keep(hh, 0, thr) ? dp[t][2 * rp] * dsc : 0.f;
               dp[t][2 * rp + 1] = attn_half_keep(hh, 1, thr) ? dp[t][2 * rp + 1] * dsc : 0.f;
             }
@@ -547,7 +561,7 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
         for (int r = 0; r < 4; ++r) ds[t][r] = 0.f;
       }
     }
-    if (kb + 64 > T) {
+    if (LAST && kb + 64 > T) {
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -565,7 +579,13 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
       for (int dt = 0; dt < 4; ++dt)
         dq[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rd_tr(Kt, 32 * c, 32 * c + 16, 16 * dt, lane), da, dq[dt], 0, 0, 0);
     }
-  }
+  };
+#if NRSE_ATTN_NOPEEL
+  for (int it = 0; it < ntiles; ++it) tile(it, std::true_type{});
+#else
+  for (int it = 0; it + 1 < ntiles; ++it) tile(it, std::false_type{});
+  tile(ntiles - 1, std::true_type{});
+#endif
   dgate = xor32_sum(xor16_sum(dgate));
   if (g == 0 && qv) p.dgate[bh * T + qi] = dgate;
   // dQ^T accumulated (K^T in the A slot): lane (g, i16) holds query qi, dims 16 dt + 4g .. + 3
@@ -818,8 +838,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const uint32_t qa = (uint32_t)(bh * T + qb + 16 * t + 4 * g + 2 * par);
-        const uint32_t ha = mix32((qa * tp2 + colpair) ^ key);
-        const uint32_t hb = mix32(((qa + 1) * tp2 + colpair) ^ key);
+        const uint32_t ha = attn_mix((qa * tp2 + colpair) ^ key);
+        const uint32_t hb = attn_mix(((qa + 1) * tp2 + colpair) ^ key);
         const uint32_t xa = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ha, 0xB1, 0xF, 0xF, false);
         const uint32_t xb = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hb, 0xB1, 0xF, 0xF, false);
         const uint32_t hr[4] = {par ? xa : ha, par ? xb : hb, par ? ha : xa, par ? hb : xb};
@@ -998,7 +1018,7 @@ __global__ __launch_bounds__(256) void attn_mask_kernel(uint16_t* __restrict__ m
         for (int t = 0; t < 4; ++t)
 #pragma unroll
           for (int rp = 0; rp < 2; ++rp) {
-            const uint32_t hh = mix32((rowpair + (uint32_t)((kb >> 1) + 8 * t + rp)) ^ key);
+            const uint32_t hh = attn_mix((rowpair + (uint32_t)((kb >> 1) + 8 * t + rp)) ^ key);
             mb |= (attn_half_keep(hh, 0, thr) ? 1u : 0u) << (4 * t + 2 * rp);
             mb |= (attn_half_keep(hh, 1, thr) ? 1u : 0u) << (4 * t + 2 * rp + 1);
           }

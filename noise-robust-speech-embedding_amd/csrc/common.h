@@ -348,14 +348,32 @@ NRSE_DEV void dropout_apply(uint32_t key, uint32_t idx0, uint32_t thr16, float s
 // Attention-probability dropout (the [B, H, T, T] site, the largest): one mixer hash per PAIR of
 // keys of a query row, 16 bits per element, so the two 32-bit multiplies of mix32 (quarter-rate
 // VALU) are paid once per two elements. Element (row, k), row = (b*H + h)*T + q:
-//   hash = mix32((row * ((T + 1) / 2) + k / 2) ^ key), half = k odd ? hash >> 16 : hash & 0xffff,
+//   hash = attn_mix((row * ((T + 1) / 2) + k / 2) ^ key), half = k odd ? hash >> 16 : hash & 0xffff,
 //   keep = half >= thr16, thr16 = round(p * 65536) (P(drop) within 8e-6 of p).
 __host__ __device__ inline uint32_t dropout_threshold16(float p) {
   const double t = (double)p * 65536.0 + 0.5;
   return t >= 65536.0 ? 65536u : (uint32_t)t;
 }
+// ABI 10: the pair hash is attn_mix, a mixer of full-rate VALU only -- two 24-bit multiplies
+// (v_mul_u32_u24) between xor-shifts that fold every input bit into the multiplied 24 (6 issue
+// slots against mix32's ~12: its two 32-bit multiplies are quarter-rate); the attention forward
+// hashes 8 pairs per lane and key tile, about a third of its vector work. Drop rate and pair /
+// neighbour / row independence match mix32's (tests/test_hostside.py, oracle/masks.py attn_mix).
+// NRSE_ATTN_MIX32=1 builds the former mix32 form (timing A/B only: the oracle replays attn_mix).
+NRSE_DEV uint32_t attn_mix(uint32_t x) {
+#if NRSE_ATTN_MIX32
+  return mix32(x);
+#else
+  x ^= x >> 16;
+  x = (x & 0xffffffu) * 0xebca6bu;
+  x ^= x >> 13;
+  x = (x & 0xffffffu) * 0xb2ae35u;
+  x ^= x >> 16;
+  return x;
+#endif
+}
 NRSE_DEV uint32_t attn_pair_hash(uint32_t key, uint32_t row, uint32_t tp2, int k) {
-  return mix32((row * tp2 + (uint32_t)(k >> 1)) ^ key);
+  return attn_mix((row * tp2 + (uint32_t)(k >> 1)) ^ key);
 }
 NRSE_DEV bool attn_half_keep(uint32_t hash, int odd, uint32_t thr16) {
   return (odd ? (hash >> 16) : (hash & 0xffffu)) >= thr16;

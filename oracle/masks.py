@@ -56,13 +56,25 @@ def threshold16(p: float) -> int:
     return 65536 if t >= 65536.0 else int(t)
 
 
+def attn_mix(x):
+    """csrc/common.h attn_mix (ABI 10): the attention pair hash of full-rate VALU ops, two 24-bit
+    multiplies (v_mul_u32_u24) between xor-shifts."""
+    x = np.asarray(x, dtype=np.uint64) & M32
+    x ^= x >> np.uint64(16)
+    x = ((x & np.uint64(0xFFFFFF)) * np.uint64(0xEBCA6B)) & M32
+    x ^= x >> np.uint64(13)
+    x = ((x & np.uint64(0xFFFFFF)) * np.uint64(0xB2AE35)) & M32
+    x ^= x >> np.uint64(16)
+    return x
+
+
 def attn_keep_mask(seed: int, p: float, rows: int, T: int) -> np.ndarray:
-    """keep[row, k] of the attention-probability site (csrc/common.h attn_keep): one mix32 hash per
-    pair of keys of a query row, 16 bits per element; row = (b*H + h)*T + q."""
+    """keep[row, k] of the attention-probability site (csrc/common.h attn_keep): one attn_mix hash
+    per pair of keys of a query row, 16 bits per element; row = (b*H + h)*T + q."""
     r = np.arange(rows, dtype=np.uint64)[:, None]
     kk = np.arange(T, dtype=np.uint64)[None, :]
     tp2 = np.uint64((T + 1) // 2)
-    h = mix32(((r * tp2 + (kk >> np.uint64(1))) & M32) ^ site_key(seed))
+    h = attn_mix(((r * tp2 + (kk >> np.uint64(1))) & M32) ^ site_key(seed))
     half = np.where((kk & np.uint64(1)) == 1, h >> np.uint64(16), h & np.uint64(0xFFFF))
     return half >= np.uint64(threshold16(p))
 

@@ -119,6 +119,18 @@ def test_attention_pair_hash_mask_statistics():
     both = float((~pairs[..., 0] & ~pairs[..., 1]).mean())
     assert abs(both - p * p) < 0.002
     assert MK.threshold16(0.0) == 0 and MK.threshold16(1.0) == 65536
+    # ABI 10's full-rate mixer (attn_mix): neighbouring pairs and rows independent too, and the
+    # 16-bit halves uniform (chi-square over the top byte within its expectation)
+    d = (~keep).astype(np.float64)
+    for joint in ((d[:, 1:T - 1:2] * d[:, 2:T:2]).mean(), (d[:-1] * d[1:]).mean(), (d[:-8] * d[8:]).mean()):
+        assert abs(joint - p * p) < 0.002, joint
+    r = np.arange(rows, dtype=np.uint64)[:, None]
+    kp = np.arange((T + 1) // 2, dtype=np.uint64)[None, :]     # one hash per key pair
+    h = MK.attn_mix(((r * np.uint64((T + 1) // 2) + kp) & MK.M32) ^ MK.site_key(1234))
+    for sh in (0, 8, 16, 24):
+        cnt = np.bincount(((h >> np.uint64(sh)) & np.uint64(255)).astype(np.int64).ravel(), minlength=256)
+        e = h.size / 256
+        assert ((cnt - e) ** 2 / e).sum() / 255 < 1.4, sh
     m = MK.attn_dropout_mask(7, p, (2, 3, T, T))
     assert set(np.unique(m)).issubset({0.0, np.float32(1 / (1 - p))})
 
