@@ -20,11 +20,6 @@
 
 namespace {
 
-// NRSE_ATTN_LATEHASH=1 (timing A/B only): the forward's dropout hashes inside the tile, after the
-// exponentials (the pre-r06 placement); the default hashes one tile ahead
-#ifndef NRSE_ATTN_LATEHASH
-#define NRSE_ATTN_LATEHASH 0
-#endif
 constexpr int D = 64;
 constexpr int TILE_B = 64 * 128;  // bytes per 64x64 bf16 tile
 // dK/dV kernel: diagonal accumulator arrays of ndiag(T) = Tp + 80 floats, the diagonal d = kj - qi
@@ -246,23 +241,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
   // current tile computes (the top-of-tile vmcnt(0) covers it)
   const uint16_t* mrow = DM == 2 ? p.drop_mask + (bh * ntiles * 4 + g) * (long long)(ntiles * 64) + (qv ? qi : 0)
                                  : nullptr;
-  // DM 1 (ABI 10): the same word hashed one tile ahead -- the 8 pair hashes of tile it+1 are issued
-  // at the top of tile it, beside its S MFMAs and LDS waits, instead of between its exponentials
-  // and its P.V MFMAs, where the whole hash / compare / bit-assembly chain sat on the critical path
-  // (p = 0.1 with the record: 73.5 us against 56 us reading precomputed bits, tools/bench_attn.py)
-  auto keep_word = [&](int it2) {
-    uint32_t mb = 0;  // bit 4t + r = keep of key 64 it2 + 16t + 4g + r
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int rp = 0; rp < 2; ++rp) {
-        const uint32_t hh = attn_mix((rowpair + (uint32_t)(32 * it2 + 8 * t + rp)) ^ key);
-        mb |= (attn_half_keep(hh, 0, thr) ? 1u : 0u) << (4 * t + 2 * rp);
-        mb |= (attn_half_keep(hh, 1, thr) ? 1u : 0u) << (4 * t + 2 * rp + 1);
-      }
-    return mb;
-  };
-  uint32_t mnext = DM == 2 ? (uint32_t)mrow[0] : (DM == 1 && !NRSE_ATTN_LATEHASH ? keep_word(0) : 0u);
+  uint32_t mnext = DM == 2 ? (uint32_t)mrow[0] : 0u;
   // Lazy rescaling in the base-2 domain: mref is the row's reference maximum, and a tile's scores
   // are formed relative to it in two packed fmas, v = s * c1 + (gl * bias - mref) (no separate
   // subtract before the exponential). Only when some lane of the wave sees a score more than
@@ -298,7 +277,6 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
       kv_dma_issue(kd, Kn, kb + 64, w);
       kv_dma_issue(vd, Kn + TILE_B, kb + 64, w);
       if (DM == 2) mnext = mrow[(long long)(it + 1) * 4 * (ntiles * 64)];
-      if (DM == 1 && !NRSE_ATTN_LATEHASH) mnext = keep_word(it + 1);
     }
     if (!wlive) return;
     // the MFMAs run on every sub-tile (a conditional MFMA makes the compiler stage its result
@@ -355,7 +333,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
       for (int r = 0; r < 4; ++r) pd[t][r] = exp2_(v[t][r]);
 #pragma unroll
     for (int t = 0; t < 4; ++t) lpart2 += f32x2{pd[t][0], pd[t][1]} + f32x2{pd[t][2], pd[t][3]};
-    if constexpr (DM == 2 || (DM == 1 && !NRSE_ATTN_LATEHASH)) {
+    if constexpr (DM == 2) {
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -363,8 +341,6 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
           pd[t][r] = (mcur >> (4 * t + r)) & 1u ? pd[t][r] : 0.f;
           asm("" : "+v"(pd[t][r]));  // keep the packed bf16 conversions (see DM 1)
         }
-      // the backward reads the bits instead of re-hashing: [bh][key tile][g][Tp] u16
-      if (DM == 1 && p.drop_mask && qv) p.drop_mask[((bh * ntiles + it) * 4 + g) * Tp + qi] = (uint16_t)mcur;
     } else if constexpr (DROP) {
       uint32_t mb = 0;  // this lane's 16 keep bits of the tile: bit 4t + r = key kb + 16t + 4g + r
 #pragma unroll
