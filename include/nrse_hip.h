@@ -28,7 +28,9 @@
 #include <stdint.h>
 #include <string.h>
 
-#define NRSE_ABI_VERSION 10
+#define NRSE_ABI_VERSION 11
+/* ABI 11: the MXFP6 correction-plane dtype (4) and nrse_split_lo_mx6 / nrse_cast_mx6 retired; the
+ * params structs are unchanged from ABI 10 (the *_dtype fields now accept 0 / NRSE_FP8 only) */
 /* zero-initialise a params struct and stamp its size: nrse_gemm_params p; NRSE_PARAMS_INIT(p); */
 #define NRSE_PARAMS_INIT(s)            \
   do {                                 \
@@ -49,14 +51,9 @@ typedef enum {
   NRSE_ERR_UNSUPPORTED = -5 /* configuration outside what the kernels implement */
 } nrse_status;
 
-typedef enum { NRSE_F32 = 0, NRSE_BF16 = 1, NRSE_BF16X3 = 2, NRSE_FP8 = 3, NRSE_MX6 = 4 } nrse_dtype;
-/* NRSE_MX6 (ABI 8): OCP MXFP6 e2m3 in blocks of 32 consecutive elements along a row, each block
- * with its own E8M0 scale, stored in NRSE_FP8's footprint (one byte per element): block b of a row
- * is the 32 bytes at element offset 32b = [24 bytes: value j at bits 6j..6j+5 (little-endian) |
- * 1 byte scale s, the block's values times 2^(s-127) | 7 zero bytes]. The scale is the smallest
- * power of two with max|x| <= 7.5 * 2^(s-127); values round to nearest even. The block-scaled MFMA
- * runs e2m3 at twice the e4m3 rate (4x bf16): the split-weight mode's correction operands
- * (nrse_gemm_params.a8 / b8 with dtype NRSE_MX6). Rows must hold whole blocks. */
+typedef enum { NRSE_F32 = 0, NRSE_BF16 = 1, NRSE_BF16X3 = 2, NRSE_FP8 = 3 } nrse_dtype;
+/* (dtype 4 was NRSE_MX6, OCP MXFP6 correction planes, ABI 8-10: measured slower than fp8 at the
+ * same accuracy and retired in ABI 11; every entry point refuses it.) */
 /* NRSE_FP8 (ABI 6): OCP fp8 e4m3fn (gfx950's native fp8), one byte per element, saturated at +-448;
  * the split-weight mode's correction operands (nrse_gemm_params.a8 / b8). */
 /* NRSE_BF16X3 (an OUTPUT format of nrse_layernorm_fwd and nrse_conv0_fwd only): the split-bf16
@@ -164,10 +161,7 @@ typedef struct {
    * GELU output feeding FFN-down's correction segment). ldc8 % 16 == 0, 16-byte aligned. */
   void* c8;
   long long ldc8;
-  /* ABI 8: a8 / b8 may both be NRSE_MX6 (then b8_exp must be 0: the scales are in the blocks);
-   * c8_dtype NRSE_MX6 writes c8 as MXFP6 blocks of the stored bf16 values (the register epilogue
-   * forms only); 0 or NRSE_FP8: fp8 */
-  int c8_dtype;
+  int c8_dtype;                   /* 0 or NRSE_FP8 (fp8); anything else is refused */
 } nrse_gemm_params;
 
 int nrse_gemm(const nrse_gemm_params* p, void* stream);
@@ -209,9 +203,7 @@ typedef struct {
    * stack's split-weight form): y8 [2, rows, C] = [fp8((o - bf16(o)) 2^y8_exp) |
    * fp8(bf16(o))], y = bf16(o); the next conv GEMM's a8 segments against [fp8(w_hi) | fp8(w_lo 2^e)] */
   int y8_split; int y8_exp;
-  /* ABI 8: y8_dtype NRSE_MX6 writes y8 (either form) as MXFP6 blocks instead of fp8 (y8_exp is
-   * then unused: the blocks carry their scales); 0 or NRSE_FP8: fp8 */
-  int y8_dtype;
+  int y8_dtype;                   /* 0 or NRSE_FP8 (fp8); anything else is refused */
   /* ABI 10, optional: sat_count[0] += the number of y8 values whose fp8 conversion saturated
    * (|v| > 448 before rounding; the scaled correction plane and the unscaled hi / fp8(bf16 y) plane
    * alike). Never touched when nothing saturates; the engine reads it back lagged and re-derives
@@ -318,8 +310,7 @@ typedef struct {
   void* ctx8;                     /* ABI 6, optional (bf16 MFMA path): [B*T, Hd] NRSE_FP8 copy of ctx,
                                      fp8(bf16 ctx) (the out-projection's fp8 correction operand);
                                      4-byte aligned. NULL: none */
-  int ctx8_dtype;                 /* ABI 8: NRSE_MX6 = ctx8 as MXFP6 blocks (head_dim 64, 32-byte
-                                     aligned); 0 or NRSE_FP8: fp8 */
+  int ctx8_dtype;                 /* 0 or NRSE_FP8 (fp8); anything else is refused */
 } nrse_attn_fwd_params;
 
 typedef struct {
@@ -379,8 +370,7 @@ typedef struct {
    * output o, y8 [2, B*T0, C] NRSE_FP8 = [fp8((o - bf16(o)) 2^y8_exp) | fp8(bf16(o))] (as
    * nrse_ln_fwd_params.y8_split); out = bf16(o). 16-byte aligned */
   void* y8; int y8_exp;
-  int y8_dtype;                   /* fwd, ABI 8: NRSE_MX6 = the two planes as MXFP6 blocks (no y8_exp);
-                                     0 or NRSE_FP8: fp8 */
+  int y8_dtype;                   /* fwd: 0 or NRSE_FP8 (fp8); anything else is refused */
   unsigned int* sat_count;        /* fwd, ABI 10, optional: as nrse_ln_fwd_params.sat_count, for y8 */
 } nrse_conv0_params;
 int nrse_conv0_fwd(const nrse_conv0_params* p, void* stream);
@@ -449,10 +439,6 @@ int nrse_split_lo8(const float* x, void* lo8, int lo8_exp, long long n, unsigned
 /* (ABI 10: sat_count optional, += the saturated conversions, as nrse_adamw_params.sat_count) */
 /* ABI 6: y8[i] = fp8(x[i]) of a bf16 / f32 tensor (NRSE_FP8, saturated at +-448), n elements */
 int nrse_cast_fp8(const void* x, int x_dtype, void* y8, long long n, void* stream);
-/* ABI 8: the MXFP6 forms (NRSE_MX6 blocks, n a multiple of 32, 32-byte aligned y):
- * lo6 = MXFP6(x - bf16(x)) of an f32 tensor, y6 = MXFP6(x) of a bf16 / f32 tensor */
-int nrse_split_lo_mx6(const float* x, void* lo6, long long n, void* stream);
-int nrse_cast_mx6(const void* x, int x_dtype, void* y6, long long n, void* stream);
 /* ABI 6: dst[i] = 0 for i < n floats (the step's small accumulators: no torch fill kernel) */
 int nrse_zero(float* dst, long long n, void* stream);
 /* Split-K reduction of a weight gradient (the Linear wgrads of the backward, train_byol.py:65):
@@ -573,10 +559,7 @@ typedef struct {
   /* ABI 6, optional: nonzero stores 0 to every g[i] after reading it, so the gradient buffer is
    * zeroed for the next step's accumulation inside this pass (no separate fill over g) */
   int zero_grad;
-  /* ABI 8: lo8_dtype NRSE_MX6 writes p_shadow_lo8 / ema_shadow_lo8 as MXFP6 blocks of
-   * p_new - bf16(p_new) (no lo8_exp; n, ema_n multiples of 32, 32-byte aligned planes); 0 or
-   * NRSE_FP8: fp8 */
-  int lo8_dtype;
+  int lo8_dtype;                  /* 0 or NRSE_FP8 (fp8); anything else is refused */
   /* ABI 10, optional: sat_count[0] += the number of fp8 correction values (p_shadow_lo8 and
    * ema_shadow_lo8) that saturated, |(w - bf16 w) 2^lo8_exp| > 448: lo8_exp no longer has headroom
    * for the weights (they grew in training); the caller re-derives it (see nrse_ln_fwd_params).

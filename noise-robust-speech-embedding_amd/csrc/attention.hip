@@ -616,9 +616,8 @@ extern "C" int nrse_attn_fwd(const nrse_attn_fwd_params* p, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   NRSE_REQUIRE(!p->ctx8 || (nrse_attn_use_mfma(p->dtype, p->head_dim) && ((uintptr_t)p->ctx8 & 3) == 0),
                "nrse_attn_fwd: ctx8 needs the bf16 MFMA path and 4-byte alignment");
-  NRSE_REQUIRE(!p->ctx8 || p->ctx8_dtype == 0 || p->ctx8_dtype == NRSE_FP8 ||
-                   (p->ctx8_dtype == NRSE_MX6 && p->head_dim == 64 && ((uintptr_t)p->ctx8 & 31) == 0),
-               "nrse_attn_fwd: ctx8_dtype %d (MXFP6: head_dim 64, 32-byte aligned ctx8)", p->ctx8_dtype);
+  NRSE_REQUIRE(!p->ctx8 || p->ctx8_dtype == 0 || p->ctx8_dtype == NRSE_FP8,
+               "nrse_attn_fwd: ctx8_dtype %d (0 or NRSE_FP8)", p->ctx8_dtype);
   if (nrse_attn_use_mfma(p->dtype, p->head_dim)) return nrse_attn_fwd_mfma(p, st);
   NRSE_REQUIRE(p->bias, "nrse_attn_fwd: the f32 path needs the [H, T, Tb] bias table");
   dim3 grid((p->T + 63) / 64, p->H, p->batch);

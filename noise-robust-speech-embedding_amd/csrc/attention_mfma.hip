@@ -389,27 +389,11 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
       u.x = (uint32_t)f2bf(o[dt][0] * inv) | ((uint32_t)f2bf(o[dt][1] * inv) << 16);
       u.y = (uint32_t)f2bf(o[dt][2] * inv) | ((uint32_t)f2bf(o[dt][3] * inv) << 16);
       *reinterpret_cast<uint2*>(crow + 16 * dt) = u;
-      if (p.ctx8 && p.ctx8_dtype != NRSE_MX6) {  // ABI 6: fp8(bf16 ctx), the out-projection's operand
+      if (p.ctx8) {  // ABI 6: fp8(bf16 ctx), the out-projection's operand
         float b4[4] = {bf2f(f2bf(o[dt][0] * inv)), bf2f(f2bf(o[dt][1] * inv)), bf2f(f2bf(o[dt][2] * inv)),
                        bf2f(f2bf(o[dt][3] * inv))};
         *reinterpret_cast<uint32_t*>((unsigned char*)p.ctx8 + ((long long)b * T + qi) * Hd + h * D + 4 * g + 16 * dt) =
             fp8x4(b4[0], b4[1], b4[2], b4[3]);
-      }
-    }
-    if (p.ctx8 && p.ctx8_dtype == NRSE_MX6) {
-      // ABI 8: MXFP6 blocks of bf16 ctx, dims 32c .. 32c+31 = (dt = 2c, 2c+1) x lanes i16 + 16g
-      unsigned char* c8 = (unsigned char*)p.ctx8 + ((long long)b * T + qi) * Hd + h * D + 4 * g;
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        float v0[4], v1[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          v0[r] = bf2f(f2bf(o[2 * c][r] * inv));
-          v1[r] = bf2f(f2bf(o[2 * c + 1][r] * inv));
-        }
-        const uint2 w = mx6_g4x2(v0, v1, lane, g);
-        *reinterpret_cast<uint32_t*>(c8 + 32 * c) = w.x;
-        *reinterpret_cast<uint32_t*>(c8 + 32 * c + 16) = w.y;
       }
     }
   }

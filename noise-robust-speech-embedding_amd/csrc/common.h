@@ -99,87 +99,6 @@ NRSE_DEV void fp8x4_split(const float* o, float sc, uint32_t& lo8, uint32_t& hi8
   hi8 = fp8x4(h[0], h[1], h[2], h[3]);
   if (nsat) *nsat += fp8_nsat4(l[0], l[1], l[2], l[3]) + fp8_nsat4(h[0], h[1], h[2], h[3]);
 }
-// ---- MXFP6 (ABI 8, NRSE_MX6): e2m3 values in blocks of 32 with an E8M0 scale each; block b of a
-// row = 32 bytes at byte 32b: [24 B, value j at bits 6j..6j+5 | scale byte | 7 zero bytes]
-// (the lane layout of v_mfma_scale_f32_16x16x128_f8f6f4 for fp6: lane (g, i) holds k = 32g + j,
-// packed in that order, and its scale byte scales exactly that block -- tools/probe_mx.hip)
-// the block exponent X: the smallest with amax <= 7.5 * 2^X (the largest e2m3 is 7.5 = 1.875 * 4)
-NRSE_DEV int mx6_exp(float amax) {
-  const uint32_t b = __float_as_uint(amax);
-  const int X = (int)(b >> 23) - 129 + ((b & 0x7fffffu) > 0x700000u ? 1 : 0);
-  return X < -127 ? -127 : X;
-}
-// e2m3 code (sign bit 5) of q, |q| clamped to 7.5, rounded to nearest even
-NRSE_DEV uint32_t e2m3(float q) {
-  const uint32_t s = (__float_as_uint(q) >> 26) & 32u;
-  const float a = fminf(fabsf(q), 7.5f);
-  const uint32_t sub = (uint32_t)__builtin_rintf(a * 8.f);  // a < 1: m / 8 (8 -> 1.0 = code 8)
-  uint32_t b = __float_as_uint(a);
-  b += 0x7ffffu + ((b >> 20) & 1u);                           // RNE to 3 mantissa bits
-  const uint32_t nrm = (((b >> 23) - 126u) << 3) | ((b >> 20) & 7u);
-  return s | (a < 1.f ? sub : nrm);
-}
-NRSE_DEV float mx6_inv(int X) { return __uint_as_float((uint32_t)(127 - X) << 23); }
-NRSE_DEV uint32_t e2m3x4(const float* v, float inv) {
-  return e2m3(v[0] * inv) | (e2m3(v[1] * inv) << 6) | (e2m3(v[2] * inv) << 12) | (e2m3(v[3] * inv) << 18);
-}
-// one block held as 4 consecutive values by each of 8 consecutive lanes (group q = lane & 7):
-// returns the dword this lane stores at block byte 4q. Every lane of the 8 must call it.
-NRSE_DEV uint32_t mx6_g8(const float* v, int lane) {
-  float am = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
-  am = fmaxf(am, __shfl_xor(am, 1));
-  am = fmaxf(am, __shfl_xor(am, 2));
-  am = fmaxf(am, __shfl_xor(am, 4));
-  const int X = mx6_exp(am);
-  const uint32_t c = e2m3x4(v, mx6_inv(X));   // this lane's 24 bits, at block bit 24q
-  // dword q < 6 = bits 32q .. 32q+31: the 24-bit pieces of groups la and la + 1
-  const int q = lane & 7, r = q % 3, la = (lane & ~7) + (q / 3) * 4 + r;
-  const uint32_t A = (uint32_t)__shfl((int)c, la), B = (uint32_t)__shfl((int)c, la + 1);
-  const uint32_t d = r == 0 ? (A | (B << 24)) : (r == 1 ? ((A >> 8) | (B << 16)) : ((A >> 16) | (B << 8)));
-  return q < 6 ? d : (q == 6 ? (uint32_t)(X + 127) : 0u);
-}
-// one block held as 8 consecutive values by each of 4 lanes base + S q (q = 0..3): returns the two
-// dwords this lane stores at block byte 8q. Every lane of the 4 must call it.
-NRSE_DEV uint2 mx6_g4(const float* v, int lane, int q, int S) {
-  float am = 0.f;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) am = fmaxf(am, fabsf(v[e]));
-  am = fmaxf(am, __shfl_xor(am, S));
-  am = fmaxf(am, __shfl_xor(am, 2 * S));
-  const int X = mx6_exp(am);
-  const float inv = mx6_inv(X);
-  const uint32_t lo = e2m3x4(v, inv), hi = e2m3x4(v + 4, inv);   // 48 bits at block bit 48q
-  const uint32_t nlo = (uint32_t)__shfl((int)lo, lane + S), nhi = (uint32_t)__shfl((int)hi, lane + S);
-  const uint64_t P = (uint64_t)lo | ((uint64_t)hi << 24), N = (uint64_t)nlo | ((uint64_t)nhi << 24);
-  const uint64_t d = q < 3 ? ((P >> (16 * q)) | (N << (48 - 16 * q))) : (uint64_t)(X + 127);
-  return make_uint2((uint32_t)d, (uint32_t)(d >> 32));
-}
-// one block held by 4 lanes base + 16 g (g = 0..3) as two 4-value groups each: v0 = values 4g..4g+3,
-// v1 = values 16+4g..16+4g+3 (the attention forward's context layout); returns the dwords this
-// lane stores at block bytes 4g and 16 + 4g. Every lane of the 4 must call it.
-NRSE_DEV uint2 mx6_g4x2(const float* v0, const float* v1, int lane, int g) {
-  float am = fmaxf(fmaxf(fmaxf(fabsf(v0[0]), fabsf(v0[1])), fmaxf(fabsf(v0[2]), fabsf(v0[3]))),
-                   fmaxf(fmaxf(fabsf(v1[0]), fabsf(v1[1])), fmaxf(fabsf(v1[2]), fabsf(v1[3]))));
-  am = fmaxf(am, __shfl_xor(am, 16));
-  am = fmaxf(am, __shfl_xor(am, 32));
-  const int X = mx6_exp(am);
-  const float inv = mx6_inv(X);
-  const uint32_t c0 = e2m3x4(v0, inv), c1 = e2m3x4(v1, inv);
-  // 4-value group k (block bits 24k) is held by lane base + 16 (k & 3) in its v(k >> 2)
-  auto piece = [&](int k) {
-    const int src = (lane & 15) + 16 * (k & 3);
-    const uint32_t a = (uint32_t)__shfl((int)c0, src), b = (uint32_t)__shfl((int)c1, src);
-    return k < 4 ? a : b;
-  };
-  auto dword = [&](int q) {  // bits 32q .. 32q+31 from the groups la, la + 1 (q < 6)
-    const int r = q % 3, la = (q / 3) * 4 + r;
-    const uint32_t A = piece(la), B = piece(la + 1);
-    return r == 0 ? (A | (B << 24)) : (r == 1 ? ((A >> 8) | (B << 16)) : ((A >> 16) | (B << 8)));
-  };
-  const uint32_t lo = dword(g);
-  const uint32_t hi = dword(g < 2 ? g + 4 : 0);
-  return make_uint2(lo, g < 2 ? hi : (g == 2 ? (uint32_t)(X + 127) : 0u));
-}
 // 8 packed bf16 (a 16-B row chunk) -> 8 fp8 bytes
 NRSE_DEV uint2 fp8x8_from_bf16x8(uint4 u) {
   uint2 r;

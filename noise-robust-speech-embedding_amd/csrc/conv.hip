@@ -242,21 +242,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
         *reinterpret_cast<uint4*>(dst) = u;
         if constexpr (S8) {
           uint2 l8, h8;
-          if (p.y8_dtype == NRSE_MX6) {  // ABI 8: a block = channels 32q'..+31 = lanes l + 16g, g = 0..3
-            float h[8], lo[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              h[e] = bf2f(f2bf(o[e]));
-              lo[e] = o[e] - h[e];
-            }
-            l8 = mx6_g4(lo, lane, g, 16);
-            h8 = mx6_g4(h, lane, g, 16);
-          } else {
-            int ns = 0;
-            fp8x4_split(o, sc8, l8.x, h8.x, &ns);
-            fp8x4_split(o + 4, sc8, l8.y, h8.y, &ns);
-            sat_count_add(p.sat_count, ns);
-          }
+          int ns = 0;
+          fp8x4_split(o, sc8, l8.x, h8.x, &ns);
+          fp8x4_split(o + 4, sc8, l8.y, h8.y, &ns);
+          sat_count_add(p.sat_count, ns);
           unsigned char* d8 = (unsigned char*)p.y8 + row * C + c0;
           *reinterpret_cast<uint2*>(d8) = l8;
           *reinterpret_cast<uint2*>(d8 + rows * C) = h8;
@@ -1024,9 +1013,9 @@ extern "C" int nrse_conv0_fwd(const nrse_conv0_params* p, void* stream) {
     // ABI 7 fp8 correction planes: the matrix-core kernel's split-planes form only
     NRSE_REQUIRE(k10 && p->out_dtype == NRSE_BF16 && (p->C == 512 || p->C == 256) && conv0_mfma_on() &&
                      ((uintptr_t)p->y8 & 31) == 0 && p->y8_exp >= -60 && p->y8_exp <= 60 &&
-                     (p->y8_dtype == 0 || p->y8_dtype == NRSE_FP8 || p->y8_dtype == NRSE_MX6),
+                     (p->y8_dtype == 0 || p->y8_dtype == NRSE_FP8),
                  "nrse_conv0_fwd: y8 needs k = 10, a bf16 out, C = 256 | 512, the MFMA form (NRSE_CONV0_MFMA), "
-                 "32-byte alignment, |y8_exp| <= 60 and y8_dtype fp8 / MXFP6");
+                 "32-byte alignment, |y8_exp| <= 60 and y8_dtype 0 / NRSE_FP8");
   }
   if (k10 && p->out_dtype != NRSE_F32 && (p->C == 512 || p->C == 256) && conv0_mfma_on()) {
     // matrix-core form (bf16 / split-bf16 outputs): 2 workgroups per CU, waves loop over 16-row blocks

@@ -419,20 +419,7 @@ extern "C" int nrse_gemm(const nrse_gemm_params* p, void* stream) {
       nrse_set_error("nrse_gemm: c8 needs a bf16 C, batch == splits == 1, 8-byte aligned c8 and ldc8 >= N");
       return NRSE_ERR_UNSUPPORTED;
     }
-    if (p->c8 && p->c8_dtype == NRSE_MX6) {
-      // ABI 8: MXFP6 blocks come from the register epilogue's 16-byte row stores (4 lanes per
-      // block); the general epilogue's flag sets have no such form and are refused
-      // (the bf16-output flag sets of gemm256_kernel's k-contiguous register epilogues: none, bias,
-      // bias + GELU with or without a bf16 pre-activation)
-      const int f = p->flags & ~NRSE_EPI_COLSUM;
-      const bool fast = f == 0 || f == NRSE_EPI_BIAS ||
-                        (f == (NRSE_EPI_BIAS | NRSE_EPI_GELU) && (!p->aux || p->aux_dtype == NRSE_BF16));
-      if (!fast || (p->N & 31) || (p->ldc8 & 31) || ((uintptr_t)p->c8 & 31) || !p->a.kcontig || !p->b.kcontig) {
-        nrse_set_error("nrse_gemm: an MXFP6 c8 needs the register epilogue (none, bias, bias + GELU), "
-                       "k-contiguous operands, N %% 32 == 0, ldc8 %% 32 == 0 and a 32-byte aligned c8");
-        return NRSE_ERR_UNSUPPORTED;
-      }
-    } else if (p->c8 && p->c8_dtype != 0 && p->c8_dtype != NRSE_FP8) {
+    if (p->c8 && p->c8_dtype != 0 && p->c8_dtype != NRSE_FP8) {
       nrse_set_error("nrse_gemm: bad c8_dtype %d", p->c8_dtype);
       return NRSE_ERR_UNSUPPORTED;
     }

@@ -207,22 +207,10 @@ NRSE_DEV bf16x8 frag_half(i32x8v v, int s) {
   return s == 0 ? __builtin_bit_cast(bf16x8, __builtin_shufflevector(v, v, 0, 1, 2, 3))
                 : __builtin_bit_cast(bf16x8, __builtin_shufflevector(v, v, 4, 5, 6, 7));
 }
-// MXFP6 operand (ABI 8): lane (g, i) reads its row's block g whole -- the 32 contiguous bytes
-// (chunks 2g, 2g+1 of the 128-byte K-tile row: conflict-free under the row swizzle like frag's
-// chunk pairs): dwords 0..5 the 32 e2m3 values of k = 32g..32g+31, dword 6 the block's scale
-// byte (the MFMA's opsel 0 byte)
-NRSE_DEV i32x8v frag_mx(const char* lds, int base, int lane) {
-  const int g = lane >> 4, row = base + (lane & 15), sw = (row >> 1) & 7;
-  const char* r = lds + row * 128;
-  const i32x4v a = *reinterpret_cast<const i32x4v*>(r + (((2 * g) ^ sw) << 4));
-  const i32x4v b = *reinterpret_cast<const i32x4v*>(r + (((2 * g + 1) ^ sw) << 4));
-  return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
-}
-
-// MXFP6 operand of the 32x32x64 shape (F8 == 3): lane (h, r) = (lane >> 5, lane & 31) reads row
-// base + r's block 2s + h of the 128-k K-tile (k = 64s + 32h .. +31): chunks 2(2s+h), 2(2s+h)+1,
-// the same 32-byte block reads as frag_mx, 32 rows deep instead of 16
-NRSE_DEV i32x8v frag_mx32(const char* lds, int base, int s, int lane) {
+// fp8 operand of the 32x32x64 shape (F8 == 4): lane (h, r) = (lane >> 5, lane & 31) reads row
+// base + r's 32-byte group 2s + h of the 128-k K-tile (k = 64s + 32h .. +31): chunks 2(2s+h),
+// 2(2s+h)+1, conflict-free under the row swizzle like frag's chunk pairs
+NRSE_DEV i32x8v frag_f32(const char* lds, int base, int s, int lane) {
   const int h = lane >> 5, row = base + (lane & 31), sw = (row >> 1) & 7, c = 2 * (2 * s + h);
   const char* r = lds + row * 128;
   const i32x4v a = *reinterpret_cast<const i32x4v*>(r + ((c ^ sw) << 4));
@@ -230,12 +218,6 @@ NRSE_DEV i32x8v frag_mx32(const char* lds, int base, int s, int lane) {
   return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 typedef float f32x16 __attribute__((ext_vector_type(16)));
-// bf16 operand of the 32x32x16 shape (F8 == 5): lane (h, r) reads row base + r, k = 16j + 8h .. +7
-// of the 64-k K-tile, i.e. its 16-B chunk 2j + h under the row swizzle
-NRSE_DEV bf16x8 frag_b32(const char* lds, int base, int j, int lane) {
-  const int h = lane >> 5, row = base + (lane & 31), sw = (row >> 1) & 7;
-  return *reinterpret_cast<const bf16x8*>(lds + row * 128 + (((2 * j + h) ^ sw) << 4));
-}
 
 // ------------------------------------------------------------------ register epilogue
 // The common epilogues of the step run with their flags fixed at compile time: the lane's
@@ -455,16 +437,7 @@ NRSE_DEV void fast_epilogue(const nrse_gemm_params& p, const f32x4 (&acc)[8][4],
       if constexpr (OBF) {
         // the fp8 copy of the stored bf16 values (ABI 6 c8: the next GEMM's correction operand)
         if (p.c8) {
-          uint2 w;
-          if (p.c8_dtype == NRSE_MX6) {  // ABI 8: MXFP6 blocks; the block's 4 chunks are lanes tid ^ 0..3
-            const float f[8] = {__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
-                                __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u),
-                                __uint_as_float(u.z << 16), __uint_as_float(u.z & 0xffff0000u),
-                                __uint_as_float(u.w << 16), __uint_as_float(u.w & 0xffff0000u)};
-            w = mx6_g4(f, lane, ch & 3, 1);
-          } else {
-            w = fp8x8_from_bf16x8(u);
-          }
+          const uint2 w = fp8x8_from_bf16x8(u);
           *reinterpret_cast<uint2*>((unsigned char*)p.c8 + (long long)m * p.ldc8 + n) = w;
         }
       }
@@ -491,15 +464,17 @@ NRSE_DEV void fast_epilogue(const nrse_gemm_params& p, const f32x4 (&acc)[8][4],
 // BMT: tile rows, 256 or 224 (= 7 x 32: e.g. M = 12768 = 57 x 224 frames of 32 utterances fills
 // 228 of the 256 CUs per N-column of tiles instead of 200; nrse_gemm256 picks the one that
 // needs fewer tile waves, see bm_choice)
-// F8: the split-weight mode's correction segments follow the bf16 K-tiles: 1 fp8 (ABI 6), 2 MXFP6
-// (ABI 8); 3 MXFP6 on the 32x32x64 MFMA shape, the correction K-tiles first (BMT 256 only)
+// F8: 0 bf16 K-tiles only; 1 the split-weight mode's fp8 correction segments after the bf16 K-tiles
+// (ABI 6); 4 the fp8 segments on the 32x32x64 MFMA shape, the correction K-tiles first (BMT 256
+// only). (2 and 3 were the MXFP6 forms of ABI 8, retired in ABI 11; 5, the bf16 K-tiles on
+// 32x32x16, measured 2.5 % slower in the step in r05 and was retired with them.)
 template <bool AKC, bool BKC, int BMT, int F8>
 __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params p, int mt, int nt) {
   static_assert(BMT == 256 || BMT == 224, "tile rows");
   static_assert(!F8 || (AKC && BKC), "fp8 correction segments: k-contiguous operands");
-  static_assert(F8 < 3 || BMT == 256, "the 32x32 correction blocks tile 256-row tiles");
-  constexpr bool W32 = F8 >= 3;  // the correction on the 32x32x64 shape (3 MXFP6, 4 fp8)
-  constexpr bool B32 = F8 == 5;  // the bf16 K-tiles on 32x32x16 (no correction segments)
+  static_assert(F8 == 0 || F8 == 1 || F8 == 4, "kernel forms");
+  static_assert(F8 < 4 || BMT == 256, "the 32x32 blocks tile 256-row tiles");
+  constexpr bool W32 = F8 == 4;  // the fp8 correction on the 32x32x64 shape
   constexpr int NFI_HI = (BMT / 2 - 64) / 16;  // 16-row blocks in an M-wave's high half: 4 or 3
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
   const int tid = threadIdx.x;
@@ -707,13 +682,13 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
     base = wrap(base + 4);
   }
   } else if constexpr (W32) {
-  // MXFP6 (F8 3) or fp8 (F8 4) correction on the 32x32x64 shape (e2m3 there runs at ~1.8x its 16x16x128 rate,
+  // fp8 correction on the 32x32x64 shape (e4m3 there runs at ~1.08x its 16x16x128 rate,
   // tools/probe_mx_rate.hip). The correction K-tiles run FIRST, into one 32x32 accumulator per
   // 32-row x 32-column block of the wave's 128 x 64 output (c32[MH*4 + NH*2 + bi]: M-half MH,
   // N-half NH, 32-row block bi), which are then permuted in registers into the 16x16 layout that
   // the bf16 K-tiles and the epilogue use. Same ring, phases, waits and hand-off rules as above;
   // per phase 8 MFMAs of 32x32x64 (two k-steps of 64 per 128-k K-tile) instead of 16 of 16x16x128.
-  // fp8 (F8 4): every operand byte pair meets its partner whatever k the hardware assigns a lane's
+  // every operand byte pair meets its partner whatever k the hardware assigns a lane's
   // 32 bytes (A and B lanes read the same positions); the weight operand carries 2^-b8_exp
   const int scw32 = 0x01010101 * (127 - p.b8_exp);
   f32x16 c32[8];
@@ -725,19 +700,15 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
 #define NRSE_READ_A32(SLOT)                                                              \
   _Pragma("unroll") for (int bi = 0; bi < 2; ++bi)                                     \
   _Pragma("unroll") for (int s = 0; s < 2; ++s)                                        \
-    fa32[bi][s] = frag_mx32(smem + (SLOT) * HALF, wm * 64 + 32 * bi, s, lane);
+    fa32[bi][s] = frag_f32(smem + (SLOT) * HALF, wm * 64 + 32 * bi, s, lane);
 #define NRSE_READ_B32(SLOT, FB)                                                          \
   _Pragma("unroll") for (int s = 0; s < 2; ++s)                                        \
-    FB[s] = frag_mx32(smem + (SLOT) * HALF, wn * 32, s, lane);
+    FB[s] = frag_f32(smem + (SLOT) * HALF, wn * 32, s, lane);
 #define NRSE_QUAD32(MH, NH, FB)                                                          \
   __builtin_amdgcn_s_setprio(1);                                                         \
   _Pragma("unroll") for (int s = 0; s < 2; ++s)                                        \
   _Pragma("unroll") for (int bi = 0; bi < 2; ++bi)                                     \
-    if constexpr (F8 == 3)                                                               \
-      c32[(MH) * 4 + (NH) * 2 + bi] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(   \
-          FB[s], fa32[bi][s], c32[(MH) * 4 + (NH) * 2 + bi], 2, 2, 0, FB[s][6], 0, fa32[bi][s][6]); \
-    else                                                                                 \
-      c32[(MH) * 4 + (NH) * 2 + bi] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(   \
+    c32[(MH) * 4 + (NH) * 2 + bi] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(   \
           FB[s], fa32[bi][s], c32[(MH) * 4 + (NH) * 2 + bi], 0, 0, 0, scw32, 0, 0x7f7f7f7f); \
   __builtin_amdgcn_s_setprio(0);
 #define NRSE_BAR8()                          \
@@ -823,51 +794,12 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
         }
     }
   };
-  if constexpr (!B32) convert();
-  // B32: the bf16 K-tiles on v_mfma_f32_32x32x16_bf16 into the same 32x32 accumulators (4 k-steps
-  // of 16 per 64-k K-tile, 8 MFMAs per quadrant pair as the 16x16 form's 16), converted after
-  bf16x8 fa3[2][4], fl3[4], fh3[4];
-#define NRSE_READ_A3(SLOT)                                                               \
-  _Pragma("unroll") for (int bi = 0; bi < 2; ++bi)                                     \
-  _Pragma("unroll") for (int j = 0; j < 4; ++j)                                        \
-    fa3[bi][j] = frag_b32(smem + (SLOT) * HALF, wm * 64 + 32 * bi, j, lane);
-#define NRSE_READ_B3(SLOT, FB)                                                           \
-  _Pragma("unroll") for (int j = 0; j < 4; ++j)                                        \
-    FB[j] = frag_b32(smem + (SLOT) * HALF, wn * 32, j, lane);
-#define NRSE_QUAD3(MH, NH, FB)                                                           \
-  __builtin_amdgcn_s_setprio(1);                                                         \
-  _Pragma("unroll") for (int j = 0; j < 4; ++j)                                        \
-  _Pragma("unroll") for (int bi = 0; bi < 2; ++bi)                                     \
-    c32[(MH) * 4 + (NH) * 2 + bi] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(             \
-        FB[j], fa3[bi][j], c32[(MH) * 4 + (NH) * 2 + bi], 0, 0, 0);                      \
-  __builtin_amdgcn_s_setprio(0);
+  convert();
   // the bf16 K-tiles (t + 2 staged as bf16 or dead)
   auto ktileb = [&](int t) {
     const int s0 = base, s1 = wrap(base + 1), s2 = wrap(base + 2), s3 = wrap(base + 3);
     const TilePos q2 = tile_pos_at(t + 2 < ntiles, u_sg, u_k, false);
     if (++u_k == tps) { u_k = 0; ++u_sg; }
-    if constexpr (B32) {
-      NRSE_READ_A3(s0)
-      NRSE_READ_B3(s1, fl3)
-      NRSE_READ_B3(s2, fh3)
-      stage(0, q2, wrap(base + 8));
-      stage(1, q2, wrap(base + 9));
-      NRSE_WAIT(12);
-      NRSE_BAR8();
-      NRSE_QUAD3(0, 0, fl3)
-      NRSE_QUAD3(0, 1, fh3)
-      NRSE_BAR8();
-      NRSE_READ_A3(s3)
-      stage(2, q2, base);
-      stage(3, q2, s1);
-      NRSE_WAIT(10);
-      NRSE_BAR8();
-      NRSE_QUAD3(1, 1, fh3)
-      NRSE_QUAD3(1, 0, fl3)
-      NRSE_BAR8();
-      base = wrap(base + 4);
-      return;
-    }
     NRSE_READ_A(s0, 4)
     NRSE_READ_B(s1, fbl)
     NRSE_READ_B(s2, fbh)
@@ -890,10 +822,6 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
   };
 #pragma unroll 1
   for (; t < ntiles; ++t) ktileb(t);
-  if constexpr (B32) convert();
-#undef NRSE_READ_A3
-#undef NRSE_READ_B3
-#undef NRSE_QUAD3
 #undef NRSE_READ_A32
 #undef NRSE_READ_B32
 #undef NRSE_QUAD32
@@ -913,12 +841,6 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
 #define NRSE_READ_B8(SLOT, FB)                                                           \
   _Pragma("unroll") for (int fj = 0; fj < 2; ++fj)                                     \
     FB[fj] = frag2(smem + (SLOT) * HALF, wn * 32 + fj * 16, lane);
-#define NRSE_READ_AM(SLOT, NFI)                                                          \
-  _Pragma("unroll") for (int fi = 0; fi < (NFI); ++fi)                                 \
-    fa8[fi] = frag_mx(smem + (SLOT) * HALF, wm * 64 + fi * 16, lane);
-#define NRSE_READ_BM(SLOT, FB)                                                           \
-  _Pragma("unroll") for (int fj = 0; fj < 2; ++fj)                                     \
-    FB[fj] = frag_mx(smem + (SLOT) * HALF, wn * 32 + fj * 16, lane);
 #define NRSE_QUADH(MH, NH, FB)                                                           \
   __builtin_amdgcn_s_setprio(1);                                                         \
   _Pragma("unroll") for (int s = 0; s < 2; ++s)                                        \
@@ -926,17 +848,12 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
   _Pragma("unroll") for (int fj = 0; fj < 2; ++fj)                                     \
     NRSE_MFMA(acc[(MH) * 4 + fi][(NH) * 2 + fj], frag_half(fa8[fi], s), frag_half(FB[fj], s)); \
   __builtin_amdgcn_s_setprio(0);
-// MXFP6 (F8 == 2): format 2 (e2m3) for both operands, each lane's scale the block's own byte
-// (dword 6 of its fragment); e2m3 runs at twice the e4m3 rate
+// fp8 (F8 == 1): format 0 (e4m3) for both operands
 #define NRSE_QUAD8(MH, NH, FB)                                                           \
   __builtin_amdgcn_s_setprio(1);                                                         \
   _Pragma("unroll") for (int fi = 0; fi < ((MH) ? NFI_HI : 4); ++fi)                   \
   _Pragma("unroll") for (int fj = 0; fj < 2; ++fj)                                     \
-    if constexpr (F8 == 2)                                                               \
-      acc[(MH) * 4 + fi][(NH) * 2 + fj] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4( \
-          FB[fj], fa8[fi], acc[(MH) * 4 + fi][(NH) * 2 + fj], 2, 2, 0, FB[fj][6], 0, fa8[fi][6]); \
-    else                                                                                 \
-      acc[(MH) * 4 + fi][(NH) * 2 + fj] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4( \
+    acc[(MH) * 4 + fi][(NH) * 2 + fj] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4( \
           FB[fj], fa8[fi], acc[(MH) * 4 + fi][(NH) * 2 + fj], 0, 0, 0, scw, 0, sc1);      \
   __builtin_amdgcn_s_setprio(0);
 // the raw barrier with scheduling fences: without them the compiler moved this loop's MFMAs across
@@ -982,15 +899,9 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
         stage(j, q2, slot);
       }
     };
-    if constexpr (K8 && F8 == 2) {
-      NRSE_READ_AM(s0, 4)
-      NRSE_READ_BM(s1, fbl8)
-      NRSE_READ_BM(s2, fbh8)
-    } else {
-      NRSE_READ_A8(s0, 4)
-      NRSE_READ_B8(s1, fbl8)
-      NRSE_READ_B8(s2, fbh8)
-    }
+    NRSE_READ_A8(s0, 4)
+    NRSE_READ_B8(s1, fbl8)
+    NRSE_READ_B8(s2, fbh8)
     stg(0, wrap(base + 8));
     stg(1, wrap(base + 9));
     NRSE_WAIT(12);
@@ -1003,11 +914,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
       NRSE_QUADH(0, 1, fbh8)
     }
     NRSE_BAR8();
-    if constexpr (K8 && F8 == 2) {
-      NRSE_READ_AM(s3, NFI_HI)
-    } else {
-      NRSE_READ_A8(s3, NFI_HI)
-    }
+    NRSE_READ_A8(s3, NFI_HI)
     stg(2, base);
     stg(3, s1);
     NRSE_WAIT(10);
@@ -1029,8 +936,6 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
   for (; t < ntiles; ++t) ktile(t, std::true_type{});
 #undef NRSE_READ_A8
 #undef NRSE_READ_B8
-#undef NRSE_READ_AM
-#undef NRSE_READ_BM
 #undef NRSE_QUADH
 #undef NRSE_QUAD8
 #undef NRSE_BAR8
@@ -1189,7 +1094,7 @@ int bm_choice(const nrse_gemm_params* p) {
 
 template <bool AKC, bool BKC, int F8 = 0>
 int launch(const nrse_gemm_params* p, hipStream_t st) {
-  if constexpr (F8 >= 3) {
+  if constexpr (F8 >= 4) {
     const int mt = nrse_cdiv(p->M, 256), nt = nrse_cdiv(p->N, BN);
     const long long total = (long long)mt * nt * p->batch * p->splits;
     hipLaunchKernelGGL((gemm256_kernel<AKC, BKC, 256, F8>), dim3((unsigned)total), dim3(NTHR), 0, st, *p, mt, nt);
@@ -1198,7 +1103,7 @@ int launch(const nrse_gemm_params* p, hipStream_t st) {
   const int bm = bm_choice(p);
   const int mt = nrse_cdiv(p->M, bm), nt = nrse_cdiv(p->N, BN);
   const long long total = (long long)mt * nt * p->batch * p->splits;
-  if constexpr (F8 < 3) {
+  if constexpr (F8 < 4) {
     if (bm == 224)
       hipLaunchKernelGGL((gemm256_kernel<AKC, BKC, 224, F8>), dim3((unsigned)total), dim3(NTHR), 0, st, *p, mt, nt);
     else
@@ -1241,10 +1146,7 @@ bool nrse_gemm256_f8_ok(const nrse_gemm_params* p) {
   if (p->a8.ld != p->a.ld || p->b8.ld != p->b.ld || (p->a.ld & 63) || (p->b.ld & 63)) return false;
   const long long spa = (long long)(p->nseg8 - 1) * p->a8.seg_stride + (long long)p->M * p->a8.ld + p->K;
   const long long spb = (long long)(p->nseg8 - 1) * p->b8.seg_stride + (long long)p->N * p->b8.ld + p->K;
-  // MXFP6 (ABI 8): the scales travel in the blocks, so no b8_exp; blocks start at 32-byte offsets
-  const bool mx = p->a8.dtype == NRSE_MX6;
-  if (p->a8.dtype != NRSE_FP8 && !mx) return false;
-  if (mx && (p->b8_exp != 0 || ((uintptr_t)p->a8.ptr & 31) || ((uintptr_t)p->b8.ptr & 31))) return false;
+  if (p->a8.dtype != NRSE_FP8) return false;
   return p->K % 128 == 0 && p->splits == 1 && p->a.kcontig && p->b.kcontig && spa < (1LL << 31) &&
          spb < (1LL << 31) && p->b8_exp > -127 && p->b8_exp < 127;
 }
@@ -1258,30 +1160,14 @@ static bool fp8_wide() {
   return v == 1;
 }
 
-// the forward GEMMs' bf16 K-tiles on the 32x32x16 shape (F8 = 5) with NRSE_GEMM_W32=1
-static bool bf16_wide() {
-  static int v = -1;
-  if (v < 0) v = (getenv("NRSE_GEMM_W32") && atoi(getenv("NRSE_GEMM_W32")) == 1) ? 1 : 0;
-  return v == 1;
-}
-
-// MXFP6 segments on the 32x32x64 shape unless NRSE_MX6_SHAPE=16 (the 16x16x128 form, F8 = 2)
-static bool mx6_wide() {
-  static int v = -1;
-  if (v < 0) v = (getenv("NRSE_MX6_SHAPE") && atoi(getenv("NRSE_MX6_SHAPE")) == 16) ? 0 : 1;
-  return v == 1;
-}
-
 int nrse_gemm256(const nrse_gemm_params* p, hipStream_t st) {
   if (p->nseg8 > 0) {
+    // (the 32x32 form tiles 256 rows: a problem pinned to 224-row tiles keeps the 16x16 form, whose
+    // row count the column-sum workspace was sized for)
     const bool r256 = bm_choice(p) == 256;
-    if (p->a8.dtype != NRSE_MX6) return fp8_wide() && r256 ? launch<true, true, 4>(p, st) : launch<true, true, 1>(p, st);
-    return mx6_wide() && r256 ? launch<true, true, 3>(p, st) : launch<true, true, 2>(p, st);
+    return fp8_wide() && r256 ? launch<true, true, 4>(p, st) : launch<true, true, 1>(p, st);
   }
-  // (the 32x32 forms tile 256 rows: a problem pinned to 224-row tiles keeps the 16x16 form, whose
-  // row count the column-sum workspace was sized for)
-  if (p->a.kcontig && p->b.kcontig)
-    return (bf16_wide() && bm_choice(p) == 256) ? launch<true, true, 5>(p, st) : launch<true, true>(p, st);
+  if (p->a.kcontig && p->b.kcontig) return launch<true, true>(p, st);
   if (p->a.kcontig && !p->b.kcontig) return launch<true, false>(p, st);
   if (!p->a.kcontig && p->b.kcontig) return launch<false, true>(p, st);
   return launch<false, false>(p, st);

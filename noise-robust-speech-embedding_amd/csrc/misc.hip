@@ -321,26 +321,6 @@ __global__ void cast_fp8_kernel(const void* __restrict__ x, int xdt, unsigned ch
     y[i] = fp8_1(load_as_f(x, xdt, i));
 }
 
-// ABI 8 MXFP6 forms (n % 32 == 0): quad q of 4 elements per lane, a block = 8 consecutive lanes;
-// the grid-stride loop runs whole waves (live flag) so every block's 8 lanes shuffle together
-__global__ void mx6_kernel(const void* __restrict__ x, int xdt, bool lo, uint32_t* __restrict__ y, long long n) {
-  const long long n4 = n / 4, step = (long long)gridDim.x * blockDim.x;
-  const long long nw = (n4 + 63) / 64 * 64;
-  for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < nw; q += step) {
-    const bool live = q < n4;
-    float v[4] = {0.f, 0.f, 0.f, 0.f};
-    if (live) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float f = load_as_f(x, xdt, 4 * q + e);
-        v[e] = lo ? lo_resid(f) : f;
-      }
-    }
-    const uint32_t d = mx6_g8(v, threadIdx.x & 63);
-    if (live) y[q] = d;
-  }
-}
-
 __global__ void zero_kernel(float* __restrict__ d, long long n) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
     d[i] = 0.f;
@@ -550,24 +530,6 @@ extern "C" int nrse_cast_fp8(const void* x, int xdt, void* y8, long long n, void
   hipLaunchKernelGGL(cast_fp8_kernel, dim3(blocks_for(n)), dim3(256), 0, (hipStream_t)stream, x, xdt,
                      (unsigned char*)y8, n);
   return nrse_check_launch("nrse_cast_fp8");
-}
-
-extern "C" int nrse_split_lo_mx6(const float* x, void* lo6, long long n, void* stream) {
-  NRSE_REQUIRE(x && lo6 && n >= 0 && n % 32 == 0 && ((uintptr_t)lo6 & 31) == 0 && ((uintptr_t)x & 15) == 0,
-               "nrse_split_lo_mx6: bad args (n %% 32 == 0, 32-byte aligned lo6)");
-  if (n == 0) return NRSE_OK;
-  hipLaunchKernelGGL(mx6_kernel, dim3(blocks_for(n / 4)), dim3(256), 0, (hipStream_t)stream, (const void*)x, (int)NRSE_F32,
-                     true, (uint32_t*)lo6, n);
-  return nrse_check_launch("nrse_split_lo_mx6");
-}
-
-extern "C" int nrse_cast_mx6(const void* x, int xdt, void* y6, long long n, void* stream) {
-  NRSE_REQUIRE(x && y6 && n >= 0 && n % 32 == 0 && ((uintptr_t)y6 & 31) == 0 && (xdt == NRSE_F32 || xdt == NRSE_BF16),
-               "nrse_cast_mx6: bad args (n %% 32 == 0, 32-byte aligned y6)");
-  if (n == 0) return NRSE_OK;
-  hipLaunchKernelGGL(mx6_kernel, dim3(blocks_for(n / 4)), dim3(256), 0, (hipStream_t)stream, x, xdt, false,
-                     (uint32_t*)y6, n);
-  return nrse_check_launch("nrse_cast_mx6");
 }
 
 extern "C" int nrse_zero(float* dst, long long n, void* stream) {

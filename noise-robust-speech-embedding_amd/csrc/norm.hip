@@ -54,22 +54,6 @@ NRSE_DEV void unpack_bf4(uint2 v, float* o) {
 // the fp8 copies of 4 outputs at element i: fp8(bf16 o) (ABI 6), or the split planes (ABI 7)
 NRSE_DEV void store_y8(const nrse_ln_fwd_params& p, long long i, const float* o) {
   unsigned char* y8 = (unsigned char*)p.y8 + i;
-  if (p.y8_dtype == NRSE_MX6) {  // ABI 8: MXFP6 blocks (32 consecutive = 8 lanes x 4; wave-uniform branch)
-    const int lane = threadIdx.x & 63;
-    float h[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) h[e] = bf2f(f2bf(o[e]));
-    if (p.y8_split) {
-      float l[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) l[e] = o[e] - h[e];
-      *reinterpret_cast<uint32_t*>(y8) = mx6_g8(l, lane);
-      *reinterpret_cast<uint32_t*>(y8 + p.rows * p.C) = mx6_g8(h, lane);
-    } else {
-      *reinterpret_cast<uint32_t*>(y8) = mx6_g8(h, lane);
-    }
-    return;
-  }
   if (p.y8_split) {
     uint32_t lo, hi;
     int ns = 0;
@@ -652,9 +636,8 @@ extern "C" int nrse_layernorm_fwd(const nrse_ln_fwd_params* p, void* stream) {
                "nrse_layernorm_fwd: y8 needs a bf16 y and 4-byte alignment");
   NRSE_REQUIRE((p->y8_split == 0 || p->y8_split == 1) && p->y8_exp >= -60 && p->y8_exp <= 60,
                "nrse_layernorm_fwd: y8_split %d / y8_exp %d out of range", p->y8_split, p->y8_exp);
-  NRSE_REQUIRE(!p->y8 || p->y8_dtype == 0 || p->y8_dtype == NRSE_FP8 ||
-                   (p->y8_dtype == NRSE_MX6 && ((uintptr_t)p->y8 & 31) == 0 && p->C % 32 == 0),
-               "nrse_layernorm_fwd: y8_dtype %d (MXFP6 needs a 32-byte aligned y8)", p->y8_dtype);
+  NRSE_REQUIRE(!p->y8 || p->y8_dtype == 0 || p->y8_dtype == NRSE_FP8,
+               "nrse_layernorm_fwd: y8_dtype %d (0 or NRSE_FP8)", p->y8_dtype);
   if (p->x_dtype == NRSE_BF16 && p->C <= 512 && ((uintptr_t)p->x & 7) == 0 && !p->y8) {
     constexpr int RPW = 4;
     const dim3 g((unsigned)((p->rows + 4 * RPW - 1) / (4 * RPW)));

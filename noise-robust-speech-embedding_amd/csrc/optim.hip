@@ -95,15 +95,8 @@ NRSE_DEV void ema_one(const nrse_adamw_params& p, long long i, float pn, float e
   }
 }
 
-// the fp8 correction plane of 4 consecutive weights at float4 index q (ABI 6); mx: the MXFP6 form
-// (ABI 8), a block = the 8 lanes q & ~7 .. (all live together: the host requires n % 32 == 0)
-NRSE_DEV void store_lo8x4(const nrse_adamw_params& p, void* lo8, long long q, const float* x, float sc8, bool mx,
-                         int& ns) {
-  if (mx) {
-    const float l[4] = {lo_resid(x[0]), lo_resid(x[1]), lo_resid(x[2]), lo_resid(x[3])};
-    reinterpret_cast<uint32_t*>(lo8)[q] = mx6_g8(l, threadIdx.x & 63);
-    return;
-  }
+// the fp8 correction plane of 4 consecutive weights at float4 index q (ABI 6)
+NRSE_DEV void store_lo8x4(const nrse_adamw_params& p, void* lo8, long long q, const float* x, float sc8, int& ns) {
   const float a = lo_resid(x[0]) * sc8, b = lo_resid(x[1]) * sc8, c = lo_resid(x[2]) * sc8, d = lo_resid(x[3]) * sc8;
   reinterpret_cast<uint32_t*>(lo8)[q] = fp8x4(a, b, c, d);
   const unsigned m = (fabsf(a) > 448.f ? 1u : 0u) | (fabsf(b) > 448.f ? 2u : 0u) | (fabsf(c) > 448.f ? 4u : 0u) |
@@ -130,7 +123,6 @@ __global__ __launch_bounds__(256) void adamw_kernel(const nrse_adamw_params p) {
   const long long e4 = p.ema_n / 4;  // whole quads of the fused EMA range
   const float eom = 1.f - p.ema_decay;
   const float sc8 = ldexpf(1.f, p.lo8_exp);
-  const bool mx = p.lo8_dtype == NRSE_MX6;
   const bool ema4 = p.ema_t && e4 > 0;  // uniform: a whole EMA quad exists to load
   int ns = 0;                           // saturated fp8 corrections (ABI 10 sat_count)
   for (long long q = (long long)blockIdx.x * 256 + threadIdx.x; q < n4; q += (long long)gridDim.x * 256) {
@@ -165,7 +157,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(const nrse_adamw_params p) {
         reinterpret_cast<float4*>(p.p_shadow)[q] = pv;
       }
     }
-    if (p.p_shadow_lo8) store_lo8x4(p, p.p_shadow_lo8, q, pa, sc8, mx, ns);
+    if (p.p_shadow_lo8) store_lo8x4(p, p.p_shadow_lo8, q, pa, sc8, ns);
     if (p.ema_t) {
       if (q < e4) {
         tv.x = ema_mix(tv.x, pv.x, p.ema_decay, eom); tv.y = ema_mix(tv.y, pv.y, p.ema_decay, eom);
@@ -175,7 +167,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(const nrse_adamw_params p) {
           if (p.ema_shadow_dtype == NRSE_BF16) store_bf16x4(p.ema_shadow, p.ema_shadow_lo, q, &tv.x);
           else reinterpret_cast<float4*>(p.ema_shadow)[q] = tv;
         }
-        if (p.ema_shadow_lo8) store_lo8x4(p, p.ema_shadow_lo8, q, &tv.x, sc8, mx, ns);
+        if (p.ema_shadow_lo8) store_lo8x4(p, p.ema_shadow_lo8, q, &tv.x, sc8, ns);
       } else if (q == e4) {
         // the quad holding the EMA range's end: its first ema_n - 4 q elements, from this thread's
         // updated registers
@@ -303,10 +295,8 @@ extern "C" int nrse_adamw(const nrse_adamw_params* p, void* stream) {
                    (!p->ema_shadow_lo8 || p->ema_t),
                "nrse_adamw: fp8 planes need 4-byte alignment (and ema_t for ema_shadow_lo8)");
   NRSE_REQUIRE(!p->sat_ranges || (p->sat_count && p->sat_nranges >= 0), "nrse_adamw: sat_ranges without sat_count");
-  NRSE_REQUIRE(p->lo8_dtype == 0 || p->lo8_dtype == NRSE_FP8 ||
-                   (p->lo8_dtype == NRSE_MX6 && p->n % 32 == 0 && (!p->ema_t || p->ema_n % 32 == 0) &&
-                    ((uintptr_t)p->p_shadow_lo8 & 31) == 0 && ((uintptr_t)p->ema_shadow_lo8 & 31) == 0),
-               "nrse_adamw: lo8_dtype %d (MXFP6: n, ema_n multiples of 32, 32-byte aligned planes)", p->lo8_dtype);
+  NRSE_REQUIRE(p->lo8_dtype == 0 || p->lo8_dtype == NRSE_FP8, "nrse_adamw: lo8_dtype %d (0 or NRSE_FP8)",
+               p->lo8_dtype);
   if (p->n == 0) return NRSE_OK;
   hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(p->n)), dim3(256), 0, (hipStream_t)stream, *p);
   return nrse_check_launch("nrse_adamw");

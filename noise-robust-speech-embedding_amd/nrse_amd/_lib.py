@@ -16,7 +16,6 @@ F32 = 0
 BF16 = 1
 BF16X3 = 2   # output-only split-bf16 planes [hi | lo | hi] (include/nrse_hip.h)
 FP8 = 3      # OCP fp8 e4m3fn, the split-weight mode's correction operands (ABI 6)
-MX6 = 4      # OCP MXFP6 e2m3 in 32-element blocks with E8M0 scales, fp8's byte footprint (ABI 8)
 
 EPI_BIAS = 1 << 0
 EPI_GELU = 1 << 1
@@ -46,7 +45,7 @@ class NrseCaps(ctypes.Structure):
                 ("lds_bytes_per_cu", c_int), ("hbm_bytes", c_ll), ("arch", ctypes.c_char * 32)]
 
 
-ABI_VERSION = 10   # NRSE_ABI_VERSION of include/nrse_hip.h this binding is written against
+ABI_VERSION = 11   # NRSE_ABI_VERSION of include/nrse_hip.h this binding is written against
 
 
 class _Sized(ctypes.Structure):
@@ -178,8 +177,6 @@ _SIGNATURES = {
     "nrse_split_bf16": ([c_vp, c_vp, c_vp, c_ll, c_vp], c_int),
     "nrse_split_lo8": ([c_vp, c_vp, c_int, c_ll, c_vp, c_vp], c_int),
     "nrse_cast_fp8": ([c_vp, c_int, c_vp, c_ll, c_vp], c_int),
-    "nrse_split_lo_mx6": ([c_vp, c_vp, c_ll, c_vp], c_int),
-    "nrse_cast_mx6": ([c_vp, c_int, c_vp, c_ll, c_vp], c_int),
     "nrse_zero": ([c_vp, c_ll, c_vp], c_int),
     "nrse_splitk_reduce": ([c_vp, c_vp, c_int, c_ll, c_int, c_vp], c_int),
     "nrse_rows_reduce": ([c_vp, c_ll, c_vp, c_ll, c_vp, c_ll, c_vp, c_int, c_int, c_int, c_vp], c_int),

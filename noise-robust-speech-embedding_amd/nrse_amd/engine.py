@@ -81,13 +81,6 @@ _DEFER_REDUCE = os.environ.get("NRSE_DEFER_REDUCE", "1") != "0"
 _CONV_SPLIT8 = os.environ.get("NRSE_CONV_SPLIT8", "1") != "0"
 CONV_LO8_EXP = 11   # the derived value at the seeded init (gamma = 1, beta = 0)
 _CONV_LO8_PIN = os.environ.get("NRSE_CONV_LO8_EXP")
-# the correction operands as MXFP6 blocks (ABI 8: e2m3 with a scale per 32 elements, no exponents)
-# instead of fp8 e4m3: opt-in (NRSE_SPLIT_MX6=1). Measured slower (bf16sw 455 vs 466-468 pairs/s,
-# profiles/r05_mx6_ab.txt): on this part the 16x16x128 block-scaled MFMA the 256x256 GEMM's
-# 16x16 accumulators need runs e2m3 at the e4m3 rate (tools/probe_mx_rate.hip: fp8 / fp6 / fp4
-# 3.9 / 4.0 / 4.2 PF); only the 32x32x64 shape doubles it (4.2 -> 7.1 PF), which would take a
-# 32x32 accumulator layout in the correction segments
-_SPLIT_MX6 = os.environ.get("NRSE_SPLIT_MX6", "0") == "1"
 FP8 = K.FP8
 
 
@@ -224,8 +217,7 @@ class EncoderWeights:
 class ByolEngine:
     def __init__(self, arch: WavLMArch, proj_dim: int, pred_dim: int, *, device="cuda", compute_dtype=torch.bfloat16,
                  seed: int = 1234, step_cfg: StepConfig | None = None, init_flat: torch.Tensor | None = None,
-                 do_normalize: bool = True, weight_split: bool = False, split_lo8: bool | None = None,
-                 split_mx6: bool | None = None):
+                 do_normalize: bool = True, weight_split: bool = False, split_lo8: bool | None = None):
         if arch.head_dim != 64:
             raise _lib.NrseError(f"head_dim {arch.head_dim} unsupported (attention kernels are head_dim 64)")
         if weight_split and compute_dtype != torch.bfloat16:
@@ -265,8 +257,9 @@ class ByolEngine:
         # segments in the fp8 form (nothing reads them); a forward that falls back to them (fewer
         # than 128 frames in the batch: no fp8 segments) rebuilds them first (_ensure_lo_planes)
         self._lo_stale = {"online": False, "target": False}
-        # the correction planes' dtype: fp8 e4m3 (K.FP8, default) or MXFP6 blocks (K.MX6, opt-in)
-        self.corr_dt = K.MX6 if (_SPLIT_MX6 if split_mx6 is None else split_mx6) else FP8
+        # the correction planes' dtype: fp8 e4m3 (ABI 8-10's MXFP6 alternative, measured slower at the
+        # same accuracy in profiles/r05_mx6_ab.txt, was retired in ABI 11)
+        self.corr_dt = FP8
         if self.cdt == F32:
             self.online_sh = None
             self.target_sh = None
@@ -388,13 +381,7 @@ class ByolEngine:
         correction planes (nrse_split_lo8). |w - bf16(w)| <= 2^-8 |w|, so with W = max |w| the plane's
         values stay below 448 / 2 (2x headroom for weights that grow in training; beyond it the
         conversion saturates) at lo8_exp = floor(log2(224 / (2^-8 W))); the smallest weights fall to
-        fp8 subnormals, whose absolute error (2^-9 2^-lo8_exp) is far below the bf16 residual itself.
-        MXFP6 planes (corr_dt K.MX6) carry a scale per 32 weights and need no exponent."""
-        if self.corr_dt == K.MX6:
-            self.lo8_exp = 0
-            K.split_lo8(self.online, self.online_lo8)
-            K.split_lo8(self.target, self.target_lo8)
-            return
+        fp8 subnormals, whose absolute error (2^-9 2^-lo8_exp) is far below the bf16 residual itself."""
         W = max(float(t.abs().max()) for f in (self.online, self.target) for t in self._lo8_weights(f))
         self.lo8_exp = _headroom_exp(W)
         if _CONV_LO8_PIN is None:

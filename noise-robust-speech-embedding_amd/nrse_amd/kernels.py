@@ -15,10 +15,9 @@ from . import _lib
 from ._lib import (AdamWParams, AttnBwdParams, AttnFwdParams, Conv0Params, GemmOperand, GemmParams, LnBwdParams,
                    LnFwdParams)
 
-_DT = {torch.float32: _lib.F32, torch.bfloat16: _lib.BF16, torch.float8_e4m3fn: _lib.FP8, torch.uint8: _lib.MX6}
+_DT = {torch.float32: _lib.F32, torch.bfloat16: _lib.BF16, torch.float8_e4m3fn: _lib.FP8}
 FP8 = torch.float8_e4m3fn  # NRSE_FP8: OCP e4m3fn, the split-weight mode's correction operands
-MX6 = torch.uint8          # NRSE_MX6 (ABI 8): MXFP6 blocks in fp8's byte footprint, held as raw bytes
-CORR = (FP8, MX6)          # the correction-plane dtypes
+CORR = (FP8,)              # the correction-plane dtypes (ABI 8-10's MXFP6 retired in ABI 11)
 
 
 def dtype_code(t: torch.Tensor) -> int:
@@ -194,7 +193,7 @@ def gemm(A: Operand, B: Operand, C: torch.Tensor, M: int, N: int, K: int, *, ldc
     if nseg8:
         assert a8 is not None and b8 is not None and a8.t.dtype == b8.t.dtype and a8.t.dtype in CORR
         p.a8, p.b8, p.nseg8 = a8.c(), b8.c(), nseg8
-        p.b8_exp = 0 if a8.t.dtype == MX6 else b8_exp   # MXFP6: the scales are in the blocks
+        p.b8_exp = b8_exp
     if c8 is not None:
         assert c8.dtype in CORR
         p.c8, p.ldc8, p.c8_dtype = ptr(c8), ldc8, dtype_code(c8)
@@ -221,10 +220,10 @@ def gemm(A: Operand, B: Operand, C: torch.Tensor, M: int, N: int, K: int, *, ldc
     _lib.check(_lib.lib().nrse_gemm(ctypes.byref(p), stream_ptr()), "nrse_gemm")
     if probe is not None:
         e1.record()
-        # bf16-equivalent work: an fp8 correction segment runs at twice the bf16 MFMA rate, an
-        # MXFP6 one at four times, so their FLOPs count 1/2 or 1/4 against the bf16 dense peak
-        w8 = (0.25 if a8.t.dtype == MX6 else 0.5) if nseg8 else 0.0
-        tag = ("mx6" if a8.t.dtype == MX6 else "fp8") if nseg8 else ""
+        # bf16-equivalent work: an fp8 correction segment runs at twice the bf16 MFMA rate, so its
+        # FLOPs count 1/2 against the bf16 dense peak
+        w8 = 0.5 if nseg8 else 0.0
+        tag = "fp8" if nseg8 else ""
         # shape key: M, N, K, batch (+ the correction form), the operand orientation (T: k-contiguous)
         # and the epilogue flags and split count (bench.py --detail)
         orient = ("T" if A.kcontig else "N") + ("T" if B.kcontig else "N") + f"/f{flags}/s{splits}"
@@ -830,21 +829,16 @@ def split_bf16(x, hi, lo):
 
 
 def split_lo8(x, lo8, lo8_exp=0, sat=None):
-    """lo8 = fp8((x - bf16(x)) 2^lo8_exp) (nrse_split_lo8): the fp8 correction plane of x; an MX6
-    (uint8) lo8: the MXFP6 blocks of x - bf16(x) (nrse_split_lo_mx6, no exponent). sat: the
+    """lo8 = fp8((x - bf16(x)) 2^lo8_exp) (nrse_split_lo8): the fp8 correction plane of x. sat: the
     saturation counter (ABI 10)."""
     assert x.dtype == torch.float32 and lo8.dtype in CORR and lo8.numel() == x.numel()
-    if lo8.dtype == MX6:
-        _call("nrse_split_lo_mx6", ptr(x), ptr(lo8), x.numel(), stream_ptr())
-    else:
-        _call("nrse_split_lo8", ptr(x), ptr(lo8), int(lo8_exp), x.numel(), _sat_ptr(sat), stream_ptr())
+    _call("nrse_split_lo8", ptr(x), ptr(lo8), int(lo8_exp), x.numel(), _sat_ptr(sat), stream_ptr())
 
 
 def cast_fp8(x, y8):
-    """y8 = fp8(x) (nrse_cast_fp8; x f32 or bf16); an MX6 (uint8) y8: MXFP6 blocks (nrse_cast_mx6)."""
+    """y8 = fp8(x) (nrse_cast_fp8; x f32 or bf16)."""
     assert y8.dtype in CORR and y8.numel() == x.numel()
-    fn = "nrse_cast_mx6" if y8.dtype == MX6 else "nrse_cast_fp8"
-    _call(fn, ptr(x), dtype_code(x), ptr(y8), x.numel(), stream_ptr())
+    _call("nrse_cast_fp8", ptr(x), dtype_code(x), ptr(y8), x.numel(), stream_ptr())
 
 
 def zero(t):

@@ -40,7 +40,6 @@ sys.path.insert(0, os.path.join(os.path.dirname(_HERE), "noise-robust-speech-emb
 from nrse_amd import rng  # noqa: E402  (seed derivation only; no compute)
 
 from . import masks  # noqa: E402
-from . import mx6 as _mx6  # noqa: E402
 
 
 # ------------------------------------------------------------------------- relative buckets
@@ -107,7 +106,7 @@ SPLIT8_SITES = ("qkv", "oproj", "ffn_up", "ffn_down", "conv")
 CONV_LO8_EXP = 11   # nrse_amd/engine.py CONV_LO8_EXP: conv_lo8_exponent at gamma = 1, beta = 0
 _OPERAND_DTYPE = None
 _SITES = None
-_SPLIT8 = None   # (frozenset of sites, exponent e, conv exponent c, format "fp8" | "mx6") or None
+_SPLIT8 = None   # (frozenset of sites, exponent e, conv exponent c) or None
 
 
 def set_operand_dtype(dtype, sites=None) -> None:
@@ -134,20 +133,15 @@ def operand_dtype():
     return _OPERAND_DTYPE
 
 
-def set_split8(sites=None, exponent: int = 0, conv_exponent: int = CONV_LO8_EXP, fmt: str = "fp8") -> None:
+def set_split8(sites=None, exponent: int = 0, conv_exponent: int = CONV_LO8_EXP) -> None:
     """The fp8 correction form of the split-weight mode at `sites` (None: off), lo8_exp = exponent
-    (engine: ByolEngine._set_lo8_planes), the conv stack's exponent conv_exponent; fmt "mx6": the
-    correction operands as MXFP6 blocks along K instead (ABI 8, oracle/mx6.py; no exponents)."""
+    (engine: ByolEngine._set_lo8_planes), the conv stack's exponent conv_exponent."""
     global _SPLIT8
-    assert fmt in ("fp8", "mx6"), fmt
-    _SPLIT8 = None if sites is None else (frozenset(sites), int(exponent), int(conv_exponent), fmt)
+    _SPLIT8 = None if sites is None else (frozenset(sites), int(exponent), int(conv_exponent))
 
 
 def _q8(t: torch.Tensor, e: int) -> torch.Tensor:
-    """A correction operand as the engine stores it, scaled back: fp8(t 2^e) 2^-e, or under the mx6
-    format the MXFP6 round trip of t in blocks of 32 along the last axis."""
-    if _SPLIT8[3] == "mx6":
-        return torch.from_numpy(_mx6.round_trip(t.detach().cpu().float().numpy())).to(t.dtype)
+    """A correction operand as the engine stores it, scaled back: fp8(t 2^e) 2^-e."""
     return fp8_e4m3(t * 2.0 ** e) * 2.0 ** -e
 
 
@@ -157,16 +151,6 @@ def _conv_split8(x: torch.Tensor, w: torch.Tensor, stride: int, c: int) -> torch
     fp8((w - w_hi) 2^c)], scaled by 2^-c)."""
     bf = torch.bfloat16
     x_hi, w_hi = x.to(bf).to(x.dtype), w.to(bf).to(w.dtype)
-    if _SPLIT8[3] == "mx6":
-        # blocks along the channels of a frame (activations [B, C, T]) and of a tap (w [co, ci, k])
-        def qa(t):
-            return _q8(t.transpose(1, 2), 0).transpose(1, 2)
-
-        def qw(t):
-            return _q8(t.permute(0, 2, 1), 0).permute(0, 2, 1)
-
-        corr = F.conv1d(qa(x - x_hi), qw(w_hi), stride=stride) + F.conv1d(qa(x_hi), qw(w - w_hi), stride=stride)
-        return F.conv1d(x_hi, w_hi, stride=stride) + corr
     corr = (F.conv1d(fp8_e4m3((x - x_hi) * 2.0 ** c), fp8_e4m3(w_hi), stride=stride) +
             F.conv1d(fp8_e4m3(x_hi), fp8_e4m3((w - w_hi) * 2.0 ** c), stride=stride))
     return F.conv1d(x_hi, w_hi, stride=stride) + corr * 2.0 ** -c

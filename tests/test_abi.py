@@ -38,7 +38,16 @@ def test_library_exports_every_declared_symbol(lib):
     for name in declared():
         assert hasattr(L, name), name
     version = int(re.search(r"#define NRSE_ABI_VERSION (\d+)", open(HEADER).read()).group(1))
-    assert L.nrse_abi_version() == version == lib.ABI_VERSION == 10
+    assert L.nrse_abi_version() == version == lib.ABI_VERSION == 11
+
+
+def test_retired_mxfp6_forms_are_gone(lib):
+    """ABI 11 retired ABI 8-10's MXFP6 correction planes (slower than fp8 at the same accuracy,
+    profiles/r05_mx6_ab.txt): neither the dtype nor its producers remain."""
+    text = open(HEADER).read()
+    assert "NRSE_MX6 =" not in text and not hasattr(lib, "MX6")
+    out = subprocess.run(["nm", "-D", "--defined-only", lib.LIB_PATH], capture_output=True, text=True, check=True)
+    assert "mx6" not in out.stdout
 
 
 def test_nm_dynamic_symbols(lib):

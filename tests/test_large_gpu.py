@@ -55,20 +55,20 @@ def large(request):
     return dict(z=z, arch=arch, layout=layout, flat=flat, clean=clean, noisy=noisy, tag=request.param)
 
 
-def _engine(large, dtype, wsplit=False, lo8=None, mx6=None):
+def _engine(large, dtype, wsplit=False, lo8=None):
     from nrse_amd.engine import ByolEngine
     z = large["z"]
     eng = ByolEngine(large["arch"], int(z["proj_dim"]), int(z["pred_dim"]), compute_dtype=dtype,
-                     init_flat=large["flat"], weight_split=wsplit, split_lo8=lo8, split_mx6=mx6)
+                     init_flat=large["flat"], weight_split=wsplit, split_lo8=lo8)
     eng.cfg.ema_decay = float(z["ema"])
     eng.cfg.weight_decay = float(z["wd"])
     return eng
 
 
-def _run(large, dtype, wsplit=False, lo8=None, mx6=None):
+def _run(large, dtype, wsplit=False, lo8=None):
     """Eval forward, last_hidden_state, one det train step; returns the measured deviations."""
     z = large["z"]
-    eng = _engine(large, dtype, wsplit, lo8, mx6)
+    eng = _engine(large, dtype, wsplit, lo8)
     if lo8:
         assert eng.online_lo8 is not None
     clean, noisy = large["clean"].cuda(), large["noisy"].cuda()
@@ -163,18 +163,17 @@ def test_large_bf16_deviation(nrse_device, large):
     assert m["bn_running"] < 3e-2, m
 
 
-@pytest.mark.parametrize("lo8,mx6", [(True, True), (True, False), (False, False)], ids=["mx6corr", "fp8corr", "bf16lo"])
-def test_large_bf16sw_matches_reference(nrse_device, large, lo8, mx6):
+@pytest.mark.parametrize("lo8", [True, False], ids=["fp8corr", "bf16lo"])
+def test_large_bf16sw_matches_reference(nrse_device, large, lo8):
     """The north-star mode at bf16 activation cost: bf16 activations, the forward
     GEMMs against the weights' split hi + lo pair. The oracle's site ablation
     (tools/ablate_bf16_sites.py) puts 5.1e-3 of the bf16 mode's 5.15e-3 embedding deviation on
     the WEIGHT rounding (a perturbation shared by every frame, which the time mean keeps) and
     0.7e-3 on the activations; with the weights carried to ~2^-13 (fp8corr: the correction
-    x (w - w_hi) as fp8 e4m3 x times the residual plane scaled by one exponent, the default;
-    mx6corr: both as MXFP6 blocks, opt-in) or ~2^-17 (bf16lo: a second bf16 segment) the
+    x (w - w_hi) as fp8 e4m3 x times the residual plane scaled by one exponent, the default) or ~2^-17 (bf16lo: a second bf16 segment) the
     embeddings meet the 1e-3 bound."""
-    m = _run(large, torch.bfloat16, wsplit=True, lo8=lo8, mx6=mx6)
-    _record(f"bf16sw{'_mx6' if mx6 else ('' if lo8 else '_bf16lo')}_{large['tag']}", m)
+    m = _run(large, torch.bfloat16, wsplit=True, lo8=lo8)
+    _record(f"bf16sw{'' if lo8 else '_bf16lo'}_{large['tag']}", m)
     assert m["eval_emb"] < 1e-3, m          # north-star bound on embeddings
     assert m["hidden_norms"] < 1e-3, m
     assert m["eval_pred"] < 1e-3 and m["eval_tproj"] < 1e-3, m

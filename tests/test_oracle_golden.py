@@ -213,11 +213,11 @@ def test_oracle_split_weight_mode_meets_north_star():
                                    "attention.out_proj.weight", "feed_forward.intermediate_dense.weight",
                                    "feed_forward.output_dense.weight")])
     out = {}
-    for name, sites, s8, fmt in (("split", O.SPLIT_WEIGHT_SITES, None, "fp8"),
-                                 ("split_fp8", O.SPLIT_WEIGHT_SITES, O.SPLIT8_SITES, "fp8"),
-                                 ("bf16", None, None, "fp8")):
+    for name, sites, s8 in (("split", O.SPLIT_WEIGHT_SITES, None),
+                            ("split_fp8", O.SPLIT_WEIGHT_SITES, O.SPLIT8_SITES),
+                            ("bf16", None, None)):
         O.set_operand_dtype(torch.bfloat16, sites)
-        O.set_split8(s8, e8, fmt=fmt)
+        O.set_split8(s8, e8)
         try:
             with torch.no_grad():
                 out[name] = rel(O.encoder_forward(P, arch, clean, train=False).mean(1).numpy(), ref)
@@ -227,6 +227,6 @@ def test_oracle_split_weight_mode_meets_north_star():
     print("split-weight oracle rel-L2 vs reference:", out)
     assert out["split"] < 1e-3, out
     assert out["split_fp8"] < 1e-3, out     # the engine's default bf16sw (fp8 correction segments, ABI 6 / 7)
-    # (the opt-in MXFP6 form, set_split8(..., fmt="mx6"): 3.80e-4 here, profiles/r05_mx6_ab.txt; left
-    # out of the CPU suite for its numpy block quantisation of 300 M weights per forward)
+    # (ABI 8-10's MXFP6 form of the corrections measured 3.80e-4 here, profiles/r05_mx6_ab.txt, and
+    # was retired in ABI 11: slower on this part at the same accuracy)
     assert out["bf16"] > 3e-3, out

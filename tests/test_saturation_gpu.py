@@ -150,7 +150,7 @@ def test_exponents_follow_scaled_conv_gamma_and_layer_weights(nrse_device):
     torch.set_num_threads(min(16, torch.get_num_threads()))
     arch, layout, flat, clean = _large_3s()
     eng = ByolEngine(arch, 1024, 2048, compute_dtype=torch.bfloat16, init_flat=flat, weight_split=True,
-                     split_lo8=True, split_mx6=False)
+                     split_lo8=True)
     e0, c0 = eng.lo8_exp, eng.conv_lo8_exp
     P0 = O.split_flat(layout, flat)["encoder"]
     assert c0 == O.conv_lo8_exponent(P0, arch) == 11
@@ -204,7 +204,7 @@ def test_growing_weights_fire_the_counter_and_move_the_exponent(nrse_device):
     layout = PR.byol_layout(arch, 256, 512)
     flat = PR.init_byol_flat(layout, 7)
     eng = ByolEngine(arch, 256, 512, compute_dtype=torch.bfloat16, init_flat=flat, weight_split=True,
-                     split_lo8=True, split_mx6=False)
+                     split_lo8=True)
     e0 = eng.lo8_exp
     eng.grad.zero_()
     eng.optimizer_step(1e-12)          # at the derived exponent: nothing saturates
@@ -251,7 +251,7 @@ def test_short_batch_bf16sw_forward_uses_current_lo_planes(nrse_device):
     engs = []
     for _ in range(2):
         eng = ByolEngine(arch, 256, 512, compute_dtype=torch.bfloat16, init_flat=flat, weight_split=True,
-                         split_lo8=True, split_mx6=False)
+                         split_lo8=True)
         eng.cfg.overlap_optimizer = True
         for i in range(2):
             eng.train_step(clean.cuda(), noisy.cuda(), lr=1e-3, step_seed=i)   # large lr: the lo planes move

@@ -39,12 +39,6 @@ for name, N, Kd, epi in SHAPES:
     r = torch.randn(M, N, device=dev)
     pre = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
     y8 = torch.empty(M, N, device=dev, dtype=K.FP8)
-    # MXFP6 operands (ABI 8; NRSE_MX6_SHAPE=16 selects the 16x16x128 form, default the 32x32x64 one)
-    w6 = torch.empty(N, Kd, device=dev, dtype=K.MX6)
-    K.split_lo8(w32, w6)
-    x6 = torch.empty(M, Kd, device=dev, dtype=K.MX6)
-    K.cast_fp8(x, x6)
-    y6 = torch.empty(M, N, device=dev, dtype=K.MX6)
     fl = 2.0 * M * N * Kd
 
     def epi_kw(on):
@@ -74,12 +68,6 @@ for name, N, Kd, epi in SHAPES:
             if "fp8corr" in forms:
                 res.setdefault(f"fp8corr/{tag}", []).append(
                     timeit(lambda: K.linear_fwd(x, w2[0], y, x8=x8, w8=w8, lo8_exp=19, **kw8)))
-            if "mx6corr" in forms:
-                kw6 = dict(kw)
-                if on and epi == "gelu":
-                    kw6["out8"] = y6
-                res.setdefault(f"mx6corr/{tag}", []).append(
-                    timeit(lambda: K.linear_fwd(x, w2[0], y, x8=x6, w8=w6, **kw6)))
     print(f"{name}[{epi}] {M}x{N}x{Kd}: " + "  ".join(
         f"{k} {statistics.median(v):.1f}us ({fl / statistics.median(v) / 1e6:.0f}TF/bf16-seg)" for k, v in res.items()),
         flush=True)
