@@ -369,9 +369,12 @@ def create_dataloaders(config: dict, feature_extractor=None, *, device=None, syn
                                                generator=torch.Generator().manual_seed(t.get("seed", 42)))
         tr, va = _rank_share(tr, rank, world), _rank_share(va, rank, world)
         bs = int(t["batch_size"])
-        return (torch.utils.data.DataLoader(tr, shuffle=True, batch_size=bs, num_workers=0,
+        # pinned batches: the loop's .to(device, non_blocking=True) is then an async DMA copy
+        pin = torch.cuda.is_available()
+        return (torch.utils.data.DataLoader(tr, shuffle=True, batch_size=bs, num_workers=0, pin_memory=pin,
                                             drop_last=bs > 1 and len(tr) % bs == 1),
-                torch.utils.data.DataLoader(va, shuffle=False, batch_size=bs, num_workers=0) if len(va) > 0 else None)
+                torch.utils.data.DataLoader(va, shuffle=False, batch_size=bs, num_workers=0, pin_memory=pin)
+                if len(va) > 0 else None)
     if feature_extractor is not None and hasattr(feature_extractor, "do_normalize"):
         d = {**d, "do_normalize": bool(feature_extractor.do_normalize)}
     device = device or torch.device("cuda", torch.cuda.current_device())

@@ -966,7 +966,8 @@ class ByolEngine:
             elif S <= 2 or (cdt == torch.bfloat16 and cpg == 64):
                 # at most two partial sums per element onto the zeroed dWf: an order-independent,
                 # deterministic f32 sum
-                dWf = torch.zeros(G, cpg, pk * cpg, device=dev, dtype=F32)
+                dWf = torch.empty(G, cpg, pk * cpg, device=dev, dtype=F32)
+                K.zero(dWf)   # (the library's fill: no ATen kernel in the step)
                 K.gemm(A_op, B_op, dWf, cpg, pk * cpg, T, ldc=pk * cpg, nseg=B // S, splits=S, batch=G,
                        c_z1=cpg * pk * cpg, flags=_lib.EPI_ATOMIC)
             else:
@@ -1400,9 +1401,11 @@ class ByolEngine:
         return float(self.sumsq_buf.sqrt()) / world_size
 
     def train_step(self, clean: torch.Tensor, noisy: torch.Tensor, *, lr: float, step_seed: int, rank: int = 0,
-                   allreduce=None, world_size: int = 1) -> torch.Tensor:
+                   allreduce=None, world_size: int = 1, loss_out: torch.Tensor | None = None) -> torch.Tensor:
         """One iteration of train_one_epoch (train_byol.py:47-77): forward, loss, backward,
-        clip, AdamW, EMA. Returns the device-resident loss (no sync)."""
+        clip, AdamW, EMA. Returns the device-resident loss (no sync): loss_buf, or loss_out (a
+        one-element f32 device view, e.g. a slot of the epoch's loss array) when given, so a loop
+        that keeps every step's loss needs no copy of loss_buf per step."""
         B = clean.shape[0]
         K.zero(self.health_buf)   # rows: clean, noisy, online_pred, target_proj (nrse_amd/health.py)
         K.health(clean, self.health_buf[0])
@@ -1410,16 +1413,18 @@ class ByolEngine:
         pred, tproj, ctx = self.forward(clean, noisy, train=True, step_seed=step_seed, rank=rank, need_grad=True)
         K.health(pred, self.health_buf[2])
         K.health(tproj, self.health_buf[3])
-        K.zero(self.loss_buf)
+        loss = self.loss_buf if loss_out is None else loss_out
+        assert loss.dtype == F32 and loss.numel() == 1 and loss.is_contiguous() and loss.device == self.loss_buf.device
+        K.zero(loss)
         dpred = torch.empty_like(pred)
-        K.byol_loss(pred, tproj, self.loss_buf, dpred, self.loss_stats)
+        K.byol_loss(pred, tproj, loss, dpred, self.loss_stats)
         self.sync_optimizer()  # the last update has read (and with fused_zero_grad zeroed) the gradient
         if not self._grad_zeroed:
             K.zero(self.grad)
         self._grad_zeroed = False
         self.backward(dpred, ctx, allreduce=allreduce)
         self.optimizer_step(lr, grad_scale=1.0 / world_size)
-        return self.loss_buf
+        return loss
 
     def eval_forward(self, clean, noisy):
         self.sync_optimizer()

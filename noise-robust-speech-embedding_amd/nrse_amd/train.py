@@ -138,26 +138,32 @@ def train_one_epoch(model, dataloader, optimizer, scheduler, device, config, all
     steps late (nrse_amd/health.py), so no host sync happens inside the loop."""
     model.train()
     eng = model.engine
-    losses = []
+    # every step's loss lands in its own slot (train_step(loss_out=)): no per-step copy kernel
+    try:
+        n_slots = max(1, len(dataloader))
+    except TypeError:           # a loader without a length
+        n_slots = 1024
+    losses = torch.empty(n_slots, device=eng.dev, dtype=torch.float32)
     steps = 0
     for batch in dataloader:
+        if steps == losses.numel():   # more batches than the loader announced
+            losses = torch.cat([losses, torch.empty_like(losses)])
         clean = batch["clean_input_values"].to(device, non_blocking=True)
         noisy = batch["noisy_input_values"].to(device, non_blocking=True)
-        loss = eng.train_step(clean.reshape(clean.shape[0], -1), noisy.reshape(noisy.shape[0], -1),
-                              lr=optimizer.lr, step_seed=step0 + steps, rank=rank, allreduce=allreduce,
-                              world_size=world)
+        eng.train_step(clean.reshape(clean.shape[0], -1), noisy.reshape(noisy.shape[0], -1),
+                       lr=optimizer.lr, step_seed=step0 + steps, rank=rank, allreduce=allreduce,
+                       world_size=world, loss_out=losses[steps:steps + 1])
         if health is not None:
             health.record(step0 + steps, eng.health_buf, engine=eng)
-        losses.append(loss.clone())
         scheduler.step()
         steps += 1
         if max_steps is not None and step0 + steps >= max_steps:
             break
     if health is not None:
         health.flush()
-    if not losses:
+    if not steps:
         return float("nan"), steps
-    return float(torch.stack(losses).mean()), steps  # one host sync per epoch
+    return float(losses[:steps].mean()), steps  # one host sync per epoch
 
 
 @torch.no_grad()
