@@ -77,13 +77,13 @@ def cpu_baseline(arch_large, seconds_hint=20.0):
                       f"os.cpu_count()={os.cpu_count()}"}
 
 
-TRAFFIC_FILE = "r05_gemm_traffic.json"
-SQ_TABLE_FILE = "r05_pmc_sq_table.json"
+TRAFFIC_FILE = "r06_gemm_traffic.json"
+SQ_TABLE_FILE = "r06_pmc_sq_table.json"
 
 
 def gemm_traffic():
     """HBM bytes per nrse_gemm launch from the committed rocprofv3 PMC summary of the current
-    step (tools/pmc_gemm.sh -> profiles/r05_gemm_traffic.json: FETCH_SIZE x 2 (gfx950
+    step (tools/pmc_gemm.sh -> profiles/r06_gemm_traffic.json: FETCH_SIZE x 2 (gfx950
     correction) + WRITE_SIZE, averaged over the GEMM launches of a bench step). None if absent."""
     path = os.path.join(ROOT, "profiles", TRAFFIC_FILE)
     try:
@@ -95,7 +95,7 @@ def gemm_traffic():
 
 def gemm_mfma_busy():
     """Matrix-pipe busy fraction of the 256x256 GEMM kernels from the committed counter pass
-    (tools/pmc_sq.sh -> profiles/r05_pmc_sq_table.json): SQ_VALU_MFMA_BUSY_CYCLES over all
+    (tools/pmc_sq.sh -> profiles/r06_pmc_sq_table.json): SQ_VALU_MFMA_BUSY_CYCLES over all
     SIMD-cycles of the launch (GRBM_GUI_ACTIVE / 8 XCDs x 256 CUs x 4 SIMDs), per step shape,
     isolated launches. None if absent."""
     path = os.path.join(ROOT, "profiles", SQ_TABLE_FILE)
@@ -118,7 +118,7 @@ def north_star_parity():
     profiles/): the newest round's files."""
     out = {}
     for tag in ("3s", "8s", "12s"):
-        for rnd in ("r05", "r04"):
+        for rnd in ("r06", "r05", "r04"):
             path = os.path.join(ROOT, "profiles", f"{rnd}_large_parity_bf16sw_{tag}.json")
             try:
                 with open(path) as fh:

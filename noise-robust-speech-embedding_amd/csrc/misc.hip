@@ -68,30 +68,39 @@ __global__ void pad_rows_kernel(const void* __restrict__ src, int sdt, void* __r
 // b*C + k under the step's key, then k itself, so keys never tie). The reference draws the subset
 // with numpy (np.random.choice(..., replace=False)); the distribution is the same, the stream is
 // a counter hash that oracle/masks.py specaug_mask replays bit for bit. One workgroup per
-// utterance: keys in LDS, each candidate ranked by one broadcast sweep, then each frame ORs the
+// utterance: keys in LDS, each candidate ranked by one broadcast sweep (8 LDS reads in flight per
+// step: the sweep had waited for each read, ~44 us per launch at T = 399), then each frame ORs the
 // selection flags of the L starts that cover it (one coalesced byte store per frame).
-constexpr int SPEC_CMAX = 4096;
-__global__ __launch_bounds__(256) void specaug_mask_kernel(unsigned char* __restrict__ mask, int T, int L, int n,
-                                                           uint32_t key) {
-  __shared__ unsigned long long keys[SPEC_CMAX];
+constexpr int SPEC_CMAX = 4096, SPEC_NT = 512;
+__global__ __launch_bounds__(SPEC_NT) void specaug_mask_kernel(unsigned char* __restrict__ mask, int T, int L, int n,
+                                                               uint32_t key) {
+  __shared__ unsigned long long keys[SPEC_CMAX + 8];
   __shared__ unsigned char sel[SPEC_CMAX];
   const int b = blockIdx.x, tid = threadIdx.x;
   const int C = T - L + 1;
   if (n > 0) {
-    for (int k = tid; k < C; k += 256) {
+    const int C8 = (C + 7) & ~7;
+    for (int k = tid; k < C8; k += SPEC_NT) {
       const uint32_t h = mix32(((uint32_t)b * (uint32_t)C + (uint32_t)k) ^ key);
-      keys[k] = ((unsigned long long)h << 32) | (unsigned long long)(unsigned)k;
+      // padding past C: the largest key, never below a candidate's
+      keys[k] = k < C ? ((unsigned long long)h << 32) | (unsigned long long)(unsigned)k : ~0ull;
     }
     __syncthreads();
-    for (int k = tid; k < C; k += 256) {
+    for (int k = tid; k < C; k += SPEC_NT) {
       const unsigned long long mine = keys[k];
       int rank = 0;
-      for (int j = 0; j < C; ++j) rank += keys[j] < mine ? 1 : 0;
+      for (int j = 0; j < C8; j += 8) {
+        unsigned long long v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = keys[j + u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) rank += v[u] < mine ? 1 : 0;
+      }
       sel[k] = rank < n ? 1 : 0;
     }
     __syncthreads();
   }
-  for (int t = tid; t < T; t += 256) {
+  for (int t = tid; t < T; t += SPEC_NT) {
     unsigned char m = 0;
     if (n > 0) {
       const int lo = t - L + 1 < 0 ? 0 : t - L + 1, hi = t < C - 1 ? t : C - 1;
@@ -407,7 +416,7 @@ extern "C" int nrse_specaug_mask(unsigned char* mask, int batch, int T, double m
     if (T - (mask_length - 1) < n) n = T - (mask_length - 1) > 0 ? T - (mask_length - 1) : 0;
     seed = mix32_host(key ^ 0x5bd1e995U);
   }
-  hipLaunchKernelGGL(specaug_mask_kernel, dim3(batch), dim3(256), 0, (hipStream_t)stream, mask, T, L, n, seed);
+  hipLaunchKernelGGL(specaug_mask_kernel, dim3(batch), dim3(SPEC_NT), 0, (hipStream_t)stream, mask, T, L, n, seed);
   return nrse_check_launch("nrse_specaug_mask");
 }
 
