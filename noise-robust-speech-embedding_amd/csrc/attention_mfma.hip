@@ -270,6 +270,12 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    // this tile's bias rows, read BEFORE the prefetch is issued: a read of the bias copies after
+    // it made the compiler wait for the prefetch (s_waitcnt vmcnt(0): it cannot tell the copies
+    // from the DMA's destination) right after the first S MFMAs (r06: p = 0 forward 54-55 -> 52-53 us)
+    float4 bb4[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) bb4[t] = *reinterpret_cast<const float4*>(bvl_base + kb + boff[t]);
     // prefetch tile it+1 into the other buffer (its last readers finished before this barrier)
     const uint32_t mcur = mnext;
     if (!LAST || it + 1 < ntiles) {
@@ -292,7 +298,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_param
     const f32x2 c12 = {c1, c1}, gl2 = {gl, gl}, nm2 = {-mref, -mref};
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const float4 bb = *reinterpret_cast<const float4*>(bvl_base + kb + boff[t]);
+      const float4 bb = bb4[t];
       const f32x2 r0 = pk_fma(f32x2{s[t][0], s[t][1]}, c12, pk_fma(gl2, f32x2{bb.x, bb.y}, nm2));
       const f32x2 r1 = pk_fma(f32x2{s[t][2], s[t][3]}, c12, pk_fma(gl2, f32x2{bb.z, bb.w}, nm2));
       v[t][0] = r0.x; v[t][1] = r0.y; v[t][2] = r1.x; v[t][3] = r1.y;
@@ -487,6 +493,13 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    // the bias rows before the prefetch is issued (as the forward's)
+    float bb[4][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float4 v4 = *reinterpret_cast<const float4*>(bvl_base + kb + boff[t]);
+      bb[t][0] = v4.x; bb[t][1] = v4.y; bb[t][2] = v4.z; bb[t][3] = v4.w;
+    }
     const uint32_t mcur = mnext;
     if (!LAST || it + 1 < ntiles) {
       char* const Kn = kv0 + ((it + 1) & 1) * 2 * TILE_B;
@@ -510,12 +523,7 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_par
     // Straight-line per element; wave-uniform branches for dropout and for the last (partial)
     // key tile. Rows of invalid queries need no mask: their Q, dO, gate, lse and delta are zero,
     // so d = 1 * (0 - 0) = 0.
-    float ds[4][4], bb[4][4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const float4 v4 = *reinterpret_cast<const float4*>(bvl_base + kb + boff[t]);
-      bb[t][0] = v4.x; bb[t][1] = v4.y; bb[t][2] = v4.z; bb[t][3] = v4.w;
-    }
+    float ds[4][4];
     if constexpr (DROP) {
       if constexpr (use_mask) {
 #pragma unroll
