@@ -73,8 +73,17 @@ NRSE_DEV uint32_t fp8x4(float a, float b, float c, float d) {
 }
 NRSE_DEV unsigned char fp8_1(float a) { return (unsigned char)(fp8x4(a, 0.f, 0.f, 0.f) & 0xffu); }
 // ABI 10: how many of 4 values fp8x4 saturates (|v| > 448, clamped instead of rounded), and the
-// producers' counter update (an atomic only when something saturated: never in normal operation)
+// producers' counter update (an atomic only when something saturated: never in normal operation).
+// The common case (nothing saturates) costs two max and one compare; the exact count runs only
+// in a wave where some lane saturated (wave-uniform branch)
+#ifndef NRSE_SAT_FAST
+#define NRSE_SAT_FAST 1   // 0: the exact count on every call (A/B)
+#endif
 NRSE_DEV int fp8_nsat4(float a, float b, float c, float d) {
+#if NRSE_SAT_FAST
+  const float m = fmaxf(fmaxf(fabsf(a), fabsf(b)), fmaxf(fabsf(c), fabsf(d)));
+  if (!__builtin_amdgcn_ballot_w64(m > 448.f)) return 0;
+#endif
   return (int)(fabsf(a) > 448.f) + (int)(fabsf(b) > 448.f) + (int)(fabsf(c) > 448.f) + (int)(fabsf(d) > 448.f);
 }
 NRSE_DEV void sat_count_add(unsigned int* cnt, int n) {

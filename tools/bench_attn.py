@@ -49,3 +49,7 @@ print(f"p={p} recorded mask: fwd {tf*1e3:.1f}us ({fl/tf/1e9:.0f} TF) | bwd {tb*1
 tm = timeit(lambda: K.attn_dropout_mask(mask, B, T, H, p, 1))
 tf2 = timeit(lambda: K.attn_fwd(qkv, gate, bias, ctx, lse, B, T, H, p, 1, bias_vec=bvec, drop_mask=mask, mask_in=True))
 print(f"p={p} precomputed mask: mask kernel {tm*1e3:.1f}us | fwd {tf2*1e3:.1f}us ({fl/tf2/1e9:.0f} TF)", flush=True)
+# the split-weight (bf16sw) step's form: the recorded mask plus the fp8 copy of ctx (ctx8)
+ctx8 = torch.empty(B * T, H * 64, device=dev, dtype=K.FP8)
+tf8 = timeit(lambda: K.attn_fwd(qkv, gate, bias, ctx, lse, B, T, H, p, 1, bias_vec=bvec, drop_mask=mask, ctx8=ctx8))
+print(f"p={p} recorded mask + ctx8: fwd {tf8*1e3:.1f}us ({fl/tf8/1e9:.0f} TF)", flush=True)
