@@ -2,7 +2,7 @@
 before / after ByolEngine.forward (both views joined), the loss, backward (side streams joined)
 and optimizer_step, over timed steps of the bench workload (configs[1], B = 32, 8 s). With the
 overlapped optimizer the AdamW segments run on their own stream beside the next forward; the
-'optimizer' phase is then only its enqueue point. Usage: python tools/diag_step_phases.py [bf16|bf16sw]"""
+'optimizer' phase is then only its enqueue point. Usage: python tools/diag_step_phases.py [bf16|bf16sw] [B]"""
 import math
 import os
 import sys
@@ -15,9 +15,10 @@ from nrse_amd import arch as A, kernels as K
 from nrse_amd.engine import ByolEngine, StepConfig, compute_mode
 
 mode = sys.argv[1] if len(sys.argv) > 1 else "bf16"
+B_ARG = int(sys.argv[2]) if len(sys.argv) > 2 else 32
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
-B, L = 32, 128000
+B, L = B_ARG, 128000
 gen = torch.Generator(device=dev)
 gen.manual_seed(1234)
 clean_raw = torch.randn(B, L, device=dev, generator=gen) * 0.1
@@ -53,14 +54,19 @@ def wrap(name):
 for n in ("forward", "backward", "optimizer_step"):
     wrap(n)
 
+import time
 warm, steps = 3, 8
+host = []
 for i in range(warm + steps):
     if i == warm:
         torch.cuda.synchronize()
         marks.clear()
+    h0 = time.perf_counter()
     mark("step>")
     K.snr_mix(clean_raw, noise_raw, noise_len, snr, clean_iv, noisy_iv, status, kscale, K.SNR_PEAK_ZMUV)
     eng.train_step(clean_iv, noisy_iv, lr=0.5e-5 * (1 + math.cos(math.pi * i / 1e6)), step_seed=i)
+    if i >= warm:
+        host.append((time.perf_counter() - h0) * 1e3)
 mark("end")
 torch.cuda.synchronize()
 acc = {}
@@ -68,6 +74,7 @@ for (t0, e0), (t1, e1) in zip(marks, marks[1:]):
     key = f"{t0} -> {t1}"
     acc[key] = acc.get(key, 0.0) + e0.elapsed_time(e1)
 total = marks[0][1].elapsed_time(marks[-1][1])
-print(f"{mode}: {total / steps:.2f} ms per step over {steps} steps")
+print(f"{mode} B={B}: {total / steps:.2f} ms per step over {steps} steps; host enqueue per step "
+      f"{sum(host) / len(host):.2f} ms (min {min(host):.2f}, max {max(host):.2f})")
 for k, v in acc.items():
     print(f"  {k:40s} {v / steps:8.2f} ms")
