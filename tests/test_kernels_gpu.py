@@ -649,3 +649,23 @@ def test_specaug_mask_device_matches_oracle(nrse_device, T, B):
     K.specaug_mask(m, 0.0, 10, 2, 5)
     torch.cuda.synchronize()
     assert int(m.sum()) == 0
+
+
+@pytest.mark.parametrize("T,prob,L,min_masks", [(10, 0.65, 10, 2), (12, 0.05, 5, 2), (37, 1.0, 10, 2), (23, 0.3, 1, 0)])
+def test_specaug_mask_edge_cases_match_oracle(nrse_device, T, prob, L, min_masks):
+    """The span count's clamps ([TF]modeling_wavlm.py _compute_mask_indices): one start only (T = L),
+    min_masks forcing more spans than fit (n = T // L), mask_prob 1 (n capped at T // L), spans of
+    length 1; and mask_length > T raises like the reference's ValueError."""
+    from nrse_amd import kernels as K, _lib
+    from oracle import masks as MK
+    B = 5
+    for seed in (3, 1234):
+        m = torch.empty(B, T, device="cuda", dtype=torch.uint8)
+        K.specaug_mask(m, prob, L, min_masks, seed)
+        torch.cuda.synchronize()
+        ref = MK.specaug_mask(seed, B, T, prob, L, min_masks)
+        assert np.array_equal(m.cpu().numpy().astype(bool), ref), (T, prob, L, seed)
+    with pytest.raises(_lib.NrseError, match="mask_length"):
+        K.specaug_mask(torch.empty(B, 8, device="cuda", dtype=torch.uint8), 0.5, 10, 2, 1)
+    with pytest.raises(ValueError):
+        MK.specaug_mask(1, B, 8, 0.5, 10, 2)
