@@ -490,7 +490,12 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
   const int per_z = mt * nt;
   const int z = wg / per_z;
   const int tt = wg - z * per_z;
-  constexpr int GM = 8;
+#ifndef NRSE_GEMM_GM
+#define NRSE_GEMM_GM 4
+#endif
+  // M-tiles per group of the tile order: r06 same-box step A/B 4 > 8 (+0.4-0.6 %) > 2 > 16 > 1
+  // (profiles/r06_gemm_group_ab.txt; NRSE_GEMM_GM rebuilds another)
+  constexpr int GM = NRSE_GEMM_GM;
   const int group = tt / (GM * nt);
   const int first_m = group * GM;
   const int gm = min(GM, mt - first_m);
