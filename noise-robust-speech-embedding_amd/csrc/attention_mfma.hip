@@ -183,8 +183,19 @@ NRSE_DEV void bv_stage(float* bv, const float* vec, int T, int q0, int tid) {
 // (and its keep bits recorded to drop_mask if given), 2 the keep bits read from drop_mask
 // (nrse_attn_dropout_mask computed them ahead, beside the GEMMs: the hash and the bit assembly
 // were about half of this VALU-bound loop's issue cycles)
+// 4 waves per SIMD (<= 128 VGPRs; the LDS fits 4 workgroups per CU): the dropout forms had
+// allocated 130 VGPRs, 3 waves (r06 A/B: recorded-mask forward 70.6-72.1 -> 68.4-68.5 us, the
+// step neutral, profiles/r06_attn_fwd_waves_ab.txt); 0 leaves the occupancy to the compiler
+#ifndef NRSE_ATTN_FWD_WAVES
+#define NRSE_ATTN_FWD_WAVES 4
+#endif
+#if NRSE_ATTN_FWD_WAVES
+#define NRSE_FWD_OCC __attribute__((amdgpu_waves_per_eu(NRSE_ATTN_FWD_WAVES, NRSE_ATTN_FWD_WAVES)))
+#else
+#define NRSE_FWD_OCC
+#endif
 template <int DM>
-__global__ __launch_bounds__(256) void attn_fwd_kernel(const nrse_attn_fwd_params p) {
+__global__ __launch_bounds__(256) NRSE_FWD_OCC void attn_fwd_kernel(const nrse_attn_fwd_params p) {
   constexpr bool DROP = DM != 0;
   extern __shared__ __attribute__((aligned(16))) char dyn[];
   char* const kv0 = dyn;                       // [2 buffers][K tile, V tile]
