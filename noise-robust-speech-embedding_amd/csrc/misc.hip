@@ -687,7 +687,9 @@ NRSE_DEV void rows_reduce_body(float4 (*red)[1024 / RG], const RowsDst& dst, con
   __syncthreads();
   if (r == 0 && col < n) {
     float4 t = red[0][q];
-#pragma unroll
+    // (unrolled by 8, not whole: at RG = 64 the compiler put all 63 LDS reads in flight at once
+    // and spilled ~138 VGPRs of the 1024-thread workgroup's 128; same adds in the same order)
+#pragma unroll 8
     for (int i = 1; i < RG; ++i) { t.x += red[i][q].x; t.y += red[i][q].y; t.z += red[i][q].z; t.w += red[i][q].w; }
     int j = 0;
     long long c = col;
