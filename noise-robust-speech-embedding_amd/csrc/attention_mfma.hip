@@ -61,11 +61,22 @@ NRSE_DEV bf16x8 rd_tr(const char* t, int r0, int r1, int c0, int lane) {
 // row_ror:(16 - r): lane x receives lane (x + r) mod 16), added to the accumulator of its
 // diagonal: lo if the rotation did not wrap, hi (16 further down) if it did. The wrap test is a
 // per-lane constant, so it enters as 0/1 multipliers (mlo = 1 - mhi) and each half is one fma.
+#ifndef NRSE_DIAG_DPPADD
+#define NRSE_DIAG_DPPADD 1
+#endif
 template <int R>
 NRSE_DEV void diag_rot(float v, float mlo, float mhi, float& lo, float& hi) {
+#if NRSE_DIAG_DPPADD
+  // the two halves of the rotation as row shifts (lanes with no source read 0), each folded by
+  // the compiler into a v_add_f32 with a DPP source: 2 VALU instead of a DPP move + 2 FMAs
+  (void)mlo; (void)mhi;
+  lo += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x100 + R, 0xF, 0xF, true));
+  hi += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x110 + 16 - R, 0xF, 0xF, true));
+#else
   const float u = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x120 + 16 - R, 0xF, 0xF, false));
   lo = fmaf(u, mlo, lo);
   hi = fmaf(u, mhi, hi);
+#endif
 }
 
 NRSE_DEV bf16x8 pack8(const float* a, const float* b) {

@@ -45,6 +45,27 @@ def test_layernorm_fwd_bwd(nrse_device, C, xdt, gelu):
     assert rel(dg, gr.grad) < 1e-5 and rel(db, br.grad) < 1e-5
 
 
+@pytest.mark.parametrize("rows", [1, 3, 7, 9, 17, 4099])
+@pytest.mark.parametrize("ydt", [torch.float32, torch.bfloat16])
+def test_layernorm_fwd_f32_tail_rows(nrse_device, rows, ydt):
+    """The f32-input forward (one row per wave, 4 per workgroup) at row counts that leave a
+    workgroup's last waves idle: matches torch, and nothing past the last row is written."""
+    from nrse_amd import kernels as K
+    dev = nrse_device
+    C = 1024
+    x = torch.randn(rows, C, device=dev) * 3 - 0.25
+    g = torch.randn(C, device=dev) * 0.1 + 1
+    b = torch.randn(C, device=dev) * 0.1
+    y = torch.full((rows + 1, C), 7.0, device=dev, dtype=ydt)   # one guard row past the end
+    mean = torch.full((rows + 1,), 7.0, device=dev); rstd = torch.full((rows + 1,), 7.0, device=dev)
+    K.ln_fwd(x, g, b, y[:rows], mean[:rows], rstd[:rows], 1e-5)
+    ref = F.layer_norm(x.double(), (C,), g.double(), b.double(), 1e-5)
+    assert rel(y[:rows].float(), ref) < (1e-5 if ydt == torch.float32 else 4e-3)
+    assert torch.equal(y[rows].float(), torch.full((C,), 7.0, device=dev))
+    assert mean[rows].item() == 7.0 and rstd[rows].item() == 7.0
+    assert rel(mean[:rows], x.double().mean(1)) < 1e-6
+
+
 @pytest.mark.parametrize("rows", [12768, 333, 5])
 @pytest.mark.parametrize("dvdt", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("p", [0.0, 0.1])
