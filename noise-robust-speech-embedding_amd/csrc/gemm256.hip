@@ -260,6 +260,12 @@ NRSE_DEV int fast_epi_mode(const nrse_gemm_params& p) {
   return m;
 }
 
+#ifndef NRSE_EPI_LDSBAR
+#define NRSE_EPI_LDSBAR 1  // 0: the general epilogue's passes behind __syncthreads (A/B)
+#endif
+#ifndef NRSE_EPI_FASTBAR
+#define NRSE_EPI_FASTBAR 1  // 0: the register epilogue's passes behind __syncthreads (A/B)
+#endif
 template <int FE, int BMT>
 NRSE_DEV void fast_epilogue(const nrse_gemm_params& p, const f32x4 (&acc)[8][4], char* smem, int m0, int n0, int wm,
                             int wn, int lane, int tid, long long zq, long long zr, int split,
@@ -292,6 +298,17 @@ NRSE_DEV void fast_epilogue(const nrse_gemm_params& p, const f32x4 (&acc)[8][4],
   // group behind an `if (ok)`, each load sat in its own basic block and the pass waited for the
   // memory latency 16 times (s_waitcnt vmcnt(0) after every load; the out-projection's epilogue
   // was then longer than its main loop)
+  // the image hand-offs between the passes need the LDS accesses retired, not the row stores
+  // (NRSE_EPI_FASTBAR=0: __syncthreads, which also waits for every store of the pass)
+  auto fast_bar = [] {
+#if NRSE_EPI_FASTBAR
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#else
+    __syncthreads();
+#endif
+  };
   __amdgpu_buffer_rsrc_t rrs, ars;
   if constexpr (RESID)
     rrs = make_rsrc(reinterpret_cast<const char*>((const float*)p.resid + epi.rbase + (long long)m0 * p.ldr + n0));
@@ -391,7 +408,7 @@ NRSE_DEV void fast_epilogue(const nrse_gemm_params& p, const f32x4 (&acc)[8][4],
       }
     }
     if (DIRECT) continue;
-    __syncthreads();
+    fast_bar();
     NRSE_STAMP(4 + 2 * pass);
     if (colsum) {
       // column sums of the staged values (as stored: bf16-rounded for bf16 output): thread
@@ -446,7 +463,7 @@ NRSE_DEV void fast_epilogue(const nrse_gemm_params& p, const f32x4 (&acc)[8][4],
         *reinterpret_cast<uint4*>((bf16_t*)p.aux + epi.abase + (long long)m * p.ldaux + n) = w;
       }
     }
-    __syncthreads();
+    fast_bar();
     if (pass == 0) NRSE_STAMP(5);
   }
   if (colsum && tid < 512 && n0 + (tid & 255) < p.N)
@@ -1003,6 +1020,18 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
   const int ccol = tid & 255, chalf = tid >> 8;
   float csum = 0.f;
   const int g = lane >> 4, li = lane & 15;
+  // the passes hand the staging area over with LDS-only barriers: a pass's row stores drain while
+  // the next pass stages and stores (__syncthreads waited for every store of the pass, vmcnt(0));
+  // epi8's own operand loads keep the compiler's counted waits
+  auto gen_bar = [] {
+#if NRSE_EPI_LDSBAR
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#else
+    __syncthreads();
+#endif
+  };
 #pragma unroll
   for (int pass = 0; pass < 4; ++pass) {
     const int prows = (pass & 1) ? NFI_HI * 16 : 64;  // rows of this pass: (M-wave, M-half)
@@ -1014,7 +1043,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
         for (int fn = 0; fn < 4; ++fn)
           *reinterpret_cast<f32x4*>(ct + (fi * 16 + li) * CT_LD + wn * 64 + fn * 16 + 4 * g) = acc[mh * 4 + fi][fn];
     }
-    __syncthreads();
+    gen_bar();
     if (pass == 0) NRSE_STAMP(4);
     const int mrow0 = m0 + (pass >> 1) * (BMT / 2) + (pass & 1) * 64;
     if (flags & NRSE_EPI_ATOMIC) {
@@ -1047,11 +1076,11 @@ __global__ __launch_bounds__(NTHR, 1) void gemm256_kernel(const nrse_gemm_params
         epi8(p, epi, m, n, cr, colsum);
       }
       if (colsum) {
-        __syncthreads();
+        gen_bar();
         for (int r = chalf * 32; r < chalf * 32 + 32; ++r) csum += ct[r * CT_LD + ccol];
       }
     }
-    __syncthreads();
+    gen_bar();
     if (pass == 0) NRSE_STAMP(5);
     if (pass == 1) NRSE_STAMP(6);
   }
