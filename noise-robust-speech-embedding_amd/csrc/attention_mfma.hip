@@ -431,8 +431,16 @@ __global__ __launch_bounds__(256) NRSE_FWD_OCC void attn_fwd_kernel(const nrse_a
 // ------------------------------------------------------------------------------ bwd: dQ, dgate
 // DM: dropout mode, 0 none, 1 re-hashed keep bits, 2 the forward's recorded bits (drop_mask);
 // one specialisation each (both paths in one kernel cost 20 VGPRs and a wave per SIMD)
+#ifndef NRSE_ATTN_BWDQ_WAVES
+#define NRSE_ATTN_BWDQ_WAVES 3
+#endif
+#if NRSE_ATTN_BWDQ_WAVES
+#define NRSE_BWDQ_OCC __attribute__((amdgpu_waves_per_eu(NRSE_ATTN_BWDQ_WAVES, NRSE_ATTN_BWDQ_WAVES)))
+#else
+#define NRSE_BWDQ_OCC
+#endif
 template <int DM>
-__global__ __launch_bounds__(256) void attn_bwd_q_kernel(const nrse_attn_bwd_params p) {
+__global__ __launch_bounds__(256) NRSE_BWDQ_OCC void attn_bwd_q_kernel(const nrse_attn_bwd_params p) {
   constexpr bool DROP = DM != 0;
   extern __shared__ __attribute__((aligned(16))) char dyn[];
   char* const kv0 = dyn;  // [2 buffers][K tile, V tile], LDS-DMA double buffer as in the forward
